@@ -1,0 +1,547 @@
+// conv.hip — client-batched implicit-GEMM convolution / linear on fp32 MFMA (gfx950).
+//
+// Replaces nn.Conv2d / nn.Linear forward+backward of the reference models
+// (src/shared/models_pytorch.py:59-246) as driven by LocalTrainer._train_epoch
+// (src/shared/training.py:192-197).  All three products are one kernel
+// template, one GEMM per client slot (grid.z), each client with its own
+// weights (FedAvg clients never share parameters during local training):
+//
+//   FWD   : Y[co][pix]      = sum_{ci,kh,kw} W[co][ci,kh,kw] * im2col(X)[ci,kh,kw][pix]
+//   DGRAD : dX[ci][pix_in]  = sum_{co,kh,kw} W[co][ci,kh,kw] * col(dY)[co,kh,kw][pix_in]
+//   WGRAD : dW[co][ci,kh,kw]= sum_{pix}      dY[co][pix]     * im2col(X)[ci,kh,kw][pix]
+//
+// GEMM row index m sits in the MFMA accumulator REGISTERS and the column index
+// n on the LANES, so the pixel dimension (contiguous in NCHW) is what 32
+// consecutive lanes store: every epilogue store is a 128-B coalesced segment.
+// Operands are staged global -> registers -> LDS (double buffered, one barrier
+// per K-step) in k-major [BK][B{M,N}+1] images: a lane's MFMA operand read
+// (32 consecutive m or n at one k) is bank-conflict free for ds_read_b32, and
+// the +1 pad makes the k-fast staging writes conflict free too.
+// v_mfma_f32_32x32x2_f32 (exact fp32, 64 cyc/SIMD) is the MAC engine; each
+// wave owns an FM x FN grid of 32x32 accumulators.
+#include "fh_common.h"
+
+namespace fh {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum { OP_FWD = 0, OP_DGRAD = 1, OP_WGRAD = 2 };
+
+struct ConvArgs {
+    const float* x;     // FWD/WGRAD: input activations; DGRAD: unused
+    const float* wt;    // FWD/DGRAD: weights
+    const float* dy;    // DGRAD/WGRAD: output gradient
+    const float* bias;  // FWD: bias or null
+    float* out;         // FWD: y, DGRAD: dx, WGRAD: split-K partials
+    int64_t x_cs, w_cs, dy_cs, b_cs, out_cs;
+    const int32_t* counts;
+    int batch, cin, h, w, cout, oh, ow, pad;
+    int relu;
+    int splits, kchunk;  // WGRAD
+    int M, N, K;         // GEMM extents at full batch
+    FastDiv fd_ohw, fd_ow, fd_hw, fd_w;
+};
+
+template <int OP, int KH, int KW, int S, int BM, int BN, int BK, int WAVES_M>
+__global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
+    constexpr int WAVES_N = 4 / WAVES_M;
+    constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+    constexpr int FM = WM / 32, FN = WN / 32;
+    constexpr int KHW = KH * KW;
+    constexpr int NA = BM * BK / 256, NB = BN * BK / 256;
+    static_assert(FM >= 1 && FN >= 1 && NA >= 1 && NB >= 1, "tile");
+    static_assert((256 % BN) == 0 || OP == OP_WGRAD, "n-fast B mapping needs BN | 256");
+
+    __shared__ float As[2][BK][BM + 1];
+    __shared__ float Bs[2][BK][BN + 1];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WAVES_N, wn = wid % WAVES_N;
+
+    int z, split = 0;
+    if constexpr (OP == OP_WGRAD) {
+        z = blockIdx.z / a.splits;
+        split = blockIdx.z - z * a.splits;
+    } else {
+        z = blockIdx.z;
+    }
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int ohw = a.oh * a.ow, hw = a.h * a.w;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+
+    // GEMM extents for this client (partial last batch shrinks the pixel dim).
+    int M = a.M, N = a.N, kbeg = 0, kend = a.K;
+    if constexpr (OP == OP_FWD) N = cnt * ohw;
+    if constexpr (OP == OP_DGRAD) N = cnt * hw;
+    if constexpr (OP == OP_WGRAD) {
+        const int kv = cnt * ohw;
+        kbeg = split * a.kchunk;
+        kend = min(kv, kbeg + a.kchunk);
+    } else {
+        if (n0 >= N) return;
+    }
+
+    // ---------------- per-thread fixed coordinates -----------------------
+    // FWD / DGRAD: B is loaded n-fast; thread owns column nb = tid % BN.
+    const int nb = tid % BN;
+    bool bcol_ok = false;
+    const float* bcol_base = nullptr;
+    int bi0 = 0, bj0 = 0;  // FWD: ih0/iw0 of the output pixel; DGRAD: ih/iw of the input pixel
+    if constexpr (OP == OP_FWD || OP == OP_DGRAD) {
+        const int n = n0 + nb;
+        bcol_ok = n < N;
+        uint32_t img, p, r, c;
+        if constexpr (OP == OP_FWD) {
+            a.fd_ohw.divmod(bcol_ok ? n : 0, img, p);
+            a.fd_ow.divmod(p, r, c);
+            bi0 = (int)r * S - a.pad;
+            bj0 = (int)c * S - a.pad;
+            bcol_base = a.x + z * a.x_cs + (int64_t)img * a.cin * hw;
+        } else {
+            a.fd_hw.divmod(bcol_ok ? n : 0, img, p);
+            a.fd_w.divmod(p, r, c);
+            bi0 = (int)r + a.pad;
+            bj0 = (int)c + a.pad;
+            bcol_base = a.dy + z * a.dy_cs + (int64_t)img * a.cout * ohw;
+        }
+    }
+    const float* wz = nullptr;
+    if constexpr (OP != OP_WGRAD) wz = a.wt + z * a.w_cs;
+
+    float ra[NA], rb[NB];
+
+    auto load_tiles = [&](int k0) {
+        if constexpr (OP == OP_FWD) {
+            // A[m][k] = W[m][k], k-fast.
+#pragma unroll
+            for (int i = 0; i < NA; ++i) {
+                const int e = tid + i * 256, mm = e / BK, kk = e % BK;
+                const int m = m0 + mm, k = k0 + kk;
+                ra[i] = (m < M && k < kend) ? wz[(int64_t)m * a.K + k] : 0.f;
+            }
+            // B[k][n] = X[img][ci][ih0+kh][iw0+kw], n-fast.
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int e = tid + i * 256, kk = e / BN;
+                const int k = k0 + kk;
+                const int ci = k / KHW, rr = k - ci * KHW;
+                const int kh = rr / KW, kw = rr - kh * KW;
+                const int ih = bi0 + kh, iw = bj0 + kw;
+                const bool ok = bcol_ok && k < kend && (unsigned)ih < (unsigned)a.h &&
+                                (unsigned)iw < (unsigned)a.w;
+                rb[i] = ok ? bcol_base[(int64_t)ci * hw + ih * a.w + iw] : 0.f;
+            }
+        } else if constexpr (OP == OP_DGRAD) {
+            // A[m=ci][k=(co,kh,kw)] = W[co][ci][kh][kw], k-fast.
+#pragma unroll
+            for (int i = 0; i < NA; ++i) {
+                const int e = tid + i * 256, mm = e / BK, kk = e % BK;
+                const int m = m0 + mm, k = k0 + kk;
+                const int co = k / KHW, rr = k - co * KHW;
+                ra[i] = (m < M && k < kend) ? wz[((int64_t)co * a.cin + m) * KHW + rr] : 0.f;
+            }
+            // B[k=(co,kh,kw)][n=(img,ih,iw)] = dY[img][co][oh][ow], oh*S = ih+pad-kh.
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int e = tid + i * 256, kk = e / BN;
+                const int k = k0 + kk;
+                const int co = k / KHW, rr = k - co * KHW;
+                const int kh = rr / KW, kw = rr - kh * KW;
+                int oy = bi0 - kh, ox = bj0 - kw;
+                bool ok = bcol_ok && k < kend;
+                if constexpr (S != 1) {
+                    ok = ok && oy >= 0 && ox >= 0 && (oy % S) == 0 && (ox % S) == 0;
+                    oy /= S;
+                    ox /= S;
+                }
+                ok = ok && (unsigned)oy < (unsigned)a.oh && (unsigned)ox < (unsigned)a.ow;
+                rb[i] = ok ? bcol_base[(int64_t)co * ohw + oy * a.ow + ox] : 0.f;
+            }
+        } else {
+            // WGRAD: both operands k(=pixel)-fast; thread owns pixel kk = tid % BK.
+            const int kk = tid % BK;
+            const int k = k0 + kk;
+            const bool kok = k < kend;
+            uint32_t img, p, r, c;
+            a.fd_ohw.divmod(kok ? k : 0, img, p);
+            a.fd_ow.divmod(p, r, c);
+            const float* dyb = a.dy + z * a.dy_cs + (int64_t)img * a.cout * ohw + p;
+            const float* xb = a.x + z * a.x_cs + (int64_t)img * a.cin * hw;
+            const int ih0 = (int)r * S - a.pad, iw0 = (int)c * S - a.pad;
+#pragma unroll
+            for (int i = 0; i < NA; ++i) {
+                const int m = m0 + (tid / BK) + i * (256 / BK);
+                ra[i] = (kok && m < M) ? dyb[(int64_t)m * ohw] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int n = n0 + (tid / BK) + i * (256 / BK);
+                const int ci = n / KHW, rr = n - ci * KHW;
+                const int kh = rr / KW, kw = rr - kh * KW;
+                const int ih = ih0 + kh, iw = iw0 + kw;
+                const bool ok = kok && n < N && (unsigned)ih < (unsigned)a.h &&
+                                (unsigned)iw < (unsigned)a.w;
+                rb[i] = ok ? xb[(int64_t)ci * hw + ih * a.w + iw] : 0.f;
+            }
+        }
+    };
+
+    auto store_tiles = [&](int buf) {
+        if constexpr (OP == OP_WGRAD) {
+            const int kk = tid % BK;
+#pragma unroll
+            for (int i = 0; i < NA; ++i) As[buf][kk][(tid / BK) + i * (256 / BK)] = ra[i];
+#pragma unroll
+            for (int i = 0; i < NB; ++i) Bs[buf][kk][(tid / BK) + i * (256 / BK)] = rb[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < NA; ++i) {
+                const int e = tid + i * 256;
+                As[buf][e % BK][e / BK] = ra[i];
+            }
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int e = tid + i * 256;
+                Bs[buf][e / BN][e % BN] = rb[i];
+            }
+        }
+    };
+
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    if (kbeg < kend) {
+        load_tiles(kbeg);
+        store_tiles(0);
+        __syncthreads();
+        int buf = 0;
+        const int kh_lane = lane >> 5, col = lane & 31;
+        for (int k0 = kbeg; k0 < kend; k0 += BK) {
+            const bool more = k0 + BK < kend;
+            if (more) load_tiles(k0 + BK);
+#pragma unroll
+            for (int kk = 0; kk < BK; kk += 2) {
+                float av[FM], bv[FN];
+#pragma unroll
+                for (int i = 0; i < FM; ++i) av[i] = As[buf][kk + kh_lane][wm * WM + i * 32 + col];
+#pragma unroll
+                for (int j = 0; j < FN; ++j) bv[j] = Bs[buf][kk + kh_lane][wn * WN + j * 32 + col];
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+            }
+            if (more) store_tiles(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
+    }
+
+    // ---------------- epilogue ------------------------------------------
+    // acc[i][j][r]: row m = (r&3) + 8*(r>>2) + 4*(lane>>5), col n = lane&31.
+    const int rbase = 4 * (lane >> 5), col = lane & 31;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WN + j * 32 + col;
+        if (n >= N) continue;
+        if constexpr (OP == OP_WGRAD) {
+            float* op = a.out + ((int64_t)blockIdx.z * a.M) * a.N + n;
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                    if (m < M) op[(int64_t)m * a.N] = acc[i][j][r];
+                }
+        } else {
+            uint32_t img, p;
+            if constexpr (OP == OP_FWD) {
+                a.fd_ohw.divmod(n, img, p);
+                float* op = a.out + z * a.out_cs + (int64_t)img * a.cout * ohw + p;
+                const float* bz = a.bias ? a.bias + z * a.b_cs : nullptr;
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                        if (m < M) {
+                            float v = acc[i][j][r];
+                            if (bz) v = v + bz[m];
+                            if (a.relu) v = fmaxf(v, 0.f);
+                            op[(int64_t)m * ohw] = v;
+                        }
+                    }
+            } else {
+                a.fd_hw.divmod(n, img, p);
+                float* op = a.out + z * a.out_cs + (int64_t)img * a.cin * hw + p;
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                        if (m < M) op[(int64_t)m * hw] = acc[i][j][r];
+                    }
+            }
+        }
+    }
+}
+
+// dw[z][m][n] = sum_s part[z][s][m][n] (fixed order -> deterministic)
+__global__ void splitk_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                     int64_t dw_cs, int splits, int MN) {
+    const int z = blockIdx.y;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < MN; e += gridDim.x * blockDim.x) {
+        const float* p = part + (int64_t)z * splits * MN + e;
+        float s = 0.f;
+        for (int i = 0; i < splits; ++i) s += p[(int64_t)i * MN];
+        dw[z * dw_cs + e] = s;
+    }
+}
+
+// db[z][c] = sum over valid images and pixels of dy[z][img][c][p]; one block per (c, z).
+__global__ void __launch_bounds__(256) bias_grad_kernel(const float* __restrict__ dy, int64_t dy_cs,
+                                                        float* __restrict__ db, int64_t db_cs,
+                                                        const int32_t* counts, int batch, int C,
+                                                        int HW) {
+    __shared__ double red[4];
+    const int c = blockIdx.x, z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const float* base = dy + z * dy_cs + (int64_t)c * HW;
+    double s = 0.0;
+    const int total = cnt * HW;
+    for (int e = threadIdx.x; e < total; e += 256) {
+        const int img = e / HW, p = e - img * HW;
+        s += (double)base[(int64_t)img * C * HW + p];
+    }
+    s = block_sum_256(s, red);
+    if (threadIdx.x == 0) db[z * db_cs + c] = (float)s;
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------
+struct Tile {
+    int bm, bn, bk, wavesm;
+};
+
+template <int OP, int KH, int KW, int S>
+static int launch_tile(const Tile& t, dim3 grid, const ConvArgs& a, hipStream_t st) {
+#define FH_IG(BM, BN, BK, WMV)                                                               \
+    if (t.bm == BM && t.bn == BN && t.bk == BK && t.wavesm == WMV) {                         \
+        hipLaunchKernelGGL((igemm_kernel<OP, KH, KW, S, BM, BN, BK, WMV>), grid, dim3(256), 0, \
+                           st, a);                                                           \
+        return FH_OK;                                                                        \
+    }
+    if constexpr (OP == OP_WGRAD) {
+        FH_IG(32, 128, 32, 1)
+        FH_IG(64, 128, 32, 2)
+        FH_IG(128, 128, 32, 2)
+    } else {
+        FH_IG(32, 256, 16, 1)
+        FH_IG(64, 256, 16, 1)
+        FH_IG(128, 128, 16, 2)
+        FH_IG(128, 32, 16, 4)
+    }
+#undef FH_IG
+    set_error("igemm: no tile instantiation (%d,%d,%d,%d)", t.bm, t.bn, t.bk, t.wavesm);
+    return FH_E_UNSUPPORTED;
+}
+
+template <int OP>
+static int launch_shape(int kh, int kw, int s, const Tile& t, dim3 grid, const ConvArgs& a,
+                        hipStream_t st) {
+    if (kh == 3 && kw == 3 && s == 1) return launch_tile<OP, 3, 3, 1>(t, grid, a, st);
+    if (kh == 3 && kw == 3 && s == 2) return launch_tile<OP, 3, 3, 2>(t, grid, a, st);
+    if (kh == 1 && kw == 1 && s == 1) return launch_tile<OP, 1, 1, 1>(t, grid, a, st);
+    if (kh == 1 && kw == 1 && s == 2) return launch_tile<OP, 1, 1, 2>(t, grid, a, st);
+    set_error("conv: unsupported kernel %dx%d stride %d", kh, kw, s);
+    return FH_E_UNSUPPORTED;
+}
+
+static Tile pick_mn_tile(int M, int Nmax) {
+    if (Nmax <= 32) return {128, 32, 16, 4};
+    if (M <= 32) return {32, 256, 16, 1};
+    if (M <= 64) return {64, 256, 16, 1};
+    return {128, 128, 16, 2};
+}
+
+static Tile pick_wgrad_tile(int M) {
+    if (M <= 32) return {32, 128, 32, 1};
+    if (M <= 64) return {64, 128, 32, 2};
+    return {128, 128, 32, 2};
+}
+
+static void wgrad_split(int nclients, int M, int N, int K, const Tile& t, int& splits, int& kchunk) {
+    const int64_t tiles = ceil_div(M, t.bm) * ceil_div(N, t.bn) * (int64_t)nclients;
+    int64_t want = ceil_div(2048, tiles);
+    const int64_t maxs = std::max<int64_t>(1, K / (t.bk * 4));
+    if (want > maxs) want = maxs;
+    if (want < 1) want = 1;
+    kchunk = (int)(ceil_div(ceil_div(K, want), t.bk) * t.bk);
+    splits = (int)ceil_div(K, kchunk);
+}
+
+static int conv_common_check(int nclients, int batch, int cin, int h, int w, int cout, int kh,
+                             int kw, int stride, int pad, int& oh, int& ow) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && cin > 0 && h > 0 && w > 0 && cout > 0,
+               "conv: bad shape");
+    FH_REQUIRE(stride > 0 && pad >= 0 && kh > 0 && kw > 0, "conv: bad kernel params");
+    oh = (h + 2 * pad - kh) / stride + 1;
+    ow = (w + 2 * pad - kw) / stride + 1;
+    FH_REQUIRE(oh > 0 && ow > 0, "conv: empty output");
+    FH_REQUIRE((int64_t)batch * std::max(oh * ow, h * w) < (1ll << 31), "conv: too many pixels");
+    return FH_OK;
+}
+
+static ConvArgs make_args(int batch, int cin, int h, int w, int cout, int oh, int ow, int pad,
+                          const int32_t* counts) {
+    ConvArgs a{};
+    a.batch = batch;
+    a.cin = cin;
+    a.h = h;
+    a.w = w;
+    a.cout = cout;
+    a.oh = oh;
+    a.ow = ow;
+    a.pad = pad;
+    a.counts = counts;
+    a.fd_ohw = FastDiv(oh * ow);
+    a.fd_ow = FastDiv(ow);
+    a.fd_hw = FastDiv(h * w);
+    a.fd_w = FastDiv(w);
+    return a;
+}
+
+}  // namespace fh
+
+using namespace fh;
+
+extern "C" int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                             const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                             const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
+                             int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
+                             int32_t stride, int32_t pad, int32_t relu, void* stream) {
+    int oh, ow;
+    int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
+    if (rc) return rc;
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && w && y, "conv2d_fwd: null pointer");
+    ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
+    a.x = x; a.wt = w; a.bias = bias; a.out = y;
+    a.x_cs = x_cs; a.w_cs = w_cs; a.b_cs = b_cs; a.out_cs = y_cs;
+    a.relu = relu;
+    a.M = cout; a.N = batch * oh * ow; a.K = cin * kh * kw;
+    Tile t = pick_mn_tile(a.M, a.N);
+    dim3 grid((unsigned)ceil_div(a.N, t.bn), (unsigned)ceil_div(a.M, t.bm), (unsigned)nclients);
+    rc = launch_shape<OP_FWD>(kh, kw, stride, t, grid, a, as_stream(stream));
+    if (rc) return rc;
+    FH_LAUNCH_CHECK("conv2d_fwd");
+    return FH_OK;
+}
+
+extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
+                               float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                               int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream) {
+    int oh, ow;
+    int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
+    if (rc) return rc;
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dy && w && dx, "conv2d_dgrad: null pointer");
+    ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
+    a.dy = dy; a.wt = w; a.out = dx;
+    a.dy_cs = dy_cs; a.w_cs = w_cs; a.out_cs = dx_cs;
+    a.M = cin; a.N = batch * h * w_; a.K = cout * kh * kw;
+    Tile t = pick_mn_tile(a.M, a.N);
+    dim3 grid((unsigned)ceil_div(a.N, t.bn), (unsigned)ceil_div(a.M, t.bm), (unsigned)nclients);
+    rc = launch_shape<OP_DGRAD>(kh, kw, stride, t, grid, a, as_stream(stream));
+    if (rc) return rc;
+    FH_LAUNCH_CHECK("conv2d_dgrad");
+    return FH_OK;
+}
+
+extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
+                                            int32_t w_, int32_t cout, int32_t kh, int32_t kw,
+                                            int32_t stride, int32_t pad) {
+    int oh = (h + 2 * pad - kh) / stride + 1, ow = (w_ + 2 * pad - kw) / stride + 1;
+    if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
+    const int M = cout, N = cin * kh * kw, K = batch * oh * ow;
+    Tile t = pick_wgrad_tile(M);
+    int splits, kchunk;
+    wgrad_split(nclients, M, N, K, t, splits, kchunk);
+    return (size_t)nclients * splits * M * N * sizeof(float);
+}
+
+extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                               float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
+                               size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                               int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream) {
+    int oh, ow;
+    int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
+    if (rc) return rc;
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && dy && dw && workspace, "conv2d_wgrad: null pointer");
+    const size_t need =
+        fh_conv2d_wgrad_workspace(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad);
+    FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
+    ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
+    a.x = x; a.dy = dy; a.out = (float*)workspace;
+    a.x_cs = x_cs; a.dy_cs = dy_cs;
+    a.M = cout; a.N = cin * kh * kw; a.K = batch * oh * ow;
+    Tile t = pick_wgrad_tile(a.M);
+    wgrad_split(nclients, a.M, a.N, a.K, t, a.splits, a.kchunk);
+    hipStream_t st = as_stream(stream);
+    dim3 grid((unsigned)ceil_div(a.N, t.bn), (unsigned)ceil_div(a.M, t.bm),
+              (unsigned)(nclients * a.splits));
+    rc = launch_shape<OP_WGRAD>(kh, kw, stride, t, grid, a, st);
+    if (rc) return rc;
+    FH_LAUNCH_CHECK("conv2d_wgrad");
+    const int MN = a.M * a.N;
+    dim3 rgrid((unsigned)std::min<int64_t>(ceil_div(MN, 256), 1024), (unsigned)nclients);
+    hipLaunchKernelGGL(splitk_reduce_kernel, rgrid, dim3(256), 0, st, (const float*)workspace, dw,
+                       dw_cs, a.splits, MN);
+    FH_LAUNCH_CHECK("conv2d_wgrad reduce");
+    if (db) {
+        hipLaunchKernelGGL(bias_grad_kernel, dim3(cout, nclients), dim3(256), 0, st, dy, dy_cs, db,
+                           db_cs, counts, batch, cout, oh * ow);
+        FH_LAUNCH_CHECK("conv2d_wgrad bias");
+    }
+    return FH_OK;
+}
+
+// ---- linear layers: a 1x1 convolution over a 1x1 image -------------------
+extern "C" int fh_linear_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                             const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                             const int32_t* counts, int32_t nclients, int32_t batch, int32_t in_f,
+                             int32_t out_f, int32_t relu, void* stream) {
+    return fh_conv2d_fwd(x, x_cs, w, w_cs, bias, b_cs, y, y_cs, counts, nclients, batch, in_f, 1, 1,
+                         out_f, 1, 1, 1, 0, relu, stream);
+}
+
+extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
+                               float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
+    return fh_conv2d_dgrad(dy, dy_cs, w, w_cs, dx, dx_cs, counts, nclients, batch, in_f, 1, 1,
+                           out_f, 1, 1, 1, 0, stream);
+}
+
+extern "C" size_t fh_linear_wgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f,
+                                            int32_t out_f) {
+    return fh_conv2d_wgrad_workspace(nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0);
+}
+
+extern "C" int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                               float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
+                               size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
+    return fh_conv2d_wgrad(x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs, workspace, ws_bytes, counts,
+                           nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0, stream);
+}

@@ -1,0 +1,562 @@
+// layers.hip — the non-GEMM layers of the reference CNNs, client-batched.
+//
+//   BatchNorm2d train/eval fwd + bwd   models_pytorch.py:108-120, 176-187 (nn.BatchNorm2d)
+//       fused with the following ReLU and (ResNet) the residual add
+//       (models_pytorch.py:140-160, 189-194)
+//   MaxPool2d(2,2) fwd/bwd              models_pytorch.py:72, 123 (fused with the Dropout
+//       that follows it in CIFAR10CNN, :139-155, and the ReLU before it in SimpleCNN, :85-88)
+//   Dropout fwd/bwd                     models_pytorch.py:75, 124 (F.dropout semantics:
+//       y = x * (bernoulli(1-p) / (1-p)), training-mode only)
+//   CrossEntropyLoss fwd+bwd + metrics  training.py:90, 193, 200-203
+//   AdaptiveAvgPool2d((1,1))            models_pytorch.py:216, 241
+//   batch gather                        DataLoader(batch_size=32, shuffle=True) data path
+//
+// Every kernel takes per-client valid image counts: reductions (BN stats, loss,
+// gradients) cover only valid images; invalid rows are never read by a reduction.
+// All per-(client, channel) reductions accumulate in fp64, as ATen's CPU
+// batch-norm does (acc_type<float> on CPU is double).
+#include "fh_common.h"
+
+namespace fh {
+
+// ------------------------------------------------------------------ BatchNorm
+// x, y, res: [z][img][C][HW]; gamma/beta: per-client param rows (stride p_cs);
+// running stats: stride r_cs; save_mean/save_invstd: [z][C].
+__global__ void __launch_bounds__(256)
+bn_fwd_train_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y, int64_t y_cs,
+                    const float* __restrict__ res, int64_t res_cs, const float* __restrict__ gamma,
+                    const float* __restrict__ beta, int64_t p_cs, float* __restrict__ rmean,
+                    float* __restrict__ rvar, int64_t r_cs, float* __restrict__ save_mean,
+                    float* __restrict__ save_invstd, const int32_t* __restrict__ counts, int batch,
+                    int C, int HW, float eps, float momentum, int relu) {
+    __shared__ double red[4];
+    const int c = blockIdx.x, z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int64_t n = (int64_t)cnt * HW;
+    const float* xb = x + z * x_cs + (int64_t)c * HW;
+    const int64_t istride = (int64_t)C * HW;
+    // pass 1: mean
+    double s = 0.0;
+    for (int img = 0; img < cnt; ++img)
+        for (int p = threadIdx.x; p < HW; p += 256) s += (double)xb[img * istride + p];
+    s = block_sum_256(s, red);
+    const double mean = n > 0 ? s / (double)n : 0.0;
+    // pass 2: centred sum of squares
+    double v = 0.0;
+    for (int img = 0; img < cnt; ++img)
+        for (int p = threadIdx.x; p < HW; p += 256) {
+            const double d = (double)xb[img * istride + p] - mean;
+            v += d * d;
+        }
+    v = block_sum_256(v, red);
+    const double invstd = n > 0 ? 1.0 / sqrt(v / (double)n + (double)eps) : 0.0;
+    const float meanf = (float)mean, invstdf = (float)invstd;
+    if (threadIdx.x == 0) {
+        save_mean[z * C + c] = meanf;
+        save_invstd[z * C + c] = invstdf;
+        if (rmean && n > 0) {
+            float* rm = rmean + z * r_cs + c;
+            float* rv = rvar + z * r_cs + c;
+            const double unb = n > 1 ? v / (double)(n - 1) : v;
+            *rm = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)*rm);
+            *rv = (float)((double)momentum * unb + (1.0 - (double)momentum) * (double)*rv);
+        }
+    }
+    // pass 3: y = x*alpha + beta  (alpha = invstd*w, beta = b - mean*alpha), [+res], [relu]
+    const float g = gamma[z * p_cs + c], bt = beta[z * p_cs + c];
+    const float alpha = invstdf * g;
+    const float bconst = bt - meanf * alpha;
+    float* yb = y + z * y_cs + (int64_t)c * HW;
+    const float* rb = res ? res + z * res_cs + (int64_t)c * HW : nullptr;
+    for (int img = 0; img < cnt; ++img)
+        for (int p = threadIdx.x; p < HW; p += 256) {
+            float o = xb[img * istride + p] * alpha + bconst;
+            if (rb) o = o + rb[img * istride + p];
+            if (relu) o = fmaxf(o, 0.f);
+            yb[img * istride + p] = o;
+        }
+}
+
+// eval mode: running statistics (LocalTrainer._validate_epoch / evaluate_model, training.py:218,318)
+__global__ void __launch_bounds__(256)
+bn_fwd_eval_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y, int64_t y_cs,
+                   const float* __restrict__ res, int64_t res_cs, const float* __restrict__ gamma,
+                   const float* __restrict__ beta, int64_t p_cs, const float* __restrict__ rmean,
+                   const float* __restrict__ rvar, int64_t r_cs, const int32_t* __restrict__ counts,
+                   int batch, int C, int HW, float eps, int relu) {
+    const int c = blockIdx.x, z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const float invstd = (float)(1.0 / sqrt((double)rvar[z * r_cs + c] + (double)eps));
+    const float alpha = invstd * gamma[z * p_cs + c];
+    const float bconst = beta[z * p_cs + c] - rmean[z * r_cs + c] * alpha;
+    const int64_t istride = (int64_t)C * HW;
+    const float* xb = x + z * x_cs + (int64_t)c * HW;
+    float* yb = y + z * y_cs + (int64_t)c * HW;
+    const float* rb = res ? res + z * res_cs + (int64_t)c * HW : nullptr;
+    for (int img = 0; img < cnt; ++img)
+        for (int p = threadIdx.x; p < HW; p += 256) {
+            float o = xb[img * istride + p] * alpha + bconst;
+            if (rb) o = o + rb[img * istride + p];
+            if (relu) o = fmaxf(o, 0.f);
+            yb[img * istride + p] = o;
+        }
+}
+
+// g = relu ? (yout > 0 ? dy : 0) : dy ; optionally g -> dres (residual branch);
+// dgamma = sum((x-mean)*g)*invstd, dbeta = sum(g);
+// dx = ((g - mean(g)) - (x-mean)*k) * invstd * w,  k = dotp*invstd^2/n  (ATen CPU order)
+__global__ void __launch_bounds__(256)
+bn_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const float* __restrict__ yout,
+              int64_t yo_cs, const float* __restrict__ x, int64_t x_cs,
+              const float* __restrict__ gamma, int64_t p_cs, const float* __restrict__ save_mean,
+              const float* __restrict__ save_invstd, float* __restrict__ dx, int64_t dx_cs,
+              float* __restrict__ dres, int64_t dres_cs, float* __restrict__ dgamma,
+              float* __restrict__ dbeta, int64_t g_cs, const int32_t* __restrict__ counts,
+              int batch, int C, int HW, int relu) {
+    __shared__ double red[4];
+    const int c = blockIdx.x, z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int64_t n = (int64_t)cnt * HW;
+    const int64_t istride = (int64_t)C * HW;
+    const int64_t coff = (int64_t)c * HW;
+    const float* dyb = dy + z * dy_cs + coff;
+    const float* yob = relu ? yout + z * yo_cs + coff : nullptr;
+    const float* xb = x + z * x_cs + coff;
+    float* drb = dres ? dres + z * dres_cs + coff : nullptr;
+    const float mean = save_mean[z * C + c], invstd = save_invstd[z * C + c];
+    double sg = 0.0, dot = 0.0;
+    for (int img = 0; img < cnt; ++img)
+        for (int p = threadIdx.x; p < HW; p += 256) {
+            const int64_t o = img * istride + p;
+            float g = dyb[o];
+            if (yob && !(yob[o] > 0.f)) g = 0.f;
+            if (drb) drb[o] = g;
+            sg += (double)g;
+            dot += (double)((xb[o] - mean) * g);
+        }
+    sg = block_sum_256(sg, red);
+    dot = block_sum_256(dot, red);
+    const float w = gamma[z * p_cs + c];
+    if (threadIdx.x == 0) {
+        if (dgamma) dgamma[z * g_cs + c] = (float)(dot * (double)invstd);
+        if (dbeta) dbeta[z * g_cs + c] = (float)sg;
+    }
+    if (!dx) return;
+    const float k = n > 0 ? (float)(dot * (double)invstd * (double)invstd / (double)n) : 0.f;
+    const float gm = n > 0 ? (float)(sg / (double)n) : 0.f;
+    float* dxb = dx + z * dx_cs + coff;
+    for (int img = 0; img < cnt; ++img)
+        for (int p = threadIdx.x; p < HW; p += 256) {
+            const int64_t o = img * istride + p;
+            float g = dyb[o];
+            if (yob && !(yob[o] > 0.f)) g = 0.f;
+            const float gi = (xb[o] - mean) * k;
+            dxb[o] = (((g - gm) - gi) * invstd) * w;
+        }
+}
+
+// ------------------------------------------------------------------ MaxPool 2x2 (+dropout)
+// x: [z][img][C][H][W] -> y: [z][img][C][H/2][W/2]; idx: window argmax (0..3, first max);
+// drop_mode 0: none; 1: generate keep-mask (Philox) into mask; 2: use caller mask.
+__global__ void __launch_bounds__(256)
+maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y,
+                    int64_t y_cs, uint8_t* __restrict__ idx, int64_t i_cs,
+                    uint8_t* __restrict__ mask, int64_t m_cs, const int32_t* __restrict__ counts,
+                    int batch, int C, int H, int W, int drop_mode, float keep_prob, float scale,
+                    uint64_t seed) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int OH = H / 2, OW = W / 2;
+    const int64_t per_img = (int64_t)C * OH * OW;
+    const int64_t total = cnt * per_img;
+    const float* xb = x + z * x_cs;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int ow = (int)(e % OW);
+        const int64_t t = e / OW;
+        const int oh = (int)(t % OH);
+        const int64_t plane = t / OH;  // img*C + c
+        const float* p = xb + plane * H * W + (2 * oh) * W + 2 * ow;
+        float m = p[0];
+        int a = 0;
+        if (p[1] > m) { m = p[1]; a = 1; }
+        if (p[W] > m) { m = p[W]; a = 2; }
+        if (p[W + 1] > m) { m = p[W + 1]; a = 3; }
+        idx[z * i_cs + e] = (uint8_t)a;
+        if (drop_mode) {
+            uint8_t keep;
+            if (drop_mode == 1) {
+                const uint4 r = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
+                keep = u01(r.x) <= keep_prob ? 1 : 0;
+                mask[z * m_cs + e] = keep;
+            } else {
+                keep = mask[z * m_cs + e];
+            }
+            m = keep ? m * scale : 0.f;
+        }
+        y[z * y_cs + e] = m;
+    }
+}
+
+// dx (all 4 window slots written) = dy routed to the argmax, times the dropout
+// factor; relu_in: also zero where the pooled input (a ReLU output) is not > 0.
+__global__ void __launch_bounds__(256)
+maxpool2_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const uint8_t* __restrict__ idx,
+                    int64_t i_cs, const uint8_t* __restrict__ mask, int64_t m_cs,
+                    const float* __restrict__ xin, int64_t x_cs, float* __restrict__ dx,
+                    int64_t dx_cs, const int32_t* __restrict__ counts, int batch, int C, int H,
+                    int W, float scale) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int OH = H / 2, OW = W / 2;
+    const int64_t total = cnt * (int64_t)C * OH * OW;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int ow = (int)(e % OW);
+        const int64_t t = e / OW;
+        const int oh = (int)(t % OH);
+        const int64_t plane = t / OH;
+        float g = dy[z * dy_cs + e];
+        if (mask) g = mask[z * m_cs + e] ? g * scale : 0.f;
+        const int a = idx[z * i_cs + e];
+        const int64_t base = plane * H * W + (2 * oh) * W + 2 * ow;
+        const int64_t off[4] = {0, 1, W, W + 1};
+        if (xin && !(xin[z * x_cs + base + off[a]] > 0.f)) g = 0.f;
+        float* d = dx + z * dx_cs + base;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[off[q]] = (q == a) ? g : 0.f;
+    }
+}
+
+// ------------------------------------------------------------------ Dropout (+ReLU mask)
+__global__ void __launch_bounds__(256)
+dropout_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y, int64_t y_cs,
+                   uint8_t* __restrict__ mask, int64_t m_cs, const int32_t* __restrict__ counts,
+                   int batch, int64_t per_img, int drop_mode, float keep_prob, float scale,
+                   uint64_t seed) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int64_t total = cnt * per_img;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        uint8_t keep;
+        if (drop_mode == 1) {
+            const uint4 r = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
+            keep = u01(r.x) <= keep_prob ? 1 : 0;
+            mask[z * m_cs + e] = keep;
+        } else {
+            keep = mask[z * m_cs + e];
+        }
+        const float v = x[z * x_cs + e];
+        y[z * y_cs + e] = keep ? v * scale : 0.f;
+    }
+}
+
+// dx = dy * mask * scale [* (relu_out > 0)]; mask may be NULL (pure ReLU backward).
+__global__ void __launch_bounds__(256)
+dropout_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const uint8_t* __restrict__ mask,
+                   int64_t m_cs, const float* __restrict__ relu_out, int64_t r_cs,
+                   float* __restrict__ dx, int64_t dx_cs, const int32_t* __restrict__ counts,
+                   int batch, int64_t per_img, float scale) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int64_t total = cnt * per_img;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        float g = dy[z * dy_cs + e];
+        if (mask) g = mask[z * m_cs + e] ? g * scale : 0.f;
+        if (relu_out && !(relu_out[z * r_cs + e] > 0.f)) g = 0.f;
+        dx[z * dx_cs + e] = g;
+    }
+}
+
+// ------------------------------------------------------------------ CrossEntropy
+// One block per client.  logits/dlogits: [z][img][K]; targets: int64 [z][img].
+// loss_out[z] = batch-mean loss (fp32, = loss.item()); accumulators (may be NULL):
+// acc_loss[z] += loss_out[z] (double), acc_correct[z] += #argmax==target, acc_seen[z] += cnt.
+__global__ void __launch_bounds__(256)
+ce_kernel(const float* __restrict__ logits, int64_t l_cs, const int64_t* __restrict__ targets,
+          int64_t t_cs, float* __restrict__ dlogits, int64_t d_cs, float* __restrict__ loss_out,
+          double* __restrict__ acc_loss, int64_t* __restrict__ acc_correct,
+          int64_t* __restrict__ acc_seen, const int32_t* __restrict__ counts, int batch, int K) {
+    __shared__ double sl[4];
+    __shared__ int sc[4];
+    const int z = blockIdx.x;
+    const int cnt = counts ? counts[z] : batch;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double lsum = 0.0;
+    int corr = 0;
+    const float inv_n = cnt > 0 ? 1.0f / (float)cnt : 0.f;
+    for (int img = wid; img < cnt; img += 4) {
+        const float* row = logits + z * l_cs + (int64_t)img * K;
+        const int tgt = (int)targets[z * t_cs + img];
+        float mx = -INFINITY;
+        int amax = 0;
+        for (int k = lane; k < K; k += 64) {
+            const float v = row[k];
+            if (v > mx) { mx = v; amax = k; }
+        }
+        // first index of the max (torch.max tie rule)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float om = __shfl_xor(mx, o, 64);
+            const int oa = __shfl_xor(amax, o, 64);
+            if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+        }
+        float se = 0.f;
+        for (int k = lane; k < K; k += 64) se += expf(row[k] - mx);
+        se = wave_sum(se);
+        const float lse = logf(se);
+        // loss_i = -(x_t - mx - lse)
+        if (lane == 0) {
+            lsum += (double)(-((row[tgt] - mx) - lse));
+            corr += (amax == tgt);
+        }
+        float* drow = dlogits + z * d_cs + (int64_t)img * K;
+        for (int k = lane; k < K; k += 64) {
+            const float p = expf((row[k] - mx) - lse);
+            drow[k] = (p - (k == tgt ? 1.f : 0.f)) * inv_n;
+        }
+    }
+    if (lane == 0) {
+        sl[wid] = lsum;
+        sc[wid] = corr;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double tot = sl[0] + sl[1] + sl[2] + sl[3];
+        const float batch_loss = cnt > 0 ? (float)(tot / (double)cnt) : 0.f;
+        if (loss_out) loss_out[z] = batch_loss;
+        if (acc_loss) acc_loss[z] += (double)batch_loss;
+        if (acc_correct) acc_correct[z] += sc[0] + sc[1] + sc[2] + sc[3];
+        if (acc_seen) acc_seen[z] += cnt;
+    }
+}
+
+// ------------------------------------------------------------------ global average pool
+__global__ void __launch_bounds__(256)
+avgpool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y, int64_t y_cs,
+                   const int32_t* __restrict__ counts, int batch, int C, int HW) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int lane = threadIdx.x & 63;
+    const int64_t planes = (int64_t)cnt * C;
+    for (int64_t pl = blockIdx.x * 4 + (threadIdx.x >> 6); pl < planes; pl += gridDim.x * 4) {
+        const float* b = x + z * x_cs + pl * HW;
+        float s = 0.f;
+        for (int p = lane; p < HW; p += 64) s += b[p];
+        s = wave_sum(s);
+        if (lane == 0) y[z * y_cs + pl] = s / (float)HW;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+avgpool_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, float* __restrict__ dx,
+                   int64_t dx_cs, const int32_t* __restrict__ counts, int batch, int C, int HW) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int64_t total = (int64_t)cnt * C * HW;
+    const float inv = 1.0f / (float)HW;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x)
+        dx[z * dx_cs + e] = dy[z * dy_cs + e / HW] * inv;
+}
+
+// ------------------------------------------------------------------ batch gather
+// x[z][b][:] = data[idx[z*idx_cs + b]][:] ; y[z][b] = labels[idx[..]] for b < counts[z].
+__global__ void __launch_bounds__(256)
+gather_kernel(const float* __restrict__ data, const int64_t* __restrict__ labels,
+              const int64_t* __restrict__ idx, int64_t idx_cs, float* __restrict__ x, int64_t x_cs,
+              int64_t* __restrict__ y, int64_t y_cs, int64_t sample_elems,
+              const int32_t* __restrict__ counts, int batch) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int64_t total = (int64_t)cnt * sample_elems;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = e / sample_elems, off = e - b * sample_elems;
+        const int64_t s = idx[z * idx_cs + b];
+        x[z * x_cs + e] = data[s * sample_elems + off];
+        if (off == 0 && y) y[z * y_cs + b] = labels[s];
+    }
+}
+
+static int ew_grid(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(ceil_div(n, 256), 1), 2048); }
+
+}  // namespace fh
+
+using namespace fh;
+
+extern "C" int fh_bn_fwd_train(const float* x, int64_t x_cs, float* y, int64_t y_cs,
+                               const float* res, int64_t res_cs, const float* gamma,
+                               const float* beta, int64_t p_cs, float* running_mean,
+                               float* running_var, int64_t r_cs, float* save_mean,
+                               float* save_invstd, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t C, int32_t HW, float eps, float momentum,
+                               int32_t relu, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_train: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && y && gamma && beta && save_mean && save_invstd, "bn_fwd_train: null pointer");
+    FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "bn_fwd_train: running stats");
+    hipLaunchKernelGGL(bn_fwd_train_kernel, dim3(C, nclients), dim3(256), 0, as_stream(stream), x,
+                       x_cs, y, y_cs, res, res_cs, gamma, beta, p_cs, running_mean, running_var,
+                       r_cs, save_mean, save_invstd, counts, batch, C, HW, eps, momentum, relu);
+    FH_LAUNCH_CHECK("bn_fwd_train");
+    return FH_OK;
+}
+
+extern "C" int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_cs,
+                              const float* res, int64_t res_cs, const float* gamma,
+                              const float* beta, int64_t p_cs, const float* running_mean,
+                              const float* running_var, int64_t r_cs, const int32_t* counts,
+                              int32_t nclients, int32_t batch, int32_t C, int32_t HW, float eps,
+                              int32_t relu, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_eval: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && y && gamma && beta && running_mean && running_var, "bn_fwd_eval: null pointer");
+    hipLaunchKernelGGL(bn_fwd_eval_kernel, dim3(C, nclients), dim3(256), 0, as_stream(stream), x,
+                       x_cs, y, y_cs, res, res_cs, gamma, beta, p_cs, running_mean, running_var,
+                       r_cs, counts, batch, C, HW, eps, relu);
+    FH_LAUNCH_CHECK("bn_fwd_eval");
+    return FH_OK;
+}
+
+extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs,
+                         const float* x, int64_t x_cs, const float* gamma, int64_t p_cs,
+                         const float* save_mean, const float* save_invstd, float* dx,
+                         int64_t dx_cs, float* dres, int64_t dres_cs, float* dgamma, float* dbeta,
+                         int64_t g_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                         int32_t C, int32_t HW, int32_t relu, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_bwd: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dy && x && gamma && save_mean && save_invstd, "bn_bwd: null pointer");
+    FH_REQUIRE(!relu || yout, "bn_bwd: relu needs the forward output");
+    hipLaunchKernelGGL(bn_bwd_kernel, dim3(C, nclients), dim3(256), 0, as_stream(stream), dy,
+                       dy_cs, yout, yo_cs, x, x_cs, gamma, p_cs, save_mean, save_invstd, dx, dx_cs,
+                       dres, dres_cs, dgamma, dbeta, g_cs, counts, batch, C, HW, relu);
+    FH_LAUNCH_CHECK("bn_bwd");
+    return FH_OK;
+}
+
+extern "C" int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
+                               int64_t i_cs, uint8_t* mask, int64_t m_cs, const int32_t* counts,
+                               int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                               int32_t drop_mode, float p_drop, uint64_t seed, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2, "maxpool2_fwd: bad shape");
+    FH_REQUIRE((H % 2) == 0 && (W % 2) == 0, "maxpool2_fwd: odd spatial size %dx%d", H, W);
+    FH_REQUIRE(drop_mode >= 0 && drop_mode <= 2 && (drop_mode == 0 || mask), "maxpool2_fwd: mask");
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "maxpool2_fwd: p=%g", p_drop);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && y && idx, "maxpool2_fwd: null pointer");
+    const float keep = 1.0f - p_drop, scale = 1.0f / keep;
+    const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
+    hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
+                       as_stream(stream), x, x_cs, y, y_cs, idx, i_cs, mask, m_cs, counts, batch, C,
+                       H, W, drop_mode, keep, scale, seed);
+    FH_LAUNCH_CHECK("maxpool2_fwd");
+    return FH_OK;
+}
+
+extern "C" int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,
+                               const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin,
+                               int64_t x_cs, float* dx, int64_t dx_cs, const int32_t* counts,
+                               int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                               void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2 && !(H & 1) && !(W & 1),
+               "maxpool2_bwd: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dy && idx && dx, "maxpool2_bwd: null pointer");
+    const float scale = 1.0f / (1.0f - p_drop);
+    const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
+    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
+                       as_stream(stream), dy, dy_cs, idx, i_cs, mask, m_cs, xin, x_cs, dx, dx_cs,
+                       counts, batch, C, H, W, scale);
+    FH_LAUNCH_CHECK("maxpool2_bwd");
+    return FH_OK;
+}
+
+extern "C" int fh_dropout_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* mask,
+                              int64_t m_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                              int64_t per_img, int32_t drop_mode, float p_drop, uint64_t seed,
+                              void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && per_img > 0, "dropout_fwd: bad shape");
+    FH_REQUIRE((drop_mode == 1 || drop_mode == 2) && mask, "dropout_fwd: mask mode");
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "dropout_fwd: p=%g", p_drop);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && y, "dropout_fwd: null pointer");
+    const float keep = 1.0f - p_drop, scale = 1.0f / keep;
+    hipLaunchKernelGGL(dropout_fwd_kernel, dim3(ew_grid(batch * per_img), nclients), dim3(256), 0,
+                       as_stream(stream), x, x_cs, y, y_cs, mask, m_cs, counts, batch, per_img,
+                       drop_mode, keep, scale, seed);
+    FH_LAUNCH_CHECK("dropout_fwd");
+    return FH_OK;
+}
+
+extern "C" int fh_dropout_bwd(const float* dy, int64_t dy_cs, const uint8_t* mask, int64_t m_cs,
+                              float p_drop, const float* relu_out, int64_t r_cs, float* dx,
+                              int64_t dx_cs, const int32_t* counts, int32_t nclients,
+                              int32_t batch, int64_t per_img, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && per_img > 0, "dropout_bwd: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dy && dx, "dropout_bwd: null pointer");
+    const float scale = 1.0f / (1.0f - p_drop);
+    hipLaunchKernelGGL(dropout_bwd_kernel, dim3(ew_grid(batch * per_img), nclients), dim3(256), 0,
+                       as_stream(stream), dy, dy_cs, mask, m_cs, relu_out, r_cs, dx, dx_cs, counts,
+                       batch, per_img, scale);
+    FH_LAUNCH_CHECK("dropout_bwd");
+    return FH_OK;
+}
+
+extern "C" int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets,
+                             int64_t t_cs, float* dlogits, int64_t d_cs, float* loss_out,
+                             double* acc_loss, int64_t* acc_correct, int64_t* acc_seen,
+                             const int32_t* counts, int32_t nclients, int32_t batch,
+                             int32_t num_classes, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && num_classes > 0, "ce_fwd_bwd: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(logits && targets && dlogits, "ce_fwd_bwd: null pointer");
+    hipLaunchKernelGGL(ce_kernel, dim3(nclients), dim3(256), 0, as_stream(stream), logits, l_cs,
+                       targets, t_cs, dlogits, d_cs, loss_out, acc_loss, acc_correct, acc_seen,
+                       counts, batch, num_classes);
+    FH_LAUNCH_CHECK("ce_fwd_bwd");
+    return FH_OK;
+}
+
+extern "C" int fh_avgpool_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs,
+                              const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
+                              int32_t HW, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "avgpool_fwd: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && y, "avgpool_fwd: null pointer");
+    const int64_t planes = (int64_t)batch * C;
+    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(ew_grid(planes * 64), nclients), dim3(256), 0,
+                       as_stream(stream), x, x_cs, y, y_cs, counts, batch, C, HW);
+    FH_LAUNCH_CHECK("avgpool_fwd");
+    return FH_OK;
+}
+
+extern "C" int fh_avgpool_bwd(const float* dy, int64_t dy_cs, float* dx, int64_t dx_cs,
+                              const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
+                              int32_t HW, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "avgpool_bwd: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dy && dx, "avgpool_bwd: null pointer");
+    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(ew_grid((int64_t)batch * C * HW), nclients),
+                       dim3(256), 0, as_stream(stream), dy, dy_cs, dx, dx_cs, counts, batch, C, HW);
+    FH_LAUNCH_CHECK("avgpool_bwd");
+    return FH_OK;
+}
+
+extern "C" int fh_gather_batch(const float* data, const int64_t* labels, const int64_t* idx,
+                               int64_t idx_cs, float* x, int64_t x_cs, int64_t* y, int64_t y_cs,
+                               int64_t sample_elems, const int32_t* counts, int32_t nclients,
+                               int32_t batch, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && sample_elems > 0, "gather_batch: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(data && idx && x && (!y || labels), "gather_batch: null pointer");
+    hipLaunchKernelGGL(gather_kernel, dim3(ew_grid(batch * sample_elems), nclients), dim3(256), 0,
+                       as_stream(stream), data, labels, idx, idx_cs, x, x_cs, y, y_cs, sample_elems,
+                       counts, batch);
+    FH_LAUNCH_CHECK("gather_batch");
+    return FH_OK;
+}

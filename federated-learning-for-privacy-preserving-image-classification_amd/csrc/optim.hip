@@ -1,0 +1,91 @@
+// optim.hip — optimizer steps over the packed [clients][P] parameter rows.
+//
+// Reference: LocalTrainer._create_optimizer (src/shared/training.py:244-255)
+//   'sgd'   -> torch.optim.SGD(lr, momentum=0.9)
+//   'adam'  -> torch.optim.Adam(lr)               (betas .9/.999, eps 1e-8)
+//   'adamw' -> torch.optim.AdamW(lr)              (weight_decay 0.01)
+// and the step is torch.optim's single-tensor CPU path.  The rounding
+// sequence below follows ATen's CPU kernels for those tensor ops:
+//   add(.., alpha)  -> fmadd(b, alpha, a)     lerp (w<.5) -> fmadd(w, e-s, s)
+//   addcmul         -> a + (v*b)*c            addcdiv     -> a + v*(b/c)
+// The optimizer is re-created every round (training.py:89), so callers pass
+// first_step / step counts that restart at 1 each round.
+#include "fh_common.h"
+
+namespace fh {
+
+__global__ void __launch_bounds__(256)
+sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf, int64_t n,
+           float neg_lr, float mom, float wd, int first) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float pv = p[i];
+        float gv = g[i];
+        if (wd != 0.f) gv = fmaf(pv, wd, gv);
+        float b;
+        if (mom != 0.f) {
+            b = first ? gv : (buf[i] * mom + gv);
+            buf[i] = b;
+        } else {
+            b = gv;
+        }
+        p[i] = fmaf(b, neg_lr, pv);
+    }
+}
+
+__global__ void __launch_bounds__(256)
+adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+            float* __restrict__ v, int64_t n, float wd, float decay_mul, int decoupled,
+            float one_m_b1, float b2, float one_m_b2, float bc2_sqrt, float eps,
+            float neg_step_size) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float pv = p[i];
+        float gv = g[i];
+        if (wd != 0.f) {
+            if (decoupled) pv = pv * decay_mul;
+            else gv = fmaf(pv, wd, gv);
+        }
+        const float mv = fmaf(one_m_b1, gv - m[i], m[i]);
+        const float vv = v[i] * b2 + (one_m_b2 * gv) * gv;
+        m[i] = mv;
+        v[i] = vv;
+        const float denom = sqrtf(vv) / bc2_sqrt + eps;
+        p[i] = pv + neg_step_size * (mv / denom);
+    }
+}
+
+}  // namespace fh
+
+using namespace fh;
+
+static int grid_for(int64_t n) { return (int)std::min<int64_t>(ceil_div(n, 256), 4096); }
+
+extern "C" int fh_sgd_step(float* param, const float* grad, float* momentum_buf, int64_t n,
+                           float lr, float momentum, float weight_decay, int32_t first_step,
+                           void* stream) {
+    FH_REQUIRE(n >= 0, "sgd_step: bad size");
+    if (n == 0) return FH_OK;
+    FH_REQUIRE(param && grad && (momentum == 0.f || momentum_buf), "sgd_step: null pointer");
+    hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param, grad,
+                       momentum_buf, n, -lr, momentum, weight_decay, first_step);
+    FH_LAUNCH_CHECK("sgd_step");
+    return FH_OK;
+}
+
+extern "C" int fh_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                            int64_t n, double lr, double beta1, double beta2, double eps,
+                            double weight_decay, int32_t decoupled, double step_size,
+                            double bc2_sqrt, void* stream) {
+    FH_REQUIRE(n >= 0, "adam_step: bad size");
+    if (n == 0) return FH_OK;
+    FH_REQUIRE(param && grad && exp_avg && exp_avg_sq, "adam_step: null pointer");
+    // Python-double scalars are rounded to fp32 where ATen meets the fp32 tensor.
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param, grad,
+                       exp_avg, exp_avg_sq, n, (float)weight_decay,
+                       (float)(1.0 - lr * weight_decay), decoupled, (float)(1.0 - beta1),
+                       (float)beta2, (float)(1.0 - beta2), (float)bc2_sqrt, (float)eps,
+                       (float)(-step_size));
+    FH_LAUNCH_CHECK("adam_step");
+    return FH_OK;
+}

@@ -1,0 +1,117 @@
+"""ctypes binding of libfedhip.so (the C ABI declared in include/fedhip.h).
+
+This module is the ONLY way Python reaches the HIP kernels.  There is no
+fallback: if the library is missing, or no HIP device is present, calls raise
+``FedHipError`` — the product path never silently drops to a CPU/PyTorch
+implementation.
+
+``torch`` is imported first so that the HIP runtime torch ships
+(libamdhip64.so.7) is the one libfedhip binds to: both share the soname, so
+the dynamic loader reuses torch's copy and device pointers / streams are
+interchangeable.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+
+import torch  # noqa: F401  (must precede CDLL: shared HIP runtime)
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libfedhip.so")
+
+
+class FedHipError(RuntimeError):
+    """A libfedhip entry point returned a non-zero status."""
+
+
+P = c_void_p  # every tensor argument is a raw device pointer
+I32, I64, F32, F64, U64, SZ = c_int32, c_int64, c_float, c_double, c_uint64, c_size_t
+
+# name -> (restype, [argtypes]); mirrors include/fedhip.h one for one.
+SIGNATURES = {
+    "fh_last_error": (ctypes.c_char_p, []),
+    "fh_version": (I32, []),
+    "fh_fedavg_weighted_sum": (I32, [P, I64, P, P, I32, I64, P, I32, P]),
+    "fh_update_stats": (I32, [P, I64, I32, P, I32, P, P, P]),
+    "fh_dp_delta_sqnorm": (I32, [P, I64, P, I64, I32, P, I32, P, P]),
+    "fh_dp_clip_coef": (I32, [P, I32, I32, F64, F64, F64, P, P, P, P, P]),
+    "fh_dp_apply": (I32, [P, I64, P, I64, P, I64, I32, I64, P, P, P, P, I64, U64, P]),
+    "fh_sgd_step": (I32, [P, P, P, I64, F32, F32, F32, I32, P]),
+    "fh_adam_step": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, I32, F64, F64, P]),
+    "fh_conv2d_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
+                            I32, I32, I32, I32, I32, P]),
+    "fh_conv2d_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, I32,
+                              I32, I32, I32, P]),
+    "fh_conv2d_wgrad_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
+    "fh_conv2d_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32,
+                              I32, I32, I32, I32, I32, I32, P]),
+    "fh_linear_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, P]),
+    "fh_linear_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, P]),
+    "fh_linear_wgrad_workspace": (SZ, [I32, I32, I32, I32]),
+    "fh_linear_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32, P]),
+    "fh_bn_fwd_train": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, P, P, I32, I32,
+                              I32, I32, F32, F32, I32, P]),
+    "fh_bn_fwd_eval": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, I32, I32, I32,
+                             I32, F32, I32, P]),
+    "fh_bn_bwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, P, P, I64, P, I64, P, P, I64, P,
+                        I32, I32, I32, I32, I32, P]),
+    "fh_maxpool2_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
+                              F32, U64, P]),
+    "fh_maxpool2_bwd": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I32,
+                              I32, I32, P]),
+    "fh_dropout_fwd": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I64, I32, F32, U64, P]),
+    "fh_dropout_bwd": (I32, [P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I64, P]),
+    "fh_ce_fwd_bwd": (I32, [P, I64, P, I64, P, I64, P, P, P, P, P, I32, I32, I32, P]),
+    "fh_avgpool_fwd": (I32, [P, I64, P, I64, P, I32, I32, I32, I32, P]),
+    "fh_avgpool_bwd": (I32, [P, I64, P, I64, P, I32, I32, I32, I32, P]),
+    "fh_gather_batch": (I32, [P, P, P, I64, P, I64, P, I64, I64, P, I32, I32, P]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libfedhip.so and bind every declared symbol (raises if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FedHipError(
+            f"libfedhip.so not found at {path}; build it with "
+            "`python build_native.py` (HIP/gfx950) — there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None passes NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, *args):
+    """Invoke a status-returning entry point; raise FedHipError on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.fh_last_error().decode(errors="replace")
+        raise FedHipError(f"{name} failed (rc={rc}): {msg}")
+    return rc
+
+
+def require_device(t: torch.Tensor, what: str = "tensor"):
+    if not t.is_cuda:
+        raise FedHipError(f"{what} must live on a HIP device (got {t.device}); "
+                          "libfedhip has no CPU path")

@@ -1,0 +1,246 @@
+"""Tensor-level wrappers over the libfedhip C ABI.
+
+Every function takes packed device tensors — leading dimension = client slot —
+and launches on torch's current HIP stream.  Client strides are read from the
+tensors themselves (``t.stride(0)``), so a function works equally on a dense
+[C, ...] tensor or on per-layer views into the packed parameter rows
+[C, P].  Nothing here computes on the CPU: shapes are checked on the host,
+the arithmetic is the kernels'.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, load, ptr, require_device, stream_handle
+
+__all__ = [
+    "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "linear_fwd", "linear_dgrad", "linear_wgrad",
+    "fedavg_weighted_sum", "update_stats", "dp_delta_sqnorm", "dp_clip_coef", "dp_apply",
+    "sgd_step", "adam_step", "bn_fwd_train", "bn_fwd_eval", "bn_bwd", "maxpool2_fwd",
+    "maxpool2_bwd", "dropout_fwd", "dropout_bwd", "ce_fwd_bwd", "avgpool_fwd", "avgpool_bwd",
+    "gather_batch", "Workspace",
+]
+
+
+def _cs(t):
+    return 0 if t is None else t.stride(0)
+
+
+def _counts(counts):
+    return None if counts is None else ptr(counts)
+
+
+class Workspace:
+    """Grow-only device scratch buffer (split-K partials)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buf = torch.empty(0, dtype=torch.uint8, device=device)
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        if self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(nbytes, 2 * self.buf.numel()), dtype=torch.uint8,
+                                   device=self.device)
+        return self.buf
+
+
+_WS: dict = {}
+
+
+def _ws(device) -> Workspace:
+    key = str(device)
+    if key not in _WS:
+        _WS[key] = Workspace(device)
+    return _WS[key]
+
+
+# ------------------------------------------------------------------ conv / linear
+def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad, relu=False,
+               counts=None):
+    require_device(x, "x")
+    call("fh_conv2d_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y),
+         _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(relu),
+         stream_handle())
+    return y
+
+
+def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None):
+    call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
+         nclients, batch, cin, h, wd, cout, k, k, stride, pad, stream_handle())
+    return dx
+
+
+def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None):
+    lib = load()
+    need = lib.fh_conv2d_wgrad_workspace(nclients, batch, cin, h, wd, cout, k, k, stride, pad)
+    ws = _ws(x.device).get(need)
+    call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
+         ptr(ws), ws.numel(), _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride,
+         pad, stream_handle())
+    return dw
+
+
+def linear_fwd(x, w, bias, y, nclients, batch, in_f, out_f, relu=False, counts=None):
+    require_device(x, "x")
+    call("fh_linear_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y),
+         _counts(counts), nclients, batch, in_f, out_f, int(relu), stream_handle())
+    return y
+
+
+def linear_dgrad(dy, w, dx, nclients, batch, in_f, out_f, counts=None):
+    call("fh_linear_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
+         nclients, batch, in_f, out_f, stream_handle())
+    return dx
+
+
+def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
+    lib = load()
+    need = lib.fh_linear_wgrad_workspace(nclients, batch, in_f, out_f)
+    ws = _ws(x.device).get(need)
+    call("fh_linear_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
+         ptr(ws), ws.numel(), _counts(counts), nclients, batch, in_f, out_f, stream_handle())
+    return dw
+
+
+# ------------------------------------------------------------------ FedAvg / validation
+def fedavg_weighted_sum(rows, weights_f32, out, row_index=None, accumulate=False, P=None):
+    """out = [out +] sum_k fl32(w_k) * rows[row_index[k]] (sequential, no FMA)."""
+    require_device(rows, "rows")
+    C = weights_f32.numel()
+    P = rows.shape[1] if P is None else P
+    call("fh_fedavg_weighted_sum", ptr(rows), rows.stride(0), ptr(row_index), ptr(weights_f32),
+         C, P, ptr(out), int(accumulate), stream_handle())
+    return out
+
+
+def update_stats(rows, seg_offsets, nclients):
+    nseg = seg_offsets.numel() - 1
+    absmax = torch.empty(nclients, nseg, dtype=torch.float32, device=rows.device)
+    bad = torch.empty(nclients, nseg, dtype=torch.int32, device=rows.device)
+    call("fh_update_stats", ptr(rows), rows.stride(0), nclients, ptr(seg_offsets), nseg,
+         ptr(absmax), ptr(bad), stream_handle())
+    return absmax, bad
+
+
+# ------------------------------------------------------------------ DP
+def dp_delta_sqnorm(local, global_, seg_offsets, nclients, out=None):
+    nseg = seg_offsets.numel() - 1
+    if out is None:
+        out = torch.empty(nclients, nseg, dtype=torch.float64, device=local.device)
+    call("fh_dp_delta_sqnorm", ptr(local), local.stride(0), ptr(global_), _cs(global_), nclients,
+         ptr(seg_offsets), nseg, ptr(out), stream_handle())
+    return out
+
+
+def dp_clip_coef(seg_sqnorm, max_norm, epsilon, delta):
+    C, nseg = seg_sqnorm.shape
+    dev = seg_sqnorm.device
+    total = torch.empty(C, dtype=torch.float64, device=dev)
+    coef = torch.empty(C, dtype=torch.float32, device=dev)
+    clipped = torch.empty(C, dtype=torch.int32, device=dev)
+    sigma = torch.empty(C, dtype=torch.float32, device=dev)
+    call("fh_dp_clip_coef", ptr(seg_sqnorm), C, nseg, float(max_norm), float(epsilon),
+         float(delta), ptr(total), ptr(coef), ptr(clipped), ptr(sigma), stream_handle())
+    return total, coef, clipped, sigma
+
+
+def dp_apply(local, global_, out, coef, clipped, sigma, noise=None, seed=0, P=None):
+    C = coef.numel()
+    P = local.shape[1] if P is None else P
+    call("fh_dp_apply", ptr(local), local.stride(0), ptr(global_), _cs(global_), ptr(out),
+         out.stride(0), C, P, ptr(coef), ptr(clipped), ptr(sigma), ptr(noise), _cs(noise),
+         int(seed) & 0xFFFFFFFFFFFFFFFF, stream_handle())
+    return out
+
+
+# ------------------------------------------------------------------ optimizers
+def sgd_step(param, grad, buf, lr, momentum, weight_decay=0.0, first_step=False, n=None):
+    n = param.numel() if n is None else n
+    call("fh_sgd_step", ptr(param), ptr(grad), ptr(buf), n, float(lr), float(momentum),
+         float(weight_decay), int(first_step), stream_handle())
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
+              weight_decay=0.0, decoupled=False, n=None):
+    """torch.optim.Adam/AdamW single-tensor step; bias corrections in Python double."""
+    n = param.numel() if n is None else n
+    bias_correction1 = 1 - beta1 ** step
+    bias_correction2 = 1 - beta2 ** step
+    step_size = lr / bias_correction1
+    bc2_sqrt = bias_correction2 ** 0.5
+    call("fh_adam_step", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), n, float(lr),
+         float(beta1), float(beta2), float(eps), float(weight_decay), int(decoupled),
+         float(step_size), float(bc2_sqrt), stream_handle())
+
+
+# ------------------------------------------------------------------ BN / pool / dropout / CE
+def bn_fwd_train(x, y, gamma, beta, rmean, rvar, save_mean, save_invstd, nclients, batch, C, HW,
+                 eps=1e-5, momentum=0.1, relu=False, res=None, counts=None):
+    call("fh_bn_fwd_train", ptr(x), _cs(x), ptr(y), _cs(y), ptr(res), _cs(res), ptr(gamma),
+         ptr(beta), _cs(gamma), ptr(rmean), ptr(rvar), _cs(rmean), ptr(save_mean),
+         ptr(save_invstd), _counts(counts), nclients, batch, C, HW, float(eps), float(momentum),
+         int(relu), stream_handle())
+
+
+def bn_fwd_eval(x, y, gamma, beta, rmean, rvar, nclients, batch, C, HW, eps=1e-5, relu=False,
+                res=None, counts=None):
+    call("fh_bn_fwd_eval", ptr(x), _cs(x), ptr(y), _cs(y), ptr(res), _cs(res), ptr(gamma),
+         ptr(beta), _cs(gamma), ptr(rmean), ptr(rvar), _cs(rmean), _counts(counts), nclients,
+         batch, C, HW, float(eps), int(relu), stream_handle())
+
+
+def bn_bwd(dy, yout, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclients, batch, C, HW,
+           relu=False, dres=None, counts=None):
+    call("fh_bn_bwd", ptr(dy), _cs(dy), ptr(yout), _cs(yout), ptr(x), _cs(x), ptr(gamma),
+         _cs(gamma), ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dres), _cs(dres),
+         ptr(dgamma), ptr(dbeta), _cs(dgamma), _counts(counts), nclients, batch, C, HW,
+         int(relu), stream_handle())
+
+
+def maxpool2_fwd(x, y, idx, nclients, batch, C, H, W, mask=None, drop_mode=0, p_drop=0.0, seed=0,
+                 counts=None):
+    call("fh_maxpool2_fwd", ptr(x), _cs(x), ptr(y), _cs(y), ptr(idx), _cs(idx), ptr(mask),
+         _cs(mask), _counts(counts), nclients, batch, C, H, W, int(drop_mode), float(p_drop),
+         int(seed) & 0xFFFFFFFFFFFFFFFF, stream_handle())
+
+
+def maxpool2_bwd(dy, idx, dx, nclients, batch, C, H, W, mask=None, p_drop=0.0, xin=None,
+                 counts=None):
+    call("fh_maxpool2_bwd", ptr(dy), _cs(dy), ptr(idx), _cs(idx), ptr(mask), _cs(mask),
+         float(p_drop), ptr(xin), _cs(xin), ptr(dx), _cs(dx), _counts(counts), nclients, batch, C,
+         H, W, stream_handle())
+
+
+def dropout_fwd(x, y, mask, nclients, batch, per_img, p_drop, drop_mode=1, seed=0, counts=None):
+    call("fh_dropout_fwd", ptr(x), _cs(x), ptr(y), _cs(y), ptr(mask), _cs(mask), _counts(counts),
+         nclients, batch, per_img, int(drop_mode), float(p_drop),
+         int(seed) & 0xFFFFFFFFFFFFFFFF, stream_handle())
+
+
+def dropout_bwd(dy, dx, nclients, batch, per_img, mask=None, p_drop=0.0, relu_out=None,
+                counts=None):
+    call("fh_dropout_bwd", ptr(dy), _cs(dy), ptr(mask), _cs(mask), float(p_drop), ptr(relu_out),
+         _cs(relu_out), ptr(dx), _cs(dx), _counts(counts), nclients, batch, per_img,
+         stream_handle())
+
+
+def ce_fwd_bwd(logits, targets, dlogits, nclients, batch, num_classes, loss_out=None,
+               acc_loss=None, acc_correct=None, acc_seen=None, counts=None):
+    call("fh_ce_fwd_bwd", ptr(logits), _cs(logits), ptr(targets), _cs(targets), ptr(dlogits),
+         _cs(dlogits), ptr(loss_out), ptr(acc_loss), ptr(acc_correct), ptr(acc_seen),
+         _counts(counts), nclients, batch, num_classes, stream_handle())
+
+
+def avgpool_fwd(x, y, nclients, batch, C, HW, counts=None):
+    call("fh_avgpool_fwd", ptr(x), _cs(x), ptr(y), _cs(y), _counts(counts), nclients, batch, C,
+         HW, stream_handle())
+
+
+def avgpool_bwd(dy, dx, nclients, batch, C, HW, counts=None):
+    call("fh_avgpool_bwd", ptr(dy), _cs(dy), ptr(dx), _cs(dx), _counts(counts), nclients, batch,
+         C, HW, stream_handle())
+
+
+def gather_batch(data, labels, idx, x, y, sample_elems, nclients, batch, counts=None):
+    call("fh_gather_batch", ptr(data), ptr(labels), ptr(idx), _cs(idx), ptr(x), _cs(x), ptr(y),
+         _cs(y), sample_elems, _counts(counts), nclients, batch, stream_handle())

@@ -1,0 +1,209 @@
+/*
+ * fedhip.h — C ABI of libfedhip.so, the MI355X (gfx950) hot path for
+ * per-client CNN training, update-level differential privacy and FedAvg.
+ *
+ * Every entry point:
+ *   - returns FH_OK (0) or a negative FH_E_* code; fh_last_error() gives a
+ *     thread-local message for the last failure on the calling thread;
+ *   - takes caller-owned DEVICE pointers (fp32 unless stated), contiguous,
+ *     with element strides spelled out; no hidden allocation, no host sync;
+ *   - launches on `stream` (a hipStream_t passed as void*; NULL = default).
+ *
+ * "Packed" tensors hold many simulated clients: client slot z of a tensor
+ * `t` with client stride `t_cs` starts at t + z * t_cs.  Clients are packed
+ * into slots sorted by descending step count, so the clients still active at
+ * a given step are always the prefix [0, nclients).  `counts[z]` (device
+ * int32, may be NULL = all `batch` valid) is the number of valid images of
+ * client z in this step — the reference's partial last batch
+ * (DataLoader drop_last=False, src/shared/training.py:184).
+ *
+ * Reference interfaces replaced (file:line in the reference repository):
+ *   fh_fedavg_weighted_sum   src/aggregation/fedavg.py:267-289 (_weighted_average)
+ *   fh_update_stats          src/shared/validation.py:72-91   (_validate_model_weights)
+ *   fh_dp_delta_sqnorm       src/shared/privacy.py:119-123    (GradientClipper norm)
+ *                            + src/client/federated_trainer.py:438-443 (delta)
+ *   fh_dp_clip_coef          src/shared/privacy.py:123-140, 209 (clip decision, sigma)
+ *   fh_dp_apply              src/shared/privacy.py:127-133, 212, 244-245
+ *                            + src/client/federated_trainer.py:454-459
+ *   fh_sgd_step / fh_adam_step   src/shared/training.py:244-255 + torch.optim
+ *   fh_conv2d_* / fh_linear_*    nn.Conv2d / nn.Linear in src/shared/models_pytorch.py
+ *   fh_bn_*                  nn.BatchNorm2d (models_pytorch.py:108-120, 176-187)
+ *   fh_maxpool2_*            nn.MaxPool2d(2,2) (models_pytorch.py:72,123)
+ *   fh_dropout_*             nn.Dropout (models_pytorch.py:75,124)
+ *   fh_ce_fwd_bwd            nn.CrossEntropyLoss + metrics (training.py:90,193,200-203)
+ */
+#ifndef FEDHIP_H_
+#define FEDHIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FH_OK 0
+#define FH_E_INVALID (-1)     /* bad argument / shape */
+#define FH_E_LAUNCH (-2)      /* HIP launch or runtime failure */
+#define FH_E_UNSUPPORTED (-3) /* shape/config outside what the kernels cover */
+
+const char* fh_last_error(void);
+int fh_version(void);
+
+/* ---------------- FedAvg (fedavg.py:267-289) ------------------------------
+ * out[j] = (accumulate ? out[j] : 0) + sum_{k=0..C-1} fl32(w[k]) * rows[idx[k]*row_stride + j]
+ * evaluated sequentially in k with a rounded multiply followed by a rounded
+ * add (never a fused multiply-add): bit-exact with the reference's
+ * `aggregated[l] += weight * layer` loop over the client list.
+ * row_index (device int32[C]) may be NULL (identity); weights: device float[C]. */
+int fh_fedavg_weighted_sum(const float* rows, int64_t row_stride, const int32_t* row_index,
+                           const float* weights, int32_t num_clients, int64_t P, float* out,
+                           int32_t accumulate, void* stream);
+
+/* Per client, per parameter tensor (segment [seg_off[t], seg_off[t+1]) of a row):
+ * max |w| and a non-finite flag (validation.py:81-91). seg_offsets: device int64[nseg+1]. */
+int fh_update_stats(const float* rows, int64_t row_stride, int32_t num_clients,
+                    const int64_t* seg_offsets, int32_t nseg, float* seg_absmax,
+                    int32_t* seg_nonfinite, void* stream);
+
+/* ---------------- update-level DP (privacy.py:107-144, 183-254) ----------
+ * delta = fl32(local - global) (global may be NULL: delta = local).
+ * seg_sqnorm[z*nseg+t] = sum over segment t of delta^2, accumulated in fp64. */
+int fh_dp_delta_sqnorm(const float* local, int64_t local_stride, const float* global,
+                       int64_t global_stride, int32_t num_clients, const int64_t* seg_offsets,
+                       int32_t nseg, double* seg_sqnorm, void* stream);
+
+/* Per client: total = sqrt(sum_t fl32(sqrt(seg_sqnorm_t))^2) (the reference sums
+ * squared per-tensor fp32 norms in double, privacy.py:119-123);
+ * clipped = total > max_norm; coef = fl32(max_norm/total);
+ * sigma = fl32(min(total,max_norm) * sqrt(2 ln(1.25/delta)) / epsilon) (privacy.py:209). */
+int fh_dp_clip_coef(const double* seg_sqnorm, int32_t num_clients, int32_t nseg, double max_norm,
+                    double epsilon, double delta, double* total_norm, float* coef,
+                    int32_t* clipped, float* sigma, void* stream);
+
+/* out = [global +] ( (clipped ? fl32(delta*coef) : delta) + noise ), each step fp32-rounded.
+ * noise = noise_in[z*noise_stride + j] if noise_in != NULL (parity mode: noise drawn by
+ * the caller) else sigma[z] * N(0,1) from Philox4x32-10 keyed by (seed, z, j). */
+int fh_dp_apply(const float* local, int64_t local_stride, const float* global,
+                int64_t global_stride, float* out, int64_t out_stride, int32_t num_clients,
+                int64_t P, const float* coef, const int32_t* clipped, const float* sigma,
+                const float* noise_in, int64_t noise_stride, uint64_t seed, void* stream);
+
+/* ---------------- optimizers (torch.optim single-tensor semantics) -------- */
+/* SGD(momentum, dampening=0, nesterov=False): buf = first ? g : m*buf + g; p -= lr*buf */
+int fh_sgd_step(float* param, const float* grad, float* momentum_buf, int64_t n, float lr,
+                float momentum, float weight_decay, int32_t first_step, void* stream);
+/* Adam / AdamW (decoupled=1). step_size = lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t),
+ * both computed by the caller in double exactly as torch.optim does. */
+int fh_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                 double lr, double beta1, double beta2, double eps, double weight_decay,
+                 int32_t decoupled, double step_size, double bc2_sqrt, void* stream);
+
+/* ---------------- convolution / linear (fp32 MFMA implicit GEMM) ----------
+ * x: [clients][batch][cin][h][w]; w: [cout][cin][kh][kw] per client; y: [clients][batch][cout][oh][ow].
+ * Supported: (kh,kw,stride) in {(3,3,1),(3,3,2),(1,1,1),(1,1,2)}, pad arbitrary. */
+int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs, const float* bias,
+                  int64_t b_cs, float* y, int64_t y_cs, const int32_t* counts, int32_t nclients,
+                  int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh,
+                  int32_t kw, int32_t stride, int32_t pad, int32_t relu, void* stream);
+int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs, float* dx,
+                    int64_t dx_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                    int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
+                    int32_t stride, int32_t pad, void* stream);
+/* dw (and db if non-NULL) are overwritten. workspace >= fh_conv2d_wgrad_workspace(...) bytes. */
+size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
+                                 int32_t w_, int32_t cout, int32_t kh, int32_t kw, int32_t stride,
+                                 int32_t pad);
+int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs, float* dw,
+                    int64_t dw_cs, float* db, int64_t db_cs, void* workspace, size_t ws_bytes,
+                    const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin, int32_t h,
+                    int32_t w_, int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad,
+                    void* stream);
+
+/* Linear: x [clients][batch][in_f], w [out_f][in_f], y [clients][batch][out_f]. */
+int fh_linear_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs, const float* bias,
+                  int64_t b_cs, float* y, int64_t y_cs, const int32_t* counts, int32_t nclients,
+                  int32_t batch, int32_t in_f, int32_t out_f, int32_t relu, void* stream);
+int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs, float* dx,
+                    int64_t dx_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                    int32_t in_f, int32_t out_f, void* stream);
+size_t fh_linear_wgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f);
+int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs, float* dw,
+                    int64_t dw_cs, float* db, int64_t db_cs, void* workspace, size_t ws_bytes,
+                    const int32_t* counts, int32_t nclients, int32_t batch, int32_t in_f,
+                    int32_t out_f, void* stream);
+
+/* ---------------- BatchNorm2d (+ReLU, +residual add) ----------------------
+ * x/y/res: [clients][batch][C][HW]; gamma/beta live in the per-client param
+ * rows (stride p_cs); running stats stride r_cs (NULL: not tracked);
+ * save_mean/save_invstd: [clients][C].  Train mode: batch statistics over the
+ * valid images (fp64 accumulation), running stats momentum-updated with the
+ * unbiased variance.  y = relu?( x*alpha + beta' [+ res] ). */
+int fh_bn_fwd_train(const float* x, int64_t x_cs, float* y, int64_t y_cs, const float* res,
+                    int64_t res_cs, const float* gamma, const float* beta, int64_t p_cs,
+                    float* running_mean, float* running_var, int64_t r_cs, float* save_mean,
+                    float* save_invstd, const int32_t* counts, int32_t nclients, int32_t batch,
+                    int32_t C, int32_t HW, float eps, float momentum, int32_t relu, void* stream);
+int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_cs, const float* res,
+                   int64_t res_cs, const float* gamma, const float* beta, int64_t p_cs,
+                   const float* running_mean, const float* running_var, int64_t r_cs,
+                   const int32_t* counts, int32_t nclients, int32_t batch, int32_t C, int32_t HW,
+                   float eps, int32_t relu, void* stream);
+/* g = relu ? dy*(yout>0) : dy; dres (nullable) <- g; dgamma/dbeta (stride g_cs) and dx. */
+int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs, const float* x,
+              int64_t x_cs, const float* gamma, int64_t p_cs, const float* save_mean,
+              const float* save_invstd, float* dx, int64_t dx_cs, float* dres, int64_t dres_cs,
+              float* dgamma, float* dbeta, int64_t g_cs, const int32_t* counts, int32_t nclients,
+              int32_t batch, int32_t C, int32_t HW, int32_t relu, void* stream);
+
+/* ---------------- MaxPool2d(2,2) (+ fused Dropout after it) ---------------
+ * idx: uint8 window argmax [clients][batch][C][H/2][W/2]; drop_mode 0 none,
+ * 1 generate keep-mask (Philox4x32-10 keyed by seed, slot, element) into mask,
+ * 2 apply the caller's mask (parity).  Backward writes all four window slots;
+ * xin (nullable) = the pooled ReLU output, to apply the ReLU mask at the argmax. */
+int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
+                    int64_t i_cs, uint8_t* mask, int64_t m_cs, const int32_t* counts,
+                    int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                    int32_t drop_mode, float p_drop, uint64_t seed, void* stream);
+int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,
+                    const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin, int64_t x_cs,
+                    float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
+                    int32_t batch, int32_t C, int32_t H, int32_t W, void* stream);
+
+/* ---------------- Dropout (F.dropout: x * bernoulli(1-p)/(1-p)) ------------
+ * drop_mode 1 generate mask (uint8), 2 use the caller's mask.  Backward:
+ * dx = dy*mask/(1-p) [* (relu_out > 0)]; mask NULL = ReLU backward only. */
+int fh_dropout_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* mask,
+                   int64_t m_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                   int64_t per_img, int32_t drop_mode, float p_drop, uint64_t seed, void* stream);
+int fh_dropout_bwd(const float* dy, int64_t dy_cs, const uint8_t* mask, int64_t m_cs, float p_drop,
+                   const float* relu_out, int64_t r_cs, float* dx, int64_t dx_cs,
+                   const int32_t* counts, int32_t nclients, int32_t batch, int64_t per_img,
+                   void* stream);
+
+/* ---------------- CrossEntropyLoss (mean) fwd+bwd + epoch metrics ---------
+ * targets int64 [clients][batch]; dlogits = (softmax - onehot)/count;
+ * loss_out[z] = batch mean loss; acc_* (nullable) accumulate the epoch's
+ * sum of batch losses, correct argmax predictions and samples seen. */
+int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets, int64_t t_cs,
+                  float* dlogits, int64_t d_cs, float* loss_out, double* acc_loss,
+                  int64_t* acc_correct, int64_t* acc_seen, const int32_t* counts,
+                  int32_t nclients, int32_t batch, int32_t num_classes, void* stream);
+
+/* ---------------- AdaptiveAvgPool2d((1,1)) --------------------------------- */
+int fh_avgpool_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, const int32_t* counts,
+                   int32_t nclients, int32_t batch, int32_t C, int32_t HW, void* stream);
+int fh_avgpool_bwd(const float* dy, int64_t dy_cs, float* dx, int64_t dx_cs,
+                   const int32_t* counts, int32_t nclients, int32_t batch, int32_t C, int32_t HW,
+                   void* stream);
+
+/* ---------------- on-device batch assembly (DataLoader replacement) -------
+ * x[z][b] = data[idx[z*idx_cs+b]], y[z][b] = labels[idx[..]] for b < counts[z]. */
+int fh_gather_batch(const float* data, const int64_t* labels, const int64_t* idx, int64_t idx_cs,
+                    float* x, int64_t x_cs, int64_t* y, int64_t y_cs, int64_t sample_elems,
+                    const int32_t* counts, int32_t nclients, int32_t batch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEDHIP_H_ */

@@ -1,0 +1,104 @@
+"""HIP implicit-GEMM conv / linear vs a torch fp32 CPU reference (F.conv2d +
+autograd), client-batched, including partial last batches (counts < batch).
+
+Tolerance: fp32 MFMA accumulation order differs from mkldnn's, so outputs are
+compared with  |gpu - ref| <= 2e-5 * sqrt(K) * max|ref| + 1e-6  where K is the
+reduction length of the product (stated per test).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fedhip import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(gpu, ref, K, what):
+    gpu = gpu.detach().cpu().double()
+    ref = ref.detach().cpu().double()
+    tol = 2e-5 * math.sqrt(K) * ref.abs().max().item() + 1e-6
+    err = (gpu - ref).abs().max().item()
+    assert err <= tol, f"{what}: max err {err:.3e} > tol {tol:.3e}"
+
+
+CASES = [
+    # nclients, batch, cin, h, w, cout, k, stride, pad
+    (3, 8, 3, 32, 32, 32, 3, 1, 1),
+    (2, 5, 32, 16, 16, 64, 3, 1, 1),
+    (2, 4, 64, 8, 8, 128, 3, 1, 1),
+    (2, 4, 1, 28, 28, 32, 3, 1, 1),
+    (2, 3, 32, 14, 14, 64, 3, 1, 1),
+    (2, 4, 64, 16, 16, 128, 3, 2, 1),
+    (2, 4, 64, 16, 16, 128, 1, 2, 0),
+    (2, 4, 128, 8, 8, 256, 3, 2, 1),
+    (1, 2, 96, 7, 9, 40, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_conv_fwd_bwd(case):
+    C, B, cin, h, w, cout, k, s, p = case
+    g = torch.Generator().manual_seed(1234)
+    x = torch.randn(C, B, cin, h, w, generator=g)
+    wt = torch.randn(C, cout, cin, k, k, generator=g) * (1.0 / math.sqrt(cin * k * k))
+    bias = torch.randn(C, cout, generator=g)
+    counts = torch.tensor([B - (i % 2) for i in range(C)], dtype=torch.int32)
+    oh = (h + 2 * p - k) // s + 1
+    ow = (w + 2 * p - k) // s + 1
+    dy = torch.randn(C, B, cout, oh, ow, generator=g)
+
+    xd, wd, bd, dyd = x.to(DEV), wt.to(DEV), bias.to(DEV), dy.to(DEV)
+    y = torch.zeros(C, B, cout, oh, ow, device=DEV)
+    ops.conv2d_fwd(xd, wd, bd, y, C, B, cin, h, w, cout, k, s, p, counts=counts.to(DEV))
+    dx = torch.zeros(C, B, cin, h, w, device=DEV)
+    ops.conv2d_dgrad(dyd, wd, dx, C, B, cin, h, w, cout, k, s, p, counts=counts.to(DEV))
+    dw = torch.zeros(C, cout, cin, k, k, device=DEV)
+    db = torch.zeros(C, cout, device=DEV)
+    ops.conv2d_wgrad(xd, dyd, dw, db, C, B, cin, h, w, cout, k, s, p, counts=counts.to(DEV))
+    torch.cuda.synchronize()
+
+    for z in range(C):
+        n = int(counts[z])
+        xr = x[z, :n].clone().requires_grad_(True)
+        wr = wt[z].clone().requires_grad_(True)
+        br = bias[z].clone().requires_grad_(True)
+        yr = F.conv2d(xr, wr, br, stride=s, padding=p)
+        yr.backward(dy[z, :n])
+        _close(y[z, :n], yr, cin * k * k, f"fwd z={z}")
+        _close(dx[z, :n], xr.grad, cout * k * k, f"dgrad z={z}")
+        _close(dw[z], wr.grad, n * oh * ow, f"wgrad z={z}")
+        _close(db[z], br.grad, n * oh * ow, f"bgrad z={z}")
+
+
+@pytest.mark.parametrize("C,B,inf,outf", [(3, 32, 3136, 128), (2, 17, 128, 10), (2, 32, 2048, 512)])
+def test_linear_fwd_bwd(C, B, inf, outf):
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(C, B, inf, generator=g)
+    wt = torch.randn(C, outf, inf, generator=g) / math.sqrt(inf)
+    bias = torch.randn(C, outf, generator=g)
+    dy = torch.randn(C, B, outf, generator=g)
+    counts = torch.tensor([B - i for i in range(C)], dtype=torch.int32)
+    cd = counts.to(DEV)
+    y = torch.zeros(C, B, outf, device=DEV)
+    ops.linear_fwd(x.to(DEV), wt.to(DEV), bias.to(DEV), y, C, B, inf, outf, relu=True, counts=cd)
+    dx = torch.zeros(C, B, inf, device=DEV)
+    ops.linear_dgrad(dy.to(DEV), wt.to(DEV), dx, C, B, inf, outf, counts=cd)
+    dw = torch.zeros(C, outf, inf, device=DEV)
+    db = torch.zeros(C, outf, device=DEV)
+    ops.linear_wgrad(x.to(DEV), dy.to(DEV), dw, db, C, B, inf, outf, counts=cd)
+    torch.cuda.synchronize()
+    for z in range(C):
+        n = int(counts[z])
+        xr = x[z, :n].clone().requires_grad_(True)
+        wr = wt[z].clone().requires_grad_(True)
+        br = bias[z].clone().requires_grad_(True)
+        yr = F.linear(xr, wr, br)
+        yr.backward(dy[z, :n])
+        _close(y[z, :n], torch.relu(yr), inf, "linear fwd")
+        _close(dx[z, :n], xr.grad, outf, "linear dgrad")
+        _close(dw[z], wr.grad, n, "linear wgrad")
+        _close(db[z], br.grad, n, "linear bgrad")
