@@ -41,3 +41,44 @@ def select_max_clients(num_samples, max_clients):
     Returns the kept positions in their new order."""
     order = sorted(range(len(num_samples)), key=lambda i: num_samples[i], reverse=True)
     return order[:max_clients]
+
+
+def validate_update(client_id, round_number, num_samples, training_loss, budget, compression,
+                    layers, max_weight_magnitude=10.0, min_samples=1):
+    """ModelUpdateValidator.validate_model_update (validation.py:28-111), timestamps excluded.
+    layers: list of fp32 arrays. Returns True/False (the aggregator swallows the exception)."""
+    if not client_id or not isinstance(client_id, str) or round_number < 0:
+        return False
+    if num_samples < min_samples or training_loss < 0:
+        return False
+    if not layers:
+        return False
+    for a in layers:
+        a = np.asarray(a, np.float32)
+        if np.isnan(a).any() or np.isinf(a).any():
+            return False
+        if np.abs(a).max() > max_weight_magnitude:
+            return False
+    if not (0 <= budget <= 1) or not (0 <= compression <= 1):
+        return False
+    return True
+
+
+def filter_updates(updates, validate=True):
+    """fedavg.py:209-245 on dicts with keys client_id, num_samples, training_loss, budget,
+    compression, round, layers (list). Shape-compatibility pass keeps every update whose
+    layer shapes match the first survivor's (the reference's pop-while-iterating bug,
+    fedavg.py:236-243, is NOT reproduced; see DESIGN.md divergence D6)."""
+    out = []
+    for u in updates:
+        if u["num_samples"] <= 0 or u["training_loss"] < 0:
+            continue
+        if validate and not validate_update(u["client_id"], u.get("round", 0), u["num_samples"],
+                                            u["training_loss"], u["budget"], u["compression"],
+                                            u["layers"]):
+            continue
+        out.append(u)
+    if len(out) > 1:
+        ref = [np.shape(a) for a in out[0]["layers"]]
+        out = [out[0]] + [u for u in out[1:] if [np.shape(a) for a in u["layers"]] == ref]
+    return out

@@ -15,8 +15,9 @@ import numpy as np
 
 
 def tensor_norm_fp32(t):
-    """torch.norm of an fp32 tensor, returned as fp32 then promoted (grad.norm().item())."""
-    return float(np.float32(math.sqrt(float(np.sum(np.asarray(t, np.float64) ** 2)))))
+    """grad.norm().item(): torch's CPU fp32 norm (the reference's own arithmetic), as double."""
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(t, dtype=np.float32)).norm().item()
 
 
 def clip(tensors, max_norm):

@@ -1,0 +1,160 @@
+"""Pin the CPU oracle against golden fixtures produced by the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import hashlib
+import json
+import math
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fedavg_ref, partition_ref, privacy_ref, train_ref
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+ARR = np.load(os.path.join(HERE, "golden", "golden_arrays.npz"))
+
+SIMPLE_SHAPES = [("conv1.weight", (32, 1, 3, 3)), ("conv1.bias", (32,)),
+                 ("conv2.weight", (64, 32, 3, 3)), ("conv2.bias", (64,)),
+                 ("fc1.weight", (128, 3136)), ("fc1.bias", (128,)),
+                 ("fc2.weight", (10, 128)), ("fc2.bias", (10,))]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(np.asarray(a, np.float32)).tobytes()).hexdigest()
+
+
+def rows_for(shapes, C, seed, scale=0.05):
+    rng = np.random.default_rng(seed)
+    return [{n: (rng.standard_normal(s).astype(np.float32) * scale) for n, s in shapes}
+            for _ in range(C)]
+
+
+@pytest.mark.parametrize("key", ["G1/C4_s101", "G1/C32_s102", "G1/C6_s103"])
+def test_g1_fedavg_bit_exact(key):
+    g = GOLD[key]
+    rows = rows_for(SIMPLE_SHAPES, g["C"], g["seed"])
+    w = fedavg_ref.calculate_sample_weights(g["num_samples"])
+    for name, _ in SIMPLE_SHAPES:
+        out = fedavg_ref.weighted_average([r[name].reshape(-1) for r in rows], w)
+        assert sha(out) == g["layers"][name]["sha256"], name
+    assert g["participants"] == [f"client_{i}" for i in range(g["C"])]
+
+
+def test_g1_max_clients_truncation():
+    g = GOLD["G1/trunc64"]
+    shapes = [(n, tuple(s)) for n, s in g["shapes"]]
+    rows = rows_for(shapes, 64, g["seed"])
+    keep = fedavg_ref.select_max_clients(g["num_samples"], g["max_clients"])
+    assert [f"c{i}" for i in keep] == g["participants"]
+    w = fedavg_ref.calculate_sample_weights([g["num_samples"][i] for i in keep])
+    for name, _ in shapes:
+        out = fedavg_ref.weighted_average([rows[i][name].reshape(-1) for i in keep], w)
+        assert sha(out) == g["layers"][name]["sha256"]
+
+
+def test_g1_validator_rejections():
+    g = GOLD["G1/reject"]
+    shapes = [(n, tuple(s)) for n, s in g["shapes"]]
+    rows = rows_for(shapes, 6, g["seed"])
+    rows[1]["fc2.weight"][0, 0] = 11.0
+    rows[3]["fc2.bias"][2] = np.nan
+    ups = []
+    for i in range(6):
+        ups.append(dict(client_id=f"v{i}", num_samples=(0 if i == 4 else g["num_samples"][i]),
+                        training_loss=0.5, budget=g["budgets"][i], compression=0.8, round=3,
+                        layers=[rows[i][n] for n, _ in shapes]))
+    kept = fedavg_ref.filter_updates(ups, validate=True)
+    assert [u["client_id"] for u in kept] == g["participants"]
+    w = fedavg_ref.calculate_sample_weights([u["num_samples"] for u in kept])
+    for j, (name, _) in enumerate(shapes):
+        out = fedavg_ref.weighted_average([u["layers"][j].reshape(-1) for u in kept], w)
+        assert sha(out) == g["layers"][name]["sha256"]
+
+
+def test_g1_eps2_updates_rejected():
+    g = GOLD["G1/eps2_rejected"]
+    assert g["raised"] and "Insufficient valid updates: 0 < 2" in g["msg"]
+    ups = [dict(client_id=f"e{i}", num_samples=50, training_loss=0.5, budget=2.0,
+                compression=0.8, layers=[np.zeros(3, np.float32)]) for i in range(3)]
+    assert fedavg_ref.filter_updates(ups) == []
+
+
+@pytest.mark.parametrize("tag", ["big", "small"])
+def test_g2_clip_and_noise(tag):
+    g = GOLD[f"G2/clip_{tag}"]
+    d = rows_for(SIMPLE_SHAPES, 1, g["seed"], g["scale"])[0]
+    tensors = [d[n] for n, _ in SIMPLE_SHAPES]
+    clipped, sens, total, was = privacy_ref.clip(tensors, 1.0)
+    assert sens == g["norm"]
+    for (name, _), c in zip(SIMPLE_SHAPES, clipped):
+        assert sha(c) == g["layers"][name]["sha256"], name
+    # noise: the reference draws torch.normal(0, sigma, shape) per tensor in dict order
+    gn = GOLD[f"G2/noise_{tag}"]
+    torch.manual_seed(gn["torch_seed"])
+    sig = privacy_ref.sigma(sens, gn["epsilon"], gn["delta"])
+    noises = [torch.normal(mean=0.0, std=sig, size=c.shape).numpy() for c in clipped]
+    noisy = privacy_ref.add_noise(clipped, noises)
+    for (name, _), c in zip(SIMPLE_SHAPES, noisy):
+        assert sha(c) == gn["layers"][name]["sha256"], name
+    second = GOLD[f"G2/second_call_{tag}"]
+    assert second["raised"] and "budget exhausted" in second["msg"]
+
+
+def test_g2_sigma_values():
+    for eps, st in GOLD["G2/sigma"].items():
+        s = privacy_ref.sigma(1.0, float(eps), 1e-5)
+        assert abs(st["std"] / s - 1) < 0.01
+        assert abs(st["mean_abs"] / s - math.sqrt(2 / math.pi)) < 0.01
+
+
+TRAIN_KEYS = [k for k in GOLD if k.startswith(("G3/", "G4/", "G5/"))]
+
+
+def make_batch(shape, nclass, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, *shape, generator=g), torch.randint(0, nclass, (n,), generator=g)
+
+
+def run_oracle_case(g):
+    model = train_ref.make_model(g["model"], g["init_seed"], **g["kwargs"])
+    x, y = make_batch(tuple(g["shape"]), g["classes"], g["n"], g["data_seed"])
+    batches = [(x[i:i + g["bs"]], y[i:i + g["bs"]]) for i in range(0, g["n"], g["bs"])]
+    if g["torch_seed"] is not None:
+        torch.manual_seed(g["torch_seed"])
+    m = train_ref.train_epochs(model, batches, g["epochs"], g["lr"], g["opt"])
+    return model, m
+
+
+@pytest.mark.parametrize("key", TRAIN_KEYS)
+def test_g3_g5_train_oracle_bit_exact(key):
+    """The oracle's restated step reproduces the reference LocalTrainer bit for bit."""
+    g = GOLD[key]
+    torch.set_num_threads(8)
+    model, m = run_oracle_case(g)
+    gm = g["metrics"]
+    assert m["loss"] == gm["loss"] and m["accuracy"] == gm["accuracy"]
+    assert m["samples_processed"] == gm["samples_processed"]
+    assert m["epochs_completed"] == gm["epochs_completed"]
+    for name, p in model.named_parameters():
+        assert sha(p.detach().numpy()) == g["params"][name]["sha256"], name
+    sd = model.state_dict()
+    for name, dg in g["buffers"].items():
+        assert sha(sd[name].float().numpy()) == dg["sha256"], name
+
+
+@pytest.mark.parametrize("key", [k for k in GOLD if k.startswith("G6/")])
+def test_g6_partitioner_bit_exact(key):
+    g = GOLD[key]
+    labels = np.random.default_rng(g["label_seed"]).integers(0, 10, size=g["N"])
+    random.seed(0)
+    np.random.seed(0)
+    torch.manual_seed(0)
+    parts = partition_ref.partition(labels, g["C"], g["strategy"], g["alpha"])
+    ks = sorted(parts.keys())
+    assert ks == g["clients"]
+    assert [len(parts[k]) for k in ks] == g["sizes"]
+    got = [hashlib.sha256(np.asarray(parts[k], np.int64).tobytes()).hexdigest() for k in ks]
+    assert got == g["sha256"]
