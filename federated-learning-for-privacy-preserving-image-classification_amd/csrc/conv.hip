@@ -37,6 +37,7 @@ struct ConvArgs {
     const int32_t* counts;
     int batch, cin, h, w, cout, oh, ow, pad;
     int relu;
+    int accumulate;      // DGRAD: dx += result
     int splits, kchunk;  // WGRAD
     int M, N, K;         // GEMM extents at full batch
     FastDiv fd_ohw, fd_ow, fd_hw, fd_w;
@@ -286,7 +287,10 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
-                        if (m < M) op[(int64_t)m * hw] = acc[i][j][r];
+                        if (m < M) {
+                            float* q = op + (int64_t)m * hw;
+                            *q = a.accumulate ? (*q + acc[i][j][r]) : acc[i][j][r];
+                        }
                     }
             }
         }
@@ -449,7 +453,8 @@ extern "C" int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64
 extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
                                float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
                                int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
-                               int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream) {
+                               int32_t kh, int32_t kw, int32_t stride, int32_t pad,
+                               int32_t accumulate, void* stream) {
     int oh, ow;
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
     if (rc) return rc;
@@ -458,6 +463,7 @@ extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, i
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
     a.dy = dy; a.wt = w; a.out = dx;
     a.dy_cs = dy_cs; a.w_cs = w_cs; a.out_cs = dx_cs;
+    a.accumulate = accumulate;
     a.M = cin; a.N = batch * h * w_; a.K = cout * kh * kw;
     Tile t = pick_mn_tile(a.M, a.N);
     dim3 grid((unsigned)ceil_div(a.N, t.bn), (unsigned)ceil_div(a.M, t.bm), (unsigned)nclients);
@@ -530,7 +536,7 @@ extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, i
                                float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
                                int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
     return fh_conv2d_dgrad(dy, dy_cs, w, w_cs, dx, dx_cs, counts, nclients, batch, in_f, 1, 1,
-                           out_f, 1, 1, 1, 0, stream);
+                           out_f, 1, 1, 1, 0, 0, stream);
 }
 
 extern "C" size_t fh_linear_wgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f,

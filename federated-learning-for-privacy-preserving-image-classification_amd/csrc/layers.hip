@@ -278,7 +278,8 @@ __global__ void __launch_bounds__(256)
 ce_kernel(const float* __restrict__ logits, int64_t l_cs, const int64_t* __restrict__ targets,
           int64_t t_cs, float* __restrict__ dlogits, int64_t d_cs, float* __restrict__ loss_out,
           double* __restrict__ acc_loss, int64_t* __restrict__ acc_correct,
-          int64_t* __restrict__ acc_seen, const int32_t* __restrict__ counts, int batch, int K) {
+          int64_t* __restrict__ acc_seen, const int32_t* __restrict__ reset,
+          const int32_t* __restrict__ counts, int batch, int K) {
     __shared__ double sl[4];
     __shared__ int sc[4];
     const int z = blockIdx.x;
@@ -326,10 +327,11 @@ ce_kernel(const float* __restrict__ logits, int64_t l_cs, const int64_t* __restr
     if (threadIdx.x == 0) {
         const double tot = sl[0] + sl[1] + sl[2] + sl[3];
         const float batch_loss = cnt > 0 ? (float)(tot / (double)cnt) : 0.f;
+        const bool rs = reset && reset[z];
         if (loss_out) loss_out[z] = batch_loss;
-        if (acc_loss) acc_loss[z] += (double)batch_loss;
-        if (acc_correct) acc_correct[z] += sc[0] + sc[1] + sc[2] + sc[3];
-        if (acc_seen) acc_seen[z] += cnt;
+        if (acc_loss) acc_loss[z] = (rs ? 0.0 : acc_loss[z]) + (double)batch_loss;
+        if (acc_correct) acc_correct[z] = (rs ? 0 : acc_correct[z]) + sc[0] + sc[1] + sc[2] + sc[3];
+        if (acc_seen) acc_seen[z] = (rs ? 0 : acc_seen[z]) + cnt;
     }
 }
 
@@ -510,14 +512,14 @@ extern "C" int fh_dropout_bwd(const float* dy, int64_t dy_cs, const uint8_t* mas
 extern "C" int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets,
                              int64_t t_cs, float* dlogits, int64_t d_cs, float* loss_out,
                              double* acc_loss, int64_t* acc_correct, int64_t* acc_seen,
-                             const int32_t* counts, int32_t nclients, int32_t batch,
-                             int32_t num_classes, void* stream) {
+                             const int32_t* reset, const int32_t* counts, int32_t nclients,
+                             int32_t batch, int32_t num_classes, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && num_classes > 0, "ce_fwd_bwd: bad shape");
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(logits && targets && dlogits, "ce_fwd_bwd: null pointer");
     hipLaunchKernelGGL(ce_kernel, dim3(nclients), dim3(256), 0, as_stream(stream), logits, l_cs,
                        targets, t_cs, dlogits, d_cs, loss_out, acc_loss, acc_correct, acc_seen,
-                       counts, batch, num_classes);
+                       reset, counts, batch, num_classes);
     FH_LAUNCH_CHECK("ce_fwd_bwd");
     return FH_OK;
 }

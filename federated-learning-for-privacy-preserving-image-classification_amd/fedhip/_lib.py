@@ -43,7 +43,7 @@ SIGNATURES = {
     "fh_conv2d_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
                             I32, I32, I32, I32, I32, P]),
     "fh_conv2d_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, I32,
-                              I32, I32, I32, P]),
+                              I32, I32, I32, I32, P]),
     "fh_conv2d_wgrad_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "fh_conv2d_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32,
                               I32, I32, I32, I32, I32, I32, P]),
@@ -63,7 +63,7 @@ SIGNATURES = {
                               I32, I32, P]),
     "fh_dropout_fwd": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I64, I32, F32, U64, P]),
     "fh_dropout_bwd": (I32, [P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I64, P]),
-    "fh_ce_fwd_bwd": (I32, [P, I64, P, I64, P, I64, P, P, P, P, P, I32, I32, I32, P]),
+    "fh_ce_fwd_bwd": (I32, [P, I64, P, I64, P, I64, P, P, P, P, P, P, I32, I32, I32, P]),
     "fh_avgpool_fwd": (I32, [P, I64, P, I64, P, I32, I32, I32, I32, P]),
     "fh_avgpool_bwd": (I32, [P, I64, P, I64, P, I32, I32, I32, I32, P]),
     "fh_gather_batch": (I32, [P, P, P, I64, P, I64, P, I64, I64, P, I32, I32, P]),

@@ -1,0 +1,227 @@
+"""PackedTrainer: many FedAvg clients trained as one job on one GPU.
+
+Replaces N independent ``LocalTrainer.train_local_model`` calls
+(src/shared/training.py:60-212 in the reference, one per client thread,
+src/simulation/federated_simulation.py:309-318) with one client-packed
+schedule:
+
+* every client gets a slot; per-client state is a row of the packed
+  parameter / gradient / optimizer / BN-buffer matrices;
+* a round = ``epochs`` passes over each client's shard in batches of 32
+  (DataLoader(shuffle=True), last batch partial).  Client k performs
+  T_k = epochs * ceil(n_k / B) optimizer steps back to back, exactly as its
+  own LocalTrainer would; slots are ordered by T_k descending so at global
+  step g the active clients are the prefix {k : T_k > g}, and every active
+  client is at its (g+1)-th optimizer step (one Adam bias-correction for all);
+* the optimizer is re-created at the start of each round (training.py:89):
+  momentum / Adam moments restart from zero;
+* metrics match TrainingMetrics (training.py:143-152): loss = mean of the
+  last epoch's batch losses, accuracy = last epoch correct/seen,
+  samples_processed = epochs * n_k.
+
+Device-resident data: all client shards in one [N, C, H, W] tensor; the
+per-round index plan [G, slots, B] (host-made permutations, one per client
+per epoch) drives an on-device gather, so no host->device copy happens inside
+a round.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import ops
+from ._lib import FedHipError, load
+from .net import PackedNet
+
+
+@dataclass
+class ClientMetrics:
+    loss: float
+    accuracy: float
+    epochs_completed: int
+    samples_processed: int
+
+
+class PackedTrainer:
+    def __init__(self, model, capacity, batch=32, device="cuda"):
+        load()  # fail loudly if libfedhip is missing
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise FedHipError("PackedTrainer needs a HIP device; there is no CPU path")
+        self.capacity, self.batch = capacity, batch
+        self.net = PackedNet(model, capacity, batch, self.device)
+        L = self.net.layout
+        self.layout = L
+        dev = self.device
+        self.params = torch.zeros(capacity, L.P, device=dev)
+        self.grads = torch.zeros(capacity, L.P, device=dev)
+        self.state1 = torch.zeros(capacity, L.P, device=dev)
+        self.state2 = torch.zeros(capacity, L.P, device=dev)
+        self.bufs = torch.zeros(capacity, max(L.Q, 1), device=dev)
+        self.num_batches_tracked = [0] * capacity
+        self.acc_loss = torch.zeros(capacity, dtype=torch.float64, device=dev)
+        self.acc_correct = torch.zeros(capacity, dtype=torch.int64, device=dev)
+        self.acc_seen = torch.zeros(capacity, dtype=torch.int64, device=dev)
+        self.loss_out = torch.zeros(capacity, device=dev)
+        self.seg_offsets = torch.tensor(L.seg_offsets(), dtype=torch.int64, device=dev)
+        self.opt_type, self.lr, self.opt_step = "sgd", 0.01, 0
+        self.on_step = None
+        # default BN buffers: running_mean 0, running_var 1
+        for name in L.buf_names:
+            if name.endswith("running_var"):
+                L.bview(self.bufs, name).fill_(1.0)
+
+    # ------------------------------------------------------------ state I/O
+    def load_module_state(self, slot, model):
+        """Copy an nn.Module's parameters + BN running stats into a slot."""
+        with torch.no_grad():
+            sd = dict(model.named_parameters())
+            for n in self.layout.names:
+                self.layout.view(self.params, n)[slot].copy_(sd[n].detach().reshape(-1))
+            bd = dict(model.named_buffers())
+            for n in self.layout.buf_names:
+                self.layout.bview(self.bufs, n)[slot].copy_(bd[n].detach().reshape(-1))
+            nbt = [v for k, v in bd.items() if k.endswith("num_batches_tracked")]
+            if nbt:
+                self.num_batches_tracked[slot] = int(nbt[0].item())
+
+    def store_module_state(self, slot, model):
+        """Copy a slot's parameters + BN running stats back into an nn.Module."""
+        with torch.no_grad():
+            sd = dict(model.named_parameters())
+            for n in self.layout.names:
+                p = sd[n]
+                p.data.copy_(self.layout.view(self.params, n)[slot].reshape(p.shape))
+            bd = dict(model.named_buffers())
+            for n in self.layout.buf_names:
+                b = bd[n]
+                b.copy_(self.layout.bview(self.bufs, n)[slot].reshape(b.shape))
+            for k, v in bd.items():
+                if k.endswith("num_batches_tracked"):
+                    v.fill_(self.num_batches_tracked[slot])
+
+    def set_flat(self, slot_or_slice, flat):
+        self.params[slot_or_slice].copy_(flat)
+
+    def weights_dict(self, slot):
+        """get_model_weights() of one client: clones, named_parameters order."""
+        L = self.layout
+        return {n: L.view(self.params, n)[slot].reshape(s).clone()
+                for n, s in zip(L.names, L.shapes)}
+
+    # ------------------------------------------------------------ optimizer
+    def begin_round(self, optimizer_type="sgd", lr=0.01):
+        t = optimizer_type.lower()
+        if t not in ("sgd", "adam", "adamw"):
+            raise ValueError(f"Unknown optimizer type: {optimizer_type}")
+        self.opt_type, self.lr, self.opt_step = t, float(lr), 0
+        self.state1.zero_()
+        self.state2.zero_()
+
+    def _optimizer_step(self, n):
+        self.opt_step += 1
+        cnt = n * self.layout.P
+        if self.opt_type == "sgd":
+            ops.sgd_step(self.params, self.grads, self.state1, self.lr, 0.9,
+                         first_step=(self.opt_step == 1), n=cnt)
+        else:
+            adamw = self.opt_type == "adamw"
+            ops.adam_step(self.params, self.grads, self.state1, self.state2, self.opt_step, self.lr,
+                          weight_decay=0.01 if adamw else 0.0, decoupled=adamw, n=cnt)
+
+    # ------------------------------------------------------------ one packed step
+    def step(self, n, counts, reset=None):
+        """fwd + CE + bwd + optimizer for slots [0, n) on the batch in net.x / net.y."""
+        net = self.net
+        net.forward(self.params, self.bufs, n, counts, train=True)
+        ops.ce_fwd_bwd(net.logits, net.y, net.dlogits, n, self.batch, net.num_classes,
+                       loss_out=self.loss_out, acc_loss=self.acc_loss,
+                       acc_correct=self.acc_correct, acc_seen=self.acc_seen, reset=reset,
+                       counts=counts)
+        net.backward(self.params, self.grads, n, counts)
+        self._optimizer_step(n)
+        for k in range(n):
+            self.num_batches_tracked[k] += 1
+        if self.on_step is not None:  # test/diagnostic hook (e.g. snapshot pool argmax)
+            self.on_step(self, n)
+
+    def eval_batch(self, n, counts, reset=None):
+        """Eval-mode forward + CE metrics (LocalTrainer._validate_epoch)."""
+        net = self.net
+        net.forward(self.params, self.bufs, n, counts, train=False)
+        ops.ce_fwd_bwd(net.logits, net.y, net.dlogits, n, self.batch, net.num_classes,
+                       loss_out=self.loss_out, acc_loss=self.acc_loss,
+                       acc_correct=self.acc_correct, acc_seen=self.acc_seen, reset=reset,
+                       counts=counts)
+
+    # ------------------------------------------------------------ a local-training round
+    def make_plan(self, shard_sizes, epochs, generator=None):
+        """Host-side schedule for a round.
+
+        shard_sizes[k] = train samples of slot k (slots must be sorted so that
+        ceil(n_k/B) is non-increasing).  Returns (G, counts[G,S], reset[G,S],
+        local_index[G,S,B]) where local_index are positions inside each
+        client's shard (a fresh randperm per client per epoch, as
+        DataLoader(shuffle=True) draws)."""
+        B = self.batch
+        S = len(shard_sizes)
+        steps = [math.ceil(n / B) for n in shard_sizes]
+        if any(steps[i] < steps[i + 1] for i in range(S - 1)):
+            raise FedHipError("slots must be ordered by descending step count")
+        T = [epochs * s for s in steps]
+        G = T[0] if S else 0
+        counts = torch.zeros(G, S, dtype=torch.int32)
+        reset = torch.zeros(G, S, dtype=torch.int32)
+        index = torch.zeros(G, S, B, dtype=torch.int64)
+        for k, n in enumerate(shard_sizes):
+            for e in range(epochs):
+                perm = torch.randperm(n, generator=generator)
+                for s in range(steps[k]):
+                    g = e * steps[k] + s
+                    chunk = perm[s * B:(s + 1) * B]
+                    counts[g, k] = chunk.numel()
+                    reset[g, k] = 1 if s == 0 else 0
+                    index[g, k, :chunk.numel()] = chunk
+        active = [sum(1 for t in T if t > g) for g in range(G)]
+        return dict(G=G, steps=steps, T=T, active=active, counts=counts, reset=reset, index=index)
+
+    def run_round(self, data, labels, shard_offsets, plan, optimizer_type="sgd", lr=0.01,
+                  seed=0):
+        """Train every slot over its shard per `plan`.
+
+        data [N, *in_shape] / labels [N] device tensors hold all shards back
+        to back; slot k's shard starts at shard_offsets[k]."""
+        dev = self.device
+        net = self.net
+        self.begin_round(optimizer_type, lr)
+        S = plan["counts"].shape[1]
+        counts = plan["counts"].to(dev)
+        reset = plan["reset"].to(dev)
+        off = torch.as_tensor(shard_offsets, dtype=torch.int64).view(1, S, 1)
+        gidx = (plan["index"] + off).to(dev)
+        sample_elems = int(math.prod(net.in_shape))
+        for g in range(plan["G"]):
+            n = plan["active"][g]
+            net.seed = (seed * 1000003 + g) & 0x7FFFFFFF
+            ops.gather_batch(data, labels, gidx[g], net.x, net.y, sample_elems, n, self.batch,
+                             counts=counts[g])
+            self.step(n, counts[g], reset=reset[g])
+        return self.collect_metrics(plan, epochs_of(plan))
+
+    def collect_metrics(self, plan, epochs):
+        loss = self.acc_loss.cpu()
+        corr = self.acc_correct.cpu()
+        seen = self.acc_seen.cpu()
+        out = []
+        for k, st in enumerate(plan["steps"]):
+            n_k = int(plan["counts"][:st, k].sum())
+            out.append(ClientMetrics(loss=float(loss[k]) / st,
+                                     accuracy=int(corr[k]) / max(1, int(seen[k])),
+                                     epochs_completed=epochs, samples_processed=epochs * n_k))
+        return out
+
+
+def epochs_of(plan):
+    return plan["T"][0] // plan["steps"][0] if plan["steps"] else 0

@@ -1,0 +1,494 @@
+"""Client-packed forward/backward programs for the reference CNN families.
+
+A ``PackedNet`` is built from a model instance (SimpleCNN, CIFAR10CNN or
+FederatedResNet — src/shared/models_pytorch.py:59-246 in the reference) and
+a capacity (client slots x batch).  It owns every activation / gradient
+buffer for the packed batch, preallocated once, laid out
+[slot][image][channel][h][w] (NCHW per client).  Parameters live in flat
+per-client rows ``params[slot, P]`` in ``named_parameters()`` order — the
+exact key order of ``get_model_weights`` — and BatchNorm running statistics
+in ``bufs[slot, Q]``.  A layer's weight is a strided view of those rows
+(client stride P), which is what every kernel consumes.
+
+Forward/backward are explicit programs (no autograd): each step issues a
+fixed sequence of libfedhip launches on torch's current stream.  Clients that
+have finished their shard are simply not launched: slots are sorted so the
+active ones are the prefix [0, n).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import ops
+from ._lib import FedHipError
+
+F32 = torch.float32
+
+
+@dataclass
+class ParamLayout:
+    names: list
+    shapes: list
+    offsets: list
+    P: int
+    buf_names: list = field(default_factory=list)
+    buf_shapes: list = field(default_factory=list)
+    buf_offsets: list = field(default_factory=list)
+    Q: int = 0
+
+    @classmethod
+    def from_module(cls, model):
+        names, shapes, offs, o = [], [], [], 0
+        for n, p in model.named_parameters():
+            names.append(n)
+            shapes.append(tuple(p.shape))
+            offs.append(o)
+            o += p.numel()
+        bn, bs, bo, q = [], [], [], 0
+        for n, b in model.named_buffers():
+            if n.endswith("running_mean") or n.endswith("running_var"):
+                bn.append(n)
+                bs.append(tuple(b.shape))
+                bo.append(q)
+                q += b.numel()
+        return cls(names, shapes, offs, o, bn, bs, bo, q)
+
+    def index(self, name):
+        return self.names.index(name)
+
+    def view(self, rows, name):
+        """[slots, *shape] strided view of one parameter inside packed rows."""
+        i = self.index(name)
+        n = 1
+        for s in self.shapes[i]:
+            n *= s
+        return rows[:, self.offsets[i]:self.offsets[i] + n]
+
+    def bview(self, rows, name):
+        i = self.buf_names.index(name)
+        n = 1
+        for s in self.buf_shapes[i]:
+            n *= s
+        return rows[:, self.buf_offsets[i]:self.buf_offsets[i] + n]
+
+    def seg_offsets(self):
+        return self.offsets + [self.P]
+
+
+class _Buf:
+    """Allocator for named activation buffers of one PackedNet."""
+
+    def __init__(self, cap, batch, device):
+        self.cap, self.batch, self.device = cap, batch, device
+        self.t = {}
+
+    def __call__(self, name, *shape, dtype=F32):
+        if name not in self.t:
+            self.t[name] = torch.zeros(self.cap, self.batch, *shape, dtype=dtype,
+                                       device=self.device)
+        return self.t[name]
+
+
+def model_family(model):
+    cls = type(model).__name__
+    if cls in ("SimpleCNN", "CIFAR10CNN", "FederatedResNet"):
+        return cls
+    raise FedHipError(f"model {cls} is not on the HIP path (supported: SimpleCNN, CIFAR10CNN, "
+                      "FederatedResNet)")
+
+
+class PackedNet:
+    """Packed-client program for one model architecture."""
+
+    def __init__(self, model, capacity, batch, device):
+        self.family = model_family(model)
+        self.layout = ParamLayout.from_module(model)
+        self.cap, self.batch, self.device = capacity, batch, torch.device(device)
+        self.A = _Buf(capacity, batch, self.device)
+        self.num_classes = model.num_classes
+        self.dropout_p = float(getattr(model, "dropout_rate", 0.0))
+        self.bn_eps, self.bn_momentum = 1e-5, 0.1
+        self.in_shape = {"SimpleCNN": (1, 28, 28)}.get(self.family, None)
+        if self.family == "FederatedResNet":
+            self.in_shape = (model.conv1.in_channels, 32, 32)
+            self.blocks = self._resnet_blocks(model)
+        elif self.family == "CIFAR10CNN":
+            self.in_shape = (3, 32, 32)
+        C = self.num_classes
+        self.logits = self.A("logits", C)
+        self.dlogits = self.A("dlogits", C)
+        self.x = self.A("x", *self.in_shape)
+        self.y = self.A("y", dtype=torch.int64)
+        # dropout: per-layer keep masks; mask_mode 1 = generate (Philox), 2 = injected
+        self.mask_mode = 1
+        self.seed = 0
+
+    # -------------------------------------------------------------- helpers
+    def W(self, rows, name):
+        return self.layout.view(rows, name)
+
+    def _resnet_blocks(self, model):
+        blocks = []
+        h = 32
+        for li, layer in enumerate((model.layer1, model.layer2, model.layer3), 1):
+            for bi, blk in enumerate(layer):
+                cin, cout = blk.conv1.in_channels, blk.conv1.out_channels
+                s = blk.conv1.stride[0]
+                blocks.append(dict(pfx=f"layer{li}.{bi}", cin=cin, cout=cout, stride=s, hin=h,
+                                   hout=h // s, proj=len(blk.shortcut) > 0))
+                h //= s
+        return blocks
+
+    def _seed(self, layer_id):
+        return (self.seed * 1000003 + layer_id * 7919) & 0xFFFFFFFFFFFFFFFF
+
+    def _drop_mode(self, train):
+        if not train or self.dropout_p == 0.0:
+            return 0
+        return self.mask_mode
+
+    # -------------------------------------------------------------- forward
+    def forward(self, params, bufs, n, counts, train=True):
+        if n == 0:
+            return self.logits
+        fam = self.family
+        if fam == "SimpleCNN":
+            self._fwd_simple(params, n, counts, train)
+        elif fam == "CIFAR10CNN":
+            self._fwd_cifar(params, bufs, n, counts, train)
+        else:
+            self._fwd_resnet(params, bufs, n, counts, train)
+        return self.logits
+
+    def backward(self, params, grads, n, counts):
+        if n == 0:
+            return
+        fam = self.family
+        if fam == "SimpleCNN":
+            self._bwd_simple(params, grads, n, counts)
+        elif fam == "CIFAR10CNN":
+            self._bwd_cifar(params, grads, n, counts)
+        else:
+            self._bwd_resnet(params, grads, n, counts)
+
+    # ---------------- SimpleCNN (models_pytorch.py:82-97)
+    def _fwd_simple(self, P_, n, cnt, train):
+        A, B, W = self.A, self.batch, self.W
+        a1, p1 = A("a1", 32, 28, 28), A("p1", 32, 14, 14)
+        a2, p2 = A("a2", 64, 14, 14), A("p2", 64, 7, 7)
+        i1, i2 = A("i1", 32, 14, 14, dtype=torch.uint8), A("i2", 64, 7, 7, dtype=torch.uint8)
+        h1, d1 = A("h1", 128), A("d1", 128)
+        m1 = A("m1", 128, dtype=torch.uint8)
+        ops.conv2d_fwd(self.x, W(P_, "conv1.weight"), W(P_, "conv1.bias"), a1, n, B, 1, 28, 28,
+                       32, 3, 1, 1, relu=True, counts=cnt)
+        ops.maxpool2_fwd(a1, p1, i1, n, B, 32, 28, 28, counts=cnt)
+        ops.conv2d_fwd(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, n, B, 32, 14, 14, 64,
+                       3, 1, 1, relu=True, counts=cnt)
+        ops.maxpool2_fwd(a2, p2, i2, n, B, 64, 14, 14, counts=cnt)
+        ops.linear_fwd(p2, W(P_, "fc1.weight"), W(P_, "fc1.bias"), h1, n, B, 3136, 128, relu=True,
+                       counts=cnt)
+        dm = self._drop_mode(train)
+        x3 = h1
+        if dm:
+            ops.dropout_fwd(h1, d1, m1, n, B, 128, self.dropout_p, dm, self._seed(1), counts=cnt)
+            x3 = d1
+        self._fc_in = x3
+        ops.linear_fwd(x3, W(P_, "fc2.weight"), W(P_, "fc2.bias"), self.logits, n, B, 128,
+                       self.num_classes, counts=cnt)
+
+    def _bwd_simple(self, P_, G, n, cnt):
+        A, B, W = self.A, self.batch, self.W
+        K = self.num_classes
+        ops.linear_wgrad(self._fc_in, self.dlogits, W(G, "fc2.weight"), W(G, "fc2.bias"), n, B,
+                         128, K, counts=cnt)
+        dd1 = A("dd1", 128)
+        ops.linear_dgrad(self.dlogits, W(P_, "fc2.weight"), dd1, n, B, 128, K, counts=cnt)
+        dh1 = A("dh1", 128)
+        mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
+        ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
+                        relu_out=A("h1", 128), counts=cnt)
+        ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136,
+                         128, counts=cnt)
+        dp2 = A("dp2", 64, 7, 7)
+        ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
+        da2 = A("da2", 64, 14, 14)
+        ops.maxpool2_bwd(dp2, A("i2", 64, 7, 7, dtype=torch.uint8), da2, n, B, 64, 14, 14,
+                         xin=A("a2", 64, 14, 14), counts=cnt)
+        ops.conv2d_wgrad(A("p1", 32, 14, 14), da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B,
+                         32, 14, 14, 64, 3, 1, 1, counts=cnt)
+        dp1 = A("dp1", 32, 14, 14)
+        ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, 14, 14, 64, 3, 1, 1,
+                         counts=cnt)
+        da1 = A("da1", 32, 28, 28)
+        ops.maxpool2_bwd(dp1, A("i1", 32, 14, 14, dtype=torch.uint8), da1, n, B, 32, 28, 28,
+                         xin=A("a1", 32, 28, 28), counts=cnt)
+        ops.conv2d_wgrad(self.x, da1, W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 1, 28, 28, 32,
+                         3, 1, 1, counts=cnt)
+
+    # ---------------- CIFAR10CNN (models_pytorch.py:136-165)
+    _CIFAR_CONVS = [  # name, cin, cout, hw, bn
+        ("conv1", 3, 32, 32, "bn1"), ("conv2", 32, 32, 32, "bn2"),
+        ("conv3", 32, 64, 16, "bn3"), ("conv4", 64, 64, 16, "bn4"),
+        ("conv5", 64, 128, 8, "bn5"), ("conv6", 128, 128, 8, "bn6")]
+
+    def _bn_train(self, P_, bufs, name, x, y, n, C, HW, cnt, relu, res=None, train=True):
+        A = self.A
+        sm, si = self._bn_save(name, C)
+        gamma, beta = self.W(P_, f"{name}.weight"), self.W(P_, f"{name}.bias")
+        rm = self.layout.bview(bufs, f"{name}.running_mean")
+        rv = self.layout.bview(bufs, f"{name}.running_var")
+        if train:
+            ops.bn_fwd_train(x, y, gamma, beta, rm, rv, sm, si, n, self.batch, C, HW,
+                             self.bn_eps, self.bn_momentum, relu=relu, res=res, counts=cnt)
+        else:
+            ops.bn_fwd_eval(x, y, gamma, beta, rm, rv, n, self.batch, C, HW, self.bn_eps,
+                            relu=relu, res=res, counts=cnt)
+        del A
+
+    def _bn_save(self, name, C):
+        key = f"{name}.save"
+        if key not in self.A.t:
+            self.A.t[key] = (torch.zeros(self.cap, C, device=self.device),
+                             torch.zeros(self.cap, C, device=self.device))
+        return self.A.t[key]
+
+    def _fwd_cifar(self, P_, bufs, n, cnt, train):
+        A, B, W = self.A, self.batch, self.W
+        dm = self._drop_mode(train)
+        xin = self.x
+        for i, (cv, ci, co, hw, bn) in enumerate(self._CIFAR_CONVS):
+            c = A(f"c_{cv}", co, hw, hw)
+            r = A(f"r_{cv}", co, hw, hw)
+            ops.conv2d_fwd(xin, W(P_, f"{cv}.weight"), W(P_, f"{cv}.bias"), c, n, B, ci, hw, hw, co,
+                           3, 1, 1, counts=cnt)
+            self._bn_train(P_, bufs, bn, c, r, n, co, hw * hw, cnt, relu=True, train=train)
+            xin = r
+            if i % 2 == 1:
+                q = A(f"q_{cv}", co, hw // 2, hw // 2)
+                idx = A(f"i_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8)
+                msk = A(f"m_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8) if dm else None
+                ops.maxpool2_fwd(r, q, idx, n, B, co, hw, hw, mask=msk, drop_mode=dm,
+                                 p_drop=self.dropout_p, seed=self._seed(10 + i), counts=cnt)
+                xin = q
+        # classifier: fc1 -> relu -> drop -> fc2 -> relu -> drop -> fc3
+        h1, h2 = A("h1", 512), A("h2", 256)
+        ops.linear_fwd(xin, W(P_, "fc1.weight"), W(P_, "fc1.bias"), h1, n, B, 2048, 512, relu=True,
+                       counts=cnt)
+        e1 = h1
+        if dm:
+            e1 = A("e1", 512)
+            ops.dropout_fwd(h1, e1, A("m_fc1", 512, dtype=torch.uint8), n, B, 512, self.dropout_p,
+                            dm, self._seed(21), counts=cnt)
+        ops.linear_fwd(e1, W(P_, "fc2.weight"), W(P_, "fc2.bias"), h2, n, B, 512, 256, relu=True,
+                       counts=cnt)
+        e2 = h2
+        if dm:
+            e2 = A("e2", 256)
+            ops.dropout_fwd(h2, e2, A("m_fc2", 256, dtype=torch.uint8), n, B, 256, self.dropout_p,
+                            dm, self._seed(22), counts=cnt)
+        self._e1, self._e2, self._dm = e1, e2, dm
+        ops.linear_fwd(e2, W(P_, "fc3.weight"), W(P_, "fc3.bias"), self.logits, n, B, 256,
+                       self.num_classes, counts=cnt)
+
+    def _bwd_cifar(self, P_, G, n, cnt):
+        A, B, W = self.A, self.batch, self.W
+        K, dm, p = self.num_classes, self._dm, self.dropout_p
+        ops.linear_wgrad(self._e2, self.dlogits, W(G, "fc3.weight"), W(G, "fc3.bias"), n, B, 256, K,
+                         counts=cnt)
+        de2 = A("de2", 256)
+        ops.linear_dgrad(self.dlogits, W(P_, "fc3.weight"), de2, n, B, 256, K, counts=cnt)
+        dh2 = A("dh2", 256)
+        ops.dropout_bwd(de2, dh2, n, B, 256, mask=A("m_fc2", 256, dtype=torch.uint8) if dm else None,
+                        p_drop=p, relu_out=A("h2", 256), counts=cnt)
+        ops.linear_wgrad(self._e1, dh2, W(G, "fc2.weight"), W(G, "fc2.bias"), n, B, 512, 256,
+                         counts=cnt)
+        de1 = A("de1", 512)
+        ops.linear_dgrad(dh2, W(P_, "fc2.weight"), de1, n, B, 512, 256, counts=cnt)
+        dh1 = A("dh1", 512)
+        ops.dropout_bwd(de1, dh1, n, B, 512, mask=A("m_fc1", 512, dtype=torch.uint8) if dm else None,
+                        p_drop=p, relu_out=A("h1", 512), counts=cnt)
+        q3 = A("q_conv6", 128, 4, 4)
+        ops.linear_wgrad(q3, dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 2048, 512, counts=cnt)
+        dq = A("dq_conv6", 128, 4, 4)
+        ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dq, n, B, 2048, 512, counts=cnt)
+        convs = self._CIFAR_CONVS
+        for i in range(len(convs) - 1, -1, -1):
+            cv, ci, co, hw, bn = convs[i]
+            r = A(f"r_{cv}", co, hw, hw)
+            dr = A(f"dr_{cv}", co, hw, hw)
+            if i % 2 == 1:
+                ops.maxpool2_bwd(dq, A(f"i_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8), dr, n, B,
+                                 co, hw, hw,
+                                 mask=A(f"m_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8) if dm else None,
+                                 p_drop=p, counts=cnt)
+            # else: dr was written by the next conv's dgrad
+            dc = A(f"dc_{cv}", co, hw, hw)
+            sm, si = self._bn_save(bn, co)
+            ops.bn_bwd(dr, r, A(f"c_{cv}", co, hw, hw), W(P_, f"{bn}.weight"), sm, si, dc,
+                       W(G, f"{bn}.weight"), W(G, f"{bn}.bias"), n, B, co, hw * hw, relu=True,
+                       counts=cnt)
+            if i == 0:
+                xin = self.x
+            elif i % 2 == 0:
+                pcv = convs[i - 1][0]
+                xin = A(f"q_{pcv}", ci, hw, hw)
+            else:
+                xin = A(f"r_{convs[i - 1][0]}", ci, hw, hw)
+            ops.conv2d_wgrad(xin, dc, W(G, f"{cv}.weight"), W(G, f"{cv}.bias"), n, B, ci, hw, hw,
+                             co, 3, 1, 1, counts=cnt)
+            if i == 0:
+                break
+            pcv = convs[i - 1][0]
+            if i % 2 == 0:  # input came from a pool: gradient goes to the pool output grad
+                dq = A(f"dq_{pcv}", ci, hw, hw)
+                ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), dq, n, B, ci, hw, hw, co, 3, 1, 1,
+                                 counts=cnt)
+            else:
+                ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), A(f"dr_{pcv}", ci, hw, hw), n, B, ci,
+                                 hw, hw, co, 3, 1, 1, counts=cnt)
+
+    # ---------------- FederatedResNet (models_pytorch.py:230-246, block :189-194)
+    def _fwd_resnet(self, P_, bufs, n, cnt, train):
+        A, B, W = self.A, self.batch, self.W
+        cin0 = self.in_shape[0]
+        c0, r0 = A("c_stem", 64, 32, 32), A("r_stem", 64, 32, 32)
+        ops.conv2d_fwd(self.x, W(P_, "conv1.weight"), None, c0, n, B, cin0, 32, 32, 64, 3, 1, 1,
+                       counts=cnt)
+        self._bn_train(P_, bufs, "bn1", c0, r0, n, 64, 1024, cnt, relu=True, train=train)
+        xin = r0
+        for b in self.blocks:
+            pf, ci, co, s, hi, ho = b["pfx"], b["cin"], b["cout"], b["stride"], b["hin"], b["hout"]
+            a, ar = A(f"{pf}.a", co, ho, ho), A(f"{pf}.ar", co, ho, ho)
+            bb, out = A(f"{pf}.b", co, ho, ho), A(f"{pf}.out", co, ho, ho)
+            ops.conv2d_fwd(xin, W(P_, f"{pf}.conv1.weight"), None, a, n, B, ci, hi, hi, co, 3, s, 1,
+                           counts=cnt)
+            self._bn_train(P_, bufs, f"{pf}.bn1", a, ar, n, co, ho * ho, cnt, relu=True, train=train)
+            ops.conv2d_fwd(ar, W(P_, f"{pf}.conv2.weight"), None, bb, n, B, co, ho, ho, co, 3, 1, 1,
+                           counts=cnt)
+            if b["proj"]:
+                sc, scb = A(f"{pf}.sc", co, ho, ho), A(f"{pf}.scb", co, ho, ho)
+                ops.conv2d_fwd(xin, W(P_, f"{pf}.shortcut.0.weight"), None, sc, n, B, ci, hi, hi, co,
+                               1, s, 0, counts=cnt)
+                self._bn_train(P_, bufs, f"{pf}.shortcut.1", sc, scb, n, co, ho * ho, cnt,
+                               relu=False, train=train)
+                res = scb
+            else:
+                res = xin
+            self._bn_train(P_, bufs, f"{pf}.bn2", bb, out, n, co, ho * ho, cnt, relu=True, res=res,
+                           train=train)
+            b["xin"] = xin
+            xin = out
+        f = A("feat", 256)
+        ho = self.blocks[-1]["hout"]
+        ops.avgpool_fwd(xin, f, n, B, 256, ho * ho, counts=cnt)
+        ops.linear_fwd(f, W(P_, "fc.weight"), W(P_, "fc.bias"), self.logits, n, B, 256,
+                       self.num_classes, counts=cnt)
+
+    def _bwd_resnet(self, P_, G, n, cnt):
+        A, B, W = self.A, self.batch, self.W
+        K = self.num_classes
+        f = A("feat", 256)
+        ops.linear_wgrad(f, self.dlogits, W(G, "fc.weight"), W(G, "fc.bias"), n, B, 256, K,
+                         counts=cnt)
+        df = A("dfeat", 256)
+        ops.linear_dgrad(self.dlogits, W(P_, "fc.weight"), df, n, B, 256, K, counts=cnt)
+        last = self.blocks[-1]
+        dout = A(f"{last['pfx']}.dout", last["cout"], last["hout"], last["hout"])
+        ops.avgpool_bwd(df, dout, n, B, 256, last["hout"] ** 2, counts=cnt)
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            b = self.blocks[bi]
+            pf, ci, co, s, hi, ho = b["pfx"], b["cin"], b["cout"], b["stride"], b["hin"], b["hout"]
+            dout = A(f"{pf}.dout", co, ho, ho)
+            # gradient w.r.t. this block's input
+            if bi > 0:
+                pb = self.blocks[bi - 1]
+                din = A(f"{pb['pfx']}.dout", ci, hi, hi)
+            else:
+                din = A("dstem", ci, hi, hi)
+            db = A(f"{pf}.db", co, ho, ho)
+            sm2, si2 = self._bn_save(f"{pf}.bn2", co)
+            if b["proj"]:
+                dres = A(f"{pf}.dres", co, ho, ho)
+            else:
+                dres = din  # identity shortcut: masked grad flows straight to the input grad
+            ops.bn_bwd(dout, A(f"{pf}.out", co, ho, ho), A(f"{pf}.b", co, ho, ho),
+                       W(P_, f"{pf}.bn2.weight"), sm2, si2, db, W(G, f"{pf}.bn2.weight"),
+                       W(G, f"{pf}.bn2.bias"), n, B, co, ho * ho, relu=True, dres=dres, counts=cnt)
+            ar = A(f"{pf}.ar", co, ho, ho)
+            ops.conv2d_wgrad(ar, db, W(G, f"{pf}.conv2.weight"), None, n, B, co, ho, ho, co, 3, 1, 1,
+                             counts=cnt)
+            dar = A(f"{pf}.dar", co, ho, ho)
+            ops.conv2d_dgrad(db, W(P_, f"{pf}.conv2.weight"), dar, n, B, co, ho, ho, co, 3, 1, 1,
+                             counts=cnt)
+            da = A(f"{pf}.da", co, ho, ho)
+            sm1, si1 = self._bn_save(f"{pf}.bn1", co)
+            ops.bn_bwd(dar, ar, A(f"{pf}.a", co, ho, ho), W(P_, f"{pf}.bn1.weight"), sm1, si1, da,
+                       W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co, ho * ho,
+                       relu=True, counts=cnt)
+            xin = b["xin"]
+            ops.conv2d_wgrad(xin, da, W(G, f"{pf}.conv1.weight"), None, n, B, ci, hi, hi, co, 3, s, 1,
+                             counts=cnt)
+            if b["proj"]:
+                dsc = A(f"{pf}.dsc", co, ho, ho)
+                sms, sis = self._bn_save(f"{pf}.shortcut.1", co)
+                ops.bn_bwd(dres, None, A(f"{pf}.sc", co, ho, ho), W(P_, f"{pf}.shortcut.1.weight"),
+                           sms, sis, dsc, W(G, f"{pf}.shortcut.1.weight"),
+                           W(G, f"{pf}.shortcut.1.bias"), n, B, co, ho * ho, relu=False, counts=cnt)
+                ops.conv2d_wgrad(xin, dsc, W(G, f"{pf}.shortcut.0.weight"), None, n, B, ci, hi, hi,
+                                 co, 1, s, 0, counts=cnt)
+                ops.conv2d_dgrad(dsc, W(P_, f"{pf}.shortcut.0.weight"), din, n, B, ci, hi, hi, co,
+                                 1, s, 0, counts=cnt)
+            ops.conv2d_dgrad(da, W(P_, f"{pf}.conv1.weight"), din, n, B, ci, hi, hi, co, 3, s, 1,
+                             counts=cnt, accumulate=True)
+        # stem: bn1 (relu) then conv1 weight grad
+        dstem = A("dstem", 64, 32, 32)
+        dc0 = A("dc_stem", 64, 32, 32)
+        sm, si = self._bn_save("bn1", 64)
+        ops.bn_bwd(dstem, A("r_stem", 64, 32, 32), A("c_stem", 64, 32, 32), W(P_, "bn1.weight"), sm,
+                   si, dc0, W(G, "bn1.weight"), W(G, "bn1.bias"), n, B, 64, 1024, relu=True,
+                   counts=cnt)
+        ops.conv2d_wgrad(self.x, dc0, W(G, "conv1.weight"), None, n, B, self.in_shape[0], 32, 32, 64,
+                         3, 1, 1, counts=cnt)
+
+    # -------------------------------------------------------------- decision buffers
+    def pool_index_buffers(self):
+        """(idx buffer, H, W) of every max-pool in forward order (uint8 window codes)."""
+        A = self.A
+        if self.family == "SimpleCNN":
+            return [(A("i1", 32, 14, 14, dtype=torch.uint8), 28, 28),
+                    (A("i2", 64, 7, 7, dtype=torch.uint8), 14, 14)]
+        if self.family == "CIFAR10CNN":
+            return [(A(f"i_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8), hw, hw)
+                    for i, (cv, ci, co, hw, bn) in enumerate(self._CIFAR_CONVS) if i % 2 == 1]
+        return []
+
+    def relu_output_buffers(self):
+        """Post-ReLU activations in forward order (their > 0 pattern is the ReLU mask)."""
+        A = self.A
+        if self.family == "SimpleCNN":
+            return [A("a1", 32, 28, 28), A("a2", 64, 14, 14), A("h1", 128)]
+        if self.family == "CIFAR10CNN":
+            return [A(f"r_{cv}", co, hw, hw) for cv, ci, co, hw, bn in self._CIFAR_CONVS] + \
+                [A("h1", 512), A("h2", 256)]
+        out = [A("r_stem", 64, 32, 32)]
+        for b in self.blocks:
+            pf, co, ho = b["pfx"], b["cout"], b["hout"]
+            out += [A(f"{pf}.ar", co, ho, ho), A(f"{pf}.out", co, ho, ho)]
+        return out
+
+    def mask_buffers(self):
+        """Dropout keep-mask buffers in forward order (for parity-mode injection)."""
+        A = self.A
+        if self.family == "SimpleCNN":
+            return [A("m1", 128, dtype=torch.uint8)]
+        if self.family == "CIFAR10CNN":
+            out = []
+            for i, (cv, ci, co, hw, bn) in enumerate(self._CIFAR_CONVS):
+                if i % 2 == 1:
+                    out.append(A(f"m_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8))
+            out.append(A("m_fc1", 512, dtype=torch.uint8))
+            out.append(A("m_fc2", 256, dtype=torch.uint8))
+            return out
+        return []

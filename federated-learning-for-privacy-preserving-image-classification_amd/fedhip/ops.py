@@ -64,9 +64,10 @@ def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad,
     return y
 
 
-def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None):
+def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
+                 accumulate=False):
     call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
-         nclients, batch, cin, h, wd, cout, k, k, stride, pad, stream_handle())
+         nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(accumulate), stream_handle())
     return dx
 
 
@@ -225,9 +226,9 @@ def dropout_bwd(dy, dx, nclients, batch, per_img, mask=None, p_drop=0.0, relu_ou
 
 
 def ce_fwd_bwd(logits, targets, dlogits, nclients, batch, num_classes, loss_out=None,
-               acc_loss=None, acc_correct=None, acc_seen=None, counts=None):
+               acc_loss=None, acc_correct=None, acc_seen=None, reset=None, counts=None):
     call("fh_ce_fwd_bwd", ptr(logits), _cs(logits), ptr(targets), _cs(targets), ptr(dlogits),
-         _cs(dlogits), ptr(loss_out), ptr(acc_loss), ptr(acc_correct), ptr(acc_seen),
+         _cs(dlogits), ptr(loss_out), ptr(acc_loss), ptr(acc_correct), ptr(acc_seen), ptr(reset),
          _counts(counts), nclients, batch, num_classes, stream_handle())
 
 

@@ -106,10 +106,11 @@ int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs, co
                   int64_t b_cs, float* y, int64_t y_cs, const int32_t* counts, int32_t nclients,
                   int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh,
                   int32_t kw, int32_t stride, int32_t pad, int32_t relu, void* stream);
+/* accumulate = 1: dx += result (residual-branch gradient sums, ResNet shortcut). */
 int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs, float* dx,
                     int64_t dx_cs, const int32_t* counts, int32_t nclients, int32_t batch,
                     int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
-                    int32_t stride, int32_t pad, void* stream);
+                    int32_t stride, int32_t pad, int32_t accumulate, void* stream);
 /* dw (and db if non-NULL) are overwritten. workspace >= fh_conv2d_wgrad_workspace(...) bytes. */
 size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
                                  int32_t w_, int32_t cout, int32_t kh, int32_t kw, int32_t stride,
@@ -184,11 +185,13 @@ int fh_dropout_bwd(const float* dy, int64_t dy_cs, const uint8_t* mask, int64_t 
 /* ---------------- CrossEntropyLoss (mean) fwd+bwd + epoch metrics ---------
  * targets int64 [clients][batch]; dlogits = (softmax - onehot)/count;
  * loss_out[z] = batch mean loss; acc_* (nullable) accumulate the epoch's
- * sum of batch losses, correct argmax predictions and samples seen. */
+ * sum of batch losses, correct argmax predictions and samples seen;
+ * reset[z] != 0 (nullable) restarts client z's accumulators (epoch boundary). */
 int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets, int64_t t_cs,
                   float* dlogits, int64_t d_cs, float* loss_out, double* acc_loss,
-                  int64_t* acc_correct, int64_t* acc_seen, const int32_t* counts,
-                  int32_t nclients, int32_t batch, int32_t num_classes, void* stream);
+                  int64_t* acc_correct, int64_t* acc_seen, const int32_t* reset,
+                  const int32_t* counts, int32_t nclients, int32_t batch, int32_t num_classes,
+                  void* stream);
 
 /* ---------------- AdaptiveAvgPool2d((1,1)) --------------------------------- */
 int fh_avgpool_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, const int32_t* counts,

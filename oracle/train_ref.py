@@ -23,13 +23,29 @@ import torch.nn.functional as F
 
 
 class _Dropout:
-    """F.dropout in train mode, optionally recording / replaying the keep-mask."""
+    """Per-step context: F.dropout in train mode (optionally recording / replaying
+    the keep-mask) and 2x2 max-pooling (optionally replaying given argmax
+    indices — used by the fp64 "same decisions" oracle of the GPU tests)."""
 
-    def __init__(self, p, masks=None, capture=False):
+    def __init__(self, p, masks=None, capture=False, pools=None, relus=None):
         self.p = p
         self.masks = list(masks) if masks is not None else None
         self.capture = capture
         self.captured = []
+        self.pools = list(pools) if pools is not None else None
+        self.relus = list(relus) if relus is not None else None
+
+    def relu(self, x):
+        if self.relus is None:
+            return F.relu(x)
+        return x * self.relus.pop(0).to(x.dtype)
+
+    def pool(self, x):
+        if self.pools is None:
+            return F.max_pool2d(x, 2, 2)
+        idx = self.pools.pop(0)
+        n, c, h, w = x.shape
+        return x.flatten(2).gather(2, idx.flatten(2)).view(n, c, h // 2, w // 2)
 
     def __call__(self, x, training=True):
         if not training or self.p == 0.0:
@@ -61,10 +77,10 @@ class SimpleCNN(nn.Module):
 
     def forward(self, x, drop=None):
         drop = drop or _Dropout(self.dropout_rate)
-        x = self.pool(F.relu(self.conv1(x)))
-        x = self.pool(F.relu(self.conv2(x)))
+        x = drop.pool(drop.relu(self.conv1(x)))
+        x = drop.pool(drop.relu(self.conv2(x)))
         x = x.view(-1, 64 * 7 * 7)
-        x = F.relu(self.fc1(x))
+        x = drop.relu(self.fc1(x))
         x = drop(x, self.training)
         return self.fc2(x)
 
@@ -96,18 +112,18 @@ class CIFAR10CNN(nn.Module):
     def forward(self, x, drop=None):
         drop = drop or _Dropout(self.dropout_rate)
         t = self.training
-        x = F.relu(self.bn1(self.conv1(x)))
-        x = F.relu(self.bn2(self.conv2(x)))
-        x = drop(self.pool(x), t)
-        x = F.relu(self.bn3(self.conv3(x)))
-        x = F.relu(self.bn4(self.conv4(x)))
-        x = drop(self.pool(x), t)
-        x = F.relu(self.bn5(self.conv5(x)))
-        x = F.relu(self.bn6(self.conv6(x)))
-        x = drop(self.pool(x), t)
+        x = drop.relu(self.bn1(self.conv1(x)))
+        x = drop.relu(self.bn2(self.conv2(x)))
+        x = drop(drop.pool(x), t)
+        x = drop.relu(self.bn3(self.conv3(x)))
+        x = drop.relu(self.bn4(self.conv4(x)))
+        x = drop(drop.pool(x), t)
+        x = drop.relu(self.bn5(self.conv5(x)))
+        x = drop.relu(self.bn6(self.conv6(x)))
+        x = drop(drop.pool(x), t)
         x = x.view(-1, 128 * 4 * 4)
-        x = drop(F.relu(self.fc1(x)), t)
-        x = drop(F.relu(self.fc2(x)), t)
+        x = drop(drop.relu(self.fc1(x)), t)
+        x = drop(drop.relu(self.fc2(x)), t)
         return self.fc3(x)
 
 
@@ -125,11 +141,12 @@ class ResNetBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
                                           nn.BatchNorm2d(cout))
 
-    def forward(self, x):
-        out = F.relu(self.bn1(self.conv1(x)))
+    def forward(self, x, drop=None):
+        drop = drop or _Dropout(0.0)
+        out = drop.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         out = out + self.shortcut(x)
-        return F.relu(out)
+        return drop.relu(out)
 
 
 class FederatedResNet(nn.Module):
@@ -154,7 +171,7 @@ class FederatedResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x, drop=None):
-        x = F.relu(self.bn1(self.conv1(x)))
+        x = drop.relu(self.bn1(self.conv1(x)))
         x = self.layer3(self.layer2(self.layer1(x)))
         x = self.avg_pool(x).view(x.size(0), -1)
         return self.fc(x)
@@ -181,10 +198,14 @@ def make_optimizer(model, optimizer_type, lr):
     raise ValueError(f"Unknown optimizer type: {optimizer_type}")
 
 
-def train_step(model, opt, data, targets, masks=None, capture_masks=False):
-    """One iteration of training.py:184-203. Returns (loss_item, n_correct, logits, drop)."""
+def train_step(model, opt, data, targets, masks=None, capture_masks=False, pools=None,
+               relus=None):
+    """One iteration of training.py:184-203. Returns (loss_item, n_correct, logits, drop).
+    pools / relus: replay another implementation's discrete decisions (max-pool argmax,
+    ReLU masks) — used only by the fp64 "same decisions" checks of the GPU tests."""
     model.train()
-    drop = _Dropout(getattr(model, "dropout_rate", 0.0), masks=masks, capture=capture_masks)
+    drop = _Dropout(getattr(model, "dropout_rate", 0.0), masks=masks, capture=capture_masks,
+                    pools=pools, relus=relus)
     opt.zero_grad()
     out = model(data, drop)
     loss = F.cross_entropy(out, targets)
@@ -194,7 +215,7 @@ def train_step(model, opt, data, targets, masks=None, capture_masks=False):
     return loss.item(), int((pred == targets).sum().item()), out.detach(), drop
 
 
-def train_epochs(model, batches, epochs, lr, optimizer_type, masks=None):
+def train_epochs(model, batches, epochs, lr, optimizer_type, masks=None, pools=None, relus=None):
     """train_local_model (training.py:60-171) minus validation/checkpoints.
 
     batches: list of (data, targets) for one epoch, replayed each epoch.
@@ -202,6 +223,8 @@ def train_epochs(model, batches, epochs, lr, optimizer_type, masks=None):
     opt = make_optimizer(model, optimizer_type, lr)
     total = 0
     mi = iter(masks) if masks is not None else None
+    pi = iter(pools) if pools is not None else None
+    ri = iter(relus) if relus is not None else None
     loss, acc = 0.0, 0.0
     for _ in range(epochs):
         # iter(DataLoader) draws the worker base seed from the default generator
@@ -211,7 +234,9 @@ def train_epochs(model, batches, epochs, lr, optimizer_type, masks=None):
         running, correct, seen = 0.0, 0, 0
         for data, targets in batches:
             m = next(mi) if mi is not None else None
-            li, c, _, _ = train_step(model, opt, data, targets, masks=m)
+            pl = next(pi) if pi is not None else None
+            rl = next(ri) if ri is not None else None
+            li, c, _, _ = train_step(model, opt, data, targets, masks=m, pools=pl, relus=rl)
             running += li
             correct += c
             seen += targets.size(0)
