@@ -1,0 +1,230 @@
+"""Benchmark: client-images/sec/node of the federated hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config KT]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One "step" = one federated round over synthetic CIFAR/MNIST-shaped data
+resident in HBM: every client trains its shard for the configured local
+epochs (packed, all clients of a rank in one job), update-level DP when the
+config has it, then FedAvg (RCCL all-reduce across ranks).  value =
+sum over ranks of samples_processed / max-over-ranks wall time of the K timed
+rounds.  Weak scaling: each GPU hosts the config's clients-per-GPU.
+
+Also reported (one JSON line):
+  roofline      the dominant conv kernel, timed live with HIP events on its
+                launch stream during the timed rounds: algorithmic FLOPs per
+                launch / average launch duration vs the fp32 MFMA peak;
+  cpu_baseline  rank 0 at N=1 only: the reference algorithm (oracle/ — a
+                CPU restatement pinned bit-exact to the reference LocalTrainer)
+                timed on the host cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "federated-learning-for-privacy-preserving-image-classification_amd")
+sys.path[:0] = [REPO, PKG]
+
+from fedhip import ops  # noqa: E402
+from fedhip.partition import lpt_assign, partition, train_split_sizes  # noqa: E402
+from fedhip.round import DPConfig, RankRound  # noqa: E402
+from src.shared import models_pytorch as hm  # noqa: E402
+
+# BASELINE.json configs; KT = north_star target (CIFAR10CNN, 32 clients, 1 GPU).
+CONFIGS = {
+    "KT": dict(model="cifar10_cnn", kw={}, shape=(3, 32, 32), classes=10, clients=32,
+               samples=50000, strategy="non_iid", alpha=0.5, epochs=1, dp=None),
+    "K1": dict(model="simple_cnn", kw={}, shape=(1, 28, 28), classes=10, clients=4,
+               samples=60000, strategy="iid", alpha=0.5, epochs=1, dp=None),
+    "K2": dict(model="simple_cnn", kw={}, shape=(1, 28, 28), classes=10, clients=32,
+               samples=60000, strategy="non_iid", alpha=0.5, epochs=1, dp=1.0),
+    "K3": dict(model="federated_resnet", kw={"num_blocks": [1, 1, 1]}, shape=(3, 32, 32),
+               classes=10, clients=64, samples=50000, strategy="non_iid", alpha=0.5, epochs=1,
+               dp=4.0),
+    "K4": dict(model="federated_resnet", kw={}, shape=(3, 32, 32), classes=10, clients=128,
+               samples=50000, strategy="non_iid", alpha=0.5, epochs=5, dp=None),
+    "K5": dict(model="federated_resnet", kw={"num_classes": 100}, shape=(3, 32, 32),
+               classes=100, clients=256, samples=50000, strategy="non_iid", alpha=0.1, epochs=1,
+               dp=2.0),
+}
+# train FLOPs / image = 6*MACs - 2*MACs(first layer)
+TRAIN_FLOPS = {"simple_cnn": 24_995_328, "cifar10_cnn": 237_124_608,
+               "federated_resnet[1,1,1]": 1_164_721_152, "federated_resnet[2,2,2]": 2_523_675_648}
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def log(msg):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(msg, file=sys.stderr, flush=True)
+
+
+def setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def build_clients(cfg, world, seed=0):
+    """Weak scaling: clients-per-GPU fixed; the synthetic dataset scales with N."""
+    C = cfg["clients"] * world
+    N = cfg["samples"] * world
+    labels = np.random.default_rng(seed).integers(0, cfg["classes"], size=N)
+    import random
+    random.seed(seed)
+    np.random.seed(seed)
+    parts = partition(labels, C, cfg["strategy"], cfg["alpha"])
+    shard = [len(parts.get(c, [])) for c in range(C)]
+    train = train_split_sizes(shard, 0.1)
+    return labels, train
+
+
+def make_rank_data(cfg, train_sizes, my_slots, device, seed):
+    """Synthetic N(0,1) inputs for this rank's clients, laid out slot after slot."""
+    total = sum(train_sizes[k] for k in my_slots)
+    g = torch.Generator(device=device).manual_seed(1000 + seed)
+    data = torch.randn(total, *cfg["shape"], generator=g, device=device)
+    labels = torch.randint(0, cfg["classes"], (total,), generator=g, device=device)
+    offs = np.cumsum([0] + [train_sizes[k] for k in my_slots][:-1]).tolist()
+    return data, labels, offs
+
+
+def flops_key(cfg):
+    if cfg["model"] == "federated_resnet":
+        nb = cfg["kw"].get("num_blocks", [2, 2, 2])
+        return f"federated_resnet[{','.join(map(str, nb))}]"
+    return cfg["model"]
+
+
+def cpu_baseline(cfg, seconds=12.0):
+    """Reference algorithm (oracle restatement, bit-exact with the reference LocalTrainer)
+    on host cores: one client's local SGD steps at batch 32 for ~`seconds`."""
+    from oracle import train_ref
+    threads = torch.get_num_threads()
+    model = train_ref.make_model(cfg["model"], 0, **cfg["kw"])
+    opt = train_ref.make_optimizer(model, "sgd", 0.01)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(32, *cfg["shape"], generator=g)
+    y = torch.randint(0, cfg["classes"], (32,), generator=g)
+    train_ref.train_step(model, opt, x, y)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        train_ref.train_step(model, opt, x, y)
+        n += 32
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "client-images/s", "cores": threads, "kind": "port",
+            "sample": f"{cfg['model']} local SGD steps, batch 32, {n} images in {dt:.1f}s "
+                      f"(oracle/train_ref.py, torch CPU, {threads} threads)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="KT", choices=sorted(CONFIGS))
+    ap.add_argument("--opt", default="sgd")
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--probe", default=None, help="conv launch tag to time (default: auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    world, rank, dev = setup(args)
+
+    labels, train = build_clients(cfg, world)
+    C = len(train)
+    assign = lpt_assign(train, world)
+    mine = assign[rank]
+    torch.manual_seed(0)
+    template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
+    dp = DPConfig(epsilon=cfg["dp"]) if cfg["dp"] else None
+    rr = RankRound(template, train, mine, epochs=cfg["epochs"], device=dev, dp=dp)
+    data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, rank)
+    my_images = cfg["epochs"] * sum(train[k] for k in mine)
+    total_images = cfg["epochs"] * sum(train)
+
+    # launch probe: dominant conv kernel (the largest-FLOP 3x3 fwd launch of the model)
+    probe_tag = args.probe or {
+        "cifar10_cnn": "conv_dgrad:c32x32x32->32k3s1",
+        "simple_cnn": "conv_dgrad:c32x14x14->64k3s1",
+        "federated_resnet": "conv_dgrad:c64x32x32->64k3s1"}[cfg["model"]]
+    ops.PROBE.tag = probe_tag
+    S = len(rr.slots)
+    rr.trainer.pre_step = lambda g, n, plan: setattr(
+        ops.PROBE, "enabled", bool(timing[0]) and n == S and bool((plan["counts"][g, :n] == 32).all()))
+    timing = [False]
+
+    gen = torch.Generator().manual_seed(7)
+    for w in range(args.warmup):
+        rr.run(data, lab, offs, args.opt, args.lr, seed=w, generator=gen)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timing[0] = True
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        rr.run(data, lab, offs, args.opt, args.lr, seed=100 + s, generator=gen)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timing[0] = False
+    ops.PROBE.enabled = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    probe = ops.PROBE.summary()
+
+    if rank == 0:
+        value = total_images * args.steps / elapsed
+        fl = TRAIN_FLOPS[flops_key(cfg)]
+        roof = None
+        if probe:
+            ach = probe["flops_per_launch"] / (probe["avg_ms"] * 1e-3) / 1e12
+            roof = {"bound": "mfma", "kernel": probe_tag, "achieved": round(ach, 2),
+                    "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                    "launches_timed": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4)}
+        out = {
+            "metric": "client-images/sec/node", "value": round(value, 1),
+            "unit": "client-images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic N(0,1) CIFAR/MNIST-shaped tensors resident in HBM; "
+                    "Dirichlet shard sizes from the reference partitioner restatement",
+            "config": {"workload": f"{args.config}: {cfg['model']} {C} clients "
+                                   f"({cfg['clients']}/GPU), {cfg['strategy']}"
+                                   f"{'(a=' + str(cfg['alpha']) + ')' if cfg['strategy'] == 'non_iid' else ''}, "
+                                   f"{cfg['epochs']} local epoch(s), batch 32, {args.opt} lr {args.lr}, "
+                                   f"DP eps={cfg['dp']}, FedAvg{' RCCL all-reduce' if world > 1 else ''}",
+                       "clients": C, "images_per_round": total_images, "batch": 32,
+                       "parallelism": f"client-packed x{world} GPU"},
+            "achieved_tflops_step": round(value * fl / 1e12, 2),
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

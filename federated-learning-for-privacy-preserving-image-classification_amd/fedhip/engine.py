@@ -68,6 +68,7 @@ class PackedTrainer:
         self.seg_offsets = torch.tensor(L.seg_offsets(), dtype=torch.int64, device=dev)
         self.opt_type, self.lr, self.opt_step = "sgd", 0.01, 0
         self.on_step = None
+        self.pre_step = None
         # default BN buffers: running_mean 0, running_var 1
         for name in L.buf_names:
             if name.endswith("running_var"):
@@ -204,6 +205,8 @@ class PackedTrainer:
         sample_elems = int(math.prod(net.in_shape))
         for g in range(plan["G"]):
             n = plan["active"][g]
+            if self.pre_step is not None:  # bench hook (e.g. arm the launch probe on full steps)
+                self.pre_step(g, n, plan)
             net.seed = (seed * 1000003 + g) & 0x7FFFFFFF
             ops.gather_batch(data, labels, gidx[g], net.x, net.y, sample_elems, n, self.batch,
                              counts=counts[g])

@@ -47,6 +47,51 @@ class Workspace:
 _WS: dict = {}
 
 
+class LaunchProbe:
+    """Times one chosen kernel launch with HIP events on the launch stream.
+
+    bench.py points ``tag`` at the dominant kernel (e.g. "conv_wgrad:c32x32x32->32k3s1");
+    every matching launch while ``enabled`` records (start, end, algorithmic flops)."""
+
+    def __init__(self):
+        self.tag = None
+        self.enabled = False
+        self.records = []
+        self.seen = {}
+
+    def begin(self, tag):
+        if not self.enabled:
+            return None
+        self.seen[tag] = self.seen.get(tag, 0) + 1
+        if tag != self.tag:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, ev, flops):
+        if ev is None:
+            return
+        e2 = torch.cuda.Event(enable_timing=True)
+        e2.record()
+        self.records.append((ev, e2, flops))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        if not self.records:
+            return None
+        ms = [a.elapsed_time(b) for a, b, _ in self.records]
+        fl = [f for _, _, f in self.records]
+        return {"launches": len(ms), "avg_ms": sum(ms) / len(ms), "flops_per_launch": sum(fl) / len(fl)}
+
+
+PROBE = LaunchProbe()
+
+
+def _conv_tag(kind, cin, h, w, cout, k, s):
+    return f"conv_{kind}:c{cin}x{h}x{w}->{cout}k{k}s{s}"
+
+
 def _ws(device) -> Workspace:
     key = str(device)
     if key not in _WS:
@@ -55,19 +100,29 @@ def _ws(device) -> Workspace:
 
 
 # ------------------------------------------------------------------ conv / linear
+def _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad):
+    oh = (h + 2 * pad - k) // stride + 1
+    ow = (wd + 2 * pad - k) // stride + 1
+    return 2.0 * nclients * batch * oh * ow * cout * cin * k * k
+
+
 def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad, relu=False,
                counts=None):
     require_device(x, "x")
+    ev = PROBE.begin(_conv_tag("fwd", cin, h, wd, cout, k, stride))
     call("fh_conv2d_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y),
          _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(relu),
          stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return y
 
 
 def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
                  accumulate=False):
+    ev = PROBE.begin(_conv_tag("dgrad", cin, h, wd, cout, k, stride))
     call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
          nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(accumulate), stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return dx
 
 
@@ -75,9 +130,11 @@ def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pa
     lib = load()
     need = lib.fh_conv2d_wgrad_workspace(nclients, batch, cin, h, wd, cout, k, k, stride, pad)
     ws = _ws(x.device).get(need)
+    ev = PROBE.begin(_conv_tag("wgrad", cin, h, wd, cout, k, stride))
     call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
          ptr(ws), ws.numel(), _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride,
          pad, stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return dw
 
 
