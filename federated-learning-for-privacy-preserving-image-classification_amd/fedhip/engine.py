@@ -159,34 +159,7 @@ class PackedTrainer:
 
     # ------------------------------------------------------------ a local-training round
     def make_plan(self, shard_sizes, epochs, generator=None):
-        """Host-side schedule for a round.
-
-        shard_sizes[k] = train samples of slot k (slots must be sorted so that
-        ceil(n_k/B) is non-increasing).  Returns (G, counts[G,S], reset[G,S],
-        local_index[G,S,B]) where local_index are positions inside each
-        client's shard (a fresh randperm per client per epoch, as
-        DataLoader(shuffle=True) draws)."""
-        B = self.batch
-        S = len(shard_sizes)
-        steps = [math.ceil(n / B) for n in shard_sizes]
-        if any(steps[i] < steps[i + 1] for i in range(S - 1)):
-            raise FedHipError("slots must be ordered by descending step count")
-        T = [epochs * s for s in steps]
-        G = T[0] if S else 0
-        counts = torch.zeros(G, S, dtype=torch.int32)
-        reset = torch.zeros(G, S, dtype=torch.int32)
-        index = torch.zeros(G, S, B, dtype=torch.int64)
-        for k, n in enumerate(shard_sizes):
-            for e in range(epochs):
-                perm = torch.randperm(n, generator=generator)
-                for s in range(steps[k]):
-                    g = e * steps[k] + s
-                    chunk = perm[s * B:(s + 1) * B]
-                    counts[g, k] = chunk.numel()
-                    reset[g, k] = 1 if s == 0 else 0
-                    index[g, k, :chunk.numel()] = chunk
-        active = [sum(1 for t in T if t > g) for g in range(G)]
-        return dict(G=G, steps=steps, T=T, active=active, counts=counts, reset=reset, index=index)
+        return plan_round(shard_sizes, epochs, self.batch, generator)
 
     def run_round(self, data, labels, shard_offsets, plan, optimizer_type="sgd", lr=0.01,
                   seed=0):
@@ -224,6 +197,41 @@ class PackedTrainer:
                                      accuracy=int(corr[k]) / max(1, int(seen[k])),
                                      epochs_completed=epochs, samples_processed=epochs * n_k))
         return out
+
+
+def plan_round(shard_sizes, epochs, batch, generator=None):
+    """Host-side schedule for one round (integer bookkeeping only).
+
+    shard_sizes[k] = train samples of slot k; slots must be ordered so that
+    ceil(n_k / batch) is non-increasing.  Returns a dict with
+      G        number of global steps (= epochs * steps of slot 0)
+      steps[k] batches per epoch of slot k;  T[k] = epochs * steps[k]
+      active[g] slots still training at global step g (always a prefix)
+      counts[g,k] valid images of slot k at step g (last batch partial, 0 when done)
+      reset[g,k]  1 at the first batch of each of slot k's epochs
+      index[g,k,:] positions inside slot k's shard: a fresh torch.randperm per
+               client per epoch, as DataLoader(shuffle=True) draws them."""
+    B = batch
+    S = len(shard_sizes)
+    steps = [math.ceil(n / B) for n in shard_sizes]
+    if any(steps[i] < steps[i + 1] for i in range(S - 1)):
+        raise FedHipError("slots must be ordered by descending step count")
+    T = [epochs * s for s in steps]
+    G = T[0] if S else 0
+    counts = torch.zeros(G, S, dtype=torch.int32)
+    reset = torch.zeros(G, S, dtype=torch.int32)
+    index = torch.zeros(G, S, B, dtype=torch.int64)
+    for k, n in enumerate(shard_sizes):
+        for e in range(epochs):
+            perm = torch.randperm(n, generator=generator)
+            for s in range(steps[k]):
+                g = e * steps[k] + s
+                chunk = perm[s * B:(s + 1) * B]
+                counts[g, k] = chunk.numel()
+                reset[g, k] = 1 if s == 0 else 0
+                index[g, k, :chunk.numel()] = chunk
+    active = [sum(1 for t in T if t > g) for g in range(G)]
+    return dict(G=G, steps=steps, T=T, active=active, counts=counts, reset=reset, index=index)
 
 
 def epochs_of(plan):
