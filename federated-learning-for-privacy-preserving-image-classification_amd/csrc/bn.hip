@@ -1,0 +1,358 @@
+// bn.hip — BatchNorm2d for client-packed activations (train fwd / eval fwd / bwd).
+//
+// Reference: nn.BatchNorm2d in CIFAR10CNN and FederatedResNet
+// (src/shared/models_pytorch.py:108-120, 176-187), train-mode statistics over
+// the valid images of each client, momentum 0.1, eps 1e-5, unbiased running
+// variance — ATen CPU accumulates these in double (acc_type<float>); so do we.
+//
+// Each (client, channel) reduction is split over S blocks ("slices" of the
+// channel's cnt*HW elements) so that even one client fills the chip; the S
+// partials go to a caller workspace and are merged in a fixed order by the
+// second kernel (deterministic).  Element loops are float4 when HW % 4 == 0.
+//   train fwd : stats  (read x)            -> partial (sum x, sum x^2) in fp64
+//               apply  (read x [,res], write y = relu?(x*alpha + beta [+res]))
+//   bwd       : reduce (read dy, y, x [, write dres])  -> partial (sum g, sum (x-mean) g)
+//               apply  (read dy, y, x, write dx = ((g - mean g) - (x-mean) k) invstd w)
+// Fused: the ReLU that follows BN (forward) and its mask (backward, g = dy*(y>0)),
+// and the ResNet residual add (forward) / residual-branch gradient (backward).
+#include "fh_common.h"
+
+namespace fh {
+
+struct BNArgs {
+    const float* x;
+    float* y;
+    const float* res;
+    const float* dy;
+    const float* yout;
+    float* dx;
+    float* dres;
+    const float* gamma;
+    const float* beta;
+    float* rmean;
+    float* rvar;
+    float* save_mean;
+    float* save_invstd;
+    float* dgamma;
+    float* dbeta;
+    double* part;  // [z][C][S][2]
+    int64_t x_cs, y_cs, res_cs, dy_cs, yo_cs, dx_cs, dres_cs, p_cs, r_cs, g_cs;
+    const int32_t* counts;
+    int batch, C, HW, S, chunk;  // chunk: elements per slice (multiple of 4)
+    float eps, momentum;
+    int relu;
+    FastDiv fd_hw;
+};
+
+// Visit this block's slice of channel c of client z: f(offset_within_client_tensor, nvec)
+// nvec = 4 (float4 at offset) or 1 (scalar).
+template <class F>
+__device__ __forceinline__ void for_slice(const BNArgs& a, int z, int c, int s, F&& f) {
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int n = cnt * a.HW;
+    const int e0 = s * a.chunk, e1 = min(n, e0 + a.chunk);
+    const int64_t istride = (int64_t)a.C * a.HW, coff = (int64_t)c * a.HW;
+    if ((a.HW & 3) == 0) {
+        for (int e = e0 + threadIdx.x * 4; e < e1; e += 256 * 4) {
+            uint32_t img, p;
+            a.fd_hw.divmod(e, img, p);
+            f(img * istride + coff + p, 4);
+        }
+    } else {
+        for (int e = e0 + threadIdx.x; e < e1; e += 256) {
+            uint32_t img, p;
+            a.fd_hw.divmod(e, img, p);
+            f(img * istride + coff + p, 1);
+        }
+    }
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+// merge this channel's S partials (fixed order) -> (n, sum0, sum1)
+__device__ __forceinline__ void merge(const BNArgs& a, int z, int c, double& s0, double& s1) {
+    const double* p = a.part + (((int64_t)z * a.C + c) * a.S) * 2;
+    s0 = 0.0;
+    s1 = 0.0;
+    for (int i = 0; i < a.S; ++i) {
+        s0 += p[2 * i];
+        s1 += p[2 * i + 1];
+    }
+}
+
+__global__ void __launch_bounds__(256) bn_stats_kernel(const BNArgs a) {
+    __shared__ double red[4];
+    const int s = blockIdx.x, c = blockIdx.y, z = blockIdx.z;
+    const float* xz = a.x + z * a.x_cs;
+    double s0 = 0.0, s1 = 0.0;
+    for_slice(a, z, c, s, [&](int64_t o, int nv) {
+        if (nv == 4) {
+            const float4 v = ld4(xz + o);
+            s0 += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+            s1 += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
+        } else {
+            const double v = xz[o];
+            s0 += v;
+            s1 += v * v;
+        }
+    });
+    s0 = block_sum_256(s0, red);
+    s1 = block_sum_256(s1, red);
+    if (threadIdx.x == 0) {
+        double* p = a.part + ((((int64_t)z * a.C + c) * a.S) + s) * 2;
+        p[0] = s0;
+        p[1] = s1;
+    }
+}
+
+__global__ void __launch_bounds__(256) bn_apply_kernel(const BNArgs a) {
+    const int s = blockIdx.x, c = blockIdx.y, z = blockIdx.z;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int64_t n = (int64_t)cnt * a.HW;
+    double sum, sq;
+    merge(a, z, c, sum, sq);
+    const double mean = n > 0 ? sum / (double)n : 0.0;
+    double var = n > 0 ? sq / (double)n - mean * mean : 0.0;
+    if (var < 0.0) var = 0.0;
+    const double invstd = n > 0 ? 1.0 / sqrt(var + (double)a.eps) : 0.0;
+    const float meanf = (float)mean, invstdf = (float)invstd;
+    if (s == 0 && threadIdx.x == 0) {
+        a.save_mean[z * a.C + c] = meanf;
+        a.save_invstd[z * a.C + c] = invstdf;
+        if (a.rmean && n > 0) {
+            const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+            float* rm = a.rmean + z * a.r_cs + c;
+            float* rv = a.rvar + z * a.r_cs + c;
+            *rm = (float)((double)a.momentum * mean + (1.0 - (double)a.momentum) * (double)*rm);
+            *rv = (float)((double)a.momentum * unb + (1.0 - (double)a.momentum) * (double)*rv);
+        }
+    }
+    // y = x*alpha + beta'  (alpha = invstd*w, beta' = b - mean*alpha), [+res], [relu]
+    const float alpha = invstdf * a.gamma[z * a.p_cs + c];
+    const float bconst = a.beta[z * a.p_cs + c] - meanf * alpha;
+    const float* xz = a.x + z * a.x_cs;
+    float* yz = a.y + z * a.y_cs;
+    const float* rz = a.res ? a.res + z * a.res_cs : nullptr;
+    const int relu = a.relu;
+    for_slice(a, z, c, s, [&](int64_t o, int nv) {
+        if (nv == 4) {
+            float4 v = ld4(xz + o);
+            v.x = v.x * alpha + bconst;
+            v.y = v.y * alpha + bconst;
+            v.z = v.z * alpha + bconst;
+            v.w = v.w * alpha + bconst;
+            if (rz) {
+                const float4 r = ld4(rz + o);
+                v.x = v.x + r.x; v.y = v.y + r.y; v.z = v.z + r.z; v.w = v.w + r.w;
+            }
+            if (relu) {
+                v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f);
+                v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+            }
+            st4(yz + o, v);
+        } else {
+            float v = xz[o] * alpha + bconst;
+            if (rz) v = v + rz[o];
+            if (relu) v = fmaxf(v, 0.f);
+            yz[o] = v;
+        }
+    });
+}
+
+// eval mode: running statistics (LocalTrainer._validate_epoch / evaluate_model)
+__global__ void __launch_bounds__(256) bn_eval_kernel(const BNArgs a) {
+    const int s = blockIdx.x, c = blockIdx.y, z = blockIdx.z;
+    const float invstd = (float)(1.0 / sqrt((double)a.rvar[z * a.r_cs + c] + (double)a.eps));
+    const float alpha = invstd * a.gamma[z * a.p_cs + c];
+    const float bconst = a.beta[z * a.p_cs + c] - a.rmean[z * a.r_cs + c] * alpha;
+    const float* xz = a.x + z * a.x_cs;
+    float* yz = a.y + z * a.y_cs;
+    const float* rz = a.res ? a.res + z * a.res_cs : nullptr;
+    for_slice(a, z, c, s, [&](int64_t o, int nv) {
+        for (int q = 0; q < nv; ++q) {
+            float v = xz[o + q] * alpha + bconst;
+            if (rz) v = v + rz[o + q];
+            if (a.relu) v = fmaxf(v, 0.f);
+            yz[o + q] = v;
+        }
+    });
+}
+
+__device__ __forceinline__ float gmask(float d, const float* yo, int64_t o) {
+    return (yo && !(yo[o] > 0.f)) ? 0.f : d;
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const BNArgs a) {
+    __shared__ double red[4];
+    const int s = blockIdx.x, c = blockIdx.y, z = blockIdx.z;
+    const float mean = a.save_mean[z * a.C + c];
+    const float* dyz = a.dy + z * a.dy_cs;
+    const float* yoz = a.relu ? a.yout + z * a.yo_cs : nullptr;
+    const float* xz = a.x + z * a.x_cs;
+    float* drz = a.dres ? a.dres + z * a.dres_cs : nullptr;
+    double sg = 0.0, dot = 0.0;
+    for_slice(a, z, c, s, [&](int64_t o, int nv) {
+        for (int q = 0; q < nv; ++q) {
+            const float g = gmask(dyz[o + q], yoz, o + q);
+            if (drz) drz[o + q] = g;
+            sg += (double)g;
+            dot += (double)((xz[o + q] - mean) * g);
+        }
+    });
+    sg = block_sum_256(sg, red);
+    dot = block_sum_256(dot, red);
+    if (threadIdx.x == 0) {
+        double* p = a.part + ((((int64_t)z * a.C + c) * a.S) + s) * 2;
+        p[0] = sg;
+        p[1] = dot;
+    }
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const BNArgs a) {
+    const int s = blockIdx.x, c = blockIdx.y, z = blockIdx.z;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int64_t n = (int64_t)cnt * a.HW;
+    double sg, dot;
+    merge(a, z, c, sg, dot);
+    const float mean = a.save_mean[z * a.C + c], invstd = a.save_invstd[z * a.C + c];
+    if (s == 0 && threadIdx.x == 0) {
+        if (a.dgamma) a.dgamma[z * a.g_cs + c] = (float)(dot * (double)invstd);
+        if (a.dbeta) a.dbeta[z * a.g_cs + c] = (float)sg;
+    }
+    if (!a.dx) return;
+    const float w = a.gamma[z * a.p_cs + c];
+    const float k = n > 0 ? (float)(dot * (double)invstd * (double)invstd / (double)n) : 0.f;
+    const float gm = n > 0 ? (float)(sg / (double)n) : 0.f;
+    const float* dyz = a.dy + z * a.dy_cs;
+    const float* yoz = a.relu ? a.yout + z * a.yo_cs : nullptr;
+    const float* xz = a.x + z * a.x_cs;
+    float* dxz = a.dx + z * a.dx_cs;
+    for_slice(a, z, c, s, [&](int64_t o, int nv) {
+        if (nv == 4) {
+            const float4 d = ld4(dyz + o), xv = ld4(xz + o);
+            float4 g = d;
+            if (yoz) {
+                const float4 yv = ld4(yoz + o);
+                g.x = yv.x > 0.f ? d.x : 0.f; g.y = yv.y > 0.f ? d.y : 0.f;
+                g.z = yv.z > 0.f ? d.z : 0.f; g.w = yv.w > 0.f ? d.w : 0.f;
+            }
+            float4 r;
+            r.x = (((g.x - gm) - (xv.x - mean) * k) * invstd) * w;
+            r.y = (((g.y - gm) - (xv.y - mean) * k) * invstd) * w;
+            r.z = (((g.z - gm) - (xv.z - mean) * k) * invstd) * w;
+            r.w = (((g.w - gm) - (xv.w - mean) * k) * invstd) * w;
+            st4(dxz + o, r);
+        } else {
+            const float g = gmask(dyz[o], yoz, o);
+            dxz[o] = (((g - gm) - (xz[o] - mean) * k) * invstd) * w;
+        }
+    });
+}
+
+static void bn_geometry(int nclients, int batch, int C, int HW, int& S, int& chunk) {
+    const int64_t nmax = (int64_t)batch * HW;
+    int64_t want = ceil_div(2048, (int64_t)C * std::max(nclients, 1));
+    const int64_t maxs = std::max<int64_t>(1, nmax / 2048);  // >= 2048 elements per slice
+    if (want > maxs) want = maxs;
+    if (want < 1) want = 1;
+    chunk = (int)(ceil_div(ceil_div(nmax, want), 4) * 4);
+    S = (int)ceil_div(nmax, chunk);
+}
+
+static BNArgs bn_args(int nclients, int batch, int C, int HW, const int32_t* counts) {
+    BNArgs a{};
+    a.counts = counts;
+    a.batch = batch;
+    a.C = C;
+    a.HW = HW;
+    bn_geometry(nclients, batch, C, HW, a.S, a.chunk);
+    a.fd_hw = FastDiv(HW);
+    return a;
+}
+
+}  // namespace fh
+
+using namespace fh;
+
+extern "C" size_t fh_bn_workspace(int32_t nclients, int32_t batch, int32_t C, int32_t HW) {
+    if (nclients <= 0 || batch <= 0 || C <= 0 || HW <= 0) return 0;
+    int S, chunk;
+    bn_geometry(nclients, batch, C, HW, S, chunk);
+    return (size_t)nclients * C * S * 2 * sizeof(double);
+}
+
+extern "C" int fh_bn_fwd_train(const float* x, int64_t x_cs, float* y, int64_t y_cs,
+                               const float* res, int64_t res_cs, const float* gamma,
+                               const float* beta, int64_t p_cs, float* running_mean,
+                               float* running_var, int64_t r_cs, float* save_mean,
+                               float* save_invstd, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t C, int32_t HW, float eps, float momentum,
+                               int32_t relu, void* workspace, size_t ws_bytes, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_train: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && y && gamma && beta && save_mean && save_invstd, "bn_fwd_train: null pointer");
+    FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "bn_fwd_train: running stats");
+    const size_t need = fh_bn_workspace(nclients, batch, C, HW);
+    FH_REQUIRE(workspace && ws_bytes >= need, "bn_fwd_train: workspace %zu < %zu", ws_bytes, need);
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.x = x; a.y = y; a.res = res; a.gamma = gamma; a.beta = beta;
+    a.rmean = running_mean; a.rvar = running_var; a.save_mean = save_mean;
+    a.save_invstd = save_invstd; a.part = (double*)workspace;
+    a.x_cs = x_cs; a.y_cs = y_cs; a.res_cs = res_cs; a.p_cs = p_cs; a.r_cs = r_cs;
+    a.eps = eps; a.momentum = momentum; a.relu = relu;
+    hipStream_t st = as_stream(stream);
+    dim3 grid(a.S, C, nclients);
+    hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH_CHECK("bn_fwd_train stats");
+    hipLaunchKernelGGL(bn_apply_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH_CHECK("bn_fwd_train apply");
+    return FH_OK;
+}
+
+extern "C" int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_cs,
+                              const float* res, int64_t res_cs, const float* gamma,
+                              const float* beta, int64_t p_cs, const float* running_mean,
+                              const float* running_var, int64_t r_cs, const int32_t* counts,
+                              int32_t nclients, int32_t batch, int32_t C, int32_t HW, float eps,
+                              int32_t relu, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_eval: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && y && gamma && beta && running_mean && running_var, "bn_fwd_eval: null pointer");
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.x = x; a.y = y; a.res = res; a.gamma = gamma; a.beta = beta;
+    a.rmean = (float*)running_mean; a.rvar = (float*)running_var;
+    a.x_cs = x_cs; a.y_cs = y_cs; a.res_cs = res_cs; a.p_cs = p_cs; a.r_cs = r_cs;
+    a.eps = eps; a.relu = relu;
+    hipLaunchKernelGGL(bn_eval_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
+    FH_LAUNCH_CHECK("bn_fwd_eval");
+    return FH_OK;
+}
+
+extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs,
+                         const float* x, int64_t x_cs, const float* gamma, int64_t p_cs,
+                         const float* save_mean, const float* save_invstd, float* dx,
+                         int64_t dx_cs, float* dres, int64_t dres_cs, float* dgamma, float* dbeta,
+                         int64_t g_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                         int32_t C, int32_t HW, int32_t relu, void* workspace, size_t ws_bytes,
+                         void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_bwd: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dy && x && gamma && save_mean && save_invstd, "bn_bwd: null pointer");
+    FH_REQUIRE(!relu || yout, "bn_bwd: relu needs the forward output");
+    const size_t need = fh_bn_workspace(nclients, batch, C, HW);
+    FH_REQUIRE(workspace && ws_bytes >= need, "bn_bwd: workspace %zu < %zu", ws_bytes, need);
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.dy = dy; a.yout = yout; a.x = x; a.gamma = gamma; a.save_mean = (float*)save_mean;
+    a.save_invstd = (float*)save_invstd; a.dx = dx; a.dres = dres; a.dgamma = dgamma;
+    a.dbeta = dbeta; a.part = (double*)workspace;
+    a.dy_cs = dy_cs; a.yo_cs = yo_cs; a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs;
+    a.dres_cs = dres_cs; a.g_cs = g_cs; a.relu = relu;
+    hipStream_t st = as_stream(stream);
+    dim3 grid(a.S, C, nclients);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH_CHECK("bn_bwd reduce");
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH_CHECK("bn_bwd apply");
+    return FH_OK;
+}

@@ -38,7 +38,8 @@ struct ConvArgs {
     int batch, cin, h, w, cout, oh, ow, pad;
     int relu;
     int accumulate;      // DGRAD: dx += result
-    int splits, kchunk;  // WGRAD
+    int splits, kchunk;  // split-K (WGRAD always; FWD/DGRAD when the grid is small)
+    float* bias_part;    // WGRAD: per-split conv-bias partial sums [z][split][M] (or null)
     int M, N, K;         // GEMM extents at full batch
     FastDiv fd_ohw, fd_ow, fd_hw, fd_w;
 };
@@ -60,13 +61,10 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WAVES_N, wn = wid % WAVES_N;
 
-    int z, split = 0;
-    if constexpr (OP == OP_WGRAD) {
-        z = blockIdx.z / a.splits;
-        split = blockIdx.z - z * a.splits;
-    } else {
-        z = blockIdx.z;
-    }
+    // blockIdx.z = client * splits + split (split-K: WGRAD always, FWD/DGRAD on small grids)
+    const int z = blockIdx.z / a.splits;
+    const int split = blockIdx.z - z * a.splits;
+    const bool partial_out = (OP == OP_WGRAD) || a.splits > 1;
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int ohw = a.oh * a.ow, hw = a.h * a.w;
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
@@ -81,6 +79,8 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
         kend = min(kv, kbeg + a.kchunk);
     } else {
         if (n0 >= N) return;
+        kbeg = split * a.kchunk;
+        kend = min(a.K, kbeg + a.kchunk);
     }
 
     // ---------------- per-thread fixed coordinates -----------------------
@@ -217,6 +217,8 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    const bool do_bias = (OP == OP_WGRAD) && a.bias_part != nullptr && blockIdx.x == 0;
+    float bsum = 0.f;
     if (kbeg < kend) {
         load_tiles(kbeg);
         store_tiles(0);
@@ -226,6 +228,14 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
         for (int k0 = kbeg; k0 < kend; k0 += BK) {
             const bool more = k0 + BK < kend;
             if (more) load_tiles(k0 + BK);
+            if constexpr (OP == OP_WGRAD) {
+                // conv bias gradient = row sums of A = dY over the pixel (k) range: folded in
+                // here (first n-tile only) instead of a separate pass over dY.
+                if (do_bias && tid < BM) {
+#pragma unroll
+                    for (int kk = 0; kk < BK; ++kk) bsum += As[buf][kk][tid];
+                }
+            }
 #pragma unroll
             for (int kk = 0; kk < BK; kk += 2) {
                 float av[FM], bv[FN];
@@ -246,13 +256,16 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     }
 
     // ---------------- epilogue ------------------------------------------
+    if (do_bias && tid < BM && m0 + tid < M)
+        a.bias_part[(int64_t)blockIdx.z * a.M + m0 + tid] = bsum;
     // acc[i][j][r]: row m = (r&3) + 8*(r>>2) + 4*(lane>>5), col n = lane&31.
     const int rbase = 4 * (lane >> 5), col = lane & 31;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
         const int n = n0 + wn * WN + j * 32 + col;
         if (n >= N) continue;
-        if constexpr (OP == OP_WGRAD) {
+        if (partial_out) {
+            // split-K partial slab part[z][split][m][n] (n over the full-batch extent a.N)
             float* op = a.out + ((int64_t)blockIdx.z * a.M) * a.N + n;
 #pragma unroll
             for (int i = 0; i < FM; ++i)
@@ -261,7 +274,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
                     const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
                     if (m < M) op[(int64_t)m * a.N] = acc[i][j][r];
                 }
-        } else {
+        } else if constexpr (OP != OP_WGRAD) {
             uint32_t img, p;
             if constexpr (OP == OP_FWD) {
                 a.fd_ohw.divmod(n, img, p);
@@ -297,35 +310,49 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     }
 }
 
-// dw[z][m][n] = sum_s part[z][s][m][n] (fixed order -> deterministic)
-__global__ void splitk_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
-                                     int64_t dw_cs, int splits, int MN) {
-    const int z = blockIdx.y;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < MN; e += gridDim.x * blockDim.x) {
-        const float* p = part + (int64_t)z * splits * MN + e;
-        float s = 0.f;
-        for (int i = 0; i < splits; ++i) s += p[(int64_t)i * MN];
-        dw[z * dw_cs + e] = s;
+// Split-K sums, deterministic: 64 outputs per block, 4 wave-groups each summing an
+// interleaved quarter of the splits, combined in a fixed order.  Blocks past the
+// weight part reduce the conv-bias partials the WGRAD kernel folded in.
+__global__ void __launch_bounds__(256)
+splitk_sum_kernel(const float* __restrict__ part, float* __restrict__ dw, int64_t dw_cs, int splits,
+                  int MN, int wblocks, const float* __restrict__ bpart, float* __restrict__ db,
+                  int64_t db_cs, int Mb) {
+    __shared__ float red[4][64];
+    const int z = blockIdx.y, l = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const bool is_w = (int)blockIdx.x < wblocks;
+    const int e = (is_w ? blockIdx.x : blockIdx.x - wblocks) * 64 + l;
+    const int lim = is_w ? MN : Mb;
+    const float* src = is_w ? part + (int64_t)z * splits * MN : bpart + (int64_t)z * splits * Mb;
+    float s = 0.f;
+    if (e < lim)
+        for (int i = q; i < splits; i += 4) s += src[(int64_t)i * lim + e];
+    red[q][l] = s;
+    __syncthreads();
+    if (q == 0 && e < lim) {
+        const float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+        if (is_w) dw[z * dw_cs + e] = v;
+        else db[z * db_cs + e] = v;
     }
 }
 
-// db[z][c] = sum over valid images and pixels of dy[z][img][c][p]; one block per (c, z).
-__global__ void __launch_bounds__(256) bias_grad_kernel(const float* __restrict__ dy, int64_t dy_cs,
-                                                        float* __restrict__ db, int64_t db_cs,
-                                                        const int32_t* counts, int batch, int C,
-                                                        int HW) {
-    __shared__ double red[4];
-    const int c = blockIdx.x, z = blockIdx.y;
+// FWD/DGRAD split-K epilogue: out[z][img][m][p] (=|+=) sum_s part[z][s][m][n] (+bias, relu).
+__global__ void __launch_bounds__(256)
+splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nfull,
+                       float* __restrict__ out, int64_t out_cs, const float* __restrict__ bias,
+                       int64_t b_cs, int relu, int accumulate, const int32_t* __restrict__ counts,
+                       int batch, int sp) {
+    const int z = blockIdx.z, m = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
-    const float* base = dy + z * dy_cs + (int64_t)c * HW;
-    double s = 0.0;
-    const int total = cnt * HW;
-    for (int e = threadIdx.x; e < total; e += 256) {
-        const int img = e / HW, p = e - img * HW;
-        s += (double)base[(int64_t)img * C * HW + p];
-    }
-    s = block_sum_256(s, red);
-    if (threadIdx.x == 0) db[z * db_cs + c] = (float)s;
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= cnt * sp) return;
+    const float* p = part + ((int64_t)z * splits * M + m) * Nfull + n;
+    float s = 0.f;
+    for (int i = 0; i < splits; ++i) s += p[(int64_t)i * M * Nfull];
+    if (bias) s = s + bias[z * b_cs + m];
+    if (relu) s = fmaxf(s, 0.f);
+    const int img = n / sp, pix = n - img * sp;
+    float* o = out + z * out_cs + ((int64_t)img * M + m) * sp + pix;
+    *o = accumulate ? (*o + s) : s;
 }
 
 // ---------------------------------------------------------------------------
@@ -382,14 +409,51 @@ static Tile pick_wgrad_tile(int M) {
     return {128, 128, 32, 2};
 }
 
-static void wgrad_split(int nclients, int M, int N, int K, const Tile& t, int& splits, int& kchunk) {
-    const int64_t tiles = ceil_div(M, t.bm) * ceil_div(N, t.bn) * (int64_t)nclients;
-    int64_t want = ceil_div(2048, tiles);
-    const int64_t maxs = std::max<int64_t>(1, K / (t.bk * 4));
-    if (want > maxs) want = maxs;
+// Split K so that (tiles x splits) fills the chip, each split keeping >= min_chunks K-steps.
+static void choose_split(int64_t tiles, int K, int bk, int64_t target, int min_chunks, int& splits,
+                         int& kchunk) {
+    int64_t want = ceil_div(target, std::max<int64_t>(tiles, 1));
+    const int64_t maxs = std::max<int64_t>(1, K / (bk * min_chunks));
+    want = std::min(want, maxs);
     if (want < 1) want = 1;
-    kchunk = (int)(ceil_div(ceil_div(K, want), t.bk) * t.bk);
+    kchunk = (int)(ceil_div(ceil_div(K, want), bk) * bk);
     splits = (int)ceil_div(K, kchunk);
+}
+
+struct Plan {
+    Tile t;
+    int splits, kchunk;
+    int M, N, K;
+};
+
+// FWD/DGRAD: split K only when the output tiling leaves most CUs idle (the
+// latency-bound tail of a round, when few clients are still training).
+static Plan plan_mn(int M, int N, int K, int nclients) {
+    Plan p{pick_mn_tile(M, N), 1, K, M, N, K};
+    const int64_t tiles = ceil_div(N, p.t.bn) * ceil_div(M, p.t.bm) * (int64_t)nclients;
+    if (tiles < 192) choose_split(tiles, K, p.t.bk, 768, 4, p.splits, p.kchunk);
+    if (p.splits <= 1) {
+        p.splits = 1;
+        p.kchunk = K;
+    }
+    return p;
+}
+
+static Plan plan_wgrad(int M, int N, int K, int nclients) {
+    Plan p{pick_wgrad_tile(M), 1, K, M, N, K};
+    const int64_t tiles = ceil_div(N, p.t.bn) * ceil_div(M, p.t.bm) * (int64_t)nclients;
+    choose_split(tiles, K, p.t.bk, 2048, 4, p.splits, p.kchunk);
+    return p;
+}
+
+static size_t mn_ws_bytes(const Plan& p, int nclients) {
+    return p.splits > 1 ? (size_t)nclients * p.splits * p.M * p.N * sizeof(float) : 0;
+}
+
+static size_t wgrad_ws_bytes(const Plan& p, int nclients) {
+    const size_t w = (size_t)nclients * p.splits * p.M * p.N * sizeof(float);
+    const size_t b = (size_t)nclients * p.splits * p.M * sizeof(float);
+    return ((w + 255) / 256) * 256 + b;
 }
 
 static int conv_common_check(int nclients, int batch, int cin, int h, int w, int cout, int kh,
@@ -416,6 +480,7 @@ static ConvArgs make_args(int batch, int cin, int h, int w, int cout, int oh, in
     a.ow = ow;
     a.pad = pad;
     a.counts = counts;
+    a.splits = 1;
     a.fd_ohw = FastDiv(oh * ow);
     a.fd_ow = FastDiv(ow);
     a.fd_hw = FastDiv(h * w);
@@ -423,15 +488,60 @@ static ConvArgs make_args(int batch, int cin, int h, int w, int cout, int oh, in
     return a;
 }
 
+// Launch an FWD/DGRAD product, split-K through `ws` when the plan asks for it and
+// the caller provided enough scratch; otherwise the single-pass kernel.
+template <int OP>
+static int run_mn(ConvArgs a, int kh, int kw, int stride, int nclients, void* ws, size_t ws_bytes,
+                  float* out, int64_t out_cs, const float* bias, int64_t b_cs, int relu, int accum,
+                  int sp, hipStream_t st, const char* name) {
+    Plan p = plan_mn(a.M, a.N, a.K, nclients);
+    if (p.splits > 1 && (!ws || ws_bytes < mn_ws_bytes(p, nclients))) {
+        p.splits = 1;
+        p.kchunk = a.K;
+    }
+    a.splits = p.splits;
+    a.kchunk = p.kchunk;
+    if (p.splits > 1) a.out = (float*)ws;
+    dim3 grid((unsigned)ceil_div(a.N, p.t.bn), (unsigned)ceil_div(a.M, p.t.bm),
+              (unsigned)(nclients * p.splits));
+    int rc = launch_shape<OP>(kh, kw, stride, p.t, grid, a, st);
+    if (rc) return rc;
+    FH_LAUNCH_CHECK(name);
+    if (p.splits > 1) {
+        dim3 eg((unsigned)ceil_div(a.N, 256), (unsigned)a.M, (unsigned)nclients);
+        hipLaunchKernelGGL(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
+                           a.M, a.N, out, out_cs, bias, b_cs, relu, accum, a.counts, a.batch, sp);
+        FH_LAUNCH_CHECK(name);
+    }
+    return FH_OK;
+}
+
 }  // namespace fh
 
 using namespace fh;
+
+extern "C" size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
+                                          int32_t w_, int32_t cout, int32_t kh, int32_t kw,
+                                          int32_t stride, int32_t pad) {
+    int oh = (h + 2 * pad - kh) / stride + 1, ow = (w_ + 2 * pad - kw) / stride + 1;
+    if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
+    return mn_ws_bytes(plan_mn(cout, batch * oh * ow, cin * kh * kw, nclients), nclients);
+}
+
+extern "C" size_t fh_conv2d_dgrad_workspace(int32_t nclients, int32_t batch, int32_t cin,
+                                            int32_t h, int32_t w_, int32_t cout, int32_t kh,
+                                            int32_t kw, int32_t stride, int32_t pad) {
+    int oh = (h + 2 * pad - kh) / stride + 1, ow = (w_ + 2 * pad - kw) / stride + 1;
+    if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
+    return mn_ws_bytes(plan_mn(cin, batch * h * w_, cout * kh * kw, nclients), nclients);
+}
 
 extern "C" int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
                              const float* bias, int64_t b_cs, float* y, int64_t y_cs,
                              const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
                              int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
-                             int32_t stride, int32_t pad, int32_t relu, void* stream) {
+                             int32_t stride, int32_t pad, int32_t relu, void* workspace,
+                             size_t ws_bytes, void* stream) {
     int oh, ow;
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
     if (rc) return rc;
@@ -442,19 +552,16 @@ extern "C" int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64
     a.x_cs = x_cs; a.w_cs = w_cs; a.b_cs = b_cs; a.out_cs = y_cs;
     a.relu = relu;
     a.M = cout; a.N = batch * oh * ow; a.K = cin * kh * kw;
-    Tile t = pick_mn_tile(a.M, a.N);
-    dim3 grid((unsigned)ceil_div(a.N, t.bn), (unsigned)ceil_div(a.M, t.bm), (unsigned)nclients);
-    rc = launch_shape<OP_FWD>(kh, kw, stride, t, grid, a, as_stream(stream));
-    if (rc) return rc;
-    FH_LAUNCH_CHECK("conv2d_fwd");
-    return FH_OK;
+    return run_mn<OP_FWD>(a, kh, kw, stride, nclients, workspace, ws_bytes, y, y_cs, bias, b_cs,
+                          relu, 0, oh * ow, as_stream(stream), "conv2d_fwd");
 }
 
 extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
                                float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
                                int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
                                int32_t kh, int32_t kw, int32_t stride, int32_t pad,
-                               int32_t accumulate, void* stream) {
+                               int32_t accumulate, void* workspace, size_t ws_bytes,
+                               void* stream) {
     int oh, ow;
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
     if (rc) return rc;
@@ -465,12 +572,8 @@ extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, i
     a.dy_cs = dy_cs; a.w_cs = w_cs; a.out_cs = dx_cs;
     a.accumulate = accumulate;
     a.M = cin; a.N = batch * h * w_; a.K = cout * kh * kw;
-    Tile t = pick_mn_tile(a.M, a.N);
-    dim3 grid((unsigned)ceil_div(a.N, t.bn), (unsigned)ceil_div(a.M, t.bm), (unsigned)nclients);
-    rc = launch_shape<OP_DGRAD>(kh, kw, stride, t, grid, a, as_stream(stream));
-    if (rc) return rc;
-    FH_LAUNCH_CHECK("conv2d_dgrad");
-    return FH_OK;
+    return run_mn<OP_DGRAD>(a, kh, kw, stride, nclients, workspace, ws_bytes, dx, dx_cs, nullptr, 0,
+                            0, accumulate, h * w_, as_stream(stream), "conv2d_dgrad");
 }
 
 extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
@@ -478,11 +581,7 @@ extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int
                                             int32_t stride, int32_t pad) {
     int oh = (h + 2 * pad - kh) / stride + 1, ow = (w_ + 2 * pad - kw) / stride + 1;
     if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
-    const int M = cout, N = cin * kh * kw, K = batch * oh * ow;
-    Tile t = pick_wgrad_tile(M);
-    int splits, kchunk;
-    wgrad_split(nclients, M, N, K, t, splits, kchunk);
-    return (size_t)nclients * splits * M * N * sizeof(float);
+    return wgrad_ws_bytes(plan_wgrad(cout, cin * kh * kw, batch * oh * ow, nclients), nclients);
 }
 
 extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
@@ -495,48 +594,60 @@ extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, in
     if (rc) return rc;
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && dy && dw && workspace, "conv2d_wgrad: null pointer");
-    const size_t need =
-        fh_conv2d_wgrad_workspace(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad);
-    FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
-    a.x = x; a.dy = dy; a.out = (float*)workspace;
+    a.x = x; a.dy = dy;
     a.x_cs = x_cs; a.dy_cs = dy_cs;
     a.M = cout; a.N = cin * kh * kw; a.K = batch * oh * ow;
-    Tile t = pick_wgrad_tile(a.M);
-    wgrad_split(nclients, a.M, a.N, a.K, t, a.splits, a.kchunk);
+    Plan p = plan_wgrad(a.M, a.N, a.K, nclients);
+    const size_t need = wgrad_ws_bytes(p, nclients);
+    FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
+    a.splits = p.splits;
+    a.kchunk = p.kchunk;
+    a.out = (float*)workspace;
+    const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
+    a.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
     hipStream_t st = as_stream(stream);
-    dim3 grid((unsigned)ceil_div(a.N, t.bn), (unsigned)ceil_div(a.M, t.bm),
-              (unsigned)(nclients * a.splits));
-    rc = launch_shape<OP_WGRAD>(kh, kw, stride, t, grid, a, st);
+    dim3 grid((unsigned)ceil_div(a.N, p.t.bn), (unsigned)ceil_div(a.M, p.t.bm),
+              (unsigned)(nclients * p.splits));
+    rc = launch_shape<OP_WGRAD>(kh, kw, stride, p.t, grid, a, st);
     if (rc) return rc;
     FH_LAUNCH_CHECK("conv2d_wgrad");
     const int MN = a.M * a.N;
-    dim3 rgrid((unsigned)std::min<int64_t>(ceil_div(MN, 256), 1024), (unsigned)nclients);
-    hipLaunchKernelGGL(splitk_reduce_kernel, rgrid, dim3(256), 0, st, (const float*)workspace, dw,
-                       dw_cs, a.splits, MN);
+    const int wblocks = (int)ceil_div(MN, 64);
+    const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
+    hipLaunchKernelGGL(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+                       (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
+                       (const float*)a.bias_part, db, db_cs, a.M);
     FH_LAUNCH_CHECK("conv2d_wgrad reduce");
-    if (db) {
-        hipLaunchKernelGGL(bias_grad_kernel, dim3(cout, nclients), dim3(256), 0, st, dy, dy_cs, db,
-                           db_cs, counts, batch, cout, oh * ow);
-        FH_LAUNCH_CHECK("conv2d_wgrad bias");
-    }
     return FH_OK;
 }
 
 // ---- linear layers: a 1x1 convolution over a 1x1 image -------------------
+extern "C" size_t fh_linear_fwd_workspace(int32_t nclients, int32_t batch, int32_t in_f,
+                                          int32_t out_f) {
+    return fh_conv2d_fwd_workspace(nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0);
+}
+
+extern "C" size_t fh_linear_dgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f,
+                                            int32_t out_f) {
+    return fh_conv2d_dgrad_workspace(nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0);
+}
+
 extern "C" int fh_linear_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
                              const float* bias, int64_t b_cs, float* y, int64_t y_cs,
                              const int32_t* counts, int32_t nclients, int32_t batch, int32_t in_f,
-                             int32_t out_f, int32_t relu, void* stream) {
+                             int32_t out_f, int32_t relu, void* workspace, size_t ws_bytes,
+                             void* stream) {
     return fh_conv2d_fwd(x, x_cs, w, w_cs, bias, b_cs, y, y_cs, counts, nclients, batch, in_f, 1, 1,
-                         out_f, 1, 1, 1, 0, relu, stream);
+                         out_f, 1, 1, 1, 0, relu, workspace, ws_bytes, stream);
 }
 
 extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
                                float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
-                               int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
+                               int32_t batch, int32_t in_f, int32_t out_f, void* workspace,
+                               size_t ws_bytes, void* stream) {
     return fh_conv2d_dgrad(dy, dy_cs, w, w_cs, dx, dx_cs, counts, nclients, batch, in_f, 1, 1,
-                           out_f, 1, 1, 1, 0, 0, stream);
+                           out_f, 1, 1, 1, 0, 0, workspace, ws_bytes, stream);
 }
 
 extern "C" size_t fh_linear_wgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f,

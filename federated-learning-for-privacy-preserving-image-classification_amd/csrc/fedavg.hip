@@ -115,17 +115,18 @@ extern "C" int fh_fedavg_weighted_sum(const float* rows, int64_t row_stride,
     if (P == 0) return FH_OK;
     FH_REQUIRE(out && (num_clients == 0 || (rows && weights)), "fedavg: null pointer");
     hipStream_t st = as_stream(stream);
-    const bool vec_ok = (P % 4 == 0) && (row_stride % 4 == 0) &&
-                        (reinterpret_cast<uintptr_t>(rows) % 16 == 0) &&
+    // 16-B path over the 4-aligned prefix (packed rows are padded to a multiple of 64
+    // floats by the engine), scalar kernel for the < 4-element tail.
+    const bool vec_ok = (row_stride % 4 == 0) && (reinterpret_cast<uintptr_t>(rows) % 16 == 0) &&
                         (reinterpret_cast<uintptr_t>(out) % 16 == 0);
     int64_t done = 0;
-    if (vec_ok) {
+    if (vec_ok && P >= 4) {
         const int64_t P4 = P / 4;
         const int grid = (int)std::min<int64_t>(ceil_div(P4, 256), 8192);
         hipLaunchKernelGGL(fedavg_vec4_kernel, dim3(grid), dim3(256), 0, st, rows, row_stride,
                            row_index, weights, num_clients, P4, out, accumulate);
         FH_LAUNCH_CHECK("fedavg_vec4");
-        done = P;
+        done = P4 * 4;
     }
     if (done < P) {
         const int grid = (int)std::min<int64_t>(ceil_div(P - done, 256), 8192);

@@ -1,8 +1,6 @@
 // layers.hip — the non-GEMM layers of the reference CNNs, client-batched.
 //
-//   BatchNorm2d train/eval fwd + bwd   models_pytorch.py:108-120, 176-187 (nn.BatchNorm2d)
-//       fused with the following ReLU and (ResNet) the residual add
-//       (models_pytorch.py:140-160, 189-194)
+//   (BatchNorm2d lives in bn.hip)
 //   MaxPool2d(2,2) fwd/bwd              models_pytorch.py:72, 123 (fused with the Dropout
 //       that follows it in CIFAR10CNN, :139-155, and the ReLU before it in SimpleCNN, :85-88)
 //   Dropout fwd/bwd                     models_pytorch.py:75, 124 (F.dropout semantics:
@@ -18,142 +16,6 @@
 #include "fh_common.h"
 
 namespace fh {
-
-// ------------------------------------------------------------------ BatchNorm
-// x, y, res: [z][img][C][HW]; gamma/beta: per-client param rows (stride p_cs);
-// running stats: stride r_cs; save_mean/save_invstd: [z][C].
-__global__ void __launch_bounds__(256)
-bn_fwd_train_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y, int64_t y_cs,
-                    const float* __restrict__ res, int64_t res_cs, const float* __restrict__ gamma,
-                    const float* __restrict__ beta, int64_t p_cs, float* __restrict__ rmean,
-                    float* __restrict__ rvar, int64_t r_cs, float* __restrict__ save_mean,
-                    float* __restrict__ save_invstd, const int32_t* __restrict__ counts, int batch,
-                    int C, int HW, float eps, float momentum, int relu) {
-    __shared__ double red[4];
-    const int c = blockIdx.x, z = blockIdx.y;
-    const int cnt = counts ? counts[z] : batch;
-    const int64_t n = (int64_t)cnt * HW;
-    const float* xb = x + z * x_cs + (int64_t)c * HW;
-    const int64_t istride = (int64_t)C * HW;
-    // pass 1: mean
-    double s = 0.0;
-    for (int img = 0; img < cnt; ++img)
-        for (int p = threadIdx.x; p < HW; p += 256) s += (double)xb[img * istride + p];
-    s = block_sum_256(s, red);
-    const double mean = n > 0 ? s / (double)n : 0.0;
-    // pass 2: centred sum of squares
-    double v = 0.0;
-    for (int img = 0; img < cnt; ++img)
-        for (int p = threadIdx.x; p < HW; p += 256) {
-            const double d = (double)xb[img * istride + p] - mean;
-            v += d * d;
-        }
-    v = block_sum_256(v, red);
-    const double invstd = n > 0 ? 1.0 / sqrt(v / (double)n + (double)eps) : 0.0;
-    const float meanf = (float)mean, invstdf = (float)invstd;
-    if (threadIdx.x == 0) {
-        save_mean[z * C + c] = meanf;
-        save_invstd[z * C + c] = invstdf;
-        if (rmean && n > 0) {
-            float* rm = rmean + z * r_cs + c;
-            float* rv = rvar + z * r_cs + c;
-            const double unb = n > 1 ? v / (double)(n - 1) : v;
-            *rm = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)*rm);
-            *rv = (float)((double)momentum * unb + (1.0 - (double)momentum) * (double)*rv);
-        }
-    }
-    // pass 3: y = x*alpha + beta  (alpha = invstd*w, beta = b - mean*alpha), [+res], [relu]
-    const float g = gamma[z * p_cs + c], bt = beta[z * p_cs + c];
-    const float alpha = invstdf * g;
-    const float bconst = bt - meanf * alpha;
-    float* yb = y + z * y_cs + (int64_t)c * HW;
-    const float* rb = res ? res + z * res_cs + (int64_t)c * HW : nullptr;
-    for (int img = 0; img < cnt; ++img)
-        for (int p = threadIdx.x; p < HW; p += 256) {
-            float o = xb[img * istride + p] * alpha + bconst;
-            if (rb) o = o + rb[img * istride + p];
-            if (relu) o = fmaxf(o, 0.f);
-            yb[img * istride + p] = o;
-        }
-}
-
-// eval mode: running statistics (LocalTrainer._validate_epoch / evaluate_model, training.py:218,318)
-__global__ void __launch_bounds__(256)
-bn_fwd_eval_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y, int64_t y_cs,
-                   const float* __restrict__ res, int64_t res_cs, const float* __restrict__ gamma,
-                   const float* __restrict__ beta, int64_t p_cs, const float* __restrict__ rmean,
-                   const float* __restrict__ rvar, int64_t r_cs, const int32_t* __restrict__ counts,
-                   int batch, int C, int HW, float eps, int relu) {
-    const int c = blockIdx.x, z = blockIdx.y;
-    const int cnt = counts ? counts[z] : batch;
-    const float invstd = (float)(1.0 / sqrt((double)rvar[z * r_cs + c] + (double)eps));
-    const float alpha = invstd * gamma[z * p_cs + c];
-    const float bconst = beta[z * p_cs + c] - rmean[z * r_cs + c] * alpha;
-    const int64_t istride = (int64_t)C * HW;
-    const float* xb = x + z * x_cs + (int64_t)c * HW;
-    float* yb = y + z * y_cs + (int64_t)c * HW;
-    const float* rb = res ? res + z * res_cs + (int64_t)c * HW : nullptr;
-    for (int img = 0; img < cnt; ++img)
-        for (int p = threadIdx.x; p < HW; p += 256) {
-            float o = xb[img * istride + p] * alpha + bconst;
-            if (rb) o = o + rb[img * istride + p];
-            if (relu) o = fmaxf(o, 0.f);
-            yb[img * istride + p] = o;
-        }
-}
-
-// g = relu ? (yout > 0 ? dy : 0) : dy ; optionally g -> dres (residual branch);
-// dgamma = sum((x-mean)*g)*invstd, dbeta = sum(g);
-// dx = ((g - mean(g)) - (x-mean)*k) * invstd * w,  k = dotp*invstd^2/n  (ATen CPU order)
-__global__ void __launch_bounds__(256)
-bn_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const float* __restrict__ yout,
-              int64_t yo_cs, const float* __restrict__ x, int64_t x_cs,
-              const float* __restrict__ gamma, int64_t p_cs, const float* __restrict__ save_mean,
-              const float* __restrict__ save_invstd, float* __restrict__ dx, int64_t dx_cs,
-              float* __restrict__ dres, int64_t dres_cs, float* __restrict__ dgamma,
-              float* __restrict__ dbeta, int64_t g_cs, const int32_t* __restrict__ counts,
-              int batch, int C, int HW, int relu) {
-    __shared__ double red[4];
-    const int c = blockIdx.x, z = blockIdx.y;
-    const int cnt = counts ? counts[z] : batch;
-    const int64_t n = (int64_t)cnt * HW;
-    const int64_t istride = (int64_t)C * HW;
-    const int64_t coff = (int64_t)c * HW;
-    const float* dyb = dy + z * dy_cs + coff;
-    const float* yob = relu ? yout + z * yo_cs + coff : nullptr;
-    const float* xb = x + z * x_cs + coff;
-    float* drb = dres ? dres + z * dres_cs + coff : nullptr;
-    const float mean = save_mean[z * C + c], invstd = save_invstd[z * C + c];
-    double sg = 0.0, dot = 0.0;
-    for (int img = 0; img < cnt; ++img)
-        for (int p = threadIdx.x; p < HW; p += 256) {
-            const int64_t o = img * istride + p;
-            float g = dyb[o];
-            if (yob && !(yob[o] > 0.f)) g = 0.f;
-            if (drb) drb[o] = g;
-            sg += (double)g;
-            dot += (double)((xb[o] - mean) * g);
-        }
-    sg = block_sum_256(sg, red);
-    dot = block_sum_256(dot, red);
-    const float w = gamma[z * p_cs + c];
-    if (threadIdx.x == 0) {
-        if (dgamma) dgamma[z * g_cs + c] = (float)(dot * (double)invstd);
-        if (dbeta) dbeta[z * g_cs + c] = (float)sg;
-    }
-    if (!dx) return;
-    const float k = n > 0 ? (float)(dot * (double)invstd * (double)invstd / (double)n) : 0.f;
-    const float gm = n > 0 ? (float)(sg / (double)n) : 0.f;
-    float* dxb = dx + z * dx_cs + coff;
-    for (int img = 0; img < cnt; ++img)
-        for (int p = threadIdx.x; p < HW; p += 256) {
-            const int64_t o = img * istride + p;
-            float g = dyb[o];
-            if (yob && !(yob[o] > 0.f)) g = 0.f;
-            const float gi = (xb[o] - mean) * k;
-            dxb[o] = (((g - gm) - gi) * invstd) * w;
-        }
-}
 
 // ------------------------------------------------------------------ MaxPool 2x2 (+dropout)
 // x: [z][img][C][H][W] -> y: [z][img][C][H/2][W/2]; idx: window argmax (0..3, first max);
@@ -388,57 +250,6 @@ static int ew_grid(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(
 }  // namespace fh
 
 using namespace fh;
-
-extern "C" int fh_bn_fwd_train(const float* x, int64_t x_cs, float* y, int64_t y_cs,
-                               const float* res, int64_t res_cs, const float* gamma,
-                               const float* beta, int64_t p_cs, float* running_mean,
-                               float* running_var, int64_t r_cs, float* save_mean,
-                               float* save_invstd, const int32_t* counts, int32_t nclients,
-                               int32_t batch, int32_t C, int32_t HW, float eps, float momentum,
-                               int32_t relu, void* stream) {
-    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_train: bad shape");
-    if (nclients == 0) return FH_OK;
-    FH_REQUIRE(x && y && gamma && beta && save_mean && save_invstd, "bn_fwd_train: null pointer");
-    FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "bn_fwd_train: running stats");
-    hipLaunchKernelGGL(bn_fwd_train_kernel, dim3(C, nclients), dim3(256), 0, as_stream(stream), x,
-                       x_cs, y, y_cs, res, res_cs, gamma, beta, p_cs, running_mean, running_var,
-                       r_cs, save_mean, save_invstd, counts, batch, C, HW, eps, momentum, relu);
-    FH_LAUNCH_CHECK("bn_fwd_train");
-    return FH_OK;
-}
-
-extern "C" int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_cs,
-                              const float* res, int64_t res_cs, const float* gamma,
-                              const float* beta, int64_t p_cs, const float* running_mean,
-                              const float* running_var, int64_t r_cs, const int32_t* counts,
-                              int32_t nclients, int32_t batch, int32_t C, int32_t HW, float eps,
-                              int32_t relu, void* stream) {
-    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_eval: bad shape");
-    if (nclients == 0) return FH_OK;
-    FH_REQUIRE(x && y && gamma && beta && running_mean && running_var, "bn_fwd_eval: null pointer");
-    hipLaunchKernelGGL(bn_fwd_eval_kernel, dim3(C, nclients), dim3(256), 0, as_stream(stream), x,
-                       x_cs, y, y_cs, res, res_cs, gamma, beta, p_cs, running_mean, running_var,
-                       r_cs, counts, batch, C, HW, eps, relu);
-    FH_LAUNCH_CHECK("bn_fwd_eval");
-    return FH_OK;
-}
-
-extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs,
-                         const float* x, int64_t x_cs, const float* gamma, int64_t p_cs,
-                         const float* save_mean, const float* save_invstd, float* dx,
-                         int64_t dx_cs, float* dres, int64_t dres_cs, float* dgamma, float* dbeta,
-                         int64_t g_cs, const int32_t* counts, int32_t nclients, int32_t batch,
-                         int32_t C, int32_t HW, int32_t relu, void* stream) {
-    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_bwd: bad shape");
-    if (nclients == 0) return FH_OK;
-    FH_REQUIRE(dy && x && gamma && save_mean && save_invstd, "bn_bwd: null pointer");
-    FH_REQUIRE(!relu || yout, "bn_bwd: relu needs the forward output");
-    hipLaunchKernelGGL(bn_bwd_kernel, dim3(C, nclients), dim3(256), 0, as_stream(stream), dy,
-                       dy_cs, yout, yo_cs, x, x_cs, gamma, p_cs, save_mean, save_invstd, dx, dx_cs,
-                       dres, dres_cs, dgamma, dbeta, g_cs, counts, batch, C, HW, relu);
-    FH_LAUNCH_CHECK("bn_bwd");
-    return FH_OK;
-}
 
 extern "C" int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
                                int64_t i_cs, uint8_t* mask, int64_t m_cs, const int32_t* counts,

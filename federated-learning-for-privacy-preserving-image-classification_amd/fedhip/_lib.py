@@ -40,23 +40,28 @@ SIGNATURES = {
     "fh_dp_apply": (I32, [P, I64, P, I64, P, I64, I32, I64, P, P, P, P, I64, U64, P]),
     "fh_sgd_step": (I32, [P, P, P, I64, F32, F32, F32, I32, P]),
     "fh_adam_step": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, I32, F64, F64, P]),
+    "fh_conv2d_fwd_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
+    "fh_conv2d_dgrad_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "fh_conv2d_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
-                            I32, I32, I32, I32, I32, P]),
+                            I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_conv2d_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, I32,
-                              I32, I32, I32, I32, P]),
+                              I32, I32, I32, I32, P, SZ, P]),
     "fh_conv2d_wgrad_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "fh_conv2d_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32,
                               I32, I32, I32, I32, I32, I32, P]),
-    "fh_linear_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, P]),
-    "fh_linear_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, P]),
+    "fh_linear_fwd_workspace": (SZ, [I32, I32, I32, I32]),
+    "fh_linear_dgrad_workspace": (SZ, [I32, I32, I32, I32]),
+    "fh_linear_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_linear_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, P, SZ, P]),
     "fh_linear_wgrad_workspace": (SZ, [I32, I32, I32, I32]),
     "fh_linear_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32, P]),
+    "fh_bn_workspace": (SZ, [I32, I32, I32, I32]),
     "fh_bn_fwd_train": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, P, P, I32, I32,
-                              I32, I32, F32, F32, I32, P]),
+                              I32, I32, F32, F32, I32, P, SZ, P]),
     "fh_bn_fwd_eval": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, I32, I32, I32,
                              I32, F32, I32, P]),
     "fh_bn_bwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, P, P, I64, P, I64, P, P, I64, P,
-                        I32, I32, I32, I32, I32, P]),
+                        I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_maxpool2_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
                               F32, U64, P]),
     "fh_maxpool2_bwd": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I32,

@@ -55,10 +55,13 @@ class PackedTrainer:
         L = self.net.layout
         self.layout = L
         dev = self.device
-        self.params = torch.zeros(capacity, L.P, device=dev)
-        self.grads = torch.zeros(capacity, L.P, device=dev)
-        self.state1 = torch.zeros(capacity, L.P, device=dev)
-        self.state2 = torch.zeros(capacity, L.P, device=dev)
+        # rows padded to 64 floats (256 B): every client row starts 16-B aligned for the
+        # vectorised HBM kernels; padding stays 0 (zero gradients) and is never federated.
+        self.Ppad = ((L.P + 63) // 64) * 64
+        self.params = torch.zeros(capacity, self.Ppad, device=dev)
+        self.grads = torch.zeros(capacity, self.Ppad, device=dev)
+        self.state1 = torch.zeros(capacity, self.Ppad, device=dev)
+        self.state2 = torch.zeros(capacity, self.Ppad, device=dev)
         self.bufs = torch.zeros(capacity, max(L.Q, 1), device=dev)
         self.num_batches_tracked = [0] * capacity
         self.acc_loss = torch.zeros(capacity, dtype=torch.float64, device=dev)
@@ -123,7 +126,7 @@ class PackedTrainer:
 
     def _optimizer_step(self, n):
         self.opt_step += 1
-        cnt = n * self.layout.P
+        cnt = n * self.Ppad
         if self.opt_type == "sgd":
             ops.sgd_step(self.params, self.grads, self.state1, self.lr, 0.9,
                          first_step=(self.opt_step == 1), n=cnt)

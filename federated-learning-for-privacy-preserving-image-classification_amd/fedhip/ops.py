@@ -99,6 +99,21 @@ def _ws(device) -> Workspace:
     return _WS[key]
 
 
+_WS_SIZE: dict = {}
+
+
+def _ws_for(fn_name, device, *args):
+    """Scratch for a split-K launch; the size query is cached per shape."""
+    key = (fn_name,) + args
+    need = _WS_SIZE.get(key)
+    if need is None:
+        need = _WS_SIZE[key] = getattr(load(), fn_name)(*args)
+    if need == 0:
+        return None, 0
+    buf = _ws(device).get(need)
+    return buf, buf.numel()
+
+
 # ------------------------------------------------------------------ conv / linear
 def _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad):
     oh = (h + 2 * pad - k) // stride + 1
@@ -109,27 +124,31 @@ def _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad):
 def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad, relu=False,
                counts=None):
     require_device(x, "x")
+    ws, nb = _ws_for("fh_conv2d_fwd_workspace", x.device, nclients, batch, cin, h, wd, cout, k, k,
+                     stride, pad)
     ev = PROBE.begin(_conv_tag("fwd", cin, h, wd, cout, k, stride))
     call("fh_conv2d_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y),
          _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(relu),
-         stream_handle())
+         ptr(ws), nb, stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return y
 
 
 def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
                  accumulate=False):
+    ws, nb = _ws_for("fh_conv2d_dgrad_workspace", dy.device, nclients, batch, cin, h, wd, cout, k,
+                     k, stride, pad)
     ev = PROBE.begin(_conv_tag("dgrad", cin, h, wd, cout, k, stride))
     call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
-         nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(accumulate), stream_handle())
+         nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(accumulate), ptr(ws), nb,
+         stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return dx
 
 
 def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None):
-    lib = load()
-    need = lib.fh_conv2d_wgrad_workspace(nclients, batch, cin, h, wd, cout, k, k, stride, pad)
-    ws = _ws(x.device).get(need)
+    ws, _ = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, cin, h, wd, cout, k, k,
+                    stride, pad)
     ev = PROBE.begin(_conv_tag("wgrad", cin, h, wd, cout, k, stride))
     call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
          ptr(ws), ws.numel(), _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride,
@@ -140,21 +159,21 @@ def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pa
 
 def linear_fwd(x, w, bias, y, nclients, batch, in_f, out_f, relu=False, counts=None):
     require_device(x, "x")
+    ws, nb = _ws_for("fh_linear_fwd_workspace", x.device, nclients, batch, in_f, out_f)
     call("fh_linear_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y),
-         _counts(counts), nclients, batch, in_f, out_f, int(relu), stream_handle())
+         _counts(counts), nclients, batch, in_f, out_f, int(relu), ptr(ws), nb, stream_handle())
     return y
 
 
 def linear_dgrad(dy, w, dx, nclients, batch, in_f, out_f, counts=None):
+    ws, nb = _ws_for("fh_linear_dgrad_workspace", dy.device, nclients, batch, in_f, out_f)
     call("fh_linear_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
-         nclients, batch, in_f, out_f, stream_handle())
+         nclients, batch, in_f, out_f, ptr(ws), nb, stream_handle())
     return dx
 
 
 def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
-    lib = load()
-    need = lib.fh_linear_wgrad_workspace(nclients, batch, in_f, out_f)
-    ws = _ws(x.device).get(need)
+    ws, _ = _ws_for("fh_linear_wgrad_workspace", x.device, nclients, batch, in_f, out_f)
     call("fh_linear_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
          ptr(ws), ws.numel(), _counts(counts), nclients, batch, in_f, out_f, stream_handle())
     return dw
@@ -234,10 +253,11 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999
 # ------------------------------------------------------------------ BN / pool / dropout / CE
 def bn_fwd_train(x, y, gamma, beta, rmean, rvar, save_mean, save_invstd, nclients, batch, C, HW,
                  eps=1e-5, momentum=0.1, relu=False, res=None, counts=None):
+    ws, nb = _ws_for("fh_bn_workspace", x.device, nclients, batch, C, HW)
     call("fh_bn_fwd_train", ptr(x), _cs(x), ptr(y), _cs(y), ptr(res), _cs(res), ptr(gamma),
          ptr(beta), _cs(gamma), ptr(rmean), ptr(rvar), _cs(rmean), ptr(save_mean),
          ptr(save_invstd), _counts(counts), nclients, batch, C, HW, float(eps), float(momentum),
-         int(relu), stream_handle())
+         int(relu), ptr(ws), nb, stream_handle())
 
 
 def bn_fwd_eval(x, y, gamma, beta, rmean, rvar, nclients, batch, C, HW, eps=1e-5, relu=False,
@@ -249,10 +269,11 @@ def bn_fwd_eval(x, y, gamma, beta, rmean, rvar, nclients, batch, C, HW, eps=1e-5
 
 def bn_bwd(dy, yout, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclients, batch, C, HW,
            relu=False, dres=None, counts=None):
+    ws, nb = _ws_for("fh_bn_workspace", dy.device, nclients, batch, C, HW)
     call("fh_bn_bwd", ptr(dy), _cs(dy), ptr(yout), _cs(yout), ptr(x), _cs(x), ptr(gamma),
          _cs(gamma), ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dres), _cs(dres),
          ptr(dgamma), ptr(dbeta), _cs(dgamma), _counts(counts), nclients, batch, C, HW,
-         int(relu), stream_handle())
+         int(relu), ptr(ws), nb, stream_handle())
 
 
 def maxpool2_fwd(x, y, idx, nclients, batch, C, H, W, mask=None, drop_mode=0, p_drop=0.0, seed=0,

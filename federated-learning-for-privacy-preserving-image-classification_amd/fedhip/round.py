@@ -73,7 +73,7 @@ class RankRound:
         """One round. data/labels: this rank's train shards, slot k's at slot_offsets[k]."""
         tr = self.trainer
         S = len(self.slots)
-        tr.params[:S].copy_(self.global_flat.expand(S, -1))  # every client starts from global
+        tr.params[:S, :self.P].copy_(self.global_flat.expand(S, -1))  # all start from global
         sizes = [self.all_sizes[k] for k in self.slots]
         plan = tr.make_plan(sizes, self.epochs, generator=generator)
         metrics = tr.run_round(data, labels, slot_offsets, plan, optimizer_type=optimizer_type,
@@ -96,6 +96,6 @@ class RankRound:
                                  tr.seg_offsets, S)
         total, coef, clipped, sigma = ops.dp_clip_coef(sq, dp.max_grad_norm, dp.epsilon, dp.delta)
         g = self.global_flat.view(1, -1).expand(S, -1)
-        ops.dp_apply(tr.params, g, tr.params, coef, clipped, sigma,
+        ops.dp_apply(tr.params, g, tr.params, coef, clipped, sigma, P=self.P,
                      seed=(seed * 6364136223846793005 + 1442695040888963407) & ((1 << 64) - 1))
         self.last_dp = (total, clipped, sigma)

@@ -102,16 +102,27 @@ int fh_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg
 /* ---------------- convolution / linear (fp32 MFMA implicit GEMM) ----------
  * x: [clients][batch][cin][h][w]; w: [cout][cin][kh][kw] per client; y: [clients][batch][cout][oh][ow].
  * Supported: (kh,kw,stride) in {(3,3,1),(3,3,2),(1,1,1),(1,1,2)}, pad arbitrary. */
+/* FWD/DGRAD split K through `workspace` when the output tiling leaves the chip mostly
+ * idle (few clients still training); size it with fh_*_workspace (0 = never splits;
+ * a NULL / too-small workspace just disables the split). */
+size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
+                               int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad);
+size_t fh_conv2d_dgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
+                                 int32_t w_, int32_t cout, int32_t kh, int32_t kw, int32_t stride,
+                                 int32_t pad);
 int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs, const float* bias,
                   int64_t b_cs, float* y, int64_t y_cs, const int32_t* counts, int32_t nclients,
                   int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh,
-                  int32_t kw, int32_t stride, int32_t pad, int32_t relu, void* stream);
+                  int32_t kw, int32_t stride, int32_t pad, int32_t relu, void* workspace,
+                  size_t ws_bytes, void* stream);
 /* accumulate = 1: dx += result (residual-branch gradient sums, ResNet shortcut). */
 int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs, float* dx,
                     int64_t dx_cs, const int32_t* counts, int32_t nclients, int32_t batch,
                     int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
-                    int32_t stride, int32_t pad, int32_t accumulate, void* stream);
-/* dw (and db if non-NULL) are overwritten. workspace >= fh_conv2d_wgrad_workspace(...) bytes. */
+                    int32_t stride, int32_t pad, int32_t accumulate, void* workspace,
+                    size_t ws_bytes, void* stream);
+/* dw (and db if non-NULL) are overwritten; the conv-bias gradient is folded into the
+ * weight-gradient kernel.  workspace >= fh_conv2d_wgrad_workspace(...) bytes. */
 size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
                                  int32_t w_, int32_t cout, int32_t kh, int32_t kw, int32_t stride,
                                  int32_t pad);
@@ -122,12 +133,15 @@ int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs
                     void* stream);
 
 /* Linear: x [clients][batch][in_f], w [out_f][in_f], y [clients][batch][out_f]. */
+size_t fh_linear_fwd_workspace(int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f);
+size_t fh_linear_dgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f);
 int fh_linear_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs, const float* bias,
                   int64_t b_cs, float* y, int64_t y_cs, const int32_t* counts, int32_t nclients,
-                  int32_t batch, int32_t in_f, int32_t out_f, int32_t relu, void* stream);
+                  int32_t batch, int32_t in_f, int32_t out_f, int32_t relu, void* workspace,
+                  size_t ws_bytes, void* stream);
 int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs, float* dx,
                     int64_t dx_cs, const int32_t* counts, int32_t nclients, int32_t batch,
-                    int32_t in_f, int32_t out_f, void* stream);
+                    int32_t in_f, int32_t out_f, void* workspace, size_t ws_bytes, void* stream);
 size_t fh_linear_wgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f);
 int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs, float* dw,
                     int64_t dw_cs, float* db, int64_t db_cs, void* workspace, size_t ws_bytes,
@@ -139,12 +153,17 @@ int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs
  * rows (stride p_cs); running stats stride r_cs (NULL: not tracked);
  * save_mean/save_invstd: [clients][C].  Train mode: batch statistics over the
  * valid images (fp64 accumulation), running stats momentum-updated with the
- * unbiased variance.  y = relu?( x*alpha + beta' [+ res] ). */
+ * unbiased variance.  y = relu?( x*alpha + beta' [+ res] ).
+ * Each (client, channel) reduction is split over several workgroups; their
+ * partials go to `workspace` (>= fh_bn_workspace bytes, shared by train fwd
+ * and bwd) and are merged in a fixed order: results are deterministic. */
+size_t fh_bn_workspace(int32_t nclients, int32_t batch, int32_t C, int32_t HW);
 int fh_bn_fwd_train(const float* x, int64_t x_cs, float* y, int64_t y_cs, const float* res,
                     int64_t res_cs, const float* gamma, const float* beta, int64_t p_cs,
                     float* running_mean, float* running_var, int64_t r_cs, float* save_mean,
                     float* save_invstd, const int32_t* counts, int32_t nclients, int32_t batch,
-                    int32_t C, int32_t HW, float eps, float momentum, int32_t relu, void* stream);
+                    int32_t C, int32_t HW, float eps, float momentum, int32_t relu,
+                    void* workspace, size_t ws_bytes, void* stream);
 int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_cs, const float* res,
                    int64_t res_cs, const float* gamma, const float* beta, int64_t p_cs,
                    const float* running_mean, const float* running_var, int64_t r_cs,
@@ -155,7 +174,8 @@ int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs, 
               int64_t x_cs, const float* gamma, int64_t p_cs, const float* save_mean,
               const float* save_invstd, float* dx, int64_t dx_cs, float* dres, int64_t dres_cs,
               float* dgamma, float* dbeta, int64_t g_cs, const int32_t* counts, int32_t nclients,
-              int32_t batch, int32_t C, int32_t HW, int32_t relu, void* stream);
+              int32_t batch, int32_t C, int32_t HW, int32_t relu, void* workspace,
+              size_t ws_bytes, void* stream);
 
 /* ---------------- MaxPool2d(2,2) (+ fused Dropout after it) ---------------
  * idx: uint8 window argmax [clients][batch][C][H/2][W/2]; drop_mode 0 none,

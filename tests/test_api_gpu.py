@@ -139,7 +139,7 @@ def test_rank_round_dp_and_fedavg():
 
     def spy(S, seed):
         orig(S, seed)
-        captured["rows"] = rr.trainer.params[:S].clone()
+        captured["rows"] = rr.trainer.params[:S, :rr.P].clone()
     rr._apply_dp = spy
     rr.run(data, lab, offs, "sgd", 0.01, seed=3)
     rows = captured["rows"].cpu().numpy()

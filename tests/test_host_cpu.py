@@ -45,7 +45,7 @@ def test_error_path_without_gpu():
     """Argument validation runs on the host: a bad call fails with a message, no launch."""
     with pytest.raises(_lib.FedHipError, match="bad shape"):
         _lib.call("fh_conv2d_fwd", None, 0, None, 0, None, 0, None, 0, None, 1, 0, 1, 1, 1, 1,
-                  3, 3, 1, 1, 0, None)
+                  3, 3, 1, 1, 0, None, 0, None)
     with pytest.raises(_lib.FedHipError, match="invalid privacy parameters"):
         _lib.call("fh_dp_clip_coef", None, 1, 1, 1.0, -1.0, 1e-5, None, None, None, None, None)
 

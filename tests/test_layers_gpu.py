@@ -1,0 +1,117 @@
+"""BatchNorm2d (+ReLU, +residual) kernels vs a float64 torch reference of the same op,
+per client over its valid images (nn.BatchNorm2d train/eval, models_pytorch.py:108-120,
+176-187).  Shapes cover the split-reduction geometry: one client / many clients,
+small and large HW, HW % 4 != 0 (scalar path), ragged counts."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fedhip import ops
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+CASES = [  # (clients, batch, C, H, W)
+    (1, 32, 32, 32, 32),
+    (3, 32, 64, 16, 16),
+    (7, 32, 128, 8, 8),
+    (2, 32, 64, 4, 4),
+    (4, 16, 8, 7, 7),     # HW = 49: scalar path
+    (1, 8, 5, 3, 5),      # HW = 15
+]
+
+
+def _counts(nc, B, seed):
+    g = np.random.default_rng(seed)
+    c = [B] + [int(v) for v in g.integers(1, B + 1, size=nc - 1)]
+    return c
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("relu,residual", [(False, False), (True, False), (True, True)])
+def test_bn_train_fwd_bwd(case, relu, residual):
+    nc, B, C, H, W = case
+    HW = H * W
+    torch.manual_seed(sum(case) + relu + 2 * residual)
+    cnt = _counts(nc, B, sum(case))
+    x = torch.randn(nc, B, C, H, W, device=DEV) * 2 + 0.5
+    res = torch.randn_like(x) if residual else None
+    gamma = torch.rand(nc, C, device=DEV) + 0.5
+    beta = torch.randn(nc, C, device=DEV) * 0.1
+    rmean = torch.randn(nc, C, device=DEV) * 0.1
+    rvar = torch.rand(nc, C, device=DEV) + 0.5
+    rm0, rv0 = rmean.clone(), rvar.clone()
+    y = torch.zeros_like(x)
+    sm = torch.zeros(nc, C, device=DEV)
+    si = torch.zeros(nc, C, device=DEV)
+    counts = torch.tensor(cnt, dtype=torch.int32, device=DEV)
+    ops.bn_fwd_train(x, y, gamma, beta, rmean, rvar, sm, si, nc, B, C, HW, relu=relu, res=res,
+                     counts=counts)
+    dy = torch.randn_like(x)
+    dx = torch.zeros_like(x)
+    dres = torch.zeros_like(x) if residual else None
+    dg = torch.zeros(nc, C, device=DEV)
+    db = torch.zeros(nc, C, device=DEV)
+    ops.bn_bwd(dy, y, x, gamma, sm, si, dx, dg, db, nc, B, C, HW, relu=relu, dres=dres,
+               counts=counts)
+    torch.cuda.synchronize()
+    for z in range(nc):
+        n = cnt[z]
+        xr = x[z, :n].double().cpu().requires_grad_(True)
+        g = gamma[z].double().cpu().requires_grad_(True)
+        b = beta[z].double().cpu().requires_grad_(True)
+        rm, rv = rm0[z].double().cpu(), rv0[z].double().cpu()
+        out = F.batch_norm(xr, rm, rv, g, b, training=True, momentum=0.1, eps=1e-5)
+        if residual:
+            out = out + res[z, :n].double().cpu()
+        if relu:
+            out = F.relu(out)
+        out.backward(dy[z, :n].double().cpu())
+        yz = y[z, :n].double().cpu()
+        assert (yz - out.detach()).abs().max().item() <= 2e-5 * (1 + out.abs().max().item())
+        assert torch.allclose(rmean[z].double().cpu(), rm, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(rvar[z].double().cpu(), rv, rtol=1e-5, atol=1e-6)
+        # float32 arithmetic against fp64: tolerances relative to the gradient scale
+        gs = xr.grad.abs().max().item()
+        assert (dx[z, :n].double().cpu() - xr.grad).abs().max().item() <= 1e-4 * gs + 1e-6
+        assert torch.allclose(dg[z].double().cpu(), g.grad, rtol=1e-4, atol=1e-4)
+        assert torch.allclose(db[z].double().cpu(), b.grad, rtol=1e-4, atol=1e-4)
+        if residual:
+            gm = dy[z, :n] * (y[z, :n] > 0) if relu else dy[z, :n]
+            assert torch.equal(dres[z, :n], gm)
+
+
+@pytest.mark.parametrize("case", CASES[:3] + CASES[4:5])
+def test_bn_eval(case):
+    nc, B, C, H, W = case
+    HW = H * W
+    torch.manual_seed(7)
+    x = torch.randn(nc, B, C, H, W, device=DEV)
+    gamma = torch.rand(nc, C, device=DEV) + 0.5
+    beta = torch.randn(nc, C, device=DEV) * 0.1
+    rmean = torch.randn(nc, C, device=DEV) * 0.1
+    rvar = torch.rand(nc, C, device=DEV) + 0.5
+    y = torch.zeros_like(x)
+    ops.bn_fwd_eval(x, y, gamma, beta, rmean, rvar, nc, B, C, HW, relu=True)
+    for z in range(nc):
+        ref = F.relu(F.batch_norm(x[z].double(), rmean[z].double(), rvar[z].double(),
+                                  gamma[z].double(), beta[z].double(), training=False, eps=1e-5))
+        assert (y[z].double() - ref).abs().max().item() <= 1e-5 * (1 + ref.abs().max().item())
+
+
+def test_bn_deterministic():
+    nc, B, C, H, W = 2, 32, 32, 32, 32
+    torch.manual_seed(3)
+    x = torch.randn(nc, B, C, H, W, device=DEV)
+    gamma = torch.ones(nc, C, device=DEV)
+    beta = torch.zeros(nc, C, device=DEV)
+    outs = []
+    for _ in range(2):
+        y = torch.empty_like(x)
+        sm = torch.empty(nc, C, device=DEV)
+        si = torch.empty(nc, C, device=DEV)
+        ops.bn_fwd_train(x, y, gamma, beta, None, None, sm, si, nc, B, C, H * W)
+        outs.append((y, sm, si))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
