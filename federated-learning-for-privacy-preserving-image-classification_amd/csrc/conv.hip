@@ -310,6 +310,12 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     }
 }
 
+}  // namespace fh
+
+#include "dconv_kernels.h"
+
+namespace fh {
+
 // Split-K sums, deterministic: 64 outputs per block, 4 wave-groups each summing an
 // interleaved quarter of the splits, combined in a fixed order.  Blocks past the
 // weight part reduce the conv-bias partials the WGRAD kernel folded in.
@@ -516,6 +522,91 @@ static int run_mn(ConvArgs a, int kh, int kw, int stride, int nclients, void* ws
     return FH_OK;
 }
 
+// ---- direct 3x3 conv (dconv_kernels.h) planning ---------------------------
+struct DPlan {
+    int bm, ck, splits, cchunk;
+};
+
+static bool dconv_supported(int h, int w, int kh, int kw, int stride, int pad) {
+    return kh == 3 && kw == 3 && stride == 1 && pad == 1 && h == w && (w == 8 || w == 16 || w == 32);
+}
+
+static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients) {
+    const int64_t tn = ceil_div((int64_t)batch * hw, 256);
+    DPlan p{32, 8, 1, Cr};
+    for (int bm : {128, 64}) {
+        if (M >= bm && tn * ceil_div(M, bm) * nclients >= 1024) {
+            p.bm = bm;
+            break;
+        }
+    }
+    p.ck = (p.bm == 128 || Cr <= 4) ? 4 : 8;
+    const int64_t blocks = tn * ceil_div(M, p.bm) * nclients;
+    const int chunks = (int)ceil_div(Cr, p.ck);
+    if (blocks < 512 && chunks > 1) {
+        int want = (int)std::min<int64_t>(ceil_div(1024, blocks), chunks);
+        const int per = (int)ceil_div(chunks, want);
+        p.cchunk = per * p.ck;
+        p.splits = (int)ceil_div(Cr, p.cchunk);
+    }
+    if (p.splits <= 1) {
+        p.splits = 1;
+        p.cchunk = Cr;
+    }
+    return p;
+}
+
+static size_t dconv_ws_bytes(const DPlan& p, int nclients, int M, int batch, int hw) {
+    return p.splits > 1 ? (size_t)nclients * p.splits * M * batch * hw * sizeof(float) : 0;
+}
+
+template <int OP, int W>
+static int dconv_launch_w(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_t st) {
+#define FH_DC(BM, WMV, CK)                                                                      \
+    if (p.bm == BM && p.ck == CK) {                                                             \
+        hipLaunchKernelGGL((dconv_kernel<OP, W, BM, WMV, CK>), grid, dim3(256), 0, st, a);     \
+        return FH_OK;                                                                           \
+    }
+    FH_DC(32, 1, 8)
+    FH_DC(32, 1, 4)
+    FH_DC(64, 2, 8)
+    FH_DC(128, 2, 4)
+#undef FH_DC
+    set_error("dconv: no instantiation bm=%d ck=%d", p.bm, p.ck);
+    return FH_E_UNSUPPORTED;
+}
+
+template <int OP>
+static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes, int sp,
+                     hipStream_t st, const char* name) {
+    DPlan p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients);
+    if (p.splits > 1 && (!ws || ws_bytes < dconv_ws_bytes(p, nclients, a.M, a.batch, sp))) {
+        p.splits = 1;
+        p.cchunk = a.Cr;
+    }
+    a.splits = p.splits;
+    a.cchunk = p.cchunk;
+    a.Nfull = a.batch * sp;
+    float* out = a.out;
+    if (p.splits > 1) a.out = (float*)ws;
+    dim3 grid((unsigned)ceil_div(a.Nfull, 256), (unsigned)ceil_div(a.M, p.bm),
+              (unsigned)(nclients * p.splits));
+    int rc = w == 32 ? dconv_launch_w<OP, 32>(p, grid, a, st)
+           : w == 16 ? dconv_launch_w<OP, 16>(p, grid, a, st)
+                     : dconv_launch_w<OP, 8>(p, grid, a, st);
+    if (rc) return rc;
+    FH_LAUNCH_CHECK(name);
+    if (p.splits > 1) {
+        dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
+        hipLaunchKernelGGL(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
+                           a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
+                           OP == OP_FWD ? a.relu : 0, OP == OP_FWD ? 0 : a.accumulate, a.counts,
+                           a.batch, sp);
+        FH_LAUNCH_CHECK(name);
+    }
+    return FH_OK;
+}
+
 }  // namespace fh
 
 using namespace fh;
@@ -525,6 +616,9 @@ extern "C" size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32
                                           int32_t stride, int32_t pad) {
     int oh = (h + 2 * pad - kh) / stride + 1, ow = (w_ + 2 * pad - kw) / stride + 1;
     if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
+    if (dconv_supported(h, w_, kh, kw, stride, pad))
+        return dconv_ws_bytes(plan_dconv(cout, cin, batch, h * w_, nclients), nclients, cout, batch,
+                              h * w_);
     return mn_ws_bytes(plan_mn(cout, batch * oh * ow, cin * kh * kw, nclients), nclients);
 }
 
@@ -533,6 +627,9 @@ extern "C" size_t fh_conv2d_dgrad_workspace(int32_t nclients, int32_t batch, int
                                             int32_t kw, int32_t stride, int32_t pad) {
     int oh = (h + 2 * pad - kh) / stride + 1, ow = (w_ + 2 * pad - kw) / stride + 1;
     if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
+    if (dconv_supported(h, w_, kh, kw, stride, pad))
+        return dconv_ws_bytes(plan_dconv(cin, cout, batch, h * w_, nclients), nclients, cin, batch,
+                              h * w_);
     return mn_ws_bytes(plan_mn(cin, batch * h * w_, cout * kh * kw, nclients), nclients);
 }
 
@@ -547,6 +644,14 @@ extern "C" int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64
     if (rc) return rc;
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && w && y, "conv2d_fwd: null pointer");
+    if (dconv_supported(h, w_, kh, kw, stride, pad)) {
+        DConvArgs d{};
+        d.in = x; d.wt = w; d.bias = bias; d.out = y;
+        d.in_cs = x_cs; d.w_cs = w_cs; d.b_cs = b_cs; d.out_cs = y_cs;
+        d.counts = counts; d.batch = batch; d.Cr = cin; d.M = cout; d.relu = relu;
+        return run_dconv<OP_FWD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
+                                 "conv2d_fwd");
+    }
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
     a.x = x; a.wt = w; a.bias = bias; a.out = y;
     a.x_cs = x_cs; a.w_cs = w_cs; a.b_cs = b_cs; a.out_cs = y_cs;
@@ -567,6 +672,14 @@ extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, i
     if (rc) return rc;
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(dy && w && dx, "conv2d_dgrad: null pointer");
+    if (dconv_supported(h, w_, kh, kw, stride, pad)) {
+        DConvArgs d{};
+        d.in = dy; d.wt = w; d.out = dx;
+        d.in_cs = dy_cs; d.w_cs = w_cs; d.out_cs = dx_cs;
+        d.counts = counts; d.batch = batch; d.Cr = cout; d.M = cin; d.accumulate = accumulate;
+        return run_dconv<OP_DGRAD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
+                                   "conv2d_dgrad");
+    }
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
     a.dy = dy; a.wt = w; a.out = dx;
     a.dy_cs = dy_cs; a.w_cs = w_cs; a.out_cs = dx_cs;

@@ -1,0 +1,246 @@
+// dconv_kernels.h — direct 3x3 / stride 1 / pad 1 convolution on fp32 MFMA, input
+// patch staged once in LDS (included by conv.hip: one translation unit).
+//
+// The generic implicit GEMM (igemm_kernel) gathers every im2col element from
+// global memory: 9 loads and their address arithmetic per input value, which
+// on the CIFAR layers costs as many VALU cycles as the MFMAs it feeds.  Here a
+// workgroup owns 256 consecutive output pixels (TR whole rows of width W, one
+// image or several small ones) x BM output channels and stages, per chunk of
+// CK reduction channels,
+//   * the input rows its pixels touch, with a zero halo, once:
+//       Ps[ch][patch_row][W+2]      (the 3x3 shifts become LDS address offsets)
+//   * the weights as As[(kh*3+kw)*CK + ch][m]
+// so one staged value feeds up to 9 MFMA operands and the inner loop is pure
+// ds_read_b32 (compile-time immediates) + v_mfma_f32_32x32x2_f32.
+// The K order pairs channels (ch, ch+1) at the same (kh,kw), so the two
+// k-values one MFMA consumes (lanes 0-31 / 32-63) sit exactly one channel
+// stride apart in both images.
+//
+//   FWD   : Y[m][pix]  = sum_{ch,kh,kw} W[m][ch][kh][kw]     X[ch][pix + (kh-1, kw-1)]
+//   DGRAD : dX[m][pix] = sum_{ch,kh,kw} W[ch][m][2-kh][2-kw] dY[ch][pix + (kh-1, kw-1)]
+// (dgrad of a stride-1 pad-1 3x3 conv is the same stencil on dY with the
+// weights transposed and flipped).
+#pragma once
+
+namespace fh {
+
+struct DConvArgs {
+    const float* in;   // X (FWD) or dY (DGRAD): [client][img][Cr][H][W]
+    const float* wt;   // [client] W[cout][cin][3][3]
+    const float* bias;
+    float* out;        // [client][img][M][H][W], or the split-K slab
+    int64_t in_cs, w_cs, b_cs, out_cs;
+    const int32_t* counts;
+    int batch, Cr, M;  // Cr: reduction channels; M: output channels
+    int relu, accumulate;
+    int splits, cchunk;  // reduction channels per split (multiple of CK)
+    int Nfull;           // batch * H * W (slab row length)
+};
+
+template <int W>
+struct DGeom {
+    static constexpr int H = W;                       // square images (CIFAR 32/16/8)
+    static constexpr int HW = H * W;
+    static constexpr int TR = 256 / W;                // output rows per tile
+    static constexpr int SEGR = TR < H ? TR : H;      // rows per image segment in a tile
+    static constexpr int NI = TR / SEGR;              // image segments per tile
+    static constexpr int PW = W + 2;                  // patch row pitch
+    static constexpr int PR = NI * (SEGR + 2);        // patch rows
+    static constexpr int CSTR = PR * PW;              // patch channel stride
+    static_assert(256 % W == 0 && (TR % H == 0 || H % TR == 0), "tile geometry");
+};
+
+template <int OP, int W, int BM, int WAVES_M, int CK>
+__global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
+    using G = DGeom<W>;
+    constexpr int WAVES_N = 4 / WAVES_M;
+    constexpr int WM = BM / WAVES_M, WN = 256 / WAVES_N;
+    constexpr int FM = WM / 32, FN = WN / 32;
+    constexpr int BMP = BM + 1;                 // As row pitch (staging writes spread banks)
+    constexpr int KS = 9 * CK;                  // k-values per stage
+    constexpr int NA = (BM * KS + 255) / 256;   // A elements per thread
+    constexpr int PE = CK * G::CSTR;            // patch elements per stage
+    constexpr int NP = (PE + 255) / 256;
+    static_assert(FM >= 1 && FN >= 1 && (CK % 2) == 0, "dconv tile");
+
+    __shared__ float As[2][KS * BMP];
+    __shared__ float Ps[2][PE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WAVES_N, wn = wid % WAVES_N;
+    const int z = blockIdx.z / a.splits;
+    const int split = blockIdx.z - z * a.splits;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int t = blockIdx.x, m0 = blockIdx.y * BM;
+    const int n0 = t * 256;
+    if (n0 >= cnt * G::HW) return;
+    const int cbeg = split * a.cchunk;
+    const int cend = min(a.Cr, cbeg + a.cchunk);
+    const int M = a.M;
+
+    // ---- per-thread staging coordinates (fixed across K-steps) ----------
+    const int img0 = (t * G::TR) / G::H, y0 = (t * G::TR) % G::H;
+    int poff[NP];      // source offset within the client tensor, channel 0 of the chunk
+    int pch[NP];       // local channel, or -1 when the element is halo / out of range
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int e = tid + i * 256;
+        const int cl = e / G::CSTR, rem = e % G::CSTR;
+        const int pr = rem / G::PW, pc = rem % G::PW;
+        const int seg = pr / (G::SEGR + 2), rr = pr % (G::SEGR + 2);
+        const int img = img0 + seg, y = y0 + rr - 1, x = pc - 1;
+        const bool ok = e < PE && img < cnt && (unsigned)y < (unsigned)G::H &&
+                        (unsigned)x < (unsigned)W;
+        pch[i] = ok ? cl : -1;
+        poff[i] = ok ? ((img * a.Cr + cl) * G::H + y) * W + x : 0;
+    }
+    const float* inz = a.in + z * a.in_cs;
+    const float* wz = a.wt + z * a.w_cs;
+
+    float rp[NP], ra[NA];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+            rp[i] = (pch[i] >= 0 && c0 + pch[i] < cend) ? inz[poff[i] + (int64_t)c0 * G::HW] : 0.f;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int e = tid + i * 256;
+            float v = 0.f;
+            if (OP == OP_FWD) {
+                // e -> (m, cl, r9), r9 fastest: W[m][c0+cl][r9] contiguous per m
+                const int m = e / KS, rem = e % KS, cl = rem / 9, r9 = rem % 9;
+                if (e < BM * KS && m0 + m < M && c0 + cl < cend)
+                    v = wz[((int64_t)(m0 + m) * a.Cr + c0 + cl) * 9 + r9];
+            } else {
+                // e -> (cl, m, r9): W[c0+cl][m0+m][8-r9] contiguous per cl
+                const int cl = e / (BM * 9), rem = e % (BM * 9), m = rem / 9, r9 = rem % 9;
+                if (e < BM * KS && m0 + m < M && c0 + cl < cend)
+                    v = wz[((int64_t)(c0 + cl) * M + m0 + m) * 9 + (8 - r9)];
+            }
+            ra[i] = v;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int e = tid + i * 256;
+            if (e < PE) Ps[buf][e] = rp[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int e = tid + i * 256;
+            if (e < BM * KS) {
+                int m, cl, r9;
+                if (OP == OP_FWD) {
+                    m = e / KS;
+                    const int rem = e % KS;
+                    cl = rem / 9;
+                    r9 = rem % 9;
+                } else {
+                    cl = e / (BM * 9);
+                    const int rem = e % (BM * 9);
+                    m = rem / 9;
+                    r9 = rem % 9;
+                }
+                As[buf][(r9 * CK + cl) * BMP + m] = ra[i];
+            }
+        }
+    };
+
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // lane operand bases: half h = lane>>5 takes the odd channel of each pair
+    const int h = lane >> 5, col = lane & 31;
+    const int a_lane = h * BMP + wm * WM + col;
+    int b_lane[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int n = wn * WN + j * 32 + col;  // local pixel
+        const int ir = n / W, c = n % W;
+        const int seg = ir / G::SEGR, lr = ir % G::SEGR;
+        b_lane[j] = h * G::CSTR + (seg * (G::SEGR + 2) + lr) * G::PW + c;
+    }
+
+    if (cbeg < cend) {
+        load(cbeg);
+        store(0);
+        __syncthreads();
+        int buf = 0;
+        for (int c0 = cbeg; c0 < cend; c0 += CK) {
+            const bool more = c0 + CK < cend;
+            if (more) load(c0 + CK);
+            const float* Ab = &As[buf][a_lane];
+            const float* Pb = &Ps[buf][0];
+#pragma unroll
+            for (int s = 0; s < 9; ++s) {
+                const int kh = s / 3, kw = s % 3;
+#pragma unroll
+                for (int cp = 0; cp < CK / 2; ++cp) {
+                    float av[FM], bv[FN];
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) av[i] = Ab[(s * CK + 2 * cp) * BMP + i * 32];
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        bv[j] = Pb[b_lane[j] + 2 * cp * G::CSTR + kh * G::PW + kw];
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int j = 0; j < FN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j],
+                                                                             0, 0, 0);
+                }
+            }
+            if (more) store(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
+    }
+
+    // ---- epilogue: lanes = 32 consecutive pixels -> coalesced stores ----
+    const int rbase = 4 * h;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WN + j * 32 + col;
+        const int img = n / G::HW, p = n % G::HW;
+        if (img >= cnt) continue;
+        if (a.splits > 1) {
+            float* op = a.out + ((int64_t)blockIdx.z * M) * a.Nfull + n;
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                    if (m < M) op[(int64_t)m * a.Nfull] = acc[i][j][r];
+                }
+        } else {
+            float* op = a.out + z * a.out_cs + (int64_t)img * M * G::HW + p;
+            const float* bz = a.bias ? a.bias + z * a.b_cs : nullptr;
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                    if (m < M) {
+                        float v = acc[i][j][r];
+                        float* q = op + (int64_t)m * G::HW;
+                        if (OP == OP_FWD) {
+                            if (bz) v = v + bz[m];
+                            if (a.relu) v = fmaxf(v, 0.f);
+                        } else if (a.accumulate) {
+                            v = *q + v;
+                        }
+                        *q = v;
+                    }
+                }
+        }
+    }
+}
+
+}  // namespace fh

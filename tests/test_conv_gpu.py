@@ -36,6 +36,13 @@ CASES = [
     (2, 4, 64, 16, 16, 128, 1, 2, 0),
     (2, 4, 128, 8, 8, 256, 3, 2, 1),
     (1, 2, 96, 7, 9, 40, 3, 1, 1),
+    # direct-conv path (3x3/s1/p1, square 32/16/8): full tiles, split-K, multi-image tiles
+    (4, 32, 32, 32, 32, 32, 3, 1, 1),
+    (1, 32, 32, 32, 32, 32, 3, 1, 1),
+    (2, 32, 64, 16, 16, 64, 3, 1, 1),
+    (3, 30, 128, 8, 8, 128, 3, 1, 1),
+    (1, 32, 128, 8, 8, 128, 3, 1, 1),
+    (2, 7, 64, 8, 8, 64, 3, 1, 1),
 ]
 
 
@@ -72,6 +79,29 @@ def test_conv_fwd_bwd(case):
         _close(dx[z, :n], xr.grad, cout * k * k, f"dgrad z={z}")
         _close(dw[z], wr.grad, n * oh * ow, f"wgrad z={z}")
         _close(db[z], br.grad, n * oh * ow, f"bgrad z={z}")
+
+
+@pytest.mark.parametrize("case", [(2, 9, 32, 32, 32, 64), (3, 16, 64, 16, 16, 32),
+                                  (1, 32, 128, 8, 8, 128)])
+def test_conv_relu_and_accumulate(case):
+    """Fused ReLU epilogue (fwd) and dx += (dgrad into a residual gradient)."""
+    C, B, cin, h, w, cout = case
+    g = torch.Generator().manual_seed(99)
+    x = torch.randn(C, B, cin, h, w, generator=g).to(DEV)
+    wt = (torch.randn(C, cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)).to(DEV)
+    bias = torch.randn(C, cout, generator=g).to(DEV)
+    dy = torch.randn(C, B, cout, h, w, generator=g).to(DEV)
+    y = torch.zeros(C, B, cout, h, w, device=DEV)
+    y2 = torch.zeros_like(y)
+    ops.conv2d_fwd(x, wt, bias, y, C, B, cin, h, w, cout, 3, 1, 1)
+    ops.conv2d_fwd(x, wt, bias, y2, C, B, cin, h, w, cout, 3, 1, 1, relu=True)
+    assert torch.equal(y2, torch.relu(y))
+    base = torch.randn(C, B, cin, h, w, generator=g).to(DEV)
+    dx = torch.zeros_like(base)
+    ops.conv2d_dgrad(dy, wt, dx, C, B, cin, h, w, cout, 3, 1, 1)
+    acc = base.clone()
+    ops.conv2d_dgrad(dy, wt, acc, C, B, cin, h, w, cout, 3, 1, 1, accumulate=True)
+    assert torch.equal(acc, base + dx)
 
 
 @pytest.mark.parametrize("C,B,inf,outf", [(3, 32, 3136, 128), (2, 17, 128, 10), (2, 32, 2048, 512)])

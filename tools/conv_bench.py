@@ -1,0 +1,50 @@
+"""Per-layer conv timing (CIFAR10CNN shapes) for the fwd / dgrad / wgrad kernels."""
+import sys
+import os
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..",
+                                "federated-learning-for-privacy-preserving-image-classification_amd"))
+import torch
+from fedhip import ops
+
+LAYERS = [(3, 32, 32), (32, 32, 32), (32, 64, 16), (64, 64, 16), (64, 128, 8), (128, 128, 8)]
+
+
+def timeit(fn, it=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it
+
+
+def main():
+    dev = torch.device("cuda")
+    B = 32
+    for C in (32, 1):
+        for cin, cout, hw in LAYERS:
+            x = torch.randn(C, B, cin, hw, hw, device=dev)
+            w = torch.randn(C, cout, cin, 3, 3, device=dev) * 0.1
+            b = torch.randn(C, cout, device=dev)
+            y = torch.empty(C, B, cout, hw, hw, device=dev)
+            dy = torch.randn_like(y)
+            dx = torch.empty_like(x)
+            dw = torch.empty_like(w)
+            db = torch.empty_like(b)
+            fl = 2.0 * C * B * hw * hw * cout * cin * 9
+            tf = ops.conv2d_fwd
+            t1 = timeit(lambda: tf(x, w, b, y, C, B, cin, hw, hw, cout, 3, 1, 1))
+            t2 = timeit(lambda: ops.conv2d_dgrad(dy, w, dx, C, B, cin, hw, hw, cout, 3, 1, 1))
+            t3 = timeit(lambda: ops.conv2d_wgrad(x, dy, dw, db, C, B, cin, hw, hw, cout, 3, 1, 1))
+            print(f"C={C:2d} {cin:3d}->{cout:3d} {hw:2d}x{hw:<2d}  fwd {t1*1e3:7.1f}us {fl/t1/1e9:6.1f}TF"
+                  f"  dgrad {t2*1e3:7.1f}us {fl/t2/1e9:6.1f}TF  wgrad {t3*1e3:7.1f}us {fl/t3/1e9:6.1f}TF",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
