@@ -607,6 +607,50 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     return FH_OK;
 }
 
+// ---- direct 3x3 wgrad planning -------------------------------------------
+struct DWPlan {
+    int wco, wci, wpx, sr, splits, sps;
+};
+
+static bool dwgrad_supported(int cin, int cout, int h, int w, int kh, int kw, int stride, int pad) {
+    return dconv_supported(h, w, kh, kw, stride, pad) && cin % 32 == 0 && cout % 32 == 0;
+}
+
+static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
+    DWPlan p{1, 1, 4, 128 / w, 1, 1};
+    if (cout % 64 == 0 && cin % 64 == 0) p = {2, 2, 1, 64 / w, 1, 1};
+    else if (cout % 64 == 0) p = {2, 1, 2, 128 / w, 1, 1};
+    else if (cin % 64 == 0) p = {1, 2, 2, 128 / w, 1, 1};
+    const int64_t tiles = (int64_t)(cout / (32 * p.wco)) * (cin / (32 * p.wci)) * nclients;
+    const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
+    const int want = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(1024, tiles)), nst);
+    p.sps = (int)ceil_div(nst, want);
+    p.splits = (int)ceil_div(nst, p.sps);
+    return p;
+}
+
+static size_t dwgrad_ws_bytes(const DWPlan& p, int nclients, int M, int N) {
+    const size_t wb = (size_t)nclients * p.splits * M * N * sizeof(float);
+    return ((wb + 255) / 256) * 256 + (size_t)nclients * p.splits * M * sizeof(float);
+}
+
+template <int W>
+static int dwgrad_launch_w(const DWPlan& p, dim3 grid, const DWArgs& a, hipStream_t st) {
+#define FH_DW(WCO, WCI, WPX, SPXV)                                                             \
+    if (p.wco == WCO && p.wci == WCI && p.wpx == WPX && p.sr * W == SPXV) {                   \
+        hipLaunchKernelGGL((dconv_wgrad_kernel<W, WCO, WCI, WPX, SPXV / W>), grid, dim3(256), 0, \
+                           st, a);                                                            \
+        return FH_OK;                                                                         \
+    }
+    FH_DW(1, 1, 4, 128)
+    FH_DW(2, 1, 2, 128)
+    FH_DW(1, 2, 2, 128)
+    FH_DW(2, 2, 1, 64)
+#undef FH_DW
+    set_error("dconv_wgrad: no instantiation");
+    return FH_E_UNSUPPORTED;
+}
+
 }  // namespace fh
 
 using namespace fh;
@@ -694,7 +738,11 @@ extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int
                                             int32_t stride, int32_t pad) {
     int oh = (h + 2 * pad - kh) / stride + 1, ow = (w_ + 2 * pad - kw) / stride + 1;
     if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
-    return wgrad_ws_bytes(plan_wgrad(cout, cin * kh * kw, batch * oh * ow, nclients), nclients);
+    size_t direct = 0;
+    if (dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad))  // (misaligned data: igemm)
+        direct = dwgrad_ws_bytes(plan_dwgrad(cout, cin, batch, w_, nclients), nclients, cout, cin * 9);
+    return std::max(direct, wgrad_ws_bytes(plan_wgrad(cout, cin * kh * kw, batch * oh * ow, nclients),
+                                           nclients));
 }
 
 extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
@@ -711,6 +759,36 @@ extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, in
     a.x = x; a.dy = dy;
     a.x_cs = x_cs; a.dy_cs = dy_cs;
     a.M = cout; a.N = cin * kh * kw; a.K = batch * oh * ow;
+    const bool aligned = ((uintptr_t)x % 16 == 0) && ((uintptr_t)dy % 16 == 0) && x_cs % 4 == 0 &&
+                         dy_cs % 4 == 0;
+    if (aligned && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
+        const DWPlan p = plan_dwgrad(cout, cin, batch, w_, nclients);
+        const size_t need = dwgrad_ws_bytes(p, nclients, a.M, a.N);
+        FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
+        DWArgs d{};
+        d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
+        d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
+        d.splits = p.splits; d.stages_per_split = p.sps;
+        d.part = (float*)workspace;
+        const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
+        d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
+        hipStream_t st = as_stream(stream);
+        dim3 grid((unsigned)p.splits, (unsigned)((cout / (32 * p.wco)) * (cin / (32 * p.wci))),
+                  (unsigned)nclients);
+        rc = w_ == 32 ? dwgrad_launch_w<32>(p, grid, d, st)
+           : w_ == 16 ? dwgrad_launch_w<16>(p, grid, d, st)
+                      : dwgrad_launch_w<8>(p, grid, d, st);
+        if (rc) return rc;
+        FH_LAUNCH_CHECK("conv2d_wgrad direct");
+        const int MN = a.M * a.N;
+        const int wblocks = (int)ceil_div(MN, 64);
+        const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
+        hipLaunchKernelGGL(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+                           (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
+                           (const float*)d.bias_part, db, db_cs, a.M);
+        FH_LAUNCH_CHECK("conv2d_wgrad reduce");
+        return FH_OK;
+    }
     Plan p = plan_wgrad(a.M, a.N, a.K, nclients);
     const size_t need = wgrad_ws_bytes(p, nclients);
     FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);

@@ -243,4 +243,224 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// WGRAD: dW[co][ci][kh][kw] = sum_pix dY[co][pix] * X[ci][pix + (kh-1, kw-1)]
+//
+// The reduction runs over pixels, so MFMA lanes must span co (A) and ci (B).
+// Each wave keeps nine 32x32 accumulators, one per (kh,kw) shift: per pixel
+// pair it reads one dY operand and nine shifted patch operands (the shift is
+// again an LDS immediate) for nine MFMAs.  A stage is SR rows (64 or 128
+// pixels) of dY (staged [pix][co]) and the matching X rows with zero halo
+// (staged [ci][row][W+2], channel stride odd so 32 channels on 32 lanes hit 32
+// banks).  The four waves tile (co, ci, pixel-rows); waves that split pixels
+// are summed through LDS in a fixed order.  Every workgroup writes its
+// partial for one pixel split into the slab [z][split][co][ci*9+s] (the conv
+// bias gradient = sum of dY rows rides along), reduced by splitk_sum_kernel.
+struct DWArgs {
+    const float* x;
+    const float* dy;
+    float* part;       // [z][split][M][N]
+    float* bias_part;  // [z][split][M] or null
+    int64_t x_cs, dy_cs;
+    const int32_t* counts;
+    int batch, cin, M, N;  // M = cout, N = cin*9
+    int splits, stages_per_split;
+};
+
+template <int W, int WCO, int WCI, int WPX, int SR>
+__global__ void __launch_bounds__(256) dconv_wgrad_kernel(const DWArgs a) {
+    constexpr int H = W, HW = H * W;
+    constexpr int SPX = SR * W;                     // pixels per stage
+    constexpr int SEGR = SR < H ? SR : H;
+    constexpr int NI = SR / SEGR;
+    constexpr int PW = W + 2, PR = NI * (SEGR + 2);
+    constexpr int CSTR = (PR * PW) | 1;
+    constexpr int BM = 32 * WCO, BN = 32 * WCI;
+    constexpr int BMP = BM + 1;
+    constexpr int RPW = SR / WPX;                   // rows per wave per stage
+    // staging with float4 global loads: dY rows of SPX pixels, patch rows of W pixels
+    constexpr int DQ = SPX / 4, COI = 256 / DQ, NDY = BM / COI;
+    constexpr int PQ = W / 4, RPI = 256 / PQ, NPR = BN * PR, NPT = (NPR + RPI - 1) / RPI;
+    constexpr int DSZ = SPX * BMP, PSZ = BN * CSTR, BUF = DSZ + PSZ;
+    static_assert(WCO * WCI * WPX == 4 && RPW >= 1 && SR % WPX == 0, "wave grid");
+    static_assert(BM % COI == 0 && (SR % H == 0 || H % SR == 0), "stage geometry");
+
+    __shared__ float smem[2 * BUF];   // double-buffered [Dys | Ps]
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wpx = wid % WPX, wci = (wid / WPX) % WCI, wco = wid / (WPX * WCI);
+    const int split = blockIdx.x, z = blockIdx.z;
+    const int ntile_ci = a.cin / BN;
+    const int co0 = (blockIdx.y / ntile_ci) * BM, ci0 = (blockIdx.y % ntile_ci) * BN;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int nst = (cnt * HW + SPX - 1) / SPX;
+    const int sbeg = split * a.stages_per_split;
+    const int send = min(nst, sbeg + a.stages_per_split);
+    const float* xz = a.x + z * a.x_cs;
+    const float* dyz = a.dy + z * a.dy_cs;
+    const bool do_bias = a.bias_part != nullptr && ci0 == 0;
+
+    // halo columns of the patch are always zero (pad = 1): write them once
+    for (int q = tid; q < 2 * NPR; q += 256) {
+        const int bsel = q / NPR, row = q % NPR, cl = row / PR, pr = row % PR;
+        float* r = smem + bsel * BUF + DSZ + cl * CSTR + pr * PW;
+        r[0] = 0.f;
+        r[W + 1] = 0.f;
+    }
+
+    const int dco = tid / DQ, dp = (tid % DQ) * 4;      // dY: channel row, pixel quad
+    const int prt = tid / PQ, px = (tid % PQ) * 4;       // patch: row, column quad
+    float4 rd[NDY], rp[NPT];
+    auto load = [&](int st) {
+        const int R0 = st * SR;
+        {
+            const int row = R0 + dp / W, img = row / H, y = row % H, xx = dp % W;
+            const float* src = dyz + ((int64_t)(img * a.M + co0 + dco) * H + y) * W + xx;
+            const bool ok = img < cnt;
+#pragma unroll
+            for (int i = 0; i < NDY; ++i)
+                rd[i] = ok ? *reinterpret_cast<const float4*>(src + (int64_t)i * COI * HW)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const int img0 = R0 / H, y0 = R0 % H;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int q = prt + i * RPI;
+            const int cl = q / PR, pr = q % PR;
+            const int seg = pr / (SEGR + 2), rr = pr % (SEGR + 2);
+            const int img = img0 + seg, y = y0 + rr - 1;
+            const bool ok = q < NPR && img < cnt && (unsigned)y < (unsigned)H;
+            rp[i] = ok ? *reinterpret_cast<const float4*>(
+                             xz + ((int64_t)(img * a.cin + ci0 + cl) * H + y) * W + px)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int bsel) {
+        float* D = smem + bsel * BUF;
+#pragma unroll
+        for (int i = 0; i < NDY; ++i) {
+            float* d = D + dp * BMP + dco + i * COI;
+            d[0] = rd[i].x;
+            d[BMP] = rd[i].y;
+            d[2 * BMP] = rd[i].z;
+            d[3 * BMP] = rd[i].w;
+        }
+        float* P = D + DSZ;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int q = prt + i * RPI;
+            if (q < NPR) {
+                float* d = P + (q / PR) * CSTR + (q % PR) * PW + 1 + px;
+                d[0] = rp[i].x;
+                d[1] = rp[i].y;
+                d[2] = rp[i].z;
+                d[3] = rp[i].w;
+            }
+        }
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[s][r] = 0.f;
+    float bsum = 0.f;
+
+    const int h = lane >> 5, col = lane & 31;
+    const int a_off = h * BMP + wco * 32 + col;
+    const int b_off = DSZ + (wci * 32 + col) * CSTR + h;
+    if (sbeg < send) {
+        load(sbeg);
+        store(0);
+        __syncthreads();
+        int bsel = 0;
+        for (int st = sbeg; st < send; ++st) {
+            const bool more = st + 1 < send;
+            if (more) load(st + 1);
+            const float* Al = smem + bsel * BUF + a_off;
+            const float* Bl = smem + bsel * BUF + b_off;
+#pragma unroll 1
+            for (int rr = 0; rr < RPW; ++rr) {
+                const int r = wpx * RPW + rr;                  // stage row
+                const int prow = (r / SEGR) * (SEGR + 2) + r % SEGR;
+                const float* Ar = Al + r * W * BMP;
+                const float* Br = Bl + prow * PW;
+#pragma unroll 4
+                for (int cp = 0; cp < W / 2; ++cp) {
+                    const float av = Ar[2 * cp * BMP];
+                    bsum += av;
+                    float bv[9];
+#pragma unroll
+                    for (int s = 0; s < 9; ++s) bv[s] = Br[(s / 3) * PW + 2 * cp + (s % 3)];
+#pragma unroll
+                    for (int s = 0; s < 9; ++s)
+                        acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[s], acc[s], 0, 0, 0);
+                }
+            }
+            if (more) store(bsel ^ 1);
+            __syncthreads();
+            bsel ^= 1;
+        }
+    }
+
+    // ---- combine the WPX pixel waves (fixed order), then write the slab --
+    __syncthreads();    // halo / staging writes retired before the scratch is reused
+    float* red = smem;  // staging LDS reused as reduction scratch
+    const int64_t slab = ((int64_t)z * a.splits + split) * a.M;
+    constexpr int WT = WCO * WCI;
+    if constexpr (WPX > 1) {
+        constexpr int SG = 3;  // shifts per round
+        static_assert((WPX - 1) * WT * SG * 16 * 64 <= 2 * BUF, "reduction scratch");
+#pragma unroll
+        for (int g = 0; g < 9; g += SG) {
+            if (wpx > 0) {
+#pragma unroll
+                for (int s = 0; s < SG; ++s)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        red[((((wpx - 1) * WT + wco * WCI + wci) * SG + s) * 16 + r) * 64 + lane] =
+                            acc[g + s][r];
+            }
+            __syncthreads();
+            if (wpx == 0) {
+#pragma unroll
+                for (int q = 1; q < WPX; ++q)
+#pragma unroll
+                    for (int s = 0; s < SG; ++s)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            acc[g + s][r] +=
+                                red[((((q - 1) * WT + wco * WCI + wci) * SG + s) * 16 + r) * 64 + lane];
+            }
+            __syncthreads();
+        }
+    }
+    // bias: lanes l and l+32 hold different pixels of the same co
+    if (do_bias) {  // block-uniform: every wave reaches the barrier
+        float* bred = red;
+        if (wci == 0) bred[wid * 64 + lane] = bsum;
+        __syncthreads();
+        if (wci == 0 && wpx == 0 && lane < 32) {
+            float v = 0.f;
+#pragma unroll
+            for (int q = 0; q < WPX; ++q) {
+                const int w2 = wco * WCI * WPX + q;  // wci == 0
+                v += bred[w2 * 64 + lane] + bred[w2 * 64 + lane + 32];
+            }
+            a.bias_part[slab + co0 + wco * 32 + lane] = v;
+        }
+    }
+    if (wpx == 0) {
+        float* op = a.part + slab * a.N;
+        const int ci = ci0 + wci * 32 + col;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+            for (int s = 0; s < 9; ++s) op[(int64_t)m * a.N + ci * 9 + s] = acc[s][r];
+        }
+    }
+}
+
 }  // namespace fh
