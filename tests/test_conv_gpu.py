@@ -132,3 +132,56 @@ def test_linear_fwd_bwd(C, B, inf, outf):
         _close(dx[z, :n], xr.grad, outf, "linear dgrad")
         _close(dw[z], wr.grad, n, "linear wgrad")
         _close(db[z], br.grad, n, "linear bgrad")
+
+
+EXACT = [  # nclients, batch, cin, h, cout, k, stride, pad (square maps)
+    (1, 32, 32, 32, 32, 3, 1, 1),
+    (2, 32, 32, 32, 64, 3, 1, 1),
+    (8, 32, 32, 32, 32, 3, 1, 1),
+    (3, 30, 64, 16, 64, 3, 1, 1),
+    (1, 32, 64, 16, 128, 3, 1, 1),
+    (5, 32, 128, 8, 128, 3, 1, 1),
+    (2, 13, 64, 8, 64, 3, 1, 1),
+    (2, 9, 3, 32, 32, 3, 1, 1),
+    (2, 8, 64, 16, 128, 3, 2, 1),
+    (2, 8, 64, 16, 128, 1, 2, 0),
+    (3, 6, 32, 28, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", EXACT)
+def test_conv_exact_integer(case):
+    """Small-integer operands: every product and partial sum is exact in fp32, so
+    any summation order gives the exact answer — the HIP results must equal the
+    fp64 reference bit for bit (catches a dropped or doubled term that a
+    relative tolerance at large K would hide)."""
+    C, B, cin, h, cout, k, s, p = case
+    w_ = h
+    g = torch.Generator().manual_seed(sum(case))
+    x = torch.randint(-2, 3, (C, B, cin, h, w_), generator=g).float()
+    wt = torch.randint(-2, 3, (C, cout, cin, k, k), generator=g).float()
+    bias = torch.randint(-2, 3, (C, cout), generator=g).float()
+    oh = (h + 2 * p - k) // s + 1
+    dy = torch.randint(-2, 3, (C, B, cout, oh, oh), generator=g).float()
+    counts = torch.tensor([B - (i * 3) % min(B, 7) for i in range(C)], dtype=torch.int32)
+    cd = counts.to(DEV)
+    y = torch.zeros(C, B, cout, oh, oh, device=DEV)
+    dx = torch.zeros(C, B, cin, h, w_, device=DEV)
+    dw = torch.zeros(C, cout, cin, k, k, device=DEV)
+    db = torch.zeros(C, cout, device=DEV)
+    xd, wd, dyd = x.to(DEV), wt.to(DEV), dy.to(DEV)
+    ops.conv2d_fwd(xd, wd, bias.to(DEV), y, C, B, cin, h, w_, cout, k, s, p, counts=cd)
+    ops.conv2d_dgrad(dyd, wd, dx, C, B, cin, h, w_, cout, k, s, p, counts=cd)
+    ops.conv2d_wgrad(xd, dyd, dw, db, C, B, cin, h, w_, cout, k, s, p, counts=cd)
+    torch.cuda.synchronize()
+    for z in range(C):
+        n = int(counts[z])
+        xr = x[z, :n].double().requires_grad_(True)
+        wr = wt[z].double().requires_grad_(True)
+        br = bias[z].double().requires_grad_(True)
+        yr = F.conv2d(xr, wr, br, stride=s, padding=p)
+        yr.backward(dy[z, :n].double())
+        assert torch.equal(y[z, :n].cpu().double(), yr.detach()), f"fwd z={z}"
+        assert torch.equal(dx[z, :n].cpu().double(), xr.grad), f"dgrad z={z}"
+        assert torch.equal(dw[z].cpu().double(), wr.grad), f"wgrad z={z}"
+        assert torch.equal(db[z].cpu().double(), br.grad), f"bgrad z={z}"

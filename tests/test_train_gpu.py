@@ -81,7 +81,12 @@ def check_params(gpu_named, ref32, ref64, init, steps, lr, opt):
             keep = ~out
         e_hip = (pg - p64)[keep].norm().item()
         e_cpu = (p32 - p64)[keep].norm().item()
-        tol = 4 * e_cpu + 1e-4 * (p64 - p0).norm().item() + 1e-7 * p64.norm().item() + 1e-12
+        # Adam divides each gradient element by its running RMS, so an fp32 rounding
+        # difference in a near-zero component (different but equally valid summation
+        # order: see the exact-integer conv tests) becomes an O(lr) update difference
+        # for that element; Adam runs are held to 0.1 % of the update norm, SGD to 0.01 %.
+        rel = 1e-3 if opt in ("adam", "adamw") else 1e-4
+        tol = 4 * e_cpu + rel * (p64 - p0).norm().item() + 1e-7 * p64.norm().item() + 1e-12
         assert e_hip <= tol, (f"{name}: |hip-fp64| {e_hip:.3e} > tol {tol:.3e} "
                               f"(|cpu32-fp64| {e_cpu:.3e})")
 
