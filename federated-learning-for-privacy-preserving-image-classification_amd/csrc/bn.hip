@@ -193,11 +193,23 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const BNArgs a) {
     float* drz = a.dres ? a.dres + z * a.dres_cs : nullptr;
     double sg = 0.0, dot = 0.0;
     for_slice(a, z, c, s, [&](int64_t o, int nv) {
-        for (int q = 0; q < nv; ++q) {
-            const float g = gmask(dyz[o + q], yoz, o + q);
-            if (drz) drz[o + q] = g;
+        if (nv == 4) {
+            float4 g = ld4(dyz + o);
+            if (yoz) {
+                const float4 yv = ld4(yoz + o);
+                g.x = yv.x > 0.f ? g.x : 0.f; g.y = yv.y > 0.f ? g.y : 0.f;
+                g.z = yv.z > 0.f ? g.z : 0.f; g.w = yv.w > 0.f ? g.w : 0.f;
+            }
+            if (drz) st4(drz + o, g);
+            const float4 xv = ld4(xz + o);
+            sg += ((double)g.x + (double)g.y) + ((double)g.z + (double)g.w);
+            dot += ((double)((xv.x - mean) * g.x) + (double)((xv.y - mean) * g.y)) +
+                   ((double)((xv.z - mean) * g.z) + (double)((xv.w - mean) * g.w));
+        } else {
+            const float g = gmask(dyz[o], yoz, o);
+            if (drz) drz[o] = g;
             sg += (double)g;
-            dot += (double)((xz[o + q] - mean) * g);
+            dot += (double)((xz[o] - mean) * g);
         }
     });
     sg = block_sum_256(sg, red);

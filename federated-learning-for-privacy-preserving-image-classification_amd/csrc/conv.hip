@@ -256,8 +256,12 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     }
 
     // ---------------- epilogue ------------------------------------------
-    if (do_bias && tid < BM && m0 + tid < M)
-        a.bias_part[(int64_t)blockIdx.z * a.M + m0 + tid] = bsum;
+    // WGRAD with one split writes dW / db in place (no slab, no reduce pass)
+    const bool wdirect = (OP == OP_WGRAD) && a.splits == 1;
+    if (do_bias && tid < BM && m0 + tid < M) {
+        if (wdirect) a.bias_part[z * a.b_cs + m0 + tid] = bsum;
+        else a.bias_part[(int64_t)blockIdx.z * a.M + m0 + tid] = bsum;
+    }
     // acc[i][j][r]: row m = (r&3) + 8*(r>>2) + 4*(lane>>5), col n = lane&31.
     const int rbase = 4 * (lane >> 5), col = lane & 31;
 #pragma unroll
@@ -265,8 +269,10 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
         const int n = n0 + wn * WN + j * 32 + col;
         if (n >= N) continue;
         if (partial_out) {
-            // split-K partial slab part[z][split][m][n] (n over the full-batch extent a.N)
-            float* op = a.out + ((int64_t)blockIdx.z * a.M) * a.N + n;
+            // split-K partial slab part[z][split][m][n] (n over the full-batch extent a.N),
+            // or dW itself (row stride N, client stride out_cs)
+            float* op = wdirect ? a.out + z * a.out_cs + n
+                                : a.out + ((int64_t)blockIdx.z * a.M) * a.N + n;
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -457,6 +463,7 @@ static size_t mn_ws_bytes(const Plan& p, int nclients) {
 }
 
 static size_t wgrad_ws_bytes(const Plan& p, int nclients) {
+    if (p.splits == 1) return 0;  // written in place
     const size_t w = (size_t)nclients * p.splits * p.M * p.N * sizeof(float);
     const size_t b = (size_t)nclients * p.splits * p.M * sizeof(float);
     return ((w + 255) / 256) * 256 + b;
@@ -531,10 +538,11 @@ static bool dconv_supported(int h, int w, int kh, int kw, int stride, int pad) {
     return kh == 3 && kw == 3 && stride == 1 && pad == 1 && h == w && (w == 8 || w == 16 || w == 32);
 }
 
-static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients) {
+static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
     DPlan p{32, 8, 1, Cr};
     for (int bm : {128, 64}) {
+        if (Cr <= 4 || force_bm32) break;  // tiny-Cin first layer / scalar staging: BM=32
         if (M >= bm && tn * ceil_div(M, bm) * nclients >= 1024) {
             p.bm = bm;
             break;
@@ -562,15 +570,17 @@ static size_t dconv_ws_bytes(const DPlan& p, int nclients, int M, int batch, int
 
 template <int OP, int W>
 static int dconv_launch_w(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_t st) {
-#define FH_DC(BM, WMV, CK)                                                                      \
-    if (p.bm == BM && p.ck == CK) {                                                             \
-        hipLaunchKernelGGL((dconv_kernel<OP, W, BM, WMV, CK>), grid, dim3(256), 0, st, a);     \
+#define FH_DC(BM, WMV, CK, VEC)                                                                 \
+    if (p.bm == BM && p.ck == CK && (a.wvec != 0) == VEC) {                                     \
+        hipLaunchKernelGGL((dconv_kernel<OP, W, BM, WMV, CK, VEC>), grid, dim3(256), 0, st, a);\
         return FH_OK;                                                                           \
     }
-    FH_DC(32, 1, 8)
-    FH_DC(32, 1, 4)
-    FH_DC(64, 2, 8)
-    FH_DC(128, 2, 4)
+    FH_DC(32, 1, 8, true)
+    FH_DC(32, 1, 4, true)
+    FH_DC(64, 2, 8, true)
+    FH_DC(128, 2, 4, true)
+    FH_DC(32, 1, 8, false)
+    FH_DC(32, 1, 4, false)
 #undef FH_DC
     set_error("dconv: no instantiation bm=%d ck=%d", p.bm, p.ck);
     return FH_E_UNSUPPORTED;
@@ -580,6 +590,10 @@ template <int OP>
 static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes, int sp,
                      hipStream_t st, const char* name) {
     DPlan p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients);
+    const bool aligned = ((uintptr_t)a.wt % 16 == 0) && a.w_cs % 4 == 0;
+    if (!(aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0)) && p.bm != 32) {
+        p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients, /*force_bm32=*/true);  // scalar staging
+    }
     if (p.splits > 1 && (!ws || ws_bytes < dconv_ws_bytes(p, nclients, a.M, a.batch, sp))) {
         p.splits = 1;
         p.cchunk = a.Cr;
@@ -587,6 +601,8 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     a.splits = p.splits;
     a.cchunk = p.cchunk;
     a.Nfull = a.batch * sp;
+    // float4 weight runs: 16-B aligned slices that never run past the tensor
+    a.wvec = aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0);
     float* out = a.out;
     if (p.splits > 1) a.out = (float*)ws;
     dim3 grid((unsigned)ceil_div(a.Nfull, 256), (unsigned)ceil_div(a.M, p.bm),
@@ -754,7 +770,7 @@ extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, in
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
     if (rc) return rc;
     if (nclients == 0) return FH_OK;
-    FH_REQUIRE(x && dy && dw && workspace, "conv2d_wgrad: null pointer");
+    FH_REQUIRE(x && dy && dw, "conv2d_wgrad: null pointer");
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
     a.x = x; a.dy = dy;
     a.x_cs = x_cs; a.dy_cs = dy_cs;
@@ -794,10 +810,22 @@ extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, in
     FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
     a.splits = p.splits;
     a.kchunk = p.kchunk;
+    hipStream_t st = as_stream(stream);
+    if (p.splits == 1) {  // one K pass per tile: the kernel writes dW / db directly
+        a.out = dw;
+        a.out_cs = dw_cs;
+        a.bias_part = db;
+        a.b_cs = db_cs;
+        dim3 grid((unsigned)ceil_div(a.N, p.t.bn), (unsigned)ceil_div(a.M, p.t.bm),
+                  (unsigned)nclients);
+        rc = launch_shape<OP_WGRAD>(kh, kw, stride, p.t, grid, a, st);
+        if (rc) return rc;
+        FH_LAUNCH_CHECK("conv2d_wgrad");
+        return FH_OK;
+    }
     a.out = (float*)workspace;
     const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
     a.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
-    hipStream_t st = as_stream(stream);
     dim3 grid((unsigned)ceil_div(a.N, p.t.bn), (unsigned)ceil_div(a.M, p.t.bm),
               (unsigned)(nclients * p.splits));
     rc = launch_shape<OP_WGRAD>(kh, kw, stride, p.t, grid, a, st);

@@ -35,6 +35,7 @@ struct DConvArgs {
     int relu, accumulate;
     int splits, cchunk;  // reduction channels per split (multiple of CK)
     int Nfull;           // batch * H * W (slab row length)
+    int wvec;            // host: weight slices 16-B aligned -> float4 staging instance
 };
 
 template <int W>
@@ -50,7 +51,7 @@ struct DGeom {
     static_assert(256 % W == 0 && (TR % H == 0 || H % TR == 0), "tile geometry");
 };
 
-template <int OP, int W, int BM, int WAVES_M, int CK>
+template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC>
 __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     using G = DGeom<W>;
     constexpr int WAVES_N = 4 / WAVES_M;
@@ -58,9 +59,11 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     constexpr int FM = WM / 32, FN = WN / 32;
     constexpr int BMP = BM + 1;                 // As row pitch (staging writes spread banks)
     constexpr int KS = 9 * CK;                  // k-values per stage
-    constexpr int NA = (BM * KS + 255) / 256;   // A elements per thread
     constexpr int PE = CK * G::CSTR;            // patch elements per stage
-    constexpr int NP = (PE + 255) / 256;
+    // staging: patch interior rows as float4 (halo columns are constant zeros), weights
+    // as float4 runs of the contiguous [ch][3][3] (FWD) / [m][3][3] (DGRAD) slices
+    constexpr int PQ = W / 4, RPI = 256 / PQ, NPR = CK * G::PR, NPT = (NPR + RPI - 1) / RPI;
+    constexpr int NAV = (BM * KS / 4 + 255) / 256;   // float4 weight slots per thread
     static_assert(FM >= 1 && FN >= 1 && (CK % 2) == 0, "dconv tile");
 
     __shared__ float As[2][KS * BMP];
@@ -79,71 +82,118 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     const int cend = min(a.Cr, cbeg + a.cchunk);
     const int M = a.M;
 
-    // ---- per-thread staging coordinates (fixed across K-steps) ----------
-    const int img0 = (t * G::TR) / G::H, y0 = (t * G::TR) % G::H;
-    int poff[NP];      // source offset within the client tensor, channel 0 of the chunk
-    int pch[NP];       // local channel, or -1 when the element is halo / out of range
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-        const int e = tid + i * 256;
-        const int cl = e / G::CSTR, rem = e % G::CSTR;
-        const int pr = rem / G::PW, pc = rem % G::PW;
-        const int seg = pr / (G::SEGR + 2), rr = pr % (G::SEGR + 2);
-        const int img = img0 + seg, y = y0 + rr - 1, x = pc - 1;
-        const bool ok = e < PE && img < cnt && (unsigned)y < (unsigned)G::H &&
-                        (unsigned)x < (unsigned)W;
-        pch[i] = ok ? cl : -1;
-        poff[i] = ok ? ((img * a.Cr + cl) * G::H + y) * W + x : 0;
+    for (int q = tid; q < 2 * NPR; q += 256) {  // zero halo columns of both buffers
+        const int bsel = q / NPR, row = q % NPR;
+        float* r = &Ps[bsel][(row / G::PR) * G::CSTR + (row % G::PR) * G::PW];
+        r[0] = 0.f;
+        r[W + 1] = 0.f;
     }
+
+    const int img0 = (t * G::TR) / G::H, y0 = (t * G::TR) % G::H;
+    const int prt = tid / PQ, px = (tid % PQ) * 4;
     const float* inz = a.in + z * a.in_cs;
     const float* wz = a.wt + z * a.w_cs;
+    constexpr bool wvec = WVEC;  // scalar weight staging (costly in VGPRs) only when needed
 
-    float rp[NP], ra[NA];
+    float4 rp[NPT], ra[NAV];
     auto load = [&](int c0) {
 #pragma unroll
-        for (int i = 0; i < NP; ++i)
-            rp[i] = (pch[i] >= 0 && c0 + pch[i] < cend) ? inz[poff[i] + (int64_t)c0 * G::HW] : 0.f;
+        for (int i = 0; i < NPT; ++i) {
+            const int q = prt + i * RPI;
+            const int cl = q / G::PR, pr = q % G::PR;
+            const int seg = pr / (G::SEGR + 2), rr = pr % (G::SEGR + 2);
+            const int img = img0 + seg, y = y0 + rr - 1;
+            const bool ok = q < NPR && img < cnt && (unsigned)y < (unsigned)G::H && c0 + cl < cend;
+            rp[i] = ok ? *reinterpret_cast<const float4*>(
+                             inz + ((int64_t)(img * a.Cr + c0 + cl) * G::H + y) * W + px)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if constexpr (wvec) {
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
-            const int e = tid + i * 256;
-            float v = 0.f;
-            if (OP == OP_FWD) {
-                // e -> (m, cl, r9), r9 fastest: W[m][c0+cl][r9] contiguous per m
-                const int m = e / KS, rem = e % KS, cl = rem / 9, r9 = rem % 9;
-                if (e < BM * KS && m0 + m < M && c0 + cl < cend)
-                    v = wz[((int64_t)(m0 + m) * a.Cr + c0 + cl) * 9 + r9];
-            } else {
-                // e -> (cl, m, r9): W[c0+cl][m0+m][8-r9] contiguous per cl
-                const int cl = e / (BM * 9), rem = e % (BM * 9), m = rem / 9, r9 = rem % 9;
-                if (e < BM * KS && m0 + m < M && c0 + cl < cend)
-                    v = wz[((int64_t)(c0 + cl) * M + m0 + m) * 9 + (8 - r9)];
+            for (int i = 0; i < NAV; ++i) {
+                const int f = tid + i * 256;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (OP == OP_FWD) {  // run of 9*CK floats per m: W[m0+m][c0 .. c0+CK)[9]
+                    const int m = f / (KS / 4), j4 = f % (KS / 4);
+                    if (f < BM * KS / 4 && m0 + m < M)
+                        v = *reinterpret_cast<const float4*>(
+                            wz + ((int64_t)(m0 + m) * a.Cr + c0) * 9 + 4 * j4);
+                } else {             // run of 9*BM floats per ch: W[c0+cl][m0 .. m0+BM)[9]
+                    const int cl = f / (BM * 9 / 4), j4 = f % (BM * 9 / 4);
+                    if (f < BM * KS / 4 && c0 + cl < cend)
+                        v = *reinterpret_cast<const float4*>(
+                            wz + ((int64_t)(c0 + cl) * M + m0) * 9 + 4 * j4);
+                }
+                ra[i] = v;
             }
-            ra[i] = v;
+        } else {
+            float* rs = reinterpret_cast<float*>(ra);
+#pragma unroll
+            for (int i = 0; i < 4 * NAV; ++i) {
+                const int e = tid + i * 256;
+                float v = 0.f;
+                if (OP == OP_FWD) {
+                    const int m = e / KS, rem = e % KS, cl = rem / 9, r9 = rem % 9;
+                    if (e < BM * KS && m0 + m < M && c0 + cl < cend)
+                        v = wz[((int64_t)(m0 + m) * a.Cr + c0 + cl) * 9 + r9];
+                } else {
+                    const int cl = e / (BM * 9), rem = e % (BM * 9), m = rem / 9, r9 = rem % 9;
+                    if (e < BM * KS && m0 + m < M && c0 + cl < cend)
+                        v = wz[((int64_t)(c0 + cl) * M + m0 + m) * 9 + (8 - r9)];
+                }
+                rs[i] = v;
+            }
         }
     };
-    auto store = [&](int buf) {
+    // As[(r9*CK + cl)*BMP + m]; r9 is the patch shift (kh*3+kw) the weight multiplies
+    auto put_a = [&](int buf, int m, int cl, int r9, float v, int c0) {
+        if (m0 + m >= M || c0 + cl >= cend) v = 0.f;
+        As[buf][(r9 * CK + cl) * BMP + m] = v;
+    };
+    auto store = [&](int buf, int c0) {
 #pragma unroll
-        for (int i = 0; i < NP; ++i) {
-            const int e = tid + i * 256;
-            if (e < PE) Ps[buf][e] = rp[i];
+        for (int i = 0; i < NPT; ++i) {
+            const int q = prt + i * RPI;
+            if (q < NPR) {
+                float* d = &Ps[buf][(q / G::PR) * G::CSTR + (q % G::PR) * G::PW + 1 + px];
+                d[0] = rp[i].x;
+                d[1] = rp[i].y;
+                d[2] = rp[i].z;
+                d[3] = rp[i].w;
+            }
         }
+        if constexpr (wvec) {
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
-            const int e = tid + i * 256;
-            if (e < BM * KS) {
-                int m, cl, r9;
-                if (OP == OP_FWD) {
-                    m = e / KS;
-                    const int rem = e % KS;
-                    cl = rem / 9;
-                    r9 = rem % 9;
-                } else {
-                    cl = e / (BM * 9);
-                    const int rem = e % (BM * 9);
-                    m = rem / 9;
-                    r9 = rem % 9;
+            for (int i = 0; i < NAV; ++i) {
+                const int f = tid + i * 256;
+                if (f < BM * KS / 4) {
+                    const float vv[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (OP == OP_FWD) {
+                            const int m = f / (KS / 4), k = 4 * (f % (KS / 4)) + u;
+                            put_a(buf, m, k / 9, k % 9, vv[u], c0);
+                        } else {
+                            const int cl = f / (BM * 9 / 4), k = 4 * (f % (BM * 9 / 4)) + u;
+                            put_a(buf, k / 9, cl, 8 - k % 9, vv[u], c0);
+                        }
+                    }
                 }
-                As[buf][(r9 * CK + cl) * BMP + m] = ra[i];
+            }
+        } else {
+            const float* rs = reinterpret_cast<const float*>(ra);
+#pragma unroll
+            for (int i = 0; i < 4 * NAV; ++i) {
+                const int e = tid + i * 256;
+                if (e < BM * KS) {
+                    if (OP == OP_FWD) {
+                        const int rem = e % KS;
+                        put_a(buf, e / KS, rem / 9, rem % 9, rs[i], c0);
+                    } else {
+                        const int rem = e % (BM * 9);
+                        put_a(buf, rem / 9, e / (BM * 9), rem % 9, rs[i], c0);
+                    }
+                }
             }
         }
     };
@@ -170,34 +220,44 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 
     if (cbeg < cend) {
         load(cbeg);
-        store(0);
+        store(0, cbeg);
         __syncthreads();
         int buf = 0;
         for (int c0 = cbeg; c0 < cend; c0 += CK) {
             const bool more = c0 + CK < cend;
             if (more) load(c0 + CK);
-            const float* Ab = &As[buf][a_lane];
-            const float* Pb = &Ps[buf][0];
+            // kh rolled (bounds the compiler's LDS-read hoisting, i.e. VGPRs); the 3*CK/2
+            // (kw, channel-pair) items of a kh are unrolled with every operand offset a
+            // ds_read immediate, and operands are double-buffered in registers: item j+1
+            // is read while item j's MFMAs issue.
+            constexpr int NI = 3 * (CK / 2);
+#pragma unroll 1
+            for (int kh = 0; kh < 3; ++kh) {
+                const float* Ab = &As[buf][a_lane + kh * 3 * CK * BMP];
+                const float* Pb = &Ps[buf][kh * G::PW];
+                float av[2][FM], bv[2][FN];
+                auto fetch = [&](int j, int slot) {
+                    const int kw = j / (CK / 2), cp = j % (CK / 2);
 #pragma unroll
-            for (int s = 0; s < 9; ++s) {
-                const int kh = s / 3, kw = s % 3;
+                    for (int i = 0; i < FM; ++i)
+                        av[slot][i] = Ab[(kw * CK + 2 * cp) * BMP + i * 32];
 #pragma unroll
-                for (int cp = 0; cp < CK / 2; ++cp) {
-                    float av[FM], bv[FN];
+                    for (int jj = 0; jj < FN; ++jj)
+                        bv[slot][jj] = Pb[b_lane[jj] + 2 * cp * G::CSTR + kw];
+                };
+                fetch(0, 0);
 #pragma unroll
-                    for (int i = 0; i < FM; ++i) av[i] = Ab[(s * CK + 2 * cp) * BMP + i * 32];
-#pragma unroll
-                    for (int j = 0; j < FN; ++j)
-                        bv[j] = Pb[b_lane[j] + 2 * cp * G::CSTR + kh * G::PW + kw];
+                for (int j = 0; j < NI; ++j) {
+                    if (j + 1 < NI) fetch(j + 1, (j + 1) & 1);
 #pragma unroll
                     for (int i = 0; i < FM; ++i)
 #pragma unroll
-                        for (int j = 0; j < FN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j],
-                                                                             0, 0, 0);
+                        for (int jj = 0; jj < FN; ++jj)
+                            acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                                av[j & 1][i], bv[j & 1][jj], acc[i][jj], 0, 0, 0);
                 }
             }
-            if (more) store(buf ^ 1);
+            if (more) store(buf ^ 1, c0 + CK);
             __syncthreads();
             buf ^= 1;
         }
@@ -410,28 +470,30 @@ __global__ void __launch_bounds__(256) dconv_wgrad_kernel(const DWArgs a) {
     const int64_t slab = ((int64_t)z * a.splits + split) * a.M;
     constexpr int WT = WCO * WCI;
     if constexpr (WPX > 1) {
-        constexpr int SG = 3;  // shifts per round
-        static_assert((WPX - 1) * WT * SG * 16 * 64 <= 2 * BUF, "reduction scratch");
+        // every wave parks 3 shifts of its accumulators in LDS; then all 256 threads sum
+        // the WPX pixel partials (fixed order) and write the slab
+        constexpr int SG = 3;
+        static_assert(WPX * WT * SG * 16 * 64 <= 2 * BUF, "reduction scratch");
+        const int wt_me = wco * WCI + wci;
+        float* op = a.part + slab * a.N;
 #pragma unroll
         for (int g = 0; g < 9; g += SG) {
-            if (wpx > 0) {
 #pragma unroll
-                for (int s = 0; s < SG; ++s)
+            for (int s = 0; s < SG; ++s)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        red[((((wpx - 1) * WT + wco * WCI + wci) * SG + s) * 16 + r) * 64 + lane] =
-                            acc[g + s][r];
-            }
+                for (int r = 0; r < 16; ++r)
+                    red[(((wpx * WT + wt_me) * SG + s) * 16 + r) * 64 + lane] = acc[g + s][r];
             __syncthreads();
-            if (wpx == 0) {
+#pragma unroll 1
+            for (int e = tid; e < WT * SG * 1024; e += 256) {
+                const int wt = e / (SG * 1024), rem = e % (SG * 1024);
+                const int sh = rem / 1024, r = (rem / 64) % 16, l = rem % 64;
+                float v = 0.f;
 #pragma unroll
-                for (int q = 1; q < WPX; ++q)
-#pragma unroll
-                    for (int s = 0; s < SG; ++s)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r)
-                            acc[g + s][r] +=
-                                red[((((q - 1) * WT + wco * WCI + wci) * SG + s) * 16 + r) * 64 + lane];
+                for (int q = 0; q < WPX; ++q) v += red[((q * WT + wt) * SG * 1024) + rem];
+                const int m = co0 + (wt / WCI) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+                const int ci = ci0 + (wt % WCI) * 32 + (l & 31);
+                op[(int64_t)m * a.N + ci * 9 + g + sh] = v;
             }
             __syncthreads();
         }
@@ -451,7 +513,7 @@ __global__ void __launch_bounds__(256) dconv_wgrad_kernel(const DWArgs a) {
             a.bias_part[slab + co0 + wco * 32 + lane] = v;
         }
     }
-    if (wpx == 0) {
+    if (WPX == 1) {
         float* op = a.part + slab * a.N;
         const int ci = ci0 + wci * 32 + col;
 #pragma unroll

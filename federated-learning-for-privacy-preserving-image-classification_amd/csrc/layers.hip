@@ -25,7 +25,8 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
                     int64_t y_cs, uint8_t* __restrict__ idx, int64_t i_cs,
                     uint8_t* __restrict__ mask, int64_t m_cs, const int32_t* __restrict__ counts,
                     int batch, int C, int H, int W, int drop_mode, float keep_prob, float scale,
-                    uint64_t seed) {
+                    uint64_t seed_salt, const uint64_t* __restrict__ seed_dev) {
+    const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int OH = H / 2, OW = W / 2;
@@ -95,7 +96,8 @@ __global__ void __launch_bounds__(256)
 dropout_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y, int64_t y_cs,
                    uint8_t* __restrict__ mask, int64_t m_cs, const int32_t* __restrict__ counts,
                    int batch, int64_t per_img, int drop_mode, float keep_prob, float scale,
-                   uint64_t seed) {
+                   uint64_t seed_salt, const uint64_t* __restrict__ seed_dev) {
+    const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int64_t total = cnt * per_img;
@@ -254,7 +256,8 @@ using namespace fh;
 extern "C" int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
                                int64_t i_cs, uint8_t* mask, int64_t m_cs, const int32_t* counts,
                                int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
-                               int32_t drop_mode, float p_drop, uint64_t seed, void* stream) {
+                               int32_t drop_mode, float p_drop, uint64_t seed,
+                               const uint64_t* seed_dev, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2, "maxpool2_fwd: bad shape");
     FH_REQUIRE((H % 2) == 0 && (W % 2) == 0, "maxpool2_fwd: odd spatial size %dx%d", H, W);
     FH_REQUIRE(drop_mode >= 0 && drop_mode <= 2 && (drop_mode == 0 || mask), "maxpool2_fwd: mask");
@@ -265,7 +268,7 @@ extern "C" int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y
     const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
     hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
                        as_stream(stream), x, x_cs, y, y_cs, idx, i_cs, mask, m_cs, counts, batch, C,
-                       H, W, drop_mode, keep, scale, seed);
+                       H, W, drop_mode, keep, scale, seed, seed_dev);
     FH_LAUNCH_CHECK("maxpool2_fwd");
     return FH_OK;
 }
@@ -291,7 +294,7 @@ extern "C" int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* id
 extern "C" int fh_dropout_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* mask,
                               int64_t m_cs, const int32_t* counts, int32_t nclients, int32_t batch,
                               int64_t per_img, int32_t drop_mode, float p_drop, uint64_t seed,
-                              void* stream) {
+                              const uint64_t* seed_dev, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && per_img > 0, "dropout_fwd: bad shape");
     FH_REQUIRE((drop_mode == 1 || drop_mode == 2) && mask, "dropout_fwd: mask mode");
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "dropout_fwd: p=%g", p_drop);
@@ -300,7 +303,7 @@ extern "C" int fh_dropout_fwd(const float* x, int64_t x_cs, float* y, int64_t y_
     const float keep = 1.0f - p_drop, scale = 1.0f / keep;
     hipLaunchKernelGGL(dropout_fwd_kernel, dim3(ew_grid(batch * per_img), nclients), dim3(256), 0,
                        as_stream(stream), x, x_cs, y, y_cs, mask, m_cs, counts, batch, per_img,
-                       drop_mode, keep, scale, seed);
+                       drop_mode, keep, scale, seed, seed_dev);
     FH_LAUNCH_CHECK("dropout_fwd");
     return FH_OK;
 }

@@ -36,8 +36,12 @@ sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict
 __global__ void __launch_bounds__(256)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, int64_t n, float wd, float decay_mul, int decoupled,
-            float one_m_b1, float b2, float one_m_b2, float bc2_sqrt, float eps,
-            float neg_step_size) {
+            float one_m_b1, float b2, float one_m_b2, float bc2_sqrt_h, float eps,
+            float neg_step_size_h, const float* __restrict__ scal) {
+    // per-step bias corrections: host scalars, or [bc2_sqrt, -step_size] in device memory
+    // (lets one captured step graph serve every optimizer step)
+    const float bc2_sqrt = scal ? scal[0] : bc2_sqrt_h;
+    const float neg_step_size = scal ? scal[1] : neg_step_size_h;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         float pv = p[i];
@@ -76,7 +80,7 @@ extern "C" int fh_sgd_step(float* param, const float* grad, float* momentum_buf,
 extern "C" int fh_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                             int64_t n, double lr, double beta1, double beta2, double eps,
                             double weight_decay, int32_t decoupled, double step_size,
-                            double bc2_sqrt, void* stream) {
+                            double bc2_sqrt, const float* scal_dev, void* stream) {
     FH_REQUIRE(n >= 0, "adam_step: bad size");
     if (n == 0) return FH_OK;
     FH_REQUIRE(param && grad && exp_avg && exp_avg_sq, "adam_step: null pointer");
@@ -85,7 +89,7 @@ extern "C" int fh_adam_step(float* param, const float* grad, float* exp_avg, flo
                        exp_avg, exp_avg_sq, n, (float)weight_decay,
                        (float)(1.0 - lr * weight_decay), decoupled, (float)(1.0 - beta1),
                        (float)beta2, (float)(1.0 - beta2), (float)bc2_sqrt, (float)eps,
-                       (float)(-step_size));
+                       (float)(-step_size), scal_dev);
     FH_LAUNCH_CHECK("adam_step");
     return FH_OK;
 }

@@ -39,7 +39,7 @@ SIGNATURES = {
     "fh_dp_clip_coef": (I32, [P, I32, I32, F64, F64, F64, P, P, P, P, P]),
     "fh_dp_apply": (I32, [P, I64, P, I64, P, I64, I32, I64, P, P, P, P, I64, U64, P]),
     "fh_sgd_step": (I32, [P, P, P, I64, F32, F32, F32, I32, P]),
-    "fh_adam_step": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, I32, F64, F64, P]),
+    "fh_adam_step": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, I32, F64, F64, P, P]),
     "fh_conv2d_fwd_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "fh_conv2d_dgrad_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "fh_conv2d_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
@@ -63,10 +63,10 @@ SIGNATURES = {
     "fh_bn_bwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, P, P, I64, P, I64, P, P, I64, P,
                         I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_maxpool2_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
-                              F32, U64, P]),
+                              F32, U64, P, P]),
     "fh_maxpool2_bwd": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I32,
                               I32, I32, P]),
-    "fh_dropout_fwd": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I64, I32, F32, U64, P]),
+    "fh_dropout_fwd": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I64, I32, F32, U64, P, P]),
     "fh_dropout_bwd": (I32, [P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I64, P]),
     "fh_ce_fwd_bwd": (I32, [P, I64, P, I64, P, I64, P, P, P, P, P, P, I32, I32, I32, P]),
     "fh_avgpool_fwd": (I32, [P, I64, P, I64, P, I32, I32, I32, I32, P]),

@@ -29,6 +29,7 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from . import ops
@@ -72,6 +73,15 @@ class PackedTrainer:
         self.opt_type, self.lr, self.opt_step = "sgd", 0.01, 0
         self.on_step = None
         self.pre_step = None
+        # Step graphs: every step after the first of a round is replayed from a HIP graph
+        # captured once per (active slots, optimizer, lr, data); the per-step inputs (batch
+        # indices, counts, epoch resets, dropout key, Adam bias corrections) are copied into
+        # fixed device slots by one memcpy before each replay.  Full-width steps stay eager
+        # when probe_full is set (bench.py times their kernels with events).
+        self.use_graphs = True
+        self.probe_full = False
+        self._graphs = {}
+        self._graph_pool = None
         # default BN buffers: running_mean 0, running_var 1
         for name in L.buf_names:
             if name.endswith("running_var"):
@@ -124,20 +134,19 @@ class PackedTrainer:
         self.state1.zero_()
         self.state2.zero_()
 
-    def _optimizer_step(self, n):
-        self.opt_step += 1
+    def _optimizer_launch(self, n, first, adam_dev=None):
         cnt = n * self.Ppad
         if self.opt_type == "sgd":
-            ops.sgd_step(self.params, self.grads, self.state1, self.lr, 0.9,
-                         first_step=(self.opt_step == 1), n=cnt)
+            ops.sgd_step(self.params, self.grads, self.state1, self.lr, 0.9, first_step=first,
+                         n=cnt)
         else:
             adamw = self.opt_type == "adamw"
             ops.adam_step(self.params, self.grads, self.state1, self.state2, self.opt_step, self.lr,
-                          weight_decay=0.01 if adamw else 0.0, decoupled=adamw, n=cnt)
+                          weight_decay=0.01 if adamw else 0.0, decoupled=adamw, n=cnt,
+                          scal_dev=adam_dev)
 
-    # ------------------------------------------------------------ one packed step
-    def step(self, n, counts, reset=None):
-        """fwd + CE + bwd + optimizer for slots [0, n) on the batch in net.x / net.y."""
+    def _step_launches(self, n, counts, reset, first, adam_dev=None):
+        """The kernel sequence of one packed step (no host bookkeeping: graph-capturable)."""
         net = self.net
         net.forward(self.params, self.bufs, n, counts, train=True)
         ops.ce_fwd_bwd(net.logits, net.y, net.dlogits, n, self.batch, net.num_classes,
@@ -145,7 +154,16 @@ class PackedTrainer:
                        acc_correct=self.acc_correct, acc_seen=self.acc_seen, reset=reset,
                        counts=counts)
         net.backward(self.params, self.grads, n, counts)
-        self._optimizer_step(n)
+        self._optimizer_launch(n, first, adam_dev)
+
+    # ------------------------------------------------------------ one packed step
+    def step(self, n, counts, reset=None):
+        """fwd + CE + bwd + optimizer for slots [0, n) on the batch in net.x / net.y."""
+        self.opt_step += 1
+        self._step_launches(n, counts, reset, first=(self.opt_step == 1))
+        self._after_step(n)
+
+    def _after_step(self, n):
         for k in range(n):
             self.num_batches_tracked[k] += 1
         if self.on_step is not None:  # test/diagnostic hook (e.g. snapshot pool argmax)
@@ -170,24 +188,96 @@ class PackedTrainer:
 
         data [N, *in_shape] / labels [N] device tensors hold all shards back
         to back; slot k's shard starts at shard_offsets[k]."""
-        dev = self.device
         net = self.net
         self.begin_round(optimizer_type, lr)
-        S = plan["counts"].shape[1]
-        counts = plan["counts"].to(dev)
-        reset = plan["reset"].to(dev)
-        off = torch.as_tensor(shard_offsets, dtype=torch.int64).view(1, S, 1)
-        gidx = (plan["index"] + off).to(dev)
+        rows, cur, views = self._step_rows(plan, shard_offsets, seed)
         sample_elems = int(math.prod(net.in_shape))
-        for g in range(plan["G"]):
-            n = plan["active"][g]
-            if self.pre_step is not None:  # bench hook (e.g. arm the launch probe on full steps)
-                self.pre_step(g, n, plan)
-            net.seed = (seed * 1000003 + g) & 0x7FFFFFFF
-            ops.gather_batch(data, labels, gidx[g], net.x, net.y, sample_elems, n, self.batch,
-                             counts=counts[g])
-            self.step(n, counts[g], reset=reset[g])
+        full_batch = (plan["counts"] == self.batch).all(dim=1).tolist()
+        graphs = (self.use_graphs and self.on_step is None and self.pre_step is None
+                  and not ops.PROBE.enabled)
+        try:
+            for g in range(plan["G"]):
+                n = plan["active"][g]
+                if self.pre_step is not None:  # diagnostic hook
+                    self.pre_step(g, n, plan)
+                cur.copy_(rows[g], non_blocking=True)
+                self.opt_step += 1
+                full = n == self.capacity
+                if graphs and g > 0 and not (self.probe_full and full):
+                    self._replay(n, data, labels, views, sample_elems)
+                else:
+                    arm = self.probe_full and full and bool(full_batch[g])
+                    ops.PROBE.enabled = arm
+                    net.seed = (seed * 1000003 + g) & 0x7FFFFFFF
+                    net.seed_dev = None
+                    ops.gather_batch(data, labels, views["gidx"], net.x, net.y, sample_elems, n,
+                                     self.batch, counts=views["counts"])
+                    self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
+                                        adam_dev=views["adam"])
+                    if arm:
+                        ops.PROBE.enabled = False
+                self._after_step(n)
+        finally:
+            net.seed_dev = None
         return self.collect_metrics(plan, epochs_of(plan))
+
+    def _step_rows(self, plan, shard_offsets, seed):
+        """Per-step inputs packed as byte rows [G, R] on the device, plus the fixed
+        current-step slot `cur` [R] and typed views into it:
+          gidx  int64 [S, B]  absolute sample index of each batch slot
+          counts int32 [S], reset int32 [S]
+          seed  int64 [1]     (seed * 1000003 + g) * 1000003  -> dropout key base
+          adam  f32 [2]       {sqrt(1 - b2^t), -lr / (1 - b1^t)} for t = g + 1"""
+        G, S, B = plan["G"], plan["counts"].shape[1], self.batch
+        r8 = lambda b: (b + 7) // 8 * 8
+        o_cnt = S * B * 8
+        o_rst = o_cnt + r8(S * 4)
+        o_seed = o_rst + r8(S * 4)
+        o_adam = o_seed + 8
+        R = o_adam + 8
+        buf = np.zeros((G, R), dtype=np.uint8)
+        off = np.asarray(shard_offsets, dtype=np.int64).reshape(1, S, 1)
+        buf[:, :o_cnt] = (plan["index"].numpy() + off).reshape(G, -1).view(np.uint8)
+        buf[:, o_cnt:o_cnt + 4 * S] = plan["counts"].numpy().astype(np.int32).view(np.uint8)
+        buf[:, o_rst:o_rst + 4 * S] = plan["reset"].numpy().astype(np.int32).view(np.uint8)
+        keys = np.array([(((seed * 1000003 + g) & 0x7FFFFFFF) * 1000003) & 0xFFFFFFFFFFFFFFFF
+                         for g in range(G)], dtype=np.uint64)
+        buf[:, o_seed:o_seed + 8] = keys.view(np.uint8).reshape(G, 8)
+        adam = np.zeros((G, 2), dtype=np.float32)
+        for g in range(G):
+            step_size, bc2_sqrt = ops.adam_bias_corrections(g + 1, self.lr)
+            adam[g] = (np.float32(bc2_sqrt), np.float32(-step_size))
+        buf[:, o_adam:o_adam + 8] = adam.view(np.uint8).reshape(G, 8)
+        rows = torch.from_numpy(buf).to(self.device)
+        key = ("cur", R)
+        if key not in self.__dict__.setdefault("_cur", {}):
+            self._cur[key] = torch.zeros(R, dtype=torch.uint8, device=self.device)
+        cur = self._cur[key]
+        views = dict(gidx=cur[:o_cnt].view(torch.int64).view(S, B),
+                     counts=cur[o_cnt:o_cnt + 4 * S].view(torch.int32),
+                     reset=cur[o_rst:o_rst + 4 * S].view(torch.int32),
+                     seed=cur[o_seed:o_seed + 8].view(torch.int64),
+                     adam=cur[o_adam:o_adam + 8].view(torch.float32))
+        return rows, cur, views
+
+    def _replay(self, n, data, labels, views, sample_elems):
+        key = (n, self.opt_type, self.lr, data.data_ptr(), labels.data_ptr(),
+               views["gidx"].data_ptr(), tuple(views["gidx"].shape))
+        graph = self._graphs.get(key)
+        if graph is None:
+            net = self.net
+            net.seed_dev = views["seed"]
+            if self._graph_pool is None:
+                self._graph_pool = torch.cuda.graph_pool_handle()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, pool=self._graph_pool):
+                ops.gather_batch(data, labels, views["gidx"], net.x, net.y, sample_elems, n,
+                                 self.batch, counts=views["counts"])
+                self._step_launches(n, views["counts"], views["reset"], first=False,
+                                    adam_dev=views["adam"])
+            net.seed_dev = None
+            self._graphs[key] = graph
+        graph.replay()
 
     def collect_metrics(self, plan, epochs):
         loss = self.acc_loss.cpu()

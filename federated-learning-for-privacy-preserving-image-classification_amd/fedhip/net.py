@@ -124,6 +124,7 @@ class PackedNet:
         # dropout: per-layer keep masks; mask_mode 1 = generate (Philox), 2 = injected
         self.mask_mode = 1
         self.seed = 0
+        self.seed_dev = None  # device uint64 [1] = seed * 1000003 (graph replay)
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -142,6 +143,11 @@ class PackedNet:
         return blocks
 
     def _seed(self, layer_id):
+        """Philox key of a dropout site: seed * 1000003 + layer_id * 7919 (mod 2^64).  With
+        seed_dev set (graph replay) the per-step part lives on the device and the kernel
+        adds it to the per-layer salt returned here."""
+        if self.seed_dev is not None:
+            return (layer_id * 7919) & 0xFFFFFFFFFFFFFFFF
         return (self.seed * 1000003 + layer_id * 7919) & 0xFFFFFFFFFFFFFFFF
 
     def _drop_mode(self, train):
@@ -192,7 +198,8 @@ class PackedNet:
         dm = self._drop_mode(train)
         x3 = h1
         if dm:
-            ops.dropout_fwd(h1, d1, m1, n, B, 128, self.dropout_p, dm, self._seed(1), counts=cnt)
+            ops.dropout_fwd(h1, d1, m1, n, B, 128, self.dropout_p, dm, self._seed(1), counts=cnt,
+                            seed_dev=self.seed_dev)
             x3 = d1
         self._fc_in = x3
         ops.linear_fwd(x3, W(P_, "fc2.weight"), W(P_, "fc2.bias"), self.logits, n, B, 128,
@@ -270,7 +277,8 @@ class PackedNet:
                 idx = A(f"i_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8)
                 msk = A(f"m_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8) if dm else None
                 ops.maxpool2_fwd(r, q, idx, n, B, co, hw, hw, mask=msk, drop_mode=dm,
-                                 p_drop=self.dropout_p, seed=self._seed(10 + i), counts=cnt)
+                                 p_drop=self.dropout_p, seed=self._seed(10 + i), counts=cnt,
+                                 seed_dev=self.seed_dev)
                 xin = q
         # classifier: fc1 -> relu -> drop -> fc2 -> relu -> drop -> fc3
         h1, h2 = A("h1", 512), A("h2", 256)
@@ -280,14 +288,14 @@ class PackedNet:
         if dm:
             e1 = A("e1", 512)
             ops.dropout_fwd(h1, e1, A("m_fc1", 512, dtype=torch.uint8), n, B, 512, self.dropout_p,
-                            dm, self._seed(21), counts=cnt)
+                            dm, self._seed(21), counts=cnt, seed_dev=self.seed_dev)
         ops.linear_fwd(e1, W(P_, "fc2.weight"), W(P_, "fc2.bias"), h2, n, B, 512, 256, relu=True,
                        counts=cnt)
         e2 = h2
         if dm:
             e2 = A("e2", 256)
             ops.dropout_fwd(h2, e2, A("m_fc2", 256, dtype=torch.uint8), n, B, 256, self.dropout_p,
-                            dm, self._seed(22), counts=cnt)
+                            dm, self._seed(22), counts=cnt, seed_dev=self.seed_dev)
         self._e1, self._e2, self._dm = e1, e2, dm
         ops.linear_fwd(e2, W(P_, "fc3.weight"), W(P_, "fc3.bias"), self.logits, n, B, 256,
                        self.num_classes, counts=cnt)

@@ -36,9 +36,12 @@ class Workspace:
     def __init__(self, device):
         self.device = device
         self.buf = torch.empty(0, dtype=torch.uint8, device=device)
+        self.retired = []
 
     def get(self, nbytes: int) -> torch.Tensor:
         if self.buf.numel() < nbytes:
+            # superseded buffers stay alive: a captured step graph may still address them
+            self.retired.append(self.buf)
             self.buf = torch.empty(max(nbytes, 2 * self.buf.numel()), dtype=torch.uint8,
                                    device=self.device)
         return self.buf
@@ -237,17 +240,22 @@ def sgd_step(param, grad, buf, lr, momentum, weight_decay=0.0, first_step=False,
          float(weight_decay), int(first_step), stream_handle())
 
 
+def adam_bias_corrections(step, lr, beta1=0.9, beta2=0.999):
+    """(step_size, bc2_sqrt) for optimizer step t, in Python double as torch.optim.Adam."""
+    step_size = lr / (1 - beta1 ** step)
+    bc2_sqrt = (1 - beta2 ** step) ** 0.5
+    return step_size, bc2_sqrt
+
+
 def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
-              weight_decay=0.0, decoupled=False, n=None):
-    """torch.optim.Adam/AdamW single-tensor step; bias corrections in Python double."""
+              weight_decay=0.0, decoupled=False, n=None, scal_dev=None):
+    """torch.optim.Adam/AdamW single-tensor step; bias corrections in Python double
+    (or, with scal_dev, read on the device: float32 {bc2_sqrt, -step_size})."""
     n = param.numel() if n is None else n
-    bias_correction1 = 1 - beta1 ** step
-    bias_correction2 = 1 - beta2 ** step
-    step_size = lr / bias_correction1
-    bc2_sqrt = bias_correction2 ** 0.5
+    step_size, bc2_sqrt = adam_bias_corrections(step, lr, beta1, beta2)
     call("fh_adam_step", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), n, float(lr),
          float(beta1), float(beta2), float(eps), float(weight_decay), int(decoupled),
-         float(step_size), float(bc2_sqrt), stream_handle())
+         float(step_size), float(bc2_sqrt), ptr(scal_dev), stream_handle())
 
 
 # ------------------------------------------------------------------ BN / pool / dropout / CE
@@ -277,10 +285,10 @@ def bn_bwd(dy, yout, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclien
 
 
 def maxpool2_fwd(x, y, idx, nclients, batch, C, H, W, mask=None, drop_mode=0, p_drop=0.0, seed=0,
-                 counts=None):
+                 counts=None, seed_dev=None):
     call("fh_maxpool2_fwd", ptr(x), _cs(x), ptr(y), _cs(y), ptr(idx), _cs(idx), ptr(mask),
          _cs(mask), _counts(counts), nclients, batch, C, H, W, int(drop_mode), float(p_drop),
-         int(seed) & 0xFFFFFFFFFFFFFFFF, stream_handle())
+         int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), stream_handle())
 
 
 def maxpool2_bwd(dy, idx, dx, nclients, batch, C, H, W, mask=None, p_drop=0.0, xin=None,
@@ -290,10 +298,11 @@ def maxpool2_bwd(dy, idx, dx, nclients, batch, C, H, W, mask=None, p_drop=0.0, x
          H, W, stream_handle())
 
 
-def dropout_fwd(x, y, mask, nclients, batch, per_img, p_drop, drop_mode=1, seed=0, counts=None):
+def dropout_fwd(x, y, mask, nclients, batch, per_img, p_drop, drop_mode=1, seed=0, counts=None,
+                seed_dev=None):
     call("fh_dropout_fwd", ptr(x), _cs(x), ptr(y), _cs(y), ptr(mask), _cs(mask), _counts(counts),
          nclients, batch, per_img, int(drop_mode), float(p_drop),
-         int(seed) & 0xFFFFFFFFFFFFFFFF, stream_handle())
+         int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), stream_handle())
 
 
 def dropout_bwd(dy, dx, nclients, batch, per_img, mask=None, p_drop=0.0, relu_out=None,

@@ -94,10 +94,13 @@ int fh_dp_apply(const float* local, int64_t local_stride, const float* global,
 int fh_sgd_step(float* param, const float* grad, float* momentum_buf, int64_t n, float lr,
                 float momentum, float weight_decay, int32_t first_step, void* stream);
 /* Adam / AdamW (decoupled=1). step_size = lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t),
- * both computed by the caller in double exactly as torch.optim does. */
+ * both computed by the caller in double exactly as torch.optim does.  scal_dev
+ * (nullable): device float[2] = {bc2_sqrt, -step_size} (fp32-rounded) read at run
+ * time instead, so one captured step graph serves every step t. */
 int fh_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                  double lr, double beta1, double beta2, double eps, double weight_decay,
-                 int32_t decoupled, double step_size, double bc2_sqrt, void* stream);
+                 int32_t decoupled, double step_size, double bc2_sqrt, const float* scal_dev,
+                 void* stream);
 
 /* ---------------- convolution / linear (fp32 MFMA implicit GEMM) ----------
  * x: [clients][batch][cin][h][w]; w: [cout][cin][kh][kw] per client; y: [clients][batch][cout][oh][ow].
@@ -180,12 +183,15 @@ int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs, 
 /* ---------------- MaxPool2d(2,2) (+ fused Dropout after it) ---------------
  * idx: uint8 window argmax [clients][batch][C][H/2][W/2]; drop_mode 0 none,
  * 1 generate keep-mask (Philox4x32-10 keyed by seed, slot, element) into mask,
- * 2 apply the caller's mask (parity).  Backward writes all four window slots;
+ * 2 apply the caller's mask (parity).  The Philox key is seed + *seed_dev
+ * (seed_dev nullable: a per-step device value for graph replay).
+ * Backward writes all four window slots;
  * xin (nullable) = the pooled ReLU output, to apply the ReLU mask at the argmax. */
 int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
                     int64_t i_cs, uint8_t* mask, int64_t m_cs, const int32_t* counts,
                     int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
-                    int32_t drop_mode, float p_drop, uint64_t seed, void* stream);
+                    int32_t drop_mode, float p_drop, uint64_t seed, const uint64_t* seed_dev,
+                    void* stream);
 int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,
                     const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin, int64_t x_cs,
                     float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
@@ -196,7 +202,8 @@ int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t 
  * dx = dy*mask/(1-p) [* (relu_out > 0)]; mask NULL = ReLU backward only. */
 int fh_dropout_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* mask,
                    int64_t m_cs, const int32_t* counts, int32_t nclients, int32_t batch,
-                   int64_t per_img, int32_t drop_mode, float p_drop, uint64_t seed, void* stream);
+                   int64_t per_img, int32_t drop_mode, float p_drop, uint64_t seed,
+                   const uint64_t* seed_dev, void* stream);
 int fh_dropout_bwd(const float* dy, int64_t dy_cs, const uint8_t* mask, int64_t m_cs, float p_drop,
                    const float* relu_out, int64_t r_cs, float* dx, int64_t dx_cs,
                    const int32_t* counts, int32_t nclients, int32_t batch, int64_t per_img,
