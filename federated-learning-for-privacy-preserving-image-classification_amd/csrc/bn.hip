@@ -41,7 +41,18 @@ struct BNArgs {
     int batch, C, HW, S, chunk;  // chunk: elements per slice (multiple of 4)
     float eps, momentum;
     int relu;
+    int vec;  // float4 element path (HW % 4 == 0; pooled input also needs W % 4 == 0)
     FastDiv fd_hw;
+    // backward through a 2x2 max-pool (+dropout): dy is not materialised; the gradient
+    // of element (img,c,y,x) is dpool[img,c,y/2,x/2] (x dropout keep/scale) routed by
+    // the window argmax pidx (== (y&1)*2 + (x&1)), else 0
+    const float* dpool;
+    const uint8_t* pidx;
+    const uint8_t* pmask;
+    int64_t dp_cs, pi_cs, pm_cs;
+    float pscale;
+    int W;
+    FastDiv fd_w;
 };
 
 // Visit this block's slice of channel c of client z: f(offset_within_client_tensor, nvec)
@@ -52,7 +63,7 @@ __device__ __forceinline__ void for_slice(const BNArgs& a, int z, int c, int s, 
     const int n = cnt * a.HW;
     const int e0 = s * a.chunk, e1 = min(n, e0 + a.chunk);
     const int64_t istride = (int64_t)a.C * a.HW, coff = (int64_t)c * a.HW;
-    if ((a.HW & 3) == 0) {
+    if (a.vec) {
         for (int e = e0 + threadIdx.x * 4; e < e1; e += 256 * 4) {
             uint32_t img, p;
             a.fd_hw.divmod(e, img, p);
@@ -183,18 +194,52 @@ __device__ __forceinline__ float gmask(float d, const float* yo, int64_t o) {
     return (yo && !(yo[o] > 0.f)) ? 0.f : d;
 }
 
+// upstream gradient at client-tensor offset o (before the ReLU mask): dy[o], or routed
+// from the pooled gradient (maxpool2_bwd semantics, layers.hip)
+__device__ __forceinline__ float pooled_g(const BNArgs& a, int z, int64_t o) {
+    uint32_t y, x;
+    const int64_t plane = o / a.HW;  // img*C + c
+    a.fd_w.divmod((uint32_t)(o - plane * a.HW), y, x);
+    const int64_t e = plane * (a.HW >> 2) + (int64_t)(y >> 1) * (a.W >> 1) + (x >> 1);
+    if (a.pidx[z * a.pi_cs + e] != (int)(((y & 1) << 1) | (x & 1))) return 0.f;
+    float g = a.dpool[z * a.dp_cs + e];
+    if (a.pmask) g = a.pmask[z * a.pm_cs + e] ? g * a.pscale : 0.f;
+    return g;
+}
+
+__device__ __forceinline__ float4 upstream4(const BNArgs& a, int z, int64_t o) {
+    if (!a.dpool) return ld4(a.dy + z * a.dy_cs + o);
+    // 4 consecutive columns (x % 4 == 0) = 2 pooled windows of one pooled row
+    uint32_t y, x;
+    const int64_t plane = o / a.HW;
+    a.fd_w.divmod((uint32_t)(o - plane * a.HW), y, x);
+    const int64_t e = plane * (a.HW >> 2) + (int64_t)(y >> 1) * (a.W >> 1) + (x >> 1);
+    const int r = (y & 1) << 1;
+    float g0 = a.dpool[z * a.dp_cs + e], g1 = a.dpool[z * a.dp_cs + e + 1];
+    if (a.pmask) {
+        g0 = a.pmask[z * a.pm_cs + e] ? g0 * a.pscale : 0.f;
+        g1 = a.pmask[z * a.pm_cs + e + 1] ? g1 * a.pscale : 0.f;
+    }
+    const int i0 = a.pidx[z * a.pi_cs + e], i1 = a.pidx[z * a.pi_cs + e + 1];
+    return make_float4(i0 == r ? g0 : 0.f, i0 == (r | 1) ? g0 : 0.f, i1 == r ? g1 : 0.f,
+                       i1 == (r | 1) ? g1 : 0.f);
+}
+
+__device__ __forceinline__ float upstream1(const BNArgs& a, int z, int64_t o) {
+    return a.dpool ? pooled_g(a, z, o) : a.dy[z * a.dy_cs + o];
+}
+
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const BNArgs a) {
     __shared__ double red[4];
     const int s = blockIdx.x, c = blockIdx.y, z = blockIdx.z;
     const float mean = a.save_mean[z * a.C + c];
-    const float* dyz = a.dy + z * a.dy_cs;
     const float* yoz = a.relu ? a.yout + z * a.yo_cs : nullptr;
     const float* xz = a.x + z * a.x_cs;
     float* drz = a.dres ? a.dres + z * a.dres_cs : nullptr;
     double sg = 0.0, dot = 0.0;
     for_slice(a, z, c, s, [&](int64_t o, int nv) {
         if (nv == 4) {
-            float4 g = ld4(dyz + o);
+            float4 g = upstream4(a, z, o);
             if (yoz) {
                 const float4 yv = ld4(yoz + o);
                 g.x = yv.x > 0.f ? g.x : 0.f; g.y = yv.y > 0.f ? g.y : 0.f;
@@ -206,7 +251,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const BNArgs a) {
             dot += ((double)((xv.x - mean) * g.x) + (double)((xv.y - mean) * g.y)) +
                    ((double)((xv.z - mean) * g.z) + (double)((xv.w - mean) * g.w));
         } else {
-            const float g = gmask(dyz[o], yoz, o);
+            const float g = gmask(upstream1(a, z, o), yoz, o);
             if (drz) drz[o] = g;
             sg += (double)g;
             dot += (double)((xz[o] - mean) * g);
@@ -236,13 +281,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const BNArgs a) {
     const float w = a.gamma[z * a.p_cs + c];
     const float k = n > 0 ? (float)(dot * (double)invstd * (double)invstd / (double)n) : 0.f;
     const float gm = n > 0 ? (float)(sg / (double)n) : 0.f;
-    const float* dyz = a.dy + z * a.dy_cs;
     const float* yoz = a.relu ? a.yout + z * a.yo_cs : nullptr;
     const float* xz = a.x + z * a.x_cs;
     float* dxz = a.dx + z * a.dx_cs;
     for_slice(a, z, c, s, [&](int64_t o, int nv) {
         if (nv == 4) {
-            const float4 d = ld4(dyz + o), xv = ld4(xz + o);
+            const float4 d = upstream4(a, z, o), xv = ld4(xz + o);
             float4 g = d;
             if (yoz) {
                 const float4 yv = ld4(yoz + o);
@@ -256,7 +300,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const BNArgs a) {
             r.w = (((g.w - gm) - (xv.w - mean) * k) * invstd) * w;
             st4(dxz + o, r);
         } else {
-            const float g = gmask(dyz[o], yoz, o);
+            const float g = gmask(upstream1(a, z, o), yoz, o);
             dxz[o] = (((g - gm) - (xz[o] - mean) * k) * invstd) * w;
         }
     });
@@ -280,6 +324,7 @@ static BNArgs bn_args(int nclients, int batch, int C, int HW, const int32_t* cou
     a.HW = HW;
     bn_geometry(nclients, batch, C, HW, a.S, a.chunk);
     a.fd_hw = FastDiv(HW);
+    a.vec = (HW & 3) == 0;
     return a;
 }
 
@@ -366,5 +411,45 @@ extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int6
     FH_LAUNCH_CHECK("bn_bwd reduce");
     hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_bwd apply");
+    return FH_OK;
+}
+
+// BN backward whose upstream gradient arrives through MaxPool2d(2,2) (+ the Dropout fused
+// after it): the full-resolution gradient is routed on the fly from dpool / pidx / pmask
+// (maxpool2_bwd semantics) instead of being written and re-read.
+extern "C" int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* pidx,
+                              int64_t pi_cs, const uint8_t* pmask, int64_t pm_cs, float p_drop,
+                              const float* yout, int64_t yo_cs, const float* x, int64_t x_cs,
+                              const float* gamma, int64_t p_cs, const float* save_mean,
+                              const float* save_invstd, float* dx, int64_t dx_cs, float* dgamma,
+                              float* dbeta, int64_t g_cs, const int32_t* counts,
+                              int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                              int32_t relu, void* workspace, size_t ws_bytes, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2 && !(H & 1) && !(W & 1),
+               "bn_bwd_pool: bad shape");
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "bn_bwd_pool: p=%g", p_drop);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dpool && pidx && x && gamma && save_mean && save_invstd, "bn_bwd_pool: null pointer");
+    FH_REQUIRE(!relu || yout, "bn_bwd_pool: relu needs the forward output");
+    const int HW = H * W;
+    const size_t need = fh_bn_workspace(nclients, batch, C, HW);
+    FH_REQUIRE(workspace && ws_bytes >= need, "bn_bwd_pool: workspace %zu < %zu", ws_bytes, need);
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.dpool = dpool; a.pidx = pidx; a.pmask = pmask;
+    a.dp_cs = dp_cs; a.pi_cs = pi_cs; a.pm_cs = pm_cs;
+    a.pscale = 1.0f / (1.0f - p_drop);
+    a.W = W;
+    a.fd_w = FastDiv(W);
+    a.vec = (HW & 3) == 0 && (W & 3) == 0;
+    a.yout = yout; a.x = x; a.gamma = gamma; a.save_mean = (float*)save_mean;
+    a.save_invstd = (float*)save_invstd; a.dx = dx; a.dgamma = dgamma; a.dbeta = dbeta;
+    a.part = (double*)workspace;
+    a.yo_cs = yo_cs; a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs; a.g_cs = g_cs; a.relu = relu;
+    hipStream_t st = as_stream(stream);
+    dim3 grid(a.S, C, nclients);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH_CHECK("bn_bwd_pool reduce");
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH_CHECK("bn_bwd_pool apply");
     return FH_OK;
 }

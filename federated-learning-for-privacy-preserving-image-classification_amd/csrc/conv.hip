@@ -21,6 +21,8 @@
 // wave owns an FM x FN grid of 32x32 accumulators.
 #include "fh_common.h"
 
+#include <cstdlib>
+
 namespace fh {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -538,12 +540,26 @@ static bool dconv_supported(int h, int w, int kh, int kw, int stride, int pad) {
     return kh == 3 && kw == 3 && stride == 1 && pad == 1 && h == w && (w == 8 || w == 16 || w == 32);
 }
 
+// Tuning knobs (diagnostics; read once): FH_DCONV_BLOCKS = workgroups a larger BM must
+// still leave (default 1024), FH_DCONV_MAXBM caps BM, FH_DWGRAD_BLOCKS = wgrad split
+// target (default 1024), FH_DWGRAD_WPX forces the pixel-wave count (1, 2 or 4) when the
+// channel counts allow it.
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+static const int kDconvBlocks = env_int("FH_DCONV_BLOCKS", 1024);
+static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 128);
+static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 1024);
+static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 0);
+
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
     DPlan p{32, 8, 1, Cr};
     for (int bm : {128, 64}) {
         if (Cr <= 4 || force_bm32) break;  // tiny-Cin first layer / scalar staging: BM=32
-        if (M >= bm && tn * ceil_div(M, bm) * nclients >= 1024) {
+        if (bm > kDconvMaxBm) continue;
+        if (M >= bm && tn * ceil_div(M, bm) * nclients >= kDconvBlocks) {
             p.bm = bm;
             break;
         }
@@ -634,12 +650,34 @@ static bool dwgrad_supported(int cin, int cout, int h, int w, int kh, int kw, in
 
 static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     DWPlan p{1, 1, 4, 128 / w, 1, 1};
-    if (cout % 64 == 0 && cin % 64 == 0) p = {2, 2, 1, 64 / w, 1, 1};
-    else if (cout % 64 == 0) p = {2, 1, 2, 128 / w, 1, 1};
-    else if (cin % 64 == 0) p = {1, 2, 2, 128 / w, 1, 1};
+    const bool co64 = cout % 64 == 0, ci64 = cin % 64 == 0;
+    if (kDwgradWpx == 4) p = {1, 1, 4, 128 / w, 1, 1};
+    else if (kDwgradWpx == 2 && co64) p = {2, 1, 2, 128 / w, 1, 1};
+    else if (kDwgradWpx == 2 && ci64) p = {1, 2, 2, 128 / w, 1, 1};
+    else if (co64 && ci64) p = {2, 2, 1, 64 / w, 1, 1};
+    else if (co64) p = {2, 1, 2, 128 / w, 1, 1};
+    else if (ci64) p = {1, 2, 2, 128 / w, 1, 1};
     const int64_t tiles = (int64_t)(cout / (32 * p.wco)) * (cin / (32 * p.wci)) * nclients;
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
-    const int want = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(1024, tiles)), nst);
+    const int want =
+        (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(kDwgradBlocks, tiles)), nst);
+    p.sps = (int)ceil_div(nst, want);
+    p.splits = (int)ceil_div(nst, p.sps);
+    return p;
+}
+
+// RGB first layer (cin == 3): (ci,kh,kw) = 27 on the MFMA lanes, pixels split 4 ways
+static bool dwgrad_small_supported(int cin, int cout, int h, int w, int kh, int kw, int stride,
+                                   int pad) {
+    return dconv_supported(h, w, kh, kw, stride, pad) && cin == 3 && cout % 32 == 0;
+}
+
+static DWPlan plan_dwgrad_small(int cout, int batch, int w, int nclients) {
+    DWPlan p{1, 1, 4, 128 / w, 1, 1};
+    const int64_t tiles = (int64_t)(cout / 32) * nclients;
+    const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
+    const int want =
+        (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(kDwgradBlocks, tiles)), nst);
     p.sps = (int)ceil_div(nst, want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;
@@ -757,6 +795,8 @@ extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int
     size_t direct = 0;
     if (dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad))  // (misaligned data: igemm)
         direct = dwgrad_ws_bytes(plan_dwgrad(cout, cin, batch, w_, nclients), nclients, cout, cin * 9);
+    if (dwgrad_small_supported(cin, cout, h, w_, kh, kw, stride, pad))
+        direct = dwgrad_ws_bytes(plan_dwgrad_small(cout, batch, w_, nclients), nclients, cout, cin * 9);
     return std::max(direct, wgrad_ws_bytes(plan_wgrad(cout, cin * kh * kw, batch * oh * ow, nclients),
                                            nclients));
 }
@@ -777,6 +817,32 @@ extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, in
     a.M = cout; a.N = cin * kh * kw; a.K = batch * oh * ow;
     const bool aligned = ((uintptr_t)x % 16 == 0) && ((uintptr_t)dy % 16 == 0) && x_cs % 4 == 0 &&
                          dy_cs % 4 == 0;
+    if (aligned && dwgrad_small_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
+        const DWPlan p = plan_dwgrad_small(cout, batch, w_, nclients);
+        const size_t need = dwgrad_ws_bytes(p, nclients, a.M, a.N);
+        FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
+        DWArgs d{};
+        d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
+        d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
+        d.splits = p.splits; d.stages_per_split = p.sps;
+        d.part = (float*)workspace;
+        const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
+        d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
+        hipStream_t st = as_stream(stream);
+        dim3 grid((unsigned)p.splits, (unsigned)(cout / 32), (unsigned)nclients);
+        if (w_ == 32) hipLaunchKernelGGL((dconv_wgrad_small_kernel<32, 3>), grid, dim3(256), 0, st, d);
+        else if (w_ == 16) hipLaunchKernelGGL((dconv_wgrad_small_kernel<16, 3>), grid, dim3(256), 0, st, d);
+        else hipLaunchKernelGGL((dconv_wgrad_small_kernel<8, 3>), grid, dim3(256), 0, st, d);
+        FH_LAUNCH_CHECK("conv2d_wgrad small-cin");
+        const int MN = a.M * a.N;
+        const int wblocks = (int)ceil_div(MN, 64);
+        const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
+        hipLaunchKernelGGL(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+                           (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
+                           (const float*)d.bias_part, db, db_cs, a.M);
+        FH_LAUNCH_CHECK("conv2d_wgrad reduce");
+        return FH_OK;
+    }
     if (aligned && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
         const DWPlan p = plan_dwgrad(cout, cin, batch, w_, nclients);
         const size_t need = dwgrad_ws_bytes(p, nclients, a.M, a.N);

@@ -525,4 +525,159 @@ __global__ void __launch_bounds__(256) dconv_wgrad_kernel(const DWArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// WGRAD for a small input-channel count (CIN*9 <= 32, e.g. the RGB first layer): the
+// MFMA B lanes span the whole (ci,kh,kw) axis at once (lane l -> its own patch offset,
+// lanes >= CIN*9 read a zero), one 32x32 accumulator per wave, four waves splitting
+// the pixels of a stage; same staging, slab and bias folding as dconv_wgrad_kernel.
+template <int W, int CIN>
+__global__ void __launch_bounds__(256) dconv_wgrad_small_kernel(const DWArgs a) {
+    constexpr int H = W, HW = H * W;
+    constexpr int SR = 128 / W, SPX = SR * W;
+    constexpr int SEGR = SR < H ? SR : H;
+    constexpr int NI = SR / SEGR;
+    constexpr int PW = W + 2, PR = NI * (SEGR + 2);
+    constexpr int CSTR = PR * PW;
+    constexpr int BMP = 33;
+    constexpr int RPW = SR / 4;
+    constexpr int DQ = SPX / 4, COI = 256 / DQ, NDY = 32 / COI;
+    constexpr int PQ = W / 4, RPI = 256 / PQ, NPR = CIN * PR, NPT = (NPR + RPI - 1) / RPI;
+    constexpr int DSZ = SPX * BMP, PSZ = CIN * CSTR;
+    constexpr int BUF = DSZ + PSZ;
+    static_assert(CIN * 9 <= 32 && SR % 4 == 0 && (SR % H == 0 || H % SR == 0), "geometry");
+
+    __shared__ float smem[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wpx = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int split = blockIdx.x, z = blockIdx.z;
+    const int co0 = blockIdx.y * 32;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int nst = (cnt * HW + SPX - 1) / SPX;
+    const int sbeg = split * a.stages_per_split;
+    const int send = min(nst, sbeg + a.stages_per_split);
+    const float* xz = a.x + z * a.x_cs;
+    const float* dyz = a.dy + z * a.dy_cs;
+
+    for (int q = tid; q < 2 * NPR; q += 256) {
+        const int bsel = q / NPR, row = q % NPR;
+        float* r = smem + bsel * BUF + DSZ + (row / PR) * CSTR + (row % PR) * PW;
+        r[0] = 0.f;
+        r[W + 1] = 0.f;
+    }
+
+    const int dco = tid / DQ, dp = (tid % DQ) * 4;
+    const int prt = tid / PQ, px = (tid % PQ) * 4;
+    float4 rd[NDY], rp[NPT];
+    auto load = [&](int st) {
+        const int R0 = st * SR;
+        {
+            const int row = R0 + dp / W, img = row / H, y = row % H, xx = dp % W;
+            const float* src = dyz + ((int64_t)(img * a.M + co0 + dco) * H + y) * W + xx;
+            const bool ok = img < cnt;
+#pragma unroll
+            for (int i = 0; i < NDY; ++i)
+                rd[i] = ok ? *reinterpret_cast<const float4*>(src + (int64_t)i * COI * HW)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const int img0 = R0 / H, y0 = R0 % H;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int q = prt + i * RPI;
+            const int cl = q / PR, pr = q % PR;
+            const int seg = pr / (SEGR + 2), rr = pr % (SEGR + 2);
+            const int img = img0 + seg, y = y0 + rr - 1;
+            const bool ok = q < NPR && img < cnt && (unsigned)y < (unsigned)H;
+            rp[i] = ok ? *reinterpret_cast<const float4*>(
+                             xz + ((int64_t)(img * CIN + cl) * H + y) * W + px)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int bsel) {
+        float* D = smem + bsel * BUF;
+#pragma unroll
+        for (int i = 0; i < NDY; ++i) {
+            float* d = D + dp * BMP + dco + i * COI;
+            d[0] = rd[i].x;
+            d[BMP] = rd[i].y;
+            d[2 * BMP] = rd[i].z;
+            d[3 * BMP] = rd[i].w;
+        }
+        float* P = D + DSZ;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int q = prt + i * RPI;
+            if (q < NPR) {
+                float* d = P + (q / PR) * CSTR + (q % PR) * PW + 1 + px;
+                d[0] = rp[i].x;
+                d[1] = rp[i].y;
+                d[2] = rp[i].z;
+                d[3] = rp[i].w;
+            }
+        }
+    };
+
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    float bsum = 0.f;
+    const int h = lane >> 5, col = lane & 31;
+    // lane's (ci,kh,kw); lanes >= CIN*9 alias lane 0 (their output columns are dropped)
+    const int nl = col < CIN * 9 ? col : 0;
+    const int ci = nl / 9, kh = (nl % 9) / 3, kw = nl % 3;
+    const int a_off = h * BMP + col;
+    if (sbeg < send) {
+        load(sbeg);
+        store(0);
+        __syncthreads();
+        int bsel = 0;
+        for (int st = sbeg; st < send; ++st) {
+            const bool more = st + 1 < send;
+            if (more) load(st + 1);
+            const float* Al = smem + bsel * BUF + a_off;
+            const float* P = smem + bsel * BUF + DSZ;
+#pragma unroll 1
+            for (int rr = 0; rr < RPW; ++rr) {
+                const int r = wpx * RPW + rr;
+                const int prow = (r / SEGR) * (SEGR + 2) + r % SEGR;
+                const float* Ar = Al + r * W * BMP;
+                const float* Br = P + ci * CSTR + (prow + kh) * PW + kw + h;
+#pragma unroll 8
+                for (int cp = 0; cp < W / 2; ++cp) {
+                    const float av = Ar[2 * cp * BMP];
+                    bsum += av;
+                    const float bv = Br[2 * cp];
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+                }
+            }
+            if (more) store(bsel ^ 1);
+            __syncthreads();
+            bsel ^= 1;
+        }
+    }
+    __syncthreads();
+    float* red = smem;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(wpx * 16 + r) * 64 + lane] = acc[r];
+    red[4 * 16 * 64 + wpx * 64 + lane] = bsum;
+    __syncthreads();
+    const int64_t slab = ((int64_t)z * a.splits + split) * a.M;
+    float* op = a.part + slab * a.N;
+    for (int e = tid; e < 16 * 64; e += 256) {
+        const int r = e / 64, l = e % 64;
+        const float v = ((red[(0 * 16 + r) * 64 + l] + red[(1 * 16 + r) * 64 + l]) +
+                         red[(2 * 16 + r) * 64 + l]) + red[(3 * 16 + r) * 64 + l];
+        const int m = co0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+        const int n = l & 31;
+        if (n < CIN * 9) op[(int64_t)m * a.N + n] = v;
+    }
+    if (a.bias_part && tid < 32) {
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            v += red[4 * 16 * 64 + q * 64 + tid] + red[4 * 16 * 64 + q * 64 + tid + 32];
+        a.bias_part[slab + co0 + tid] = v;
+    }
+}
+
 }  // namespace fh

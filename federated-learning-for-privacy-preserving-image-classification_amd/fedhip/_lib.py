@@ -62,6 +62,8 @@ SIGNATURES = {
                              I32, F32, I32, P]),
     "fh_bn_bwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, P, P, I64, P, I64, P, P, I64, P,
                         I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_bn_bwd_pool": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I64, P, P, P, I64,
+                             P, P, I64, P, I32, I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_maxpool2_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
                               F32, U64, P, P]),
     "fh_maxpool2_bwd": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I32,

@@ -325,18 +325,20 @@ class PackedNet:
         for i in range(len(convs) - 1, -1, -1):
             cv, ci, co, hw, bn = convs[i]
             r = A(f"r_{cv}", co, hw, hw)
-            dr = A(f"dr_{cv}", co, hw, hw)
-            if i % 2 == 1:
-                ops.maxpool2_bwd(dq, A(f"i_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8), dr, n, B,
-                                 co, hw, hw,
-                                 mask=A(f"m_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8) if dm else None,
-                                 p_drop=p, counts=cnt)
-            # else: dr was written by the next conv's dgrad
             dc = A(f"dc_{cv}", co, hw, hw)
             sm, si = self._bn_save(bn, co)
-            ops.bn_bwd(dr, r, A(f"c_{cv}", co, hw, hw), W(P_, f"{bn}.weight"), sm, si, dc,
-                       W(G, f"{bn}.weight"), W(G, f"{bn}.bias"), n, B, co, hw * hw, relu=True,
-                       counts=cnt)
+            if i % 2 == 1:  # upstream gradient comes through pool(+dropout): fused routing
+                h2 = hw // 2
+                ops.bn_bwd_pool(dq, A(f"i_{cv}", co, h2, h2, dtype=torch.uint8), r,
+                                A(f"c_{cv}", co, hw, hw), W(P_, f"{bn}.weight"), sm, si, dc,
+                                W(G, f"{bn}.weight"), W(G, f"{bn}.bias"), n, B, co, hw, hw,
+                                relu=True,
+                                pmask=A(f"m_{cv}", co, h2, h2, dtype=torch.uint8) if dm else None,
+                                p_drop=p, counts=cnt)
+            else:           # dr was written by the next conv's dgrad
+                ops.bn_bwd(A(f"dr_{cv}", co, hw, hw), r, A(f"c_{cv}", co, hw, hw),
+                           W(P_, f"{bn}.weight"), sm, si, dc, W(G, f"{bn}.weight"),
+                           W(G, f"{bn}.bias"), n, B, co, hw * hw, relu=True, counts=cnt)
             if i == 0:
                 xin = self.x
             elif i % 2 == 0:

@@ -284,6 +284,16 @@ def bn_bwd(dy, yout, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclien
          int(relu), ptr(ws), nb, stream_handle())
 
 
+def bn_bwd_pool(dpool, pidx, yout, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclients,
+                batch, C, H, W, relu=True, pmask=None, p_drop=0.0, counts=None):
+    """BN backward fed through MaxPool2d(2,2) (+dropout): pool backward fused in."""
+    ws, nb = _ws_for("fh_bn_workspace", x.device, nclients, batch, C, H * W)
+    call("fh_bn_bwd_pool", ptr(dpool), _cs(dpool), ptr(pidx), _cs(pidx), ptr(pmask), _cs(pmask),
+         float(p_drop), ptr(yout), _cs(yout), ptr(x), _cs(x), ptr(gamma), _cs(gamma),
+         ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dgamma), ptr(dbeta), _cs(dgamma),
+         _counts(counts), nclients, batch, C, H, W, int(relu), ptr(ws), nb, stream_handle())
+
+
 def maxpool2_fwd(x, y, idx, nclients, batch, C, H, W, mask=None, drop_mode=0, p_drop=0.0, seed=0,
                  counts=None, seed_dev=None):
     call("fh_maxpool2_fwd", ptr(x), _cs(x), ptr(y), _cs(y), ptr(idx), _cs(idx), ptr(mask),

@@ -180,6 +180,18 @@ int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs, 
               int32_t batch, int32_t C, int32_t HW, int32_t relu, void* workspace,
               size_t ws_bytes, void* stream);
 
+/* BN backward whose upstream gradient comes through MaxPool2d(2,2) (+ the Dropout
+ * fused after it, p_drop / pmask as in fh_maxpool2_fwd; pmask NULL = no dropout):
+ * the full-resolution gradient is routed from dpool [clients][batch][C][H/2][W/2]
+ * by the argmax bytes pidx on the fly (fh_maxpool2_bwd + fh_bn_bwd in one pass pair). */
+int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* pidx, int64_t pi_cs,
+                   const uint8_t* pmask, int64_t pm_cs, float p_drop, const float* yout,
+                   int64_t yo_cs, const float* x, int64_t x_cs, const float* gamma, int64_t p_cs,
+                   const float* save_mean, const float* save_invstd, float* dx, int64_t dx_cs,
+                   float* dgamma, float* dbeta, int64_t g_cs, const int32_t* counts,
+                   int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W, int32_t relu,
+                   void* workspace, size_t ws_bytes, void* stream);
+
 /* ---------------- MaxPool2d(2,2) (+ fused Dropout after it) ---------------
  * idx: uint8 window argmax [clients][batch][C][H/2][W/2]; drop_mode 0 none,
  * 1 generate keep-mask (Philox4x32-10 keyed by seed, slot, element) into mask,

@@ -115,3 +115,48 @@ def test_bn_deterministic():
         outs.append((y, sm, si))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("case", [(2, 32, 32, 32), (3, 17, 64, 16), (1, 32, 128, 8), (2, 5, 8, 6)])
+@pytest.mark.parametrize("p_drop", [0.0, 0.5])
+def test_bn_bwd_pool_matches_unfused(case, p_drop):
+    """fh_bn_bwd_pool == fh_maxpool2_bwd followed by fh_bn_bwd, bit for bit."""
+    nc, B, C, H = case
+    W = H
+    torch.manual_seed(H + C)
+    cnt = _counts(nc, B, H)
+    counts = torch.tensor(cnt, dtype=torch.int32, device=DEV)
+    x = torch.randn(nc, B, C, H, W, device=DEV)
+    gamma = torch.rand(nc, C, device=DEV) + 0.5
+    beta = torch.randn(nc, C, device=DEV) * 0.1
+    y = torch.zeros_like(x)
+    sm = torch.zeros(nc, C, device=DEV)
+    si = torch.zeros(nc, C, device=DEV)
+    ops.bn_fwd_train(x, y, gamma, beta, None, None, sm, si, nc, B, C, H * W, relu=True,
+                     counts=counts)
+    q = torch.zeros(nc, B, C, H // 2, W // 2, device=DEV)
+    idx = torch.zeros(nc, B, C, H // 2, W // 2, dtype=torch.uint8, device=DEV)
+    mask = torch.zeros_like(idx) if p_drop > 0 else None
+    ops.maxpool2_fwd(y, q, idx, nc, B, C, H, W, mask=mask, drop_mode=1 if p_drop > 0 else 0,
+                     p_drop=p_drop, seed=3, counts=counts)
+    dq = torch.randn_like(q)
+    # unfused reference path
+    dr = torch.zeros_like(x)
+    ops.maxpool2_bwd(dq, idx, dr, nc, B, C, H, W, mask=mask, p_drop=p_drop, counts=counts)
+    dx1, dg1, db1 = torch.zeros_like(x), torch.zeros(nc, C, device=DEV), torch.zeros(nc, C, device=DEV)
+    ops.bn_bwd(dr, y, x, gamma, sm, si, dx1, dg1, db1, nc, B, C, H * W, relu=True, counts=counts)
+    dx2, dg2, db2 = torch.zeros_like(x), torch.zeros(nc, C, device=DEV), torch.zeros(nc, C, device=DEV)
+    ops.bn_bwd_pool(dq, idx, y, x, gamma, sm, si, dx2, dg2, db2, nc, B, C, H, W, relu=True,
+                    pmask=mask, p_drop=p_drop, counts=counts)
+    torch.cuda.synchronize()
+    if W % 4 == 0:  # same float4 element order in both paths
+        for z in range(nc):
+            n = cnt[z]
+            assert torch.equal(dx1[z, :n], dx2[z, :n])
+        assert torch.equal(dg1, dg2) and torch.equal(db1, db2)
+    else:           # fused path runs scalar (fp64 partial sums in another order)
+        for z in range(nc):
+            n = cnt[z]
+            torch.testing.assert_close(dx1[z, :n], dx2[z, :n], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(dg1, dg2, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(db1, db2, rtol=1e-6, atol=1e-6)
