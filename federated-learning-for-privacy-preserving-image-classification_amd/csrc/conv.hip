@@ -42,6 +42,8 @@ struct ConvArgs {
     int accumulate;      // DGRAD: dx += result
     int splits, kchunk;  // split-K (WGRAD always; FWD/DGRAD when the grid is small)
     float* bias_part;    // WGRAD: per-split conv-bias partial sums [z][split][M] (or null)
+    float* sq_part;      // WGRAD per-sample mode: sum of squares of each tile -> [z][split][tile]
+    int sq_bias;         //   ... including the conv-bias gradient (first n-tile)
     int M, N, K;         // GEMM extents at full batch
     FastDiv fd_ohw, fd_ow, fd_hw, fd_w;
 };
@@ -219,7 +221,8 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const bool do_bias = (OP == OP_WGRAD) && a.bias_part != nullptr && blockIdx.x == 0;
+    const bool do_bias = (OP == OP_WGRAD) && (a.bias_part != nullptr || a.sq_bias) &&
+                         blockIdx.x == 0;
     float bsum = 0.f;
     if (kbeg < kend) {
         load_tiles(kbeg);
@@ -258,6 +261,33 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     }
 
     // ---------------- epilogue ------------------------------------------
+    // per-sample squared norm (DP-SGD): one split per image; the tile's dW_i (and db_i)
+    // are reduced to a sum of squares instead of being stored
+    if constexpr (OP == OP_WGRAD) {
+        if (a.sq_part) {
+            __shared__ float sq_red[4];
+            const int rb2 = 4 * (lane >> 5), c2 = lane & 31;
+            float sq = 0.f;
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rb2;
+                        const int n = n0 + wn * WN + j * 32 + c2;
+                        if (m < M && n < N) sq += acc[i][j][r] * acc[i][j][r];
+                    }
+            if (a.sq_bias && blockIdx.x == 0 && tid < BM && m0 + tid < M) sq += bsum * bsum;
+            sq = wave_sum(sq);
+            if (lane == 0) sq_red[wid] = sq;
+            __syncthreads();
+            if (tid == 0)
+                a.sq_part[(int64_t)blockIdx.z * gridDim.x * gridDim.y + blockIdx.y * gridDim.x +
+                          blockIdx.x] = (sq_red[0] + sq_red[1]) + (sq_red[2] + sq_red[3]);
+            return;
+        }
+    }
     // WGRAD with one split writes dW / db in place (no slab, no reduce pass)
     const bool wdirect = (OP == OP_WGRAD) && a.splits == 1;
     if (do_bias && tid < BM && m0 + tid < M) {
@@ -946,4 +976,77 @@ extern "C" int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, in
                                int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
     return fh_conv2d_wgrad(x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs, workspace, ws_bytes, counts,
                            nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0, stream);
+}
+
+// ---- DP-SGD: per-sample squared gradient norms of a conv layer --------------
+// One WGRAD split per image (K = that image's pixels): each workgroup holds a tile
+// of dW_i and reduces it to a sum of squares; conv_sq_reduce adds the tiles of each
+// (client, image) in a fixed order into sqnorm[z][img] (double, accumulated over layers).
+namespace fh {
+__global__ void __launch_bounds__(256)
+conv_sq_reduce_kernel(const float* __restrict__ part, int tiles, int batch,
+                      const int32_t* __restrict__ counts, double* __restrict__ sqnorm) {
+    const int z = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int cnt = counts ? counts[z] : batch;
+    if (i >= batch) return;
+    double s = 0.0;
+    if (i < cnt) {
+        const float* p = part + ((int64_t)z * batch + i) * tiles;
+        for (int t = 0; t < tiles; ++t) s += (double)p[t];
+    }
+    sqnorm[(int64_t)z * batch + i] += s;
+}
+}  // namespace fh
+
+static Plan plan_persample(int M, int N, int ohw, int batch) {
+    Plan p{pick_wgrad_tile(M), batch, ohw, M, N, batch * ohw};
+    return p;
+}
+
+extern "C" size_t fh_conv2d_persample_sqnorm_workspace(int32_t nclients, int32_t batch,
+                                                       int32_t cin, int32_t h, int32_t w_,
+                                                       int32_t cout, int32_t kh, int32_t kw,
+                                                       int32_t stride, int32_t pad) {
+    int oh = (h + 2 * pad - kh) / stride + 1, ow = (w_ + 2 * pad - kw) / stride + 1;
+    if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
+    const Plan p = plan_persample(cout, cin * kh * kw, oh * ow, batch);
+    const int64_t tiles = ceil_div(p.N, p.t.bn) * ceil_div(p.M, p.t.bm);
+    return (size_t)nclients * batch * tiles * sizeof(float);
+}
+
+extern "C" int fh_conv2d_persample_sqnorm(const float* x, int64_t x_cs, const float* dy,
+                                          int64_t dy_cs, int32_t with_bias, double* sqnorm,
+                                          void* workspace, size_t ws_bytes,
+                                          const int32_t* counts, int32_t nclients, int32_t batch,
+                                          int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                                          int32_t kh, int32_t kw, int32_t stride, int32_t pad,
+                                          void* stream) {
+    int oh, ow;
+    int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
+    if (rc) return rc;
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && dy && sqnorm && workspace, "conv2d_persample_sqnorm: null pointer");
+    const size_t need = fh_conv2d_persample_sqnorm_workspace(nclients, batch, cin, h, w_, cout, kh,
+                                                             kw, stride, pad);
+    FH_REQUIRE(ws_bytes >= need, "conv2d_persample_sqnorm: workspace %zu < %zu", ws_bytes, need);
+    ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
+    a.x = x; a.dy = dy; a.x_cs = x_cs; a.dy_cs = dy_cs;
+    a.M = cout; a.N = cin * kh * kw; a.K = batch * oh * ow;
+    const Plan p = plan_persample(a.M, a.N, oh * ow, batch);
+    a.splits = batch;
+    a.kchunk = oh * ow;
+    a.sq_part = (float*)workspace;
+    a.sq_bias = with_bias;
+    hipStream_t st = as_stream(stream);
+    dim3 grid((unsigned)ceil_div(a.N, p.t.bn), (unsigned)ceil_div(a.M, p.t.bm),
+              (unsigned)(nclients * batch));
+    rc = launch_shape<OP_WGRAD>(kh, kw, stride, p.t, grid, a, st);
+    if (rc) return rc;
+    FH_LAUNCH_CHECK("conv2d_persample_sqnorm");
+    const int tiles = (int)(grid.x * grid.y);
+    hipLaunchKernelGGL(conv_sq_reduce_kernel, dim3((unsigned)ceil_div(batch, 256), nclients),
+                       dim3(256), 0, st, (const float*)workspace, tiles, batch, counts, sqnorm);
+    FH_LAUNCH_CHECK("conv2d_persample_sqnorm reduce");
+    return FH_OK;
 }

@@ -121,4 +121,17 @@ __device__ __forceinline__ float u01(uint32_t x) {
     return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
 }
 
+// four N(0,1) draws (Box-Muller on one Philox block)
+__device__ __forceinline__ void gauss4(uint64_t seed, uint64_t hi, uint64_t lo, float g[4]) {
+    const uint4 r = Philox::gen(seed, hi, lo);
+    const float ra = sqrtf(-2.0f * logf(u01(r.x))), rb = sqrtf(-2.0f * logf(u01(r.z)));
+    float sa, ca, sb, cb;
+    sincosf(6.2831853071795864f * u01(r.y), &sa, &ca);
+    sincosf(6.2831853071795864f * u01(r.w), &sb, &cb);
+    g[0] = ra * ca;
+    g[1] = ra * sa;
+    g[2] = rb * cb;
+    g[3] = rb * sb;
+}
+
 }  // namespace fh

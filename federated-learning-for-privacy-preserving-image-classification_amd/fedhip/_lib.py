@@ -64,6 +64,13 @@ SIGNATURES = {
                         I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_bn_bwd_pool": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I64, P, P, P, I64,
                              P, P, I64, P, I32, I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_conv2d_persample_sqnorm_workspace": (SZ, [I32] * 10),
+    "fh_conv2d_persample_sqnorm": (I32, [P, I64, P, I64, I32, P, P, SZ, P, I32, I32, I32, I32,
+                                         I32, I32, I32, I32, I32, I32, P]),
+    "fh_linear_persample_sqnorm": (I32, [P, I64, P, I64, I32, P, P, I32, I32, I32, I32, P]),
+    "fh_dpsgd_clip_coef": (I32, [P, P, I32, I32, F64, P, P]),
+    "fh_scale_rows": (I32, [P, I64, P, P, I32, I32, I64, P, I64, P]),
+    "fh_dpsgd_noise": (I32, [P, I64, I64, P, I32, I32, F32, U64, P, P]),
     "fh_maxpool2_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
                               F32, U64, P, P]),
     "fh_maxpool2_bwd": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I32,

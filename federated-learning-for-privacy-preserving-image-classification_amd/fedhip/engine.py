@@ -38,6 +38,23 @@ from .net import PackedNet
 
 
 @dataclass
+class DPSGDConfig:
+    """Per-sample-clipped DP-SGD (dpsgd.hip).  noise_multiplier None -> the reference's
+    Gaussian-mechanism sigma = sqrt(2 ln(1.25/delta)) / epsilon (privacy.py:209)."""
+    max_grad_norm: float = 1.0
+    epsilon: float = 1.0
+    delta: float = 1e-5
+    noise_multiplier: float = None
+    seed: int = 0
+
+    @property
+    def sigma(self):
+        if self.noise_multiplier is not None:
+            return float(self.noise_multiplier)
+        return math.sqrt(2.0 * math.log(1.25 / self.delta)) / self.epsilon
+
+
+@dataclass
 class ClientMetrics:
     loss: float
     accuracy: float
@@ -46,7 +63,7 @@ class ClientMetrics:
 
 
 class PackedTrainer:
-    def __init__(self, model, capacity, batch=32, device="cuda"):
+    def __init__(self, model, capacity, batch=32, device="cuda", dpsgd=None):
         load()  # fail loudly if libfedhip is missing
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -71,6 +88,10 @@ class PackedTrainer:
         self.loss_out = torch.zeros(capacity, device=dev)
         self.seg_offsets = torch.tensor(L.seg_offsets(), dtype=torch.int64, device=dev)
         self.opt_type, self.lr, self.opt_step = "sgd", 0.01, 0
+        self.dpsgd = dpsgd
+        if dpsgd is not None:
+            self._sq = torch.zeros(capacity, batch, dtype=torch.float64, device=dev)
+            self._coef = torch.zeros(capacity, batch, device=dev)
         self.on_step = None
         self.pre_step = None
         # Step graphs: every step after the first of a round is replayed from a HIP graph
@@ -153,7 +174,14 @@ class PackedTrainer:
                        loss_out=self.loss_out, acc_loss=self.acc_loss,
                        acc_correct=self.acc_correct, acc_seen=self.acc_seen, reset=reset,
                        counts=counts)
-        net.backward(self.params, self.grads, n, counts)
+        if self.dpsgd is None:
+            net.backward(self.params, self.grads, n, counts)
+        else:
+            d = self.dpsgd
+            net.backward_dpsgd(self.params, self.grads, n, counts, self._sq, self._coef,
+                               d.max_grad_norm, d.sigma * d.max_grad_norm,
+                               noise_seed=net._seed(77 + 1000 * d.seed),
+                               noise_seed_dev=net.seed_dev, P=self.layout.P)
         self._optimizer_launch(n, first, adam_dev)
 
     # ------------------------------------------------------------ one packed step

@@ -234,6 +234,62 @@ class PackedNet:
         ops.conv2d_wgrad(self.x, da1, W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 1, 28, 28, 32,
                          3, 1, 1, counts=cnt)
 
+    # ---------------- DP-SGD backward (per-sample clipping; dpsgd.hip)
+    def backward_dpsgd(self, params, grads, n, counts, sqnorm, coef, max_norm, sigma_c,
+                       noise_seed, noise_seed_dev=None, P=None):
+        """Backward with per-sample clipping + Gaussian noise.  Pass 1: the dgrad chain and
+        every layer's per-sample squared gradient norm; clip coefficients; pass 2: each
+        layer's WGRAD on its coefficient-scaled upstream gradient; noise on all grads.
+        Models with BatchNorm have no per-sample gradient (batch statistics couple the
+        samples): like Opacus, DP-SGD is refused for them."""
+        if self.family != "SimpleCNN":
+            raise FedHipError(f"DP-SGD needs a model without BatchNorm ({self.family} has it)")
+        if n == 0:
+            return
+        A, B, W, K, cnt = self.A, self.batch, self.W, self.num_classes, counts
+        P_, G = params, grads
+        sqnorm[:n].zero_()
+        # pass 1: dgrad chain + per-sample norms
+        ops.linear_persample_sqnorm(self._fc_in, self.dlogits, sqnorm, n, B, 128, K, counts=cnt)
+        dd1 = A("dd1", 128)
+        ops.linear_dgrad(self.dlogits, W(P_, "fc2.weight"), dd1, n, B, 128, K, counts=cnt)
+        dh1 = A("dh1", 128)
+        mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
+        ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
+                        relu_out=A("h1", 128), counts=cnt)
+        p2 = A("p2", 64, 7, 7)
+        ops.linear_persample_sqnorm(p2, dh1, sqnorm, n, B, 3136, 128, counts=cnt)
+        dp2 = A("dp2", 64, 7, 7)
+        ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
+        da2 = A("da2", 64, 14, 14)
+        ops.maxpool2_bwd(dp2, A("i2", 64, 7, 7, dtype=torch.uint8), da2, n, B, 64, 14, 14,
+                         xin=A("a2", 64, 14, 14), counts=cnt)
+        p1 = A("p1", 32, 14, 14)
+        ops.conv2d_persample_sqnorm(p1, da2, sqnorm, n, B, 32, 14, 14, 64, 3, 1, 1, counts=cnt)
+        dp1 = A("dp1", 32, 14, 14)
+        ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, 14, 14, 64, 3, 1, 1,
+                         counts=cnt)
+        da1 = A("da1", 32, 28, 28)
+        ops.maxpool2_bwd(dp1, A("i1", 32, 14, 14, dtype=torch.uint8), da1, n, B, 32, 28, 28,
+                         xin=A("a1", 32, 28, 28), counts=cnt)
+        ops.conv2d_persample_sqnorm(self.x, da1, sqnorm, n, B, 1, 28, 28, 32, 3, 1, 1,
+                                    counts=cnt)
+        ops.dpsgd_clip_coef(sqnorm, coef, n, B, max_norm, counts=cnt)
+        # pass 2: clipped sums = WGRAD on coef-scaled upstream rows
+        s = ops.scale_rows(self.dlogits, coef, A("s_dl", K), n, B, K, counts=cnt)
+        ops.linear_wgrad(self._fc_in, s, W(G, "fc2.weight"), W(G, "fc2.bias"), n, B, 128, K,
+                         counts=cnt)
+        s = ops.scale_rows(dh1, coef, A("s_dh1", 128), n, B, 128, counts=cnt)
+        ops.linear_wgrad(p2, s, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136, 128, counts=cnt)
+        s = ops.scale_rows(da2, coef, A("s_da2", 64, 14, 14), n, B, 64 * 196, counts=cnt)
+        ops.conv2d_wgrad(p1, s, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, 14, 14, 64,
+                         3, 1, 1, counts=cnt)
+        s = ops.scale_rows(da1, coef, A("s_da1", 32, 28, 28), n, B, 32 * 784, counts=cnt)
+        ops.conv2d_wgrad(self.x, s, W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 1, 28, 28,
+                         32, 3, 1, 1, counts=cnt)
+        ops.dpsgd_noise(G, self.layout.P if P is None else P, n, B, sigma_c, seed=noise_seed,
+                        seed_dev=noise_seed_dev, counts=cnt)
+
     # ---------------- CIFAR10CNN (models_pytorch.py:136-165)
     _CIFAR_CONVS = [  # name, cin, cout, hw, bn
         ("conv1", 3, 32, 32, "bn1"), ("conv2", 32, 32, 32, "bn2"),

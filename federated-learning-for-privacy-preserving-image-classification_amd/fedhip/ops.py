@@ -150,11 +150,11 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
 
 
 def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None):
-    ws, _ = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, cin, h, wd, cout, k, k,
-                    stride, pad)
+    ws, nb = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, cin, h, wd, cout, k,
+                     k, stride, pad)
     ev = PROBE.begin(_conv_tag("wgrad", cin, h, wd, cout, k, stride))
     call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
-         ptr(ws), ws.numel(), _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride,
+         ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride,
          pad, stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return dw
@@ -176,10 +176,42 @@ def linear_dgrad(dy, w, dx, nclients, batch, in_f, out_f, counts=None):
 
 
 def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
-    ws, _ = _ws_for("fh_linear_wgrad_workspace", x.device, nclients, batch, in_f, out_f)
+    ws, nb = _ws_for("fh_linear_wgrad_workspace", x.device, nclients, batch, in_f, out_f)
     call("fh_linear_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
-         ptr(ws), ws.numel(), _counts(counts), nclients, batch, in_f, out_f, stream_handle())
+         ptr(ws), nb, _counts(counts), nclients, batch, in_f, out_f, stream_handle())
     return dw
+
+
+# ------------------------------------------------------------------ DP-SGD (per-sample clip)
+def conv2d_persample_sqnorm(x, dy, sqnorm, nclients, batch, cin, h, wd, cout, k, stride, pad,
+                            with_bias=True, counts=None):
+    ws, nb = _ws_for("fh_conv2d_persample_sqnorm_workspace", x.device, nclients, batch, cin, h,
+                     wd, cout, k, k, stride, pad)
+    call("fh_conv2d_persample_sqnorm", ptr(x), _cs(x), ptr(dy), _cs(dy), int(with_bias),
+         ptr(sqnorm), ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k,
+         stride, pad, stream_handle())
+
+
+def linear_persample_sqnorm(x, dy, sqnorm, nclients, batch, in_f, out_f, with_bias=True,
+                            counts=None):
+    call("fh_linear_persample_sqnorm", ptr(x), _cs(x), ptr(dy), _cs(dy), int(with_bias),
+         ptr(sqnorm), _counts(counts), nclients, batch, in_f, out_f, stream_handle())
+
+
+def dpsgd_clip_coef(sqnorm, coef, nclients, batch, max_norm, counts=None):
+    call("fh_dpsgd_clip_coef", ptr(sqnorm), _counts(counts), nclients, batch, float(max_norm),
+         ptr(coef), stream_handle())
+
+
+def scale_rows(x, coef, out, nclients, batch, per_img, counts=None):
+    call("fh_scale_rows", ptr(x), _cs(x), ptr(coef), _counts(counts), nclients, batch,
+         int(per_img), ptr(out), _cs(out), stream_handle())
+    return out
+
+
+def dpsgd_noise(grad, n, nclients, batch, sigma_c, seed=0, seed_dev=None, counts=None):
+    call("fh_dpsgd_noise", ptr(grad), _cs(grad), int(n), _counts(counts), nclients, batch,
+         float(sigma_c), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), stream_handle())
 
 
 # ------------------------------------------------------------------ FedAvg / validation

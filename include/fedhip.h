@@ -192,6 +192,38 @@ int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* pidx, int64
                    int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W, int32_t relu,
                    void* workspace, size_t ws_bytes, void* stream);
 
+/* ---------------- DP-SGD: per-sample clipping (north_star extension) -------
+ * g = (sum_i min(1, C/||g_i||) g_i + sigma*C*N(0,I)) / B per optimizer step, g_i the
+ * gradient of sample i's loss over ALL parameters.  The caller accumulates
+ * ||g_i/B||^2 layer by layer into sqnorm [clients][batch] (double; zero it first):
+ *   convs   fh_conv2d_persample_sqnorm (per-image WGRAD tiles, workspace query below)
+ *   linears fh_linear_persample_sqnorm (||dy_i||^2 (||x_i||^2 + with_bias))
+ * then fh_dpsgd_clip_coef -> coef [clients][batch], fh_scale_rows scales each layer's
+ * upstream gradient rows by coef before the ordinary WGRAD (clipped sum), and
+ * fh_dpsgd_noise adds sigma*C/B * N(0,1) (Philox key seed + *seed_dev, seed_dev nullable).
+ * Replaces: nothing in the reference (its DP clips whole update deltas, privacy.py:107-144);
+ * sigma follows its Gaussian-mechanism formula (privacy.py:209). */
+size_t fh_conv2d_persample_sqnorm_workspace(int32_t nclients, int32_t batch, int32_t cin,
+                                            int32_t h, int32_t w, int32_t cout, int32_t kh,
+                                            int32_t kw, int32_t stride, int32_t pad);
+int fh_conv2d_persample_sqnorm(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                               int32_t with_bias, double* sqnorm, void* workspace,
+                               size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t cin, int32_t h, int32_t w, int32_t cout,
+                               int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream);
+int fh_linear_persample_sqnorm(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                               int32_t with_bias, double* sqnorm, const int32_t* counts,
+                               int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f,
+                               void* stream);
+int fh_dpsgd_clip_coef(const double* sqnorm, const int32_t* counts, int32_t nclients,
+                       int32_t batch, double max_norm, float* coef, void* stream);
+int fh_scale_rows(const float* in, int64_t in_cs, const float* coef, const int32_t* counts,
+                  int32_t nclients, int32_t batch, int64_t per_img, float* out, int64_t out_cs,
+                  void* stream);
+int fh_dpsgd_noise(float* grad, int64_t g_cs, int64_t n, const int32_t* counts, int32_t nclients,
+                   int32_t batch, float sigma_c, uint64_t seed, const uint64_t* seed_dev,
+                   void* stream);
+
 /* ---------------- MaxPool2d(2,2) (+ fused Dropout after it) ---------------
  * idx: uint8 window argmax [clients][batch][C][H/2][W/2]; drop_mode 0 none,
  * 1 generate keep-mask (Philox4x32-10 keyed by seed, slot, element) into mask,

@@ -1,0 +1,130 @@
+"""Per-sample-clipped DP-SGD (north_star extension; parity unpinned by the reference,
+which has no DP-SGD) against the CPU oracle oracle/dpsgd_ref.py.
+
+* sigma = 0: one packed step (3 clients, one with a partial batch) == the fp64
+  per-sample-loop oracle replaying the GPU's max-pool / ReLU decisions, within the
+  fp32-vs-fp64 tolerance used by the training parity tests;
+* C huge: clipping inactive -> identical to the ordinary (non-private) gradient step;
+* sigma > 0: the added noise has std sigma*C/B per coordinate (first SGD step moves
+  parameters by lr * noise), zero mean;
+* BatchNorm models are refused (no per-sample gradient)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from fedhip._lib import FedHipError
+from fedhip.engine import DPSGDConfig, PackedTrainer
+from oracle import dpsgd_ref, train_ref
+from src.shared import models_pytorch as hm
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _engine(sizes, dpsgd, seed=0, lr=0.05):
+    torch.manual_seed(seed)
+    model = hm.ModelFactory.create_model("simple_cnn", dropout_rate=0.0)
+    eng = PackedTrainer(model.to(DEV), capacity=len(sizes), batch=32, device=DEV, dpsgd=dpsgd)
+    for k in range(len(sizes)):
+        eng.load_module_state(k, model)
+    eng.begin_round("sgd", lr)
+    g = torch.Generator().manual_seed(seed + 1)
+    xs = [torch.randn(n, 1, 28, 28, generator=g) for n in sizes]
+    ys = [torch.randint(0, 10, (n,), generator=g) for n in sizes]
+    for k in range(len(sizes)):
+        eng.net.x[k, :sizes[k]].copy_(xs[k])
+        eng.net.y[k, :sizes[k]].copy_(ys[k])
+    return eng, xs, ys
+
+
+def _decisions(eng, slots):
+    relus = [b[:slots].cpu() > 0 for b in eng.net.relu_output_buffers()]
+    per = []
+    for slot in range(slots):
+        pools = []
+        for buf, H, W in eng.net.pool_index_buffers():
+            a = buf[slot].long().cpu()
+            OH, OW = a.shape[-2:]
+            oh = torch.arange(OH).view(1, 1, OH, 1)
+            ow = torch.arange(OW).view(1, 1, 1, OW)
+            pools.append((2 * oh + a // 2) * W + (2 * ow + a % 2))
+        per.append((pools, [r[slot] for r in relus]))
+    return per
+
+
+@pytest.mark.parametrize("max_norm", [0.05, 1.0])
+def test_dpsgd_step_matches_oracle(max_norm):
+    sizes = [32, 32, 7]
+    eng, xs, ys = _engine(sizes, DPSGDConfig(max_grad_norm=max_norm, noise_multiplier=0.0))
+    snap = {}
+    eng.on_step = lambda e, n: snap.setdefault("d", _decisions(e, n))
+    counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
+    eng.step(3, counts)
+    torch.cuda.synchronize()
+    for k, n in enumerate(sizes):
+        ref32 = train_ref.make_model("simple_cnn", 0, dropout_rate=0.0)
+        ref64 = train_ref.make_model("simple_cnn", None, dropout_rate=0.0).double()
+        ref64.load_state_dict({a: b.double() for a, b in ref32.state_dict().items()})
+        p0 = train_ref.param_vector(ref64).clone()
+        pools, relus = snap["d"][k]
+        pools = [p[:n] for p in pools]
+        relus = [r[:n] for r in relus]
+        opt32 = train_ref.make_optimizer(ref32, "sgd", 0.05)
+        opt64 = train_ref.make_optimizer(ref64, "sgd", 0.05)
+        c32, _ = dpsgd_ref.dpsgd_step(ref32, opt32, xs[k], ys[k], max_norm, pools=pools,
+                                      relus=relus)
+        c64, _ = dpsgd_ref.dpsgd_step(ref64, opt64, xs[k].double(), ys[k], max_norm,
+                                      pools=pools, relus=relus)
+        got = eng._coef[k, :n].double().cpu()
+        assert torch.allclose(got, torch.tensor(c64, dtype=torch.float64), rtol=1e-4, atol=1e-6)
+        if max_norm < 0.1:
+            assert max(c64) < 1.0  # clipping active
+        p32 = train_ref.param_vector(ref32).double()
+        p64 = train_ref.param_vector(ref64)
+        pg = eng.params[k, :eng.layout.P].double().cpu()
+        e_hip = (pg - p64).norm().item()
+        e_cpu = (p32 - p64).norm().item()
+        assert e_hip <= 4 * e_cpu + 1e-4 * (p64 - p0).norm().item() + 1e-7 * p64.norm().item(), \
+            (k, e_hip, e_cpu)
+
+
+def test_dpsgd_without_clipping_equals_plain_step():
+    sizes = [32, 20]
+    a, _, _ = _engine(sizes, DPSGDConfig(max_grad_norm=1e9, noise_multiplier=0.0))
+    b, _, _ = _engine(sizes, None)
+    counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
+    a.step(2, counts)
+    b.step(2, counts)
+    torch.cuda.synchronize()
+    assert torch.all(a._coef[0, :32] == 1.0) and torch.all(a._coef[1, :20] == 1.0)
+    d = (a.params - b.params).abs().max().item()
+    assert d <= 1e-6 * b.params.abs().max().item(), d
+
+
+def test_dpsgd_noise_scale():
+    sizes = [32, 16]
+    lr, C, sig = 0.05, 1.0, 2.0
+    a, _, _ = _engine(sizes, DPSGDConfig(max_grad_norm=C, noise_multiplier=sig), lr=lr)
+    b, _, _ = _engine(sizes, DPSGDConfig(max_grad_norm=C, noise_multiplier=0.0), lr=lr)
+    counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
+    a.step(2, counts)
+    b.step(2, counts)
+    torch.cuda.synchronize()
+    P = a.layout.P
+    for k, n in enumerate(sizes):
+        d = ((b.params[k, :P] - a.params[k, :P]) / lr).double()  # = sigma*C/B * xi
+        exp = sig * C / n
+        assert abs(d.std().item() / exp - 1) < 0.01
+        assert abs(d.mean().item()) < 5 * exp / math.sqrt(P)
+    assert torch.equal(a.params[:, P:], b.params[:, P:])  # row padding untouched
+
+
+def test_dpsgd_refuses_batchnorm_models():
+    model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.0).to(DEV)
+    eng = PackedTrainer(model, capacity=1, batch=32, device=DEV, dpsgd=DPSGDConfig())
+    eng.load_module_state(0, model)
+    eng.begin_round("sgd", 0.01)
+    with pytest.raises(FedHipError, match="BatchNorm"):
+        eng.step(1, torch.tensor([32], dtype=torch.int32, device=DEV))
