@@ -190,9 +190,6 @@ __global__ void __launch_bounds__(256) bn_eval_kernel(const BNArgs a) {
     });
 }
 
-__device__ __forceinline__ float gmask(float d, const float* yo, int64_t o) {
-    return (yo && !(yo[o] > 0.f)) ? 0.f : d;
-}
 
 // upstream gradient at client-tensor offset o (before the ReLU mask): dy[o], or routed
 // from the pooled gradient (maxpool2_bwd semantics, layers.hip)
@@ -229,32 +226,65 @@ __device__ __forceinline__ float upstream1(const BNArgs& a, int z, int64_t o) {
     return a.dpool ? pooled_g(a, z, o) : a.dy[z * a.dy_cs + o];
 }
 
+// ReLU mask of the backward: from the stored forward output (yout > 0), or — no residual
+// add in between — recomputed from x exactly as the forward evaluated it
+// (x*alpha + beta' > 0 with the same fp32 operations), which saves reading yout.
+struct ReluMask {
+    int mode;  // 0 none, 1 yout, 2 recompute
+    const float* yo;
+    float alpha, bconst;
+    __device__ ReluMask(const BNArgs& a, int z, int c, float mean, float invstd) {
+        mode = !a.relu ? 0 : (a.yout ? 1 : 2);
+        yo = mode == 1 ? a.yout + z * a.yo_cs : nullptr;
+        alpha = 0.f;
+        bconst = 0.f;
+        if (mode == 2) {
+            alpha = invstd * a.gamma[z * a.p_cs + c];
+            bconst = a.beta[z * a.p_cs + c] - mean * alpha;
+        }
+    }
+    __device__ __forceinline__ bool keep(float x, int64_t o) const {
+        if (mode == 0) return true;
+        if (mode == 1) return yo[o] > 0.f;
+        return x * alpha + bconst > 0.f;
+    }
+    __device__ __forceinline__ float4 apply4(float4 g, float4 xv, int64_t o) const {
+        if (mode == 0) return g;
+        float4 m;
+        if (mode == 1) {
+            m = ld4(yo + o);
+        } else {
+            m.x = xv.x * alpha + bconst; m.y = xv.y * alpha + bconst;
+            m.z = xv.z * alpha + bconst; m.w = xv.w * alpha + bconst;
+        }
+        g.x = m.x > 0.f ? g.x : 0.f; g.y = m.y > 0.f ? g.y : 0.f;
+        g.z = m.z > 0.f ? g.z : 0.f; g.w = m.w > 0.f ? g.w : 0.f;
+        return g;
+    }
+};
+
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const BNArgs a) {
     __shared__ double red[4];
     const int s = blockIdx.x, c = blockIdx.y, z = blockIdx.z;
-    const float mean = a.save_mean[z * a.C + c];
-    const float* yoz = a.relu ? a.yout + z * a.yo_cs : nullptr;
+    const float mean = a.save_mean[z * a.C + c], invstd = a.save_invstd[z * a.C + c];
+    const ReluMask rm(a, z, c, mean, invstd);
     const float* xz = a.x + z * a.x_cs;
     float* drz = a.dres ? a.dres + z * a.dres_cs : nullptr;
     double sg = 0.0, dot = 0.0;
     for_slice(a, z, c, s, [&](int64_t o, int nv) {
         if (nv == 4) {
-            float4 g = upstream4(a, z, o);
-            if (yoz) {
-                const float4 yv = ld4(yoz + o);
-                g.x = yv.x > 0.f ? g.x : 0.f; g.y = yv.y > 0.f ? g.y : 0.f;
-                g.z = yv.z > 0.f ? g.z : 0.f; g.w = yv.w > 0.f ? g.w : 0.f;
-            }
-            if (drz) st4(drz + o, g);
             const float4 xv = ld4(xz + o);
+            const float4 g = rm.apply4(upstream4(a, z, o), xv, o);
+            if (drz) st4(drz + o, g);
             sg += ((double)g.x + (double)g.y) + ((double)g.z + (double)g.w);
             dot += ((double)((xv.x - mean) * g.x) + (double)((xv.y - mean) * g.y)) +
                    ((double)((xv.z - mean) * g.z) + (double)((xv.w - mean) * g.w));
         } else {
-            const float g = gmask(upstream1(a, z, o), yoz, o);
+            const float xv = xz[o];
+            const float g = rm.keep(xv, o) ? upstream1(a, z, o) : 0.f;
             if (drz) drz[o] = g;
             sg += (double)g;
-            dot += (double)((xz[o] - mean) * g);
+            dot += (double)((xv - mean) * g);
         }
     });
     sg = block_sum_256(sg, red);
@@ -278,21 +308,16 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const BNArgs a) {
         if (a.dbeta) a.dbeta[z * a.g_cs + c] = (float)sg;
     }
     if (!a.dx) return;
+    const ReluMask rm(a, z, c, mean, invstd);
     const float w = a.gamma[z * a.p_cs + c];
     const float k = n > 0 ? (float)(dot * (double)invstd * (double)invstd / (double)n) : 0.f;
     const float gm = n > 0 ? (float)(sg / (double)n) : 0.f;
-    const float* yoz = a.relu ? a.yout + z * a.yo_cs : nullptr;
     const float* xz = a.x + z * a.x_cs;
     float* dxz = a.dx + z * a.dx_cs;
     for_slice(a, z, c, s, [&](int64_t o, int nv) {
         if (nv == 4) {
-            const float4 d = upstream4(a, z, o), xv = ld4(xz + o);
-            float4 g = d;
-            if (yoz) {
-                const float4 yv = ld4(yoz + o);
-                g.x = yv.x > 0.f ? d.x : 0.f; g.y = yv.y > 0.f ? d.y : 0.f;
-                g.z = yv.z > 0.f ? d.z : 0.f; g.w = yv.w > 0.f ? d.w : 0.f;
-            }
+            const float4 xv = ld4(xz + o);
+            const float4 g = rm.apply4(upstream4(a, z, o), xv, o);
             float4 r;
             r.x = (((g.x - gm) - (xv.x - mean) * k) * invstd) * w;
             r.y = (((g.y - gm) - (xv.y - mean) * k) * invstd) * w;
@@ -300,8 +325,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const BNArgs a) {
             r.w = (((g.w - gm) - (xv.w - mean) * k) * invstd) * w;
             st4(dxz + o, r);
         } else {
-            const float g = gmask(upstream1(a, z, o), yoz, o);
-            dxz[o] = (((g - gm) - (xz[o] - mean) * k) * invstd) * w;
+            const float xv = xz[o];
+            const float g = rm.keep(xv, o) ? upstream1(a, z, o) : 0.f;
+            dxz[o] = (((g - gm) - (xv - mean) * k) * invstd) * w;
         }
     });
 }
@@ -387,7 +413,8 @@ extern "C" int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_
 }
 
 extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs,
-                         const float* x, int64_t x_cs, const float* gamma, int64_t p_cs,
+                         const float* x, int64_t x_cs, const float* gamma, const float* beta,
+                         int64_t p_cs,
                          const float* save_mean, const float* save_invstd, float* dx,
                          int64_t dx_cs, float* dres, int64_t dres_cs, float* dgamma, float* dbeta,
                          int64_t g_cs, const int32_t* counts, int32_t nclients, int32_t batch,
@@ -396,11 +423,12 @@ extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int6
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_bwd: bad shape");
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(dy && x && gamma && save_mean && save_invstd, "bn_bwd: null pointer");
-    FH_REQUIRE(!relu || yout, "bn_bwd: relu needs the forward output");
+    FH_REQUIRE(!relu || yout || beta, "bn_bwd: relu needs the forward output or beta");
     const size_t need = fh_bn_workspace(nclients, batch, C, HW);
     FH_REQUIRE(workspace && ws_bytes >= need, "bn_bwd: workspace %zu < %zu", ws_bytes, need);
     BNArgs a = bn_args(nclients, batch, C, HW, counts);
-    a.dy = dy; a.yout = yout; a.x = x; a.gamma = gamma; a.save_mean = (float*)save_mean;
+    a.dy = dy; a.yout = yout; a.x = x; a.gamma = gamma; a.beta = beta;
+    a.save_mean = (float*)save_mean;
     a.save_invstd = (float*)save_invstd; a.dx = dx; a.dres = dres; a.dgamma = dgamma;
     a.dbeta = dbeta; a.part = (double*)workspace;
     a.dy_cs = dy_cs; a.yo_cs = yo_cs; a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs;
@@ -420,7 +448,8 @@ extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int6
 extern "C" int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* pidx,
                               int64_t pi_cs, const uint8_t* pmask, int64_t pm_cs, float p_drop,
                               const float* yout, int64_t yo_cs, const float* x, int64_t x_cs,
-                              const float* gamma, int64_t p_cs, const float* save_mean,
+                              const float* gamma, const float* beta, int64_t p_cs,
+                              const float* save_mean,
                               const float* save_invstd, float* dx, int64_t dx_cs, float* dgamma,
                               float* dbeta, int64_t g_cs, const int32_t* counts,
                               int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
@@ -430,7 +459,7 @@ extern "C" int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* 
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "bn_bwd_pool: p=%g", p_drop);
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(dpool && pidx && x && gamma && save_mean && save_invstd, "bn_bwd_pool: null pointer");
-    FH_REQUIRE(!relu || yout, "bn_bwd_pool: relu needs the forward output");
+    FH_REQUIRE(!relu || yout || beta, "bn_bwd_pool: relu needs the forward output or beta");
     const int HW = H * W;
     const size_t need = fh_bn_workspace(nclients, batch, C, HW);
     FH_REQUIRE(workspace && ws_bytes >= need, "bn_bwd_pool: workspace %zu < %zu", ws_bytes, need);
@@ -441,7 +470,7 @@ extern "C" int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* 
     a.W = W;
     a.fd_w = FastDiv(W);
     a.vec = (HW & 3) == 0 && (W & 3) == 0;
-    a.yout = yout; a.x = x; a.gamma = gamma; a.save_mean = (float*)save_mean;
+    a.yout = yout; a.x = x; a.gamma = gamma; a.beta = beta; a.save_mean = (float*)save_mean;
     a.save_invstd = (float*)save_invstd; a.dx = dx; a.dgamma = dgamma; a.dbeta = dbeta;
     a.part = (double*)workspace;
     a.yo_cs = yo_cs; a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs; a.g_cs = g_cs; a.relu = relu;

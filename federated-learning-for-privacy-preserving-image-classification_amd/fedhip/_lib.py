@@ -60,9 +60,9 @@ SIGNATURES = {
                               I32, I32, F32, F32, I32, P, SZ, P]),
     "fh_bn_fwd_eval": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, I32, I32, I32,
                              I32, F32, I32, P]),
-    "fh_bn_bwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, P, P, I64, P, I64, P, P, I64, P,
+    "fh_bn_bwd": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, P, I64, P, I64, P, P, I64, P,
                         I32, I32, I32, I32, I32, P, SZ, P]),
-    "fh_bn_bwd_pool": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I64, P, P, P, I64,
+    "fh_bn_bwd_pool": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, P, I64, P, P, P, I64,
                              P, P, I64, P, I32, I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_conv2d_persample_sqnorm_workspace": (SZ, [I32] * 10),
     "fh_conv2d_persample_sqnorm": (I32, [P, I64, P, I64, I32, P, P, SZ, P, I32, I32, I32, I32,

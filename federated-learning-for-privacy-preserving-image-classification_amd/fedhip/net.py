@@ -380,21 +380,21 @@ class PackedNet:
         convs = self._CIFAR_CONVS
         for i in range(len(convs) - 1, -1, -1):
             cv, ci, co, hw, bn = convs[i]
-            r = A(f"r_{cv}", co, hw, hw)
             dc = A(f"dc_{cv}", co, hw, hw)
             sm, si = self._bn_save(bn, co)
             if i % 2 == 1:  # upstream gradient comes through pool(+dropout): fused routing
                 h2 = hw // 2
-                ops.bn_bwd_pool(dq, A(f"i_{cv}", co, h2, h2, dtype=torch.uint8), r,
+                ops.bn_bwd_pool(dq, A(f"i_{cv}", co, h2, h2, dtype=torch.uint8), None,
                                 A(f"c_{cv}", co, hw, hw), W(P_, f"{bn}.weight"), sm, si, dc,
                                 W(G, f"{bn}.weight"), W(G, f"{bn}.bias"), n, B, co, hw, hw,
                                 relu=True,
                                 pmask=A(f"m_{cv}", co, h2, h2, dtype=torch.uint8) if dm else None,
-                                p_drop=p, counts=cnt)
+                                p_drop=p, counts=cnt, beta=W(P_, f"{bn}.bias"))
             else:           # dr was written by the next conv's dgrad
-                ops.bn_bwd(A(f"dr_{cv}", co, hw, hw), r, A(f"c_{cv}", co, hw, hw),
+                ops.bn_bwd(A(f"dr_{cv}", co, hw, hw), None, A(f"c_{cv}", co, hw, hw),
                            W(P_, f"{bn}.weight"), sm, si, dc, W(G, f"{bn}.weight"),
-                           W(G, f"{bn}.bias"), n, B, co, hw * hw, relu=True, counts=cnt)
+                           W(G, f"{bn}.bias"), n, B, co, hw * hw, relu=True, counts=cnt,
+                           beta=W(P_, f"{bn}.bias"))
             if i == 0:
                 xin = self.x
             elif i % 2 == 0:
@@ -490,9 +490,9 @@ class PackedNet:
                              counts=cnt)
             da = A(f"{pf}.da", co, ho, ho)
             sm1, si1 = self._bn_save(f"{pf}.bn1", co)
-            ops.bn_bwd(dar, ar, A(f"{pf}.a", co, ho, ho), W(P_, f"{pf}.bn1.weight"), sm1, si1, da,
-                       W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co, ho * ho,
-                       relu=True, counts=cnt)
+            ops.bn_bwd(dar, None, A(f"{pf}.a", co, ho, ho), W(P_, f"{pf}.bn1.weight"), sm1, si1,
+                       da, W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co, ho * ho,
+                       relu=True, counts=cnt, beta=W(P_, f"{pf}.bn1.bias"))
             xin = b["xin"]
             ops.conv2d_wgrad(xin, da, W(G, f"{pf}.conv1.weight"), None, n, B, ci, hi, hi, co, 3, s, 1,
                              counts=cnt)
@@ -512,9 +512,9 @@ class PackedNet:
         dstem = A("dstem", 64, 32, 32)
         dc0 = A("dc_stem", 64, 32, 32)
         sm, si = self._bn_save("bn1", 64)
-        ops.bn_bwd(dstem, A("r_stem", 64, 32, 32), A("c_stem", 64, 32, 32), W(P_, "bn1.weight"), sm,
-                   si, dc0, W(G, "bn1.weight"), W(G, "bn1.bias"), n, B, 64, 1024, relu=True,
-                   counts=cnt)
+        ops.bn_bwd(dstem, None, A("c_stem", 64, 32, 32), W(P_, "bn1.weight"), sm, si, dc0,
+                   W(G, "bn1.weight"), W(G, "bn1.bias"), n, B, 64, 1024, relu=True, counts=cnt,
+                   beta=W(P_, "bn1.bias"))
         ops.conv2d_wgrad(self.x, dc0, W(G, "conv1.weight"), None, n, B, self.in_shape[0], 32, 32, 64,
                          3, 1, 1, counts=cnt)
 

@@ -308,20 +308,21 @@ def bn_fwd_eval(x, y, gamma, beta, rmean, rvar, nclients, batch, C, HW, eps=1e-5
 
 
 def bn_bwd(dy, yout, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclients, batch, C, HW,
-           relu=False, dres=None, counts=None):
+           relu=False, dres=None, counts=None, beta=None):
+    """yout None with relu: the ReLU mask is recomputed from x (needs beta)."""
     ws, nb = _ws_for("fh_bn_workspace", dy.device, nclients, batch, C, HW)
     call("fh_bn_bwd", ptr(dy), _cs(dy), ptr(yout), _cs(yout), ptr(x), _cs(x), ptr(gamma),
-         _cs(gamma), ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dres), _cs(dres),
+         ptr(beta), _cs(gamma), ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dres), _cs(dres),
          ptr(dgamma), ptr(dbeta), _cs(dgamma), _counts(counts), nclients, batch, C, HW,
          int(relu), ptr(ws), nb, stream_handle())
 
 
 def bn_bwd_pool(dpool, pidx, yout, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclients,
-                batch, C, H, W, relu=True, pmask=None, p_drop=0.0, counts=None):
+                batch, C, H, W, relu=True, pmask=None, p_drop=0.0, counts=None, beta=None):
     """BN backward fed through MaxPool2d(2,2) (+dropout): pool backward fused in."""
     ws, nb = _ws_for("fh_bn_workspace", x.device, nclients, batch, C, H * W)
     call("fh_bn_bwd_pool", ptr(dpool), _cs(dpool), ptr(pidx), _cs(pidx), ptr(pmask), _cs(pmask),
-         float(p_drop), ptr(yout), _cs(yout), ptr(x), _cs(x), ptr(gamma), _cs(gamma),
+         float(p_drop), ptr(yout), _cs(yout), ptr(x), _cs(x), ptr(gamma), ptr(beta), _cs(gamma),
          ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dgamma), ptr(dbeta), _cs(dgamma),
          _counts(counts), nclients, batch, C, H, W, int(relu), ptr(ws), nb, stream_handle())
 

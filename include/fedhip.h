@@ -172,9 +172,12 @@ int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_cs, const f
                    const float* running_mean, const float* running_var, int64_t r_cs,
                    const int32_t* counts, int32_t nclients, int32_t batch, int32_t C, int32_t HW,
                    float eps, int32_t relu, void* stream);
-/* g = relu ? dy*(yout>0) : dy; dres (nullable) <- g; dgamma/dbeta (stride g_cs) and dx. */
+/* g = relu ? dy*(yout>0) : dy; dres (nullable) <- g; dgamma/dbeta (stride g_cs) and dx.
+ * With relu and yout NULL the mask is recomputed from x (x*alpha + beta' > 0, the
+ * forward's own fp32 operations; needs beta, and no residual add before the ReLU). */
 int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs, const float* x,
-              int64_t x_cs, const float* gamma, int64_t p_cs, const float* save_mean,
+              int64_t x_cs, const float* gamma, const float* beta, int64_t p_cs,
+              const float* save_mean,
               const float* save_invstd, float* dx, int64_t dx_cs, float* dres, int64_t dres_cs,
               float* dgamma, float* dbeta, int64_t g_cs, const int32_t* counts, int32_t nclients,
               int32_t batch, int32_t C, int32_t HW, int32_t relu, void* workspace,
@@ -186,8 +189,8 @@ int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs, 
  * by the argmax bytes pidx on the fly (fh_maxpool2_bwd + fh_bn_bwd in one pass pair). */
 int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* pidx, int64_t pi_cs,
                    const uint8_t* pmask, int64_t pm_cs, float p_drop, const float* yout,
-                   int64_t yo_cs, const float* x, int64_t x_cs, const float* gamma, int64_t p_cs,
-                   const float* save_mean, const float* save_invstd, float* dx, int64_t dx_cs,
+                   int64_t yo_cs, const float* x, int64_t x_cs, const float* gamma,
+                   const float* beta, int64_t p_cs, const float* save_mean, const float* save_invstd, float* dx, int64_t dx_cs,
                    float* dgamma, float* dbeta, int64_t g_cs, const int32_t* counts,
                    int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W, int32_t relu,
                    void* workspace, size_t ws_bytes, void* stream);

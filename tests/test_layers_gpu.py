@@ -160,3 +160,33 @@ def test_bn_bwd_pool_matches_unfused(case, p_drop):
             torch.testing.assert_close(dx1[z, :n], dx2[z, :n], rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(dg1, dg2, rtol=1e-6, atol=1e-6)
         torch.testing.assert_close(db1, db2, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("case", [(2, 32, 32, 16, 16), (3, 9, 64, 8, 8), (2, 7, 8, 7, 7)])
+def test_bn_bwd_recomputed_relu_mask_is_exact(case):
+    """yout=None: the ReLU mask recomputed from x equals the stored forward output's."""
+    nc, B, C, H, W = case
+    torch.manual_seed(C)
+    cnt = _counts(nc, B, C)
+    counts = torch.tensor(cnt, dtype=torch.int32, device=DEV)
+    x = torch.randn(nc, B, C, H, W, device=DEV)
+    gamma = torch.rand(nc, C, device=DEV) + 0.5
+    beta = torch.randn(nc, C, device=DEV) * 0.3
+    y = torch.zeros_like(x)
+    sm = torch.zeros(nc, C, device=DEV)
+    si = torch.zeros(nc, C, device=DEV)
+    ops.bn_fwd_train(x, y, gamma, beta, None, None, sm, si, nc, B, C, H * W, relu=True,
+                     counts=counts)
+    dy = torch.randn_like(x)
+    outs = []
+    for yout, bt in ((y, None), (None, beta)):
+        dx = torch.zeros_like(x)
+        dg = torch.zeros(nc, C, device=DEV)
+        db = torch.zeros(nc, C, device=DEV)
+        ops.bn_bwd(dy, yout, x, gamma, sm, si, dx, dg, db, nc, B, C, H * W, relu=True,
+                   counts=counts, beta=bt)
+        outs.append((dx, dg, db))
+    torch.cuda.synchronize()
+    for z in range(nc):
+        assert torch.equal(outs[0][0][z, :cnt[z]], outs[1][0][z, :cnt[z]])
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])

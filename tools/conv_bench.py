@@ -26,7 +26,7 @@ def timeit(fn, it=20):
 def main():
     dev = torch.device("cuda")
     B = 32
-    for C in (32, 1):
+    for C in ([int(v) for v in os.environ.get("FH_BENCH_CLIENTS", "32,1").split(",")]):
         for cin, cout, hw in LAYERS:
             x = torch.randn(C, B, cin, hw, hw, device=dev)
             w = torch.randn(C, cout, cin, 3, 3, device=dev) * 0.1

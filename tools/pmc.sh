@@ -1,0 +1,9 @@
+# usage (GPU box): bash tools/pmc.sh <tag> "<counters>" <python script + args...>
+set -e
+TAG=$1; shift
+CTRS=$1; shift
+cd $GRAFT_REPO_ROOT
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --pmc $CTRS --output-format csv -d $OUT -o run -- python3 "$@" > $OUT/log.txt 2>&1
