@@ -578,10 +578,13 @@ static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return (v && *v) ? atoi(v) : dflt;
 }
-static const int kDconvBlocks = env_int("FH_DCONV_BLOCKS", 1024);
-static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 128);
-static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 1024);
-static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 0);
+// defaults from the MI355X sweeps (tools/conv_sweep.py, CIFAR10CNN layers at 32 clients):
+// BM <= 64 once 512 workgroups are reached; wgrad with four pixel-waves per 32x32
+// (co, ci) tile and ~256 workgroups (one per CU at its 86 KB of LDS)
+static const int kDconvBlocks = env_int("FH_DCONV_BLOCKS", 512);
+static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 64);
+static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 256);
+static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 4);
 
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
@@ -689,8 +692,9 @@ static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     else if (ci64) p = {1, 2, 2, 128 / w, 1, 1};
     const int64_t tiles = (int64_t)(cout / (32 * p.wco)) * (cin / (32 * p.wci)) * nclients;
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
-    const int want =
-        (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(kDwgradBlocks, tiles)), nst);
+    // >= 4 stages per split: fewer, longer splits beat a wide slab in the few-client tail
+    const int want = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(kDwgradBlocks, tiles)),
+                                            std::max(1, nst / 4));
     p.sps = (int)ceil_div(nst, want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;
@@ -706,8 +710,8 @@ static DWPlan plan_dwgrad_small(int cout, int batch, int w, int nclients) {
     DWPlan p{1, 1, 4, 128 / w, 1, 1};
     const int64_t tiles = (int64_t)(cout / 32) * nclients;
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
-    const int want =
-        (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(kDwgradBlocks, tiles)), nst);
+    const int want = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(kDwgradBlocks, tiles)),
+                                            std::max(1, nst / 4));
     p.sps = (int)ceil_div(nst, want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;

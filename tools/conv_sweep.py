@@ -6,14 +6,13 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SETTINGS = [
     {},
-    {"FH_DCONV_MAXBM": "32"},
-    {"FH_DCONV_MAXBM": "64"},
-    {"FH_DCONV_BLOCKS": "512"},
-    {"FH_DCONV_BLOCKS": "2048"},
-    {"FH_DWGRAD_BLOCKS": "512"},
-    {"FH_DWGRAD_BLOCKS": "2048"},
-    {"FH_DWGRAD_WPX": "4"},
-    {"FH_DWGRAD_WPX": "2"},
+    {"FH_DWGRAD_WPX": "4", "FH_DWGRAD_BLOCKS": "256"},
+    {"FH_DWGRAD_WPX": "4", "FH_DWGRAD_BLOCKS": "384"},
+    {"FH_DWGRAD_WPX": "4", "FH_DWGRAD_BLOCKS": "512"},
+    {"FH_DWGRAD_WPX": "4", "FH_DWGRAD_BLOCKS": "768"},
+    {"FH_DCONV_BLOCKS": "256"},
+    {"FH_DCONV_BLOCKS": "512", "FH_DCONV_MAXBM": "64"},
+    {"FH_DCONV_BLOCKS": "768"},
 ]
 
 for st in SETTINGS:
