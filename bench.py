@@ -21,6 +21,7 @@ Also reported (one JSON line):
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import math
 import os
@@ -131,6 +132,21 @@ def cpu_baseline(cfg, seconds=12.0):
                       f"(oracle/train_ref.py, torch CPU, {threads} threads)"}
 
 
+def measured_traffic(probe_tag):
+    """HBM bytes per launch of the probed kernel, from the newest committed PMC
+    measurement (profiles/*/traffic.json, made by tools/traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark), else None."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    for f in sorted(glob.glob(os.path.join(here, "profiles", "*", "traffic.json")), reverse=True):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if t.get("probe") == probe_tag:
+            return int(t["traffic_bytes"])
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,7 +215,8 @@ def main():
             ach = probe["flops_per_launch"] / (probe["avg_ms"] * 1e-3) / 1e12
             roof = {"bound": "mfma", "kernel": probe_tag, "achieved": round(ach, 2),
                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                    "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                    "traffic": measured_traffic(probe_tag),
                     "launches_timed": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4)}
         out = {
             "metric": "client-images/sec/node", "value": round(value, 1),
