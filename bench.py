@@ -157,6 +157,8 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--probe", default=None, help="conv launch tag to time (default: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="concurrent client lanes per GPU (default: planner / FH_LANES)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     world, rank, dev = setup(args)
@@ -168,7 +170,8 @@ def main():
     torch.manual_seed(0)
     template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
     dp = DPConfig(epsilon=cfg["dp"]) if cfg["dp"] else None
-    rr = RankRound(template, train, mine, epochs=cfg["epochs"], device=dev, dp=dp)
+    rr = RankRound(template, train, mine, epochs=cfg["epochs"], device=dev, dp=dp,
+                   lanes=args.lanes)
     data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, rank)
     my_images = cfg["epochs"] * sum(train[k] for k in mine)
     total_images = cfg["epochs"] * sum(train)
@@ -231,7 +234,8 @@ def main():
                                    f"{cfg['epochs']} local epoch(s), batch 32, {args.opt} lr {args.lr}, "
                                    f"DP eps={cfg['dp']}, FedAvg{' RCCL all-reduce' if world > 1 else ''}",
                        "clients": C, "images_per_round": total_images, "batch": 32,
-                       "parallelism": f"client-packed x{world} GPU"},
+                       "parallelism": f"client-packed x{world} GPU",
+                       "lanes": rr.trainer.cut},
             "achieved_tflops_step": round(value * fl / 1e12, 2),
             "roofline": roof,
         }

@@ -54,6 +54,29 @@ class DPSGDConfig:
         return math.sqrt(2.0 * math.log(1.25 / self.delta)) / self.epsilon
 
 
+class SlotStorage:
+    """Per-slot training state of `capacity` clients as packed rows: parameters, gradients,
+    optimizer moments [capacity, Ppad], BN running statistics [capacity, Q] and the
+    per-client epoch accumulators.  Several PackedTrainer lanes may share one storage,
+    each owning a contiguous row range."""
+    FIELDS = ("params", "grads", "state1", "state2", "bufs", "acc_loss", "acc_correct",
+              "acc_seen", "loss_out")
+
+    def __init__(self, layout, Ppad, capacity, device):
+        z = lambda *s, **k: torch.zeros(*s, device=device, **k)
+        self.params, self.grads = z(capacity, Ppad), z(capacity, Ppad)
+        self.state1, self.state2 = z(capacity, Ppad), z(capacity, Ppad)
+        self.bufs = z(capacity, max(layout.Q, 1))
+        self.acc_loss = z(capacity, dtype=torch.float64)
+        self.acc_correct = z(capacity, dtype=torch.int64)
+        self.acc_seen = z(capacity, dtype=torch.int64)
+        self.loss_out = z(capacity)
+        # default BN buffers: running_mean 0, running_var 1
+        for name in layout.buf_names:
+            if name.endswith("running_var"):
+                layout.bview(self.bufs, name).fill_(1.0)
+
+
 @dataclass
 class ClientMetrics:
     loss: float
@@ -63,7 +86,8 @@ class ClientMetrics:
 
 
 class PackedTrainer:
-    def __init__(self, model, capacity, batch=32, device="cuda", dpsgd=None):
+    def __init__(self, model, capacity, batch=32, device="cuda", dpsgd=None, storage=None,
+                 row0=0):
         load()  # fail loudly if libfedhip is missing
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -76,16 +100,15 @@ class PackedTrainer:
         # rows padded to 64 floats (256 B): every client row starts 16-B aligned for the
         # vectorised HBM kernels; padding stays 0 (zero gradients) and is never federated.
         self.Ppad = ((L.P + 63) // 64) * 64
-        self.params = torch.zeros(capacity, self.Ppad, device=dev)
-        self.grads = torch.zeros(capacity, self.Ppad, device=dev)
-        self.state1 = torch.zeros(capacity, self.Ppad, device=dev)
-        self.state2 = torch.zeros(capacity, self.Ppad, device=dev)
-        self.bufs = torch.zeros(capacity, max(L.Q, 1), device=dev)
+        if storage is None:
+            storage = SlotStorage(L, self.Ppad, capacity, dev)
+            row0 = 0
+        # per-slot state = rows [row0, row0 + capacity) of the (possibly shared) storage
+        self.row0 = row0
+        for name in SlotStorage.FIELDS:
+            setattr(self, name, getattr(storage, name)[row0:row0 + capacity])
+        self.net.salt = (row0 * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
         self.num_batches_tracked = [0] * capacity
-        self.acc_loss = torch.zeros(capacity, dtype=torch.float64, device=dev)
-        self.acc_correct = torch.zeros(capacity, dtype=torch.int64, device=dev)
-        self.acc_seen = torch.zeros(capacity, dtype=torch.int64, device=dev)
-        self.loss_out = torch.zeros(capacity, device=dev)
         self.seg_offsets = torch.tensor(L.seg_offsets(), dtype=torch.int64, device=dev)
         self.opt_type, self.lr, self.opt_step = "sgd", 0.01, 0
         self.dpsgd = dpsgd
@@ -100,13 +123,11 @@ class PackedTrainer:
         # fixed device slots by one memcpy before each replay.  Full-width steps stay eager
         # when probe_full is set (bench.py times their kernels with events).
         self.use_graphs = True
+        self.stream = None  # set by a LanedTrainer: the lane's HIP stream
         self.probe_full = False
+        self.probe_first_only = False  # lanes: probe only the (serialised) first step
         self._graphs = {}
         self._graph_pool = None
-        # default BN buffers: running_mean 0, running_var 1
-        for name in L.buf_names:
-            if name.endswith("running_var"):
-                L.bview(self.bufs, name).fill_(1.0)
 
     # ------------------------------------------------------------ state I/O
     def load_module_state(self, slot, model):
@@ -216,38 +237,48 @@ class PackedTrainer:
 
         data [N, *in_shape] / labels [N] device tensors hold all shards back
         to back; slot k's shard starts at shard_offsets[k]."""
-        net = self.net
-        self.begin_round(optimizer_type, lr)
-        rows, cur, views = self._step_rows(plan, shard_offsets, seed)
-        sample_elems = int(math.prod(net.in_shape))
-        full_batch = (plan["counts"] == self.batch).all(dim=1).tolist()
-        graphs = (self.use_graphs and self.on_step is None and self.pre_step is None
-                  and not ops.PROBE.enabled)
+        st = self.start_round(data, labels, shard_offsets, plan, optimizer_type, lr, seed)
         try:
             for g in range(plan["G"]):
-                n = plan["active"][g]
-                if self.pre_step is not None:  # diagnostic hook
-                    self.pre_step(g, n, plan)
-                cur.copy_(rows[g], non_blocking=True)
-                self.opt_step += 1
-                full = n == self.capacity
-                if graphs and g > 0 and not (self.probe_full and full):
-                    self._replay(n, data, labels, views, sample_elems)
-                else:
-                    arm = self.probe_full and full and bool(full_batch[g])
-                    ops.PROBE.enabled = arm
-                    net.seed = (seed * 1000003 + g) & 0x7FFFFFFF
-                    net.seed_dev = None
-                    ops.gather_batch(data, labels, views["gidx"], net.x, net.y, sample_elems, n,
-                                     self.batch, counts=views["counts"])
-                    self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
-                                        adam_dev=views["adam"])
-                    if arm:
-                        ops.PROBE.enabled = False
-                self._after_step(n)
+                self.issue_step(st, g)
         finally:
-            net.seed_dev = None
+            self.net.seed_dev = None
         return self.collect_metrics(plan, epochs_of(plan))
+
+    def start_round(self, data, labels, shard_offsets, plan, optimizer_type="sgd", lr=0.01,
+                    seed=0):
+        """Reset the optimizer and upload the round's per-step rows (current stream)."""
+        self.begin_round(optimizer_type, lr)
+        rows, cur, views = self._step_rows(plan, shard_offsets, seed)
+        return dict(data=data, labels=labels, plan=plan, seed=seed, rows=rows, cur=cur,
+                    views=views, sample_elems=int(math.prod(self.net.in_shape)),
+                    full_batch=(plan["counts"] == self.batch).all(dim=1).tolist(),
+                    graphs=(self.use_graphs and self.on_step is None and self.pre_step is None
+                            and not ops.PROBE.enabled))
+
+    def issue_step(self, st, g):
+        """Launch global step g of the round (eager or graph replay) on the current stream."""
+        net, plan, views = self.net, st["plan"], st["views"]
+        n = plan["active"][g]
+        if self.pre_step is not None:  # diagnostic hook
+            self.pre_step(g, n, plan)
+        st["cur"].copy_(st["rows"][g], non_blocking=True)
+        self.opt_step += 1
+        full = n == self.capacity and (g == 0 or not self.probe_first_only)
+        if st["graphs"] and g > 0 and not (self.probe_full and full):
+            self._replay(n, st["data"], st["labels"], views, st["sample_elems"])
+        else:
+            arm = self.probe_full and full and bool(st["full_batch"][g])
+            ops.PROBE.enabled = arm
+            net.seed = (st["seed"] * 1000003 + g) & 0x7FFFFFFF
+            net.seed_dev = None
+            ops.gather_batch(st["data"], st["labels"], views["gidx"], net.x, net.y,
+                             st["sample_elems"], n, self.batch, counts=views["counts"])
+            self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
+                                adam_dev=views["adam"])
+            if arm:
+                ops.PROBE.enabled = False
+        self._after_step(n)
 
     def _step_rows(self, plan, shard_offsets, seed):
         """Per-step inputs packed as byte rows [G, R] on the device, plus the fixed
@@ -298,7 +329,9 @@ class PackedTrainer:
             if self._graph_pool is None:
                 self._graph_pool = torch.cuda.graph_pool_handle()
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, pool=self._graph_pool):
+            # capture on this trainer's own stream when it has one, so the split-K scratch
+            # (keyed by stream) is the lane's, never shared with a concurrently running lane
+            with torch.cuda.graph(graph, pool=self._graph_pool, stream=self.stream):
                 ops.gather_batch(data, labels, views["gidx"], net.x, net.y, sample_elems, n,
                                  self.batch, counts=views["counts"])
                 self._step_launches(n, views["counts"], views["reset"], first=False,

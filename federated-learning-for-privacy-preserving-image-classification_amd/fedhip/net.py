@@ -125,6 +125,7 @@ class PackedNet:
         self.mask_mode = 1
         self.seed = 0
         self.seed_dev = None  # device uint64 [1] = seed * 1000003 (graph replay)
+        self.salt = 0  # per-lane key offset (a lane's slot 0 is not another lane's slot 0)
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -147,8 +148,8 @@ class PackedNet:
         seed_dev set (graph replay) the per-step part lives on the device and the kernel
         adds it to the per-layer salt returned here."""
         if self.seed_dev is not None:
-            return (layer_id * 7919) & 0xFFFFFFFFFFFFFFFF
-        return (self.seed * 1000003 + layer_id * 7919) & 0xFFFFFFFFFFFFFFFF
+            return (layer_id * 7919 + self.salt) & 0xFFFFFFFFFFFFFFFF
+        return (self.seed * 1000003 + layer_id * 7919 + self.salt) & 0xFFFFFFFFFFFFFFFF
 
     def _drop_mode(self, train):
         if not train or self.dropout_p == 0.0:

@@ -96,7 +96,8 @@ def _conv_tag(kind, cin, h, w, cout, k, s):
 
 
 def _ws(device) -> Workspace:
-    key = str(device)
+    # one scratch buffer per (device, stream): lanes on different streams run concurrently
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
     if key not in _WS:
         _WS[key] = Workspace(device)
     return _WS[key]

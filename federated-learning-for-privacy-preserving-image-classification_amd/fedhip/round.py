@@ -24,7 +24,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from .engine import PackedTrainer
+from .lanes import LanedTrainer
 
 
 @dataclass
@@ -37,7 +37,7 @@ class DPConfig:
 class RankRound:
     def __init__(self, template_model, all_train_sizes: Sequence[int], my_clients: Sequence[int],
                  epochs: int = 1, batch: int = 32, device="cuda", dp: Optional[DPConfig] = None,
-                 group=None):
+                 group=None, lanes=None):
         self.device = torch.device(device)
         self.B, self.epochs, self.dp, self.group = batch, epochs, dp, group
         self.all_sizes = list(all_train_sizes)
@@ -45,8 +45,9 @@ class RankRound:
         self.clients = sorted(my_clients)
         self.slots = sorted(self.clients, key=lambda k: (-math.ceil(self.all_sizes[k] / batch), k))
         self.slot_of = {k: i for i, k in enumerate(self.slots)}
-        self.trainer = PackedTrainer(template_model, capacity=max(1, len(self.slots)), batch=batch,
-                                     device=self.device)
+        steps = [epochs * math.ceil(self.all_sizes[k] / batch) for k in self.slots]
+        self.trainer = LanedTrainer(template_model, steps or [0], batch=batch, device=self.device,
+                                    lanes=lanes)
         L = self.trainer.layout
         self.P = L.P
         self.global_flat = torch.zeros(self.P, device=self.device)

@@ -141,3 +141,20 @@ def test_sharded_fedavg_composition_gloo(world):
         np.testing.assert_array_equal(res[r], res[0])  # every rank holds the same global
         # different association than the sequential sum: a few ulp
         assert np.abs(res[r] - ref).max() <= 8 * np.finfo(np.float32).eps * np.abs(ref).max()
+
+
+def test_lane_planner_cuts():
+    """fedhip/lanes.py: cuts are contiguous, cover every slot, isolate step-count outliers,
+    and keep (near-)equal shards in one packed lane."""
+    from fedhip.lanes import plan_lanes
+    kt = [131, 83, 81, 71, 66, 63, 58, 58, 55, 49, 46, 44, 41, 40, 40, 40, 38, 38, 36, 36,
+          36, 35, 33, 30, 29, 26, 25, 23, 23, 23, 16, 9]
+    cut = plan_lanes(kt)
+    assert cut[0] == 0 and cut[-1] == len(kt) and cut == sorted(set(cut))
+    assert len(cut) - 1 <= 3 and cut[1] == 1  # the 131-step client runs alone
+    assert plan_lanes([422] * 4) == [0, 4]
+    assert plan_lanes([7]) == [0, 1]
+    assert plan_lanes(kt, max_lanes=1) == [0, len(kt)]
+    for steps in ([50, 10], [50, 10, 9], [9, 8, 3, 3, 2, 1, 1]):
+        c = plan_lanes(steps)
+        assert c[0] == 0 and c[-1] == len(steps) and c == sorted(set(c))
