@@ -14,6 +14,8 @@ Also reported (one JSON line):
   roofline      the dominant conv kernel, timed live with HIP events on its
                 launch stream during the timed rounds: algorithmic FLOPs per
                 launch / average launch duration vs the fp32 MFMA peak;
+  rounds_to_target  N=1 only: FedAvg rounds until the global model reaches 91 %
+                test accuracy (K1, learnable MNIST proxy), evaluated on the chip;
   cpu_baseline  rank 0 at N=1 only: the reference algorithm (oracle/ — a
                 CPU restatement pinned bit-exact to the reference LocalTrainer)
                 timed on the host cores on a bounded sample.
@@ -132,6 +134,52 @@ def cpu_baseline(cfg, seconds=12.0):
                       f"(oracle/train_ref.py, torch CPU, {threads} threads)"}
 
 
+def mnist_proxy(n, signal, seed, device, classes=10):
+    """Learnable synthetic MNIST-shaped data (no dataset download is possible here):
+    x = signal * P[y] + N(0, 1), with ten fixed class prototypes P (N(0,1) images smoothed
+    by a 5x5 box filter and rescaled to unit std).  Labels uniform."""
+    g = torch.Generator(device="cpu").manual_seed(4242)
+    proto = torch.randn(classes, 1, 28, 28, generator=g)
+    proto = torch.nn.functional.avg_pool2d(proto, 5, stride=1, padding=2)
+    proto = (proto / proto.std(dim=(1, 2, 3), keepdim=True)).to(device)
+    gd = torch.Generator(device=device).manual_seed(seed)
+    y = torch.randint(0, classes, (n,), generator=gd, device=device)
+    x = torch.randn(n, 1, 28, 28, generator=gd, device=device) + signal * proto[y]
+    return x, y
+
+
+def rounds_to_target(dev, target, max_rounds, signal, opt, lr):
+    """Second half of the BASELINE metric: FedAvg rounds until the global model's test
+    accuracy reaches `target` on config K1 (MNIST SimpleCNN, 4 IID clients, 1 local epoch),
+    on the learnable MNIST proxy (60k train / 10k test), global model evaluated after every
+    aggregation by fedhip.evaluate (eval-mode forward on the chip)."""
+    cfg = CONFIGS["K1"]
+    labels, train = build_clients(cfg, 1)
+    torch.manual_seed(0)
+    template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
+    rr = RankRound(template, train, list(range(len(train))), epochs=cfg["epochs"], device=dev)
+    xs, ys = mnist_proxy(sum(train), signal, 1, dev)
+    offs = np.cumsum([0] + [train[k] for k in rr.slots][:-1]).tolist()
+    xt, yt = mnist_proxy(10000, signal, 2, dev)
+    gen = torch.Generator().manual_seed(3)
+    curve, hit = [], None
+    t0 = time.perf_counter()
+    for r in range(max_rounds):
+        rr.run(xs, ys, offs, opt, lr, seed=r, generator=gen)
+        acc = rr.evaluate(xt, yt)["overall_accuracy"]
+        curve.append(round(acc, 4))
+        if acc >= target:
+            hit = r + 1
+            break
+    return {"target": target, "rounds": hit, "max_rounds": max_rounds, "accuracy_curve": curve,
+            "seconds": round(time.perf_counter() - t0, 2),
+            "config": f"K1: simple_cnn, 4 IID clients, 1 local epoch, batch 32, {opt} lr {lr}, "
+                      f"MNIST proxy (signal {signal}, 60k train / 10k test), no DP",
+            "data": "synthetic learnable MNIST proxy (class prototypes + N(0,1) noise); the "
+                    "real MNIST is not available offline: parity unpinned vs the reference's "
+                    "MNIST number"}
+
+
 def measured_traffic(probe_tag):
     """HBM bytes per launch of the probed kernel, from the newest committed PMC
     measurement (profiles/*/traffic.json, made by tools/traffic.py from separate
@@ -157,6 +205,10 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--probe", default=None, help="conv launch tag to time (default: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rounds-target", type=float, default=0.91,
+                    help="rounds-to-accuracy half of the metric (K1 MNIST proxy); 0 disables")
+    ap.add_argument("--rounds-max", type=int, default=30)
+    ap.add_argument("--proxy-signal", type=float, default=0.14)
     ap.add_argument("--lanes", type=int, default=None,
                     help="concurrent client lanes per GPU (default: planner / FH_LANES)")
     args = ap.parse_args()
@@ -239,6 +291,9 @@ def main():
             "achieved_tflops_step": round(value * fl / 1e12, 2),
             "roofline": roof,
         }
+        if world == 1 and args.rounds_target > 0:
+            out["rounds_to_target"] = rounds_to_target(dev, args.rounds_target, args.rounds_max,
+                                                       args.proxy_signal, args.opt, args.lr)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(out), flush=True)

@@ -199,6 +199,64 @@ ce_kernel(const float* __restrict__ logits, int64_t l_cs, const int64_t* __restr
     }
 }
 
+// ------------------------------------------------------------------ evaluation metrics
+// LocalTrainer.evaluate_model (training.py:307-360) / _validate_epoch (:214-242): per image
+// the first-index argmax (torch.max) and the CE loss; per slot the fp64 loss sum and correct
+// count (accumulated across launches, one block per slot: fixed order), per class the
+// correct / total counts (integer atomics: order-independent, deterministic).
+__global__ void __launch_bounds__(256)
+eval_metrics_kernel(const float* __restrict__ logits, int64_t l_cs,
+                    const int64_t* __restrict__ targets, int64_t t_cs,
+                    const int32_t* __restrict__ counts, int batch, int K,
+                    double* __restrict__ loss_sum, int64_t* __restrict__ correct,
+                    unsigned long long* __restrict__ class_correct,
+                    unsigned long long* __restrict__ class_total) {
+    __shared__ double sl[4];
+    __shared__ int sc[4];
+    const int z = blockIdx.x;
+    const int cnt = counts ? counts[z] : batch;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double lsum = 0.0;
+    int corr = 0;
+    for (int img = wid; img < cnt; img += 4) {
+        const float* row = logits + z * l_cs + (int64_t)img * K;
+        const int tgt = (int)targets[z * t_cs + img];
+        float mx = -INFINITY;
+        int amax = 0;
+        for (int k = lane; k < K; k += 64) {
+            const float v = row[k];
+            if (v > mx) { mx = v; amax = k; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float om = __shfl_xor(mx, o, 64);
+            const int oa = __shfl_xor(amax, o, 64);
+            if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+        }
+        float se = 0.f;
+        for (int k = lane; k < K; k += 64) se += expf(row[k] - mx);
+        se = wave_sum(se);
+        if (lane == 0) {
+            lsum += (double)(-((row[tgt] - mx) - logf(se)));
+            const int hit = amax == tgt;
+            corr += hit;
+            if (class_total && tgt >= 0 && tgt < K) {
+                atomicAdd(class_total + tgt, 1ull);
+                if (hit) atomicAdd(class_correct + tgt, 1ull);
+            }
+        }
+    }
+    if (lane == 0) {
+        sl[wid] = lsum;
+        sc[wid] = corr;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (loss_sum) loss_sum[z] += sl[0] + sl[1] + sl[2] + sl[3];
+        if (correct) correct[z] += sc[0] + sc[1] + sc[2] + sc[3];
+    }
+}
+
 // ------------------------------------------------------------------ global average pool
 __global__ void __launch_bounds__(256)
 avgpool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict__ y, int64_t y_cs,
@@ -335,6 +393,24 @@ extern "C" int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* t
                        targets, t_cs, dlogits, d_cs, loss_out, acc_loss, acc_correct, acc_seen,
                        reset, counts, batch, num_classes);
     FH_LAUNCH_CHECK("ce_fwd_bwd");
+    return FH_OK;
+}
+
+extern "C" int fh_eval_metrics(const float* logits, int64_t l_cs, const int64_t* targets,
+                               int64_t t_cs, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t num_classes, double* loss_sum,
+                               int64_t* correct, int64_t* class_correct, int64_t* class_total,
+                               void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && num_classes > 0, "eval_metrics: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(logits && targets, "eval_metrics: null pointer");
+    FH_REQUIRE((class_correct == nullptr) == (class_total == nullptr),
+               "eval_metrics: class_correct and class_total go together");
+    hipLaunchKernelGGL(eval_metrics_kernel, dim3(nclients), dim3(256), 0, as_stream(stream),
+                       logits, l_cs, targets, t_cs, counts, batch, num_classes, loss_sum, correct,
+                       reinterpret_cast<unsigned long long*>(class_correct),
+                       reinterpret_cast<unsigned long long*>(class_total));
+    FH_LAUNCH_CHECK("eval_metrics");
     return FH_OK;
 }
 

@@ -18,7 +18,7 @@ __all__ = [
     "fedavg_weighted_sum", "update_stats", "dp_delta_sqnorm", "dp_clip_coef", "dp_apply",
     "sgd_step", "adam_step", "bn_fwd_train", "bn_fwd_eval", "bn_bwd", "maxpool2_fwd",
     "maxpool2_bwd", "dropout_fwd", "dropout_bwd", "ce_fwd_bwd", "avgpool_fwd", "avgpool_bwd",
-    "gather_batch", "Workspace",
+    "gather_batch", "eval_metrics", "Workspace",
 ]
 
 
@@ -361,6 +361,13 @@ def ce_fwd_bwd(logits, targets, dlogits, nclients, batch, num_classes, loss_out=
     call("fh_ce_fwd_bwd", ptr(logits), _cs(logits), ptr(targets), _cs(targets), ptr(dlogits),
          _cs(dlogits), ptr(loss_out), ptr(acc_loss), ptr(acc_correct), ptr(acc_seen), ptr(reset),
          _counts(counts), nclients, batch, num_classes, stream_handle())
+
+
+def eval_metrics(logits, targets, nclients, batch, num_classes, counts=None, loss_sum=None,
+                 correct=None, class_correct=None, class_total=None):
+    call("fh_eval_metrics", ptr(logits), _cs(logits), ptr(targets), _cs(targets),
+         _counts(counts), nclients, batch, num_classes, ptr(loss_sum), ptr(correct),
+         ptr(class_correct), ptr(class_total), stream_handle())
 
 
 def avgpool_fwd(x, y, nclients, batch, C, HW, counts=None):

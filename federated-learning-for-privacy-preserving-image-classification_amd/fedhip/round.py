@@ -37,8 +37,9 @@ class DPConfig:
 class RankRound:
     def __init__(self, template_model, all_train_sizes: Sequence[int], my_clients: Sequence[int],
                  epochs: int = 1, batch: int = 32, device="cuda", dp: Optional[DPConfig] = None,
-                 group=None, lanes=None):
+                 group=None, lanes=None, compression=None):
         self.device = torch.device(device)
+        self._template = template_model
         self.B, self.epochs, self.dp, self.group = batch, epochs, dp, group
         self.all_sizes = list(all_train_sizes)
         # slots: this rank's clients ordered by descending step count (stable)
@@ -64,7 +65,22 @@ class RankRound:
         self.rows = torch.tensor([self.slot_of[k] for k in self.clients], dtype=torch.int32,
                                  device=self.device)
         self.partial = torch.zeros(self.P, device=self.device)
+        # global BN running statistics for evaluation (f-1; divergence D13): FedAvg of the
+        # clients' buffers with the same weights.  Clients keep their own buffers (D4).
+        self.Q = L.Q
+        self.global_bufs = torch.zeros(max(self.Q, 1), device=self.device)
+        with torch.no_grad():
+            for n, b in template_model.named_buffers():
+                if n in L.buf_names:
+                    L.bview(self.global_bufs.view(1, -1), n)[0].copy_(b.detach().reshape(-1))
         self.round_index = 0
+        self._evaluator = None
+        # update compression before FedAvg (f-3; insertion point D14): delta vs the global
+        self.compression = compression
+        self._cplan = None
+        if compression is not None:
+            from .compress import SegmentPlan
+            self._cplan = SegmentPlan(L.seg_offsets(), self.device)
 
     def set_global(self, flat: torch.Tensor):
         self.global_flat.copy_(flat)
@@ -81,13 +97,31 @@ class RankRound:
                                lr=lr, seed=seed)
         if self.dp is not None:
             self._apply_dp(S, seed)
+        if self.compression is not None:
+            from .compress import compress_rows
+            compress_rows(self._cplan, self.compression, tr.params, S,
+                          base=self.global_flat.view(1, -1).expand(S, -1))
         # FedAvg: this rank's partial sum in client-list order, then RCCL all-reduce.
         ops.fedavg_weighted_sum(tr.params, self.w32, self.partial, row_index=self.rows, P=self.P)
-        if self.group is not None or (dist.is_available() and dist.is_initialized()):
+        distributed = self.group is not None or (dist.is_available() and dist.is_initialized())
+        if distributed:
             dist.all_reduce(self.partial, op=dist.ReduceOp.SUM, group=self.group)
         self.global_flat.copy_(self.partial)
+        if self.Q:
+            ops.fedavg_weighted_sum(tr.bufs, self.w32, self.global_bufs, row_index=self.rows,
+                                    P=self.Q)
+            if distributed:
+                dist.all_reduce(self.global_bufs, op=dist.ReduceOp.SUM, group=self.group)
         self.round_index += 1
         return metrics
+
+    def evaluate(self, data, labels, template_model=None):
+        """Eval-mode metrics of the current global model on a device-resident test set
+        (fedhip/evaluate.py; LocalTrainer.evaluate_model's keys + 'loss')."""
+        if self._evaluator is None:
+            from .evaluate import GlobalEvaluator
+            self._evaluator = GlobalEvaluator(template_model or self._template, self.device)
+        return self._evaluator.evaluate(self.global_flat, self.global_bufs, data, labels)
 
     def _apply_dp(self, S, seed):
         """federated_trainer.py:434-462 for every client at once (budget bookkeeping is the

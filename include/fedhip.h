@@ -31,6 +31,9 @@
  *   fh_maxpool2_*            nn.MaxPool2d(2,2) (models_pytorch.py:72,123)
  *   fh_dropout_*             nn.Dropout (models_pytorch.py:75,124)
  *   fh_ce_fwd_bwd            nn.CrossEntropyLoss + metrics (training.py:90,193,200-203)
+ *   fh_eval_metrics          LocalTrainer.evaluate_model metrics (training.py:307-360)
+ *   fh_quantize_rows         QuantizationCompressor (compression.py:123-247)
+ *   fh_topk_rows             TopKSparsificationCompressor (compression.py:250-368)
  */
 #ifndef FEDHIP_H_
 #define FEDHIP_H_
@@ -266,6 +269,48 @@ int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets, int
                   int64_t* acc_correct, int64_t* acc_seen, const int32_t* reset,
                   const int32_t* counts, int32_t nclients, int32_t batch, int32_t num_classes,
                   void* stream);
+
+/* ---------------- update compression (compression.py:123-368) -----
+ * Per client row z and parameter segment s = [seg_offsets[s], seg_offsets[s+1]):
+ * v = x[z] - base[z] (base nullable: v = x[z]; base_cs 0 broadcasts one row) and
+ * out[z] = base[z] + decompress(compress(v)) (out nullable; may alias x).
+ * Segments are processed in chunks of fh_compress_chunk_elems() elements;
+ * chunk_offsets[s] (device int32[nseg+1]) = cumulative ceil(len_s / chunk), nchunks =
+ * chunk_offsets[nseg].
+ *
+ * fh_quantize_rows   QuantizationCompressor._quantize_tensor + _dequantize_tensor
+ *                    (:203-244), bits in [1,16]; codes (nullable, bits <= 8) get the
+ *                    uint8 wire codes; scale_out / zp_out (nullable, [C][nseg]) the
+ *                    per-segment scale (double) and zero point.  Asymmetric mode on a
+ *                    constant segment raises in the reference (round(inf)); here that
+ *                    segment passes through unchanged and zp_out = INT64_MIN.
+ * fh_topk_rows       TopKSparsificationCompressor._sparsify_tensor + _desparsify_tensor
+ *                    (:327-365) with k = seg_k[s] (device int64[nseg]); keep (nullable)
+ *                    gets the uint8 keep-mask.  Ties at the k-th magnitude: lowest
+ *                    flat indices are kept. */
+int64_t fh_compress_chunk_elems(void);
+int64_t fh_quantize_workspace(int32_t nclients, int32_t nchunks);
+int fh_quantize_rows(const float* x, int64_t x_cs, const float* base, int64_t base_cs, float* out,
+                     int64_t out_cs, uint8_t* codes, int64_t codes_cs, int32_t nclients,
+                     const int64_t* seg_offsets, const int32_t* chunk_offsets, int32_t nseg,
+                     int32_t nchunks, int32_t bits, int32_t symmetric, double* scale_out,
+                     int64_t* zp_out, void* ws, size_t ws_bytes, void* stream);
+int64_t fh_topk_workspace(int32_t nclients, int32_t nseg, int32_t nchunks);
+int fh_topk_rows(const float* x, int64_t x_cs, const float* base, int64_t base_cs, float* out,
+                 int64_t out_cs, uint8_t* keep, int64_t keep_cs, int32_t nclients,
+                 const int64_t* seg_offsets, const int32_t* chunk_offsets, const int64_t* seg_k,
+                 int32_t nseg, int32_t nchunks, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------- evaluation metrics (training.py:214-242, 307-360) ----------
+ * Eval-mode metrics of [nclients][batch][K] logits: per image the first-index
+ * argmax (torch.max) and the CE loss.  loss_sum[z] += sum of the slot's image
+ * losses (fp64) and correct[z] += its correct predictions (both nullable,
+ * accumulated across calls); class_correct[k] / class_total[k] (nullable
+ * together) count correct and seen images of label k (integer atomics). */
+int fh_eval_metrics(const float* logits, int64_t l_cs, const int64_t* targets, int64_t t_cs,
+                    const int32_t* counts, int32_t nclients, int32_t batch, int32_t num_classes,
+                    double* loss_sum, int64_t* correct, int64_t* class_correct,
+                    int64_t* class_total, void* stream);
 
 /* ---------------- AdaptiveAvgPool2d((1,1)) --------------------------------- */
 int fh_avgpool_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, const int32_t* counts,

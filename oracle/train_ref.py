@@ -171,6 +171,7 @@ class FederatedResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x, drop=None):
+        drop = drop or _Dropout(0.0)
         x = drop.relu(self.bn1(self.conv1(x)))
         x = self.layer3(self.layer2(self.layer1(x)))
         x = self.avg_pool(x).view(x.size(0), -1)
@@ -248,3 +249,28 @@ def train_epochs(model, batches, epochs, lr, optimizer_type, masks=None, pools=N
 
 def param_vector(model):
     return torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+
+
+def evaluate_model(model, data, targets, batch=32):
+    """LocalTrainer.evaluate_model (training.py:307-360): eval mode, torch.max argmax per
+    batch, overall and per-class accuracy (classes in first-seen order).  Also returns the
+    concatenated eval-mode logits (for the GPU parity tests)."""
+    model.eval()
+    correct, total, cls_ok, cls_n, outs = 0, 0, {}, {}, []
+    with torch.no_grad():
+        for i in range(0, data.shape[0], batch):
+            x, t = data[i:i + batch], targets[i:i + batch]
+            out = model(x)
+            outs.append(out)
+            _, pred = torch.max(out, 1)
+            total += t.size(0)
+            correct += int((pred == t).sum().item())
+            for j in range(t.size(0)):
+                lab = int(t[j].item())
+                cls_ok[lab] = cls_ok.get(lab, 0) + int((pred[j] == t[j]).item())
+                cls_n[lab] = cls_n.get(lab, 0) + 1
+    metrics = {"overall_accuracy": correct / total, "total_samples": total,
+               "correct_predictions": correct}
+    for c in cls_n:
+        metrics[f"class_{c}_accuracy"] = cls_ok[c] / cls_n[c]
+    return metrics, torch.cat(outs) if outs else torch.empty(0)

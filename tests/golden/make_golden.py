@@ -10,7 +10,8 @@ Writes tests/golden/golden.json (+ golden_arrays.npz).  Inputs are NOT stored:
 every input is regenerated from the seeds recorded here (numpy default_rng /
 torch.manual_seed, deterministic on this image), so the fixtures hold only
 expected outputs: sha256 of the exact fp32 bytes, per-tensor L2 norms, and
-sampled values.  Fixture ids follow SURVEY.md §8c (G1-G6).
+sampled values.  Fixture ids follow SURVEY.md §8c (G1-G6), plus G7 (evaluate_model,
+§8f-1) and G8 (compression, §8f-3).
 """
 from __future__ import annotations
 
@@ -250,13 +251,122 @@ def g6():
     return out
 
 
+# ------------------------------------------------------------------ G7 evaluate_model
+def g7():
+    """LocalTrainer.evaluate_model (training.py:307-360) after one local epoch: overall /
+    per-class accuracy and the exact eval-mode logits (sha256)."""
+    out = {}
+    cases = [  # key, model, kwargs, shape, classes, n_train, n_test, init seed, data seed
+        ("G7/simple", "simple_cnn", {}, (1, 28, 28), 10, 96, 100, 0, 11),
+        ("G7/cifar", "cifar10_cnn", {}, (3, 32, 32), 10, 64, 70, 3, 12),
+        ("G7/resnet8", "federated_resnet", {"num_blocks": [1, 1, 1]}, (3, 32, 32), 10, 16, 40, 0, 13),
+    ]
+    for key, name, kw, shp, ncls, ntr, nte, iseed, dseed in cases:
+        torch.manual_seed(iseed)
+        model = ref_models.ModelFactory.create_model(name, **kw)
+        x, y = make_batch(shp, ncls, ntr, dseed)
+        # a learnable signal: class-dependent mean shift, so accuracy is not chance
+        xt, yt = make_batch(shp, ncls, nte, dseed + 100)
+        x = x + 0.5 * y.view(-1, *([1] * len(shp))).float() / ncls
+        xt = xt + 0.5 * yt.view(-1, *([1] * len(shp))).float() / ncls
+        torch.manual_seed(iseed + 50)
+        run_local_trainer(model, x, y, 32, 1, 0.01, "sgd")
+        tr = LocalTrainer(model, device=torch.device("cpu"))
+        dl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(xt, yt), batch_size=32,
+                                         shuffle=False)
+        metrics = tr.evaluate_model(dl)
+        model.eval()
+        with torch.no_grad():
+            logits = torch.cat([model(xt[i:i + 32]) for i in range(0, nte, 32)])
+        out[key] = {"model": name, "kwargs": kw, "shape": list(shp), "classes": ncls,
+                    "n_train": ntr, "n_test": nte, "init_seed": iseed, "data_seed": dseed,
+                    "shift": 0.5, "train": {"bs": 32, "epochs": 1, "lr": 0.01, "opt": "sgd",
+                                            "torch_seed": iseed + 50},
+                    "metrics": {k: (float(v) if isinstance(v, float) else int(v))
+                                for k, v in metrics.items()},
+                    "logits_sha256": sha(logits), "logits": digest("logits", logits, key)}
+    return out
+
+
+# ------------------------------------------------------------------ G8 compression
+def _stub_lz4():
+    lz4 = types.ModuleType("lz4")
+    lz4.frame = types.ModuleType("lz4.frame")
+    sys.modules.setdefault("lz4", lz4)
+    sys.modules.setdefault("lz4.frame", lz4.frame)
+
+
+def g8_inputs():
+    """Per-case tensors (regenerated by the tests from the same recipe)."""
+    rng = np.random.default_rng(801)
+    t = {
+        "w": rng.standard_normal((64, 32, 3, 3)).astype(np.float32) * 0.05,
+        "b": rng.standard_normal(64).astype(np.float32) * 0.01,
+        "fc": rng.standard_normal((10, 200)).astype(np.float32),
+        "zero": np.zeros(17, np.float32),
+        "ties": np.array([0.5, -0.5, 0.25, 0.5, -1.0, 0.0, 0.0, 0.125, -0.25, 0.5], np.float32),
+        "pos": np.abs(rng.standard_normal(33)).astype(np.float32) + 0.1,
+        "one": np.array([-3.0], np.float32),
+    }
+    return t
+
+
+def g8():
+    """QuantizationCompressor / TopKSparsificationCompressor (compression.py:123-368):
+    scales, zero points, codes and the decompressed dense tensors.  compression.py
+    imports lz4 at module level (:8) and lz4 is not installed; the LZ4 compressor is not
+    exercised, so a stub module stands in for the import only."""
+    _stub_lz4()
+    from src.shared.compression import QuantizationCompressor, TopKSparsificationCompressor
+    out = {}
+    ins = g8_inputs()
+    weights = {k: torch.from_numpy(v.copy()) for k, v in ins.items()}
+    for bits, sym in [(8, True), (8, False), (4, True), (6, False)]:
+        q = QuantizationCompressor(bits=bits, symmetric=sym)
+        res = {}
+        for name, t in weights.items():
+            if name == "zero" or (name == "one" and not sym):
+                continue  # scale 0: division by zero in the reference (NaN codes)
+            codes, scale, zp = q._quantize_tensor(t)
+            deq = q._dequantize_tensor(codes, scale, zp, t.shape, str(t.dtype))
+            res[name] = {"scale": float(scale), "zero_point": int(zp),
+                         "codes_sha256": sha(codes), "codes": codes.reshape(-1)[:64].tolist(),
+                         "dense_sha256": sha(deq), "dense": digest(name, deq, f"G8/q{bits}{sym}")}
+        out[f"G8/quant_{bits}bit_{'sym' if sym else 'asym'}"] = res
+    for ratio in (0.9, 0.5, 0.99, 0.0):
+        c = TopKSparsificationCompressor(sparsity_ratio=ratio)
+        res = {}
+        for name, t in weights.items():
+            if name == "ties" and ratio in (0.5,):
+                continue  # 5 of 10 kept: cuts through the |0.5| tie (torch.topk order unspecified)
+            vals, idx, shp = c._sparsify_tensor(t)
+            dense = c._desparsify_tensor(vals, idx, shp, str(t.dtype))
+            res[name] = {"k": int(idx.numel()), "indices_sorted": sorted(int(i) for i in idx),
+                         "dense_sha256": sha(dense)}
+        out[f"G8/topk_{ratio}"] = res
+    return out
+
+
+GROUPS = {"g1": lambda: g1(), "g2": lambda: g2(), "g3_g5": lambda: g3_g5(), "g6": lambda: g6(),
+          "g7": lambda: g7(), "g8": lambda: g8()}
+
+
 def main():
-    gold = {"generator": "tests/golden/make_golden.py", "torch": torch.__version__,
-            "numpy": np.__version__}
-    for fn in (g1, g2, g3_g5, g6):
-        gold.update(fn())
-        print(f"{fn.__name__} done", flush=True)
-    with open(os.path.join(OUT, "golden.json"), "w") as f:
+    """No arguments: regenerate every group.  With group names (e.g. `g7 g8`): regenerate
+    only those and merge them into the existing fixtures."""
+    want = sys.argv[1:] or list(GROUPS)
+    path = os.path.join(OUT, "golden.json")
+    gold = {}
+    if sys.argv[1:]:
+        gold = json.load(open(path))
+        with np.load(os.path.join(OUT, "golden_arrays.npz")) as z:
+            ARRAYS.update({k: z[k] for k in z.files})
+    gold.update({"generator": "tests/golden/make_golden.py", "torch": torch.__version__,
+                 "numpy": np.__version__})
+    for g in want:
+        gold.update(GROUPS[g]())
+        print(f"{g} done", flush=True)
+    with open(path, "w") as f:
         json.dump(gold, f, indent=1, sort_keys=True)
     np.savez_compressed(os.path.join(OUT, "golden_arrays.npz"), **ARRAYS)
     print("wrote", len(gold), "entries")

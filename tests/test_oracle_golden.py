@@ -1,5 +1,6 @@
 """Pin the CPU oracle against golden fixtures produced by the reference itself
-(tests/golden/make_golden.py).  CPU only."""
+(tests/golden/make_golden.py; G7 evaluate_model, G8
+compression).  CPU only."""
 import hashlib
 import json
 import math
@@ -10,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle import fedavg_ref, partition_ref, privacy_ref, train_ref
+from oracle import compress_ref, fedavg_ref, partition_ref, privacy_ref, train_ref
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = json.load(open(os.path.join(HERE, "golden", "golden.json")))
@@ -158,3 +159,67 @@ def test_g6_partitioner_bit_exact(key):
     assert [len(parts[k]) for k in ks] == g["sizes"]
     got = [hashlib.sha256(np.asarray(parts[k], np.int64).tobytes()).hexdigest() for k in ks]
     assert got == g["sha256"]
+
+
+def g7_case(g):
+    """Rebuild a G7 case: one local epoch (LocalTrainer semantics) then the test split."""
+    shp = tuple(g["shape"])
+    model = train_ref.make_model(g["model"], g["init_seed"], **g["kwargs"])
+    x, y = make_batch(shp, g["classes"], g["n_train"], g["data_seed"])
+    xt, yt = make_batch(shp, g["classes"], g["n_test"], g["data_seed"] + 100)
+    x = x + g["shift"] * y.view(-1, *([1] * len(shp))).float() / g["classes"]
+    xt = xt + g["shift"] * yt.view(-1, *([1] * len(shp))).float() / g["classes"]
+    tr = g["train"]
+    batches = [(x[i:i + tr["bs"]], y[i:i + tr["bs"]]) for i in range(0, g["n_train"], tr["bs"])]
+    torch.manual_seed(tr["torch_seed"])
+    train_ref.train_epochs(model, batches, tr["epochs"], tr["lr"], tr["opt"])
+    return model, xt, yt
+
+
+@pytest.mark.parametrize("key", [k for k in GOLD if k.startswith("G7/")])
+def test_g7_evaluate_oracle_bit_exact(key):
+    g = GOLD[key]
+    torch.set_num_threads(8)
+    model, xt, yt = g7_case(g)
+    metrics, logits = train_ref.evaluate_model(model, xt, yt, batch=32)
+    assert sha(logits.numpy()) == g["logits_sha256"]
+    assert metrics == g["metrics"]
+
+
+def g8_inputs():
+    rng = np.random.default_rng(801)
+    return {
+        "w": rng.standard_normal((64, 32, 3, 3)).astype(np.float32) * 0.05,
+        "b": rng.standard_normal(64).astype(np.float32) * 0.01,
+        "fc": rng.standard_normal((10, 200)).astype(np.float32),
+        "zero": np.zeros(17, np.float32),
+        "ties": np.array([0.5, -0.5, 0.25, 0.5, -1.0, 0.0, 0.0, 0.125, -0.25, 0.5], np.float32),
+        "pos": np.abs(rng.standard_normal(33)).astype(np.float32) + 0.1,
+        "one": np.array([-3.0], np.float32),
+    }
+
+
+@pytest.mark.parametrize("key", [k for k in GOLD if k.startswith("G8/quant")])
+def test_g8_quantize_oracle_bit_exact(key):
+    bits = int(key.split("_")[1].replace("bit", ""))
+    sym = key.endswith("_sym")
+    ins = g8_inputs()
+    for name, exp in GOLD[key].items():
+        codes, scale, zp = compress_ref.quantize(ins[name], bits, sym)
+        assert scale == exp["scale"] and zp == exp["zero_point"], name
+        assert hashlib.sha256(codes.tobytes()).hexdigest() == exp["codes_sha256"], name
+        dense = compress_ref.dequantize(codes, scale, zp)
+        assert sha(dense) == exp["dense_sha256"], name
+
+
+@pytest.mark.parametrize("key", [k for k in GOLD if k.startswith("G8/topk")])
+def test_g8_topk_oracle_bit_exact(key):
+    ratio = float(key.split("_")[1])
+    ins = g8_inputs()
+    for name, exp in GOLD[key].items():
+        x = ins[name]
+        k = compress_ref.topk_k(x.size, ratio)
+        assert k == exp["k"], name
+        if name != "zero":  # all-zero input: any k indices give the same dense tensor
+            assert compress_ref.topk_indices(x, k).tolist() == exp["indices_sorted"], name
+        assert sha(compress_ref.topk_dense(x, ratio)) == exp["dense_sha256"], name
