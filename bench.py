@@ -96,11 +96,18 @@ def build_clients(cfg, world, seed=0):
     return labels, train
 
 
-def make_rank_data(cfg, train_sizes, my_slots, device, seed):
-    """Synthetic N(0,1) inputs for this rank's clients, laid out slot after slot."""
+def make_rank_data(cfg, train_sizes, my_slots, device, seed, raw=True):
+    """Synthetic inputs for this rank's clients, laid out slot after slot: raw uint8 images
+    in the torchvision dataset layout ([N, H, W, C], C omitted for MNIST) that the on-device
+    pipeline normalises / augments each step, or (raw=False) pre-normalised N(0,1) fp32."""
     total = sum(train_sizes[k] for k in my_slots)
     g = torch.Generator(device=device).manual_seed(1000 + seed)
-    data = torch.randn(total, *cfg["shape"], generator=g, device=device)
+    if raw:
+        c, h, w = cfg["shape"]
+        shp = (total, h, w) if c == 1 else (total, h, w, c)
+        data = torch.randint(0, 256, shp, generator=g, device=device, dtype=torch.uint8)
+    else:
+        data = torch.randn(total, *cfg["shape"], generator=g, device=device)
     labels = torch.randint(0, cfg["classes"], (total,), generator=g, device=device)
     offs = np.cumsum([0] + [train_sizes[k] for k in my_slots][:-1]).tolist()
     return data, labels, offs
@@ -209,6 +216,8 @@ def main():
                     help="rounds-to-accuracy half of the metric (K1 MNIST proxy); 0 disables")
     ap.add_argument("--rounds-max", type=int, default=30)
     ap.add_argument("--proxy-signal", type=float, default=0.14)
+    ap.add_argument("--fp32-data", action="store_true",
+                    help="pre-normalised fp32 shards instead of uint8 images + on-device transform")
     ap.add_argument("--lanes", type=int, default=None,
                     help="concurrent client lanes per GPU (default: planner / FH_LANES)")
     args = ap.parse_args()
@@ -222,9 +231,13 @@ def main():
     torch.manual_seed(0)
     template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
     dp = DPConfig(epsilon=cfg["dp"]) if cfg["dp"] else None
+    raw = not args.fp32_data
+    tf = None
+    if raw:  # the reference loaders' train transforms (data_loader.py:298-301, 454-458)
+        tf = ops.DataTransform.mnist() if cfg["shape"][0] == 1 else ops.DataTransform.cifar10()
     rr = RankRound(template, train, mine, epochs=cfg["epochs"], device=dev, dp=dp,
-                   lanes=args.lanes)
-    data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, rank)
+                   lanes=args.lanes, transform=tf)
+    data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, rank, raw=raw)
     my_images = cfg["epochs"] * sum(train[k] for k in mine)
     total_images = cfg["epochs"] * sum(train)
 
@@ -278,8 +291,11 @@ def main():
             "unit": "client-images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic N(0,1) CIFAR/MNIST-shaped tensors resident in HBM; "
-                    "Dirichlet shard sizes from the reference partitioner restatement",
+            "data": ("synthetic uint8 CIFAR/MNIST-shaped images resident in HBM, the "
+                     "reference loaders' transforms (crop/flip/normalise) applied on the chip "
+                     "each step" if raw else "synthetic N(0,1) CIFAR/MNIST-shaped fp32 tensors "
+                     "resident in HBM") + "; Dirichlet shard sizes from the reference "
+                    "partitioner restatement",
             "config": {"workload": f"{args.config}: {cfg['model']} {C} clients "
                                    f"({cfg['clients']}/GPU), {cfg['strategy']}"
                                    f"{'(a=' + str(cfg['alpha']) + ')' if cfg['strategy'] == 'non_iid' else ''}, "

@@ -305,6 +305,66 @@ gather_kernel(const float* __restrict__ data, const int64_t* __restrict__ labels
     }
 }
 
+// ---- uint8 dataset -> normalised (and augmented) fp32 batch -----------------------
+// torchvision's per-sample train transform of the reference's loaders
+// (data_loader.py:298-301 MNIST: ToTensor + Normalize; :454-458 CIFAR: RandomCrop(32, 4)
+// + RandomHorizontalFlip + ToTensor + Normalize), run on the chip over the raw uint8
+// images (HWC, as torchvision datasets hold them) instead of on CPU loader workers:
+//   v = (fl32(u8) / 255 - mean_c) / std_c         (to_tensor .div(255); normalize sub_, div_)
+//   crop: padded(y + i, x + j) with zero padding (fill 0 before ToTensor);  flip after crop.
+// Crop offsets / flip come from `aug_in` [S][B] uchar4 {i, j, flip, -} when given
+// (replay), else from Philox(seed, (z, b)) and are then recorded to `aug_out` (nullable).
+struct NormParams {
+    float mean[4];
+    float stdv[4];
+};
+
+__global__ void __launch_bounds__(256)
+gather_u8_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ labels,
+                 const int64_t* __restrict__ idx, int64_t idx_cs, float* __restrict__ x,
+                 int64_t x_cs, int64_t* __restrict__ y, int64_t y_cs,
+                 const int32_t* __restrict__ counts, int batch, int C, int H, int W,
+                 NormParams np, int pad, int flip, const uchar4* __restrict__ aug_in,
+                 uchar4* __restrict__ aug_out, int64_t aug_cs, uint64_t seed_salt,
+                 const uint64_t* __restrict__ seed_dev) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int64_t plane = (int64_t)H * W, per = plane * C;
+    const int64_t total = (int64_t)cnt * per;
+    const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = e / per;
+        const int64_t r = e - b * per;
+        const int c = (int)(r / plane);
+        const int64_t p = r - (int64_t)c * plane;
+        const int yy = (int)(p / W), xx = (int)(p - (int64_t)yy * W);
+        int ci = pad, cj = pad, fl = 0;
+        if (pad > 0 || flip) {
+            if (aug_in) {
+                const uchar4 a = aug_in[z * aug_cs + b];
+                ci = a.x; cj = a.y; fl = a.z;
+            } else {
+                const uint4 rr = Philox::gen(seed, (uint64_t)z, (uint64_t)b);
+                const uint32_t span = 2u * (uint32_t)pad + 1u;
+                ci = pad > 0 ? (int)(((uint64_t)rr.x * span) >> 32) : 0;
+                cj = pad > 0 ? (int)(((uint64_t)rr.y * span) >> 32) : 0;
+                fl = flip ? (int)(rr.z >> 31) : 0;
+                if (aug_out && r == 0) aug_out[z * aug_cs + b] = make_uchar4(ci, cj, fl, 0);
+            }
+        }
+        const int sx0 = fl ? (W - 1 - xx) : xx;  // flip acts on the cropped image
+        const int sy = yy + ci - pad, sx = sx0 + cj - pad;
+        const int64_t s = idx[z * idx_cs + b];
+        float u = 0.f;
+        if (sy >= 0 && sy < H && sx >= 0 && sx < W)
+            u = (float)data[((s * H + sy) * W + sx) * C + c];
+        const float v = __fdiv_rn(u, 255.f);
+        x[z * x_cs + e] = __fdiv_rn(v - np.mean[c], np.stdv[c]);
+        if (r == 0 && y) y[z * y_cs + b] = labels[s];
+    }
+}
+
 static int ew_grid(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(ceil_div(n, 256), 1), 2048); }
 
 }  // namespace fh
@@ -450,5 +510,31 @@ extern "C" int fh_gather_batch(const float* data, const int64_t* labels, const i
                        as_stream(stream), data, labels, idx, idx_cs, x, x_cs, y, y_cs, sample_elems,
                        counts, batch);
     FH_LAUNCH_CHECK("gather_batch");
+    return FH_OK;
+}
+
+extern "C" int fh_gather_u8(const uint8_t* data, const int64_t* labels, const int64_t* idx,
+                            int64_t idx_cs, float* x, int64_t x_cs, int64_t* y, int64_t y_cs,
+                            const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
+                            int32_t H, int32_t W, const float* mean, const float* stdv,
+                            int32_t pad, int32_t flip, const uint8_t* aug_in, uint8_t* aug_out,
+                            int64_t aug_cs, uint64_t seed, const uint64_t* seed_dev,
+                            void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C >= 1 && C <= 4 && H > 0 && W > 0,
+               "gather_u8: bad shape (C must be 1..4)");
+    FH_REQUIRE(pad >= 0 && pad <= 127, "gather_u8: pad out of range");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(data && idx && x && (!y || labels) && mean && stdv, "gather_u8: null pointer");
+    NormParams np;
+    for (int c = 0; c < 4; ++c) {
+        np.mean[c] = c < C ? mean[c] : 0.f;
+        np.stdv[c] = c < C ? stdv[c] : 1.f;
+    }
+    hipLaunchKernelGGL(gather_u8_kernel, dim3(ew_grid((int64_t)batch * C * H * W), nclients),
+                       dim3(256), 0, as_stream(stream), data, labels, idx, idx_cs, x, x_cs, y, y_cs,
+                       counts, batch, C, H, W, np, pad, flip,
+                       reinterpret_cast<const uchar4*>(aug_in), reinterpret_cast<uchar4*>(aug_out),
+                       aug_cs, seed, seed_dev);
+    FH_LAUNCH_CHECK("gather_u8");
     return FH_OK;
 }

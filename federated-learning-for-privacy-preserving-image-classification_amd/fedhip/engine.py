@@ -124,6 +124,8 @@ class PackedTrainer:
         # when probe_full is set (bench.py times their kernels with events).
         self.use_graphs = True
         self.stream = None  # set by a LanedTrainer: the lane's HIP stream
+        self.transform = None  # ops.DataTransform for uint8 datasets (on-device pipeline)
+        self.aug_record = None  # optional [cap, B, 4] uint8: crop/flip draws (eager steps)
         self.probe_full = False
         self.probe_first_only = False  # lanes: probe only the (serialised) first step
         self._graphs = {}
@@ -272,8 +274,7 @@ class PackedTrainer:
             ops.PROBE.enabled = arm
             net.seed = (st["seed"] * 1000003 + g) & 0x7FFFFFFF
             net.seed_dev = None
-            ops.gather_batch(st["data"], st["labels"], views["gidx"], net.x, net.y,
-                             st["sample_elems"], n, self.batch, counts=views["counts"])
+            self._gather(st["data"], st["labels"], views, n, st["sample_elems"])
             self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
                                 adam_dev=views["adam"])
             if arm:
@@ -319,8 +320,22 @@ class PackedTrainer:
                      adam=cur[o_adam:o_adam + 8].view(torch.float32))
         return rows, cur, views
 
+    def _gather(self, data, labels, views, n, sample_elems):
+        """This step's batch into net.x / net.y: a plain row gather of fp32 samples, or the
+        on-device torchvision transform of raw uint8 images (ops.DataTransform)."""
+        net = self.net
+        if data.dtype == torch.uint8:
+            if self.transform is None:
+                raise FedHipError("uint8 images need a DataTransform (PackedTrainer.transform)")
+            ops.gather_u8(data, labels, views["gidx"], net.x, net.y, self.transform, n,
+                          self.batch, counts=views["counts"], seed=net._seed(31),
+                          seed_dev=net.seed_dev, aug_out=self.aug_record)
+        else:
+            ops.gather_batch(data, labels, views["gidx"], net.x, net.y, sample_elems, n,
+                             self.batch, counts=views["counts"])
+
     def _replay(self, n, data, labels, views, sample_elems):
-        key = (n, self.opt_type, self.lr, data.data_ptr(), labels.data_ptr(),
+        key = (n, self.opt_type, self.lr, self.transform, data.data_ptr(), labels.data_ptr(),
                views["gidx"].data_ptr(), tuple(views["gidx"].shape))
         graph = self._graphs.get(key)
         if graph is None:
@@ -332,8 +347,7 @@ class PackedTrainer:
             # capture on this trainer's own stream when it has one, so the split-K scratch
             # (keyed by stream) is the lane's, never shared with a concurrently running lane
             with torch.cuda.graph(graph, pool=self._graph_pool, stream=self.stream):
-                ops.gather_batch(data, labels, views["gidx"], net.x, net.y, sample_elems, n,
-                                 self.batch, counts=views["counts"])
+                self._gather(data, labels, views, n, sample_elems)
                 self._step_launches(n, views["counts"], views["reset"], first=False,
                                     adam_dev=views["adam"])
             net.seed_dev = None

@@ -57,11 +57,15 @@ class GlobalEvaluator:
         return self._tail_counts[m]
 
     def evaluate(self, params_flat: torch.Tensor, bufs_flat: torch.Tensor, data: torch.Tensor,
-                 labels: torch.Tensor) -> Dict[str, float]:
+                 labels: torch.Tensor, transform=None) -> Dict[str, float]:
         """params_flat [>=P] (named_parameters order), bufs_flat [>=Q] (BN running stats),
-        data [N, *in_shape], labels [N] int64 — all on the device."""
+        data [N, *in_shape] fp32 — or raw uint8 images [N, H, W(, C)] with `transform`
+        (ops.DataTransform; its eval form, ToTensor + Normalize, is applied on the chip) —
+        labels [N] int64, all on the device."""
         net, S, B = self.net, self.slots, self.batch
         N = int(data.shape[0])
+        if data.dtype == torch.uint8:
+            return self._evaluate_u8(params_flat, bufs_flat, data, labels, transform)
         if tuple(data.shape[1:]) != tuple(net.in_shape) or labels.shape[0] != N:
             raise FedHipError(f"evaluate: data {tuple(data.shape)} / labels "
                               f"{tuple(labels.shape)} do not match input {net.in_shape}")
@@ -90,6 +94,36 @@ class GlobalEvaluator:
                                  class_correct=self.class_correct, class_total=self.class_total)
         finally:
             net.x, net.y = self._x_pad, self._y_pad
+        return self._metrics(N)
+
+    def _evaluate_u8(self, params_flat, bufs_flat, data, labels, transform):
+        if transform is None:
+            raise FedHipError("evaluate: uint8 images need a DataTransform")
+        tf = transform.eval()
+        net, S, B = self.net, self.slots, self.batch
+        N = int(data.shape[0])
+        chunk = S * B
+        nchunks = -(-N // chunk)
+        if getattr(self, "_idx_n", None) != N:
+            self._idx = torch.arange(nchunks * chunk, device=self.device).clamp_(max=max(N - 1, 0))
+            self._idx_n = N
+        rows = params_flat.reshape(1, -1).expand(S, -1)
+        brows = bufs_flat.reshape(1, -1).expand(S, -1)
+        for t in (self.loss_sum, self.correct, self.class_correct, self.class_total):
+            t.zero_()
+        for start in range(0, N, chunk):
+            m = min(chunk, N - start)
+            counts, n = ((self.full_counts, S) if m == chunk else
+                         (self._counts_for(m), math.ceil(m / B)))
+            idx = self._idx[start:start + chunk].view(S, B)
+            ops.gather_u8(data, labels, idx, net.x, net.y, tf, n, B, counts=counts)
+            net.forward(rows, brows, n, counts, train=False)
+            ops.eval_metrics(net.logits, net.y, n, B, self.K, counts=counts,
+                             loss_sum=self.loss_sum, correct=self.correct,
+                             class_correct=self.class_correct, class_total=self.class_total)
+        return self._metrics(N)
+
+    def _metrics(self, N):
         correct = int(self.correct.sum().item())
         cc, ct = self.class_correct.tolist(), self.class_total.tolist()
         out = {"overall_accuracy": correct / N if N else 0.0, "total_samples": N,

@@ -135,6 +135,15 @@ class LanedTrainer:
             ln.probe_first_only = True
 
     @property
+    def transform(self):
+        return self.lanes[0].transform
+
+    @transform.setter
+    def transform(self, tf):
+        for ln in self.lanes:
+            ln.transform = tf
+
+    @property
     def num_batches_tracked(self):
         return [c for ln in self.lanes for c in ln.num_batches_tracked]
 

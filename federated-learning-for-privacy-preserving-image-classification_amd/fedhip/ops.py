@@ -9,16 +9,19 @@ the arithmetic is the kernels'.
 """
 from __future__ import annotations
 
+import ctypes
+from dataclasses import dataclass
+
 import torch
 
-from ._lib import call, load, ptr, require_device, stream_handle
+from ._lib import FedHipError, call, load, ptr, require_device, stream_handle
 
 __all__ = [
     "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "linear_fwd", "linear_dgrad", "linear_wgrad",
     "fedavg_weighted_sum", "update_stats", "dp_delta_sqnorm", "dp_clip_coef", "dp_apply",
     "sgd_step", "adam_step", "bn_fwd_train", "bn_fwd_eval", "bn_bwd", "maxpool2_fwd",
     "maxpool2_bwd", "dropout_fwd", "dropout_bwd", "ce_fwd_bwd", "avgpool_fwd", "avgpool_bwd",
-    "gather_batch", "eval_metrics", "Workspace",
+    "gather_batch", "gather_u8", "DataTransform", "eval_metrics", "Workspace",
 ]
 
 
@@ -378,6 +381,49 @@ def avgpool_fwd(x, y, nclients, batch, C, HW, counts=None):
 def avgpool_bwd(dy, dx, nclients, batch, C, HW, counts=None):
     call("fh_avgpool_bwd", ptr(dy), _cs(dy), ptr(dx), _cs(dx), _counts(counts), nclients, batch,
          C, HW, stream_handle())
+
+
+@dataclass(frozen=True)
+class DataTransform:
+    """torchvision train/test transform of the reference loaders, run on the chip by
+    fh_gather_u8 over raw uint8 HWC images: RandomCrop(pad) + RandomHorizontalFlip (train,
+    CIFAR) + ToTensor + Normalize(mean, std).  data_loader.py:298-306 (MNIST), :454-463
+    (CIFAR-10)."""
+    mean: tuple
+    std: tuple
+    pad: int = 0
+    flip: bool = False
+
+    @staticmethod
+    def mnist():
+        return DataTransform((0.1307,), (0.3081,))
+
+    @staticmethod
+    def cifar10(train=True):
+        return DataTransform((0.4914, 0.4822, 0.4465), (0.2023, 0.1994, 0.2010),
+                             pad=4 if train else 0, flip=bool(train))
+
+    def eval(self):
+        return DataTransform(self.mean, self.std)
+
+
+def gather_u8(data, labels, idx, x, y, tf: DataTransform, nclients, batch, counts=None,
+              seed=0, seed_dev=None, aug_in=None, aug_out=None):
+    """x[z][b] = tf(data[idx[z][b]]) (data: uint8 [N, H, W, C]); y[z][b] = labels[...]."""
+    if data.dtype != torch.uint8 or data.dim() not in (3, 4):
+        raise FedHipError("gather_u8: data must be uint8 [N, H, W(, C)]")
+    H, W = int(data.shape[1]), int(data.shape[2])
+    C = int(data.shape[3]) if data.dim() == 4 else 1
+    if len(tf.mean) != C or len(tf.std) != C:
+        raise FedHipError(f"gather_u8: transform has {len(tf.mean)} channels, data {C}")
+    mean = (ctypes.c_float * C)(*tf.mean)
+    std = (ctypes.c_float * C)(*tf.std)
+    aug = aug_in if aug_in is not None else aug_out
+    call("fh_gather_u8", ptr(data), ptr(labels), ptr(idx), _cs(idx), ptr(x), _cs(x), ptr(y),
+         _cs(y), _counts(counts), nclients, batch, C, H, W, ctypes.addressof(mean),
+         ctypes.addressof(std), int(tf.pad), int(bool(tf.flip)), ptr(aug_in), ptr(aug_out),
+         0 if aug is None else aug.stride(0) // 4, seed & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev),
+         stream_handle())
 
 
 def gather_batch(data, labels, idx, x, y, sample_elems, nclients, batch, counts=None):

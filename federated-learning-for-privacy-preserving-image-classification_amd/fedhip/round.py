@@ -37,7 +37,7 @@ class DPConfig:
 class RankRound:
     def __init__(self, template_model, all_train_sizes: Sequence[int], my_clients: Sequence[int],
                  epochs: int = 1, batch: int = 32, device="cuda", dp: Optional[DPConfig] = None,
-                 group=None, lanes=None, compression=None):
+                 group=None, lanes=None, compression=None, transform=None):
         self.device = torch.device(device)
         self._template = template_model
         self.B, self.epochs, self.dp, self.group = batch, epochs, dp, group
@@ -49,6 +49,8 @@ class RankRound:
         steps = [epochs * math.ceil(self.all_sizes[k] / batch) for k in self.slots]
         self.trainer = LanedTrainer(template_model, steps or [0], batch=batch, device=self.device,
                                     lanes=lanes)
+        self.transform = transform  # ops.DataTransform when the shards are raw uint8 images
+        self.trainer.transform = transform
         L = self.trainer.layout
         self.P = L.P
         self.global_flat = torch.zeros(self.P, device=self.device)
@@ -121,7 +123,8 @@ class RankRound:
         if self._evaluator is None:
             from .evaluate import GlobalEvaluator
             self._evaluator = GlobalEvaluator(template_model or self._template, self.device)
-        return self._evaluator.evaluate(self.global_flat, self.global_bufs, data, labels)
+        return self._evaluator.evaluate(self.global_flat, self.global_bufs, data, labels,
+                                        transform=self.transform)
 
     def _apply_dp(self, S, seed):
         """federated_trainer.py:434-462 for every client at once (budget bookkeeping is the

@@ -270,6 +270,20 @@ int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets, int
                   const int32_t* counts, int32_t nclients, int32_t batch, int32_t num_classes,
                   void* stream);
 
+/* ---------------- on-device input pipeline (data_loader.py:298-301, 454-458) -----
+ * x[z][b] = Normalize(RandomHorizontalFlip(RandomCrop(data[idx[z][b]], pad)))
+ * from raw uint8 HWC images (torchvision layout) to fp32 NCHW: (u/255 - mean_c) /
+ * std_c (mean/stdv: HOST float[C], C <= 4); pad 0 = no crop, flip 0 = no flip.
+ * Crop/flip per image from aug_in (uchar4 {i, j, flip, -} per [z][b], stride
+ * aug_cs; replay) or Philox(seed + *seed_dev, (z, b)), then recorded to aug_out
+ * (nullable).  y[z][b] = labels[idx[z][b]] (y nullable). */
+int fh_gather_u8(const uint8_t* data, const int64_t* labels, const int64_t* idx, int64_t idx_cs,
+                 float* x, int64_t x_cs, int64_t* y, int64_t y_cs, const int32_t* counts,
+                 int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                 const float* mean, const float* stdv, int32_t pad, int32_t flip,
+                 const uint8_t* aug_in, uint8_t* aug_out, int64_t aug_cs, uint64_t seed,
+                 const uint64_t* seed_dev, void* stream);
+
 /* ---------------- update compression (compression.py:123-368) -----
  * Per client row z and parameter segment s = [seg_offsets[s], seg_offsets[s+1]):
  * v = x[z] - base[z] (base nullable: v = x[z]; base_cs 0 broadcasts one row) and

@@ -223,3 +223,15 @@ def test_g8_topk_oracle_bit_exact(key):
         if name != "zero":  # all-zero input: any k indices give the same dense tensor
             assert compress_ref.topk_indices(x, k).tolist() == exp["indices_sorted"], name
         assert sha(compress_ref.topk_dense(x, ratio)) == exp["dense_sha256"], name
+
+
+def test_data_ref_transform_known_values():
+    """oracle/data_ref.py on a hand-checked 2x2 image: crop with zero padding, flip after
+    crop, (u/255 - mean) / std in float32."""
+    from oracle import data_ref
+    img = np.array([[[10], [20]], [[30], [40]]], np.uint8)
+    out = data_ref.transform(img, (0.5,), (0.25,), pad=1, i=0, j=1, flip=True)
+    # padded 4x4, crop rows 0-1 cols 1-2 -> [[0,0],[10,20]]; flip -> [[0,0],[20,10]]
+    u = np.array([[0, 0], [20, 10]], np.float32) / np.float32(255)
+    exp = (u - np.float32(0.5)) / np.float32(0.25)
+    assert np.array_equal(out[0], exp)
