@@ -11,7 +11,7 @@ every input is regenerated from the seeds recorded here (numpy default_rng /
 torch.manual_seed, deterministic on this image), so the fixtures hold only
 expected outputs: sha256 of the exact fp32 bytes, per-tensor L2 norms, and
 sampled values.  Fixture ids follow SURVEY.md §8c (G1-G6), plus G7 (evaluate_model,
-§8f-1) and G8 (compression, §8f-3).
+§8f-1), G8 (compression, §8f-3) and G9 (wire format, convergence norms, §8f-4).
 """
 from __future__ import annotations
 
@@ -347,8 +347,34 @@ def g8():
     return out
 
 
+# ------------------------------------------------------------------ G9 wire format / convergence
+def g9():
+    """ModelWeightSerializer.serialize_weights (serialization.py:28-48: torch.save bytes, sent
+    as .hex(), :105) of a seeded weight dict, and ConvergenceDetector's weight-change norms
+    (convergence.py:189-217) between two seeded weight dicts."""
+    from src.aggregation.convergence import ConvergenceDetector
+    from src.shared.serialization import ModelWeightSerializer
+    out = {}
+    torch.manual_seed(0)
+    m = ref_models.ModelFactory.create_model("simple_cnn")
+    w = m.get_model_weights()
+    data = ModelWeightSerializer.serialize_weights(w)
+    out["G9/serialize_simple_cnn"] = {"init_seed": 0, "bytes": len(data),
+                                      "sha256": hashlib.sha256(data).hexdigest(),
+                                      "hex_sha256": hashlib.sha256(data.hex().encode()).hexdigest()}
+    for name, kw, s1, s2 in [("simple_cnn", {}, 0, 1), ("cifar10_cnn", {}, 2, 3)]:
+        torch.manual_seed(s1)
+        a = ref_models.ModelFactory.create_model(name, **kw).get_model_weights()
+        torch.manual_seed(s2)
+        b = ref_models.ModelFactory.create_model(name, **kw).get_model_weights()
+        res = ConvergenceDetector()._calculate_weight_change_metrics(a, b)
+        out[f"G9/weight_change_{name}"] = {"seeds": [s1, s2], "norm": float(res["norm"]),
+                                           "relative": float(res["relative"])}
+    return out
+
+
 GROUPS = {"g1": lambda: g1(), "g2": lambda: g2(), "g3_g5": lambda: g3_g5(), "g6": lambda: g6(),
-          "g7": lambda: g7(), "g8": lambda: g8()}
+          "g7": lambda: g7(), "g8": lambda: g8(), "g9": lambda: g9()}
 
 
 def main():

@@ -235,3 +235,37 @@ def test_data_ref_transform_known_values():
     u = np.array([[0, 0], [20, 10]], np.float32) / np.float32(255)
     exp = (u - np.float32(0.5)) / np.float32(0.25)
     assert np.array_equal(out[0], exp)
+
+
+def _seeded_weights(name, seed):
+    from src.shared import models_pytorch as hm
+    torch.manual_seed(seed)
+    return hm.ModelFactory.create_model(name).get_model_weights()
+
+
+@pytest.mark.parametrize("name", ["simple_cnn", "cifar10_cnn"])
+def test_g9_weight_change_oracle(name):
+    from oracle import wire_ref
+    g = GOLD[f"G9/weight_change_{name}"]
+    a = {k: v.numpy() for k, v in _seeded_weights(name, g["seeds"][0]).items()}
+    b = {k: v.numpy() for k, v in _seeded_weights(name, g["seeds"][1]).items()}
+    res = wire_ref.weight_change_metrics(a, b)
+    assert res["norm"] == g["norm"] and res["relative"] == g["relative"]
+
+
+def test_g9_packed_edge_serialization_byte_identical():
+    """fedhip.wire (product host code, no GPU needed): a client's weights cut from packed
+    rows serialise to exactly the reference's torch.save bytes (and hex)."""
+    from fedhip import wire
+    from fedhip.net import ParamLayout
+    g = GOLD["G9/serialize_simple_cnn"]
+    w = _seeded_weights("simple_cnn", g["init_seed"])
+    L = ParamLayout.from_module(__import__("src.shared.models_pytorch",
+                                           fromlist=["x"]).ModelFactory.create_model("simple_cnn"))
+    rows = torch.zeros(3, L.P + 64)
+    flat = torch.cat([t.reshape(-1) for t in w.values()])
+    rows[1, :L.P] = flat
+    got = wire.client_weights(rows, L, 1)
+    data = wire.serialize_weights(got)
+    assert hashlib.sha256(data).hexdigest() == g["sha256"]
+    assert hashlib.sha256(data.hex().encode()).hexdigest() == g["hex_sha256"]
