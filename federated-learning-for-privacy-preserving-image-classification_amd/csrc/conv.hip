@@ -453,6 +453,15 @@ static Tile pick_wgrad_tile(int M) {
     return {128, 128, 32, 2};
 }
 
+// Fill fraction (thread-local, fh_set_fill_fraction): the share of the chip one launch
+// should aim to fill when it splits K.  1 = the whole chip (a lone packed lane); a lane
+// that runs concurrently with others (fedhip/lanes.py) asks for less, trading split-K
+// partial slabs and their epilogue launches for longer, fuller workgroups.
+static thread_local float g_fill = 1.0f;
+static int64_t fill(int64_t workgroups) {
+    return std::max<int64_t>(1, (int64_t)((double)workgroups * g_fill));
+}
+
 // Split K so that (tiles x splits) fills the chip, each split keeping >= min_chunks K-steps.
 static void choose_split(int64_t tiles, int K, int bk, int64_t target, int min_chunks, int& splits,
                          int& kchunk) {
@@ -475,7 +484,7 @@ struct Plan {
 static Plan plan_mn(int M, int N, int K, int nclients) {
     Plan p{pick_mn_tile(M, N), 1, K, M, N, K};
     const int64_t tiles = ceil_div(N, p.t.bn) * ceil_div(M, p.t.bm) * (int64_t)nclients;
-    if (tiles < 192) choose_split(tiles, K, p.t.bk, 768, 4, p.splits, p.kchunk);
+    if (tiles < fill(192)) choose_split(tiles, K, p.t.bk, fill(768), 4, p.splits, p.kchunk);
     if (p.splits <= 1) {
         p.splits = 1;
         p.kchunk = K;
@@ -486,7 +495,7 @@ static Plan plan_mn(int M, int N, int K, int nclients) {
 static Plan plan_wgrad(int M, int N, int K, int nclients) {
     Plan p{pick_wgrad_tile(M), 1, K, M, N, K};
     const int64_t tiles = ceil_div(N, p.t.bn) * ceil_div(M, p.t.bm) * (int64_t)nclients;
-    choose_split(tiles, K, p.t.bk, 2048, 4, p.splits, p.kchunk);
+    choose_split(tiles, K, p.t.bk, fill(2048), 4, p.splits, p.kchunk);
     return p;
 }
 
@@ -585,6 +594,7 @@ static const int kDconvBlocks = env_int("FH_DCONV_BLOCKS", 512);
 static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 64);
 static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 256);
 static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 4);
+static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 2);  // tools/tail_sweep.py
 
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
@@ -600,8 +610,8 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
     p.ck = (p.bm == 128 || Cr <= 4) ? 4 : 8;
     const int64_t blocks = tn * ceil_div(M, p.bm) * nclients;
     const int chunks = (int)ceil_div(Cr, p.ck);
-    if (blocks < 512 && chunks > 1) {
-        int want = (int)std::min<int64_t>(ceil_div(1024, blocks), chunks);
+    if (blocks < fill(512) && chunks > 1) {
+        int want = (int)std::min<int64_t>(ceil_div(fill(1024), blocks), chunks);
         const int per = (int)ceil_div(chunks, want);
         p.cchunk = per * p.ck;
         p.splits = (int)ceil_div(Cr, p.cchunk);
@@ -693,8 +703,8 @@ static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     const int64_t tiles = (int64_t)(cout / (32 * p.wco)) * (cin / (32 * p.wci)) * nclients;
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
     // >= 4 stages per split: fewer, longer splits beat a wide slab in the few-client tail
-    const int want = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(kDwgradBlocks, tiles)),
-                                            std::max(1, nst / 4));
+    const int want = (int)std::min<int64_t>(
+        std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks), tiles)), std::max(1, nst / kDwgradMinSps));
     p.sps = (int)ceil_div(nst, want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;
@@ -710,8 +720,8 @@ static DWPlan plan_dwgrad_small(int cout, int batch, int w, int nclients) {
     DWPlan p{1, 1, 4, 128 / w, 1, 1};
     const int64_t tiles = (int64_t)(cout / 32) * nclients;
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
-    const int want = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(kDwgradBlocks, tiles)),
-                                            std::max(1, nst / 4));
+    const int want = (int)std::min<int64_t>(
+        std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks), tiles)), std::max(1, nst / kDwgradMinSps));
     p.sps = (int)ceil_div(nst, want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;
@@ -742,6 +752,14 @@ static int dwgrad_launch_w(const DWPlan& p, dim3 grid, const DWArgs& a, hipStrea
 }  // namespace fh
 
 using namespace fh;
+
+extern "C" int fh_set_fill_fraction(float fraction) {
+    FH_REQUIRE(fraction > 0.f && fraction <= 1.f, "fill fraction must be in (0, 1]");
+    g_fill = fraction;
+    return FH_OK;
+}
+
+extern "C" float fh_get_fill_fraction(void) { return g_fill; }
 
 extern "C" size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
                                           int32_t w_, int32_t cout, int32_t kh, int32_t kw,

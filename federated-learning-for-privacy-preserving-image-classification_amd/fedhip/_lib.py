@@ -78,6 +78,8 @@ SIGNATURES = {
     "fh_dropout_fwd": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I64, I32, F32, U64, P, P]),
     "fh_dropout_bwd": (I32, [P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32, I64, P]),
     "fh_ce_fwd_bwd": (I32, [P, I64, P, I64, P, I64, P, P, P, P, P, P, I32, I32, I32, P]),
+    "fh_set_fill_fraction": (I32, [F32]),
+    "fh_get_fill_fraction": (F32, []),
     "fh_gather_u8": (I32, [P, P, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, P, P, I32,
                            I32, P, P, I64, U64, P, P]),
     "fh_compress_chunk_elems": (I64, []),

@@ -31,6 +31,7 @@ from typing import List, Sequence
 
 import torch
 
+from . import ops
 from .engine import PackedTrainer, SlotStorage, epochs_of, plan_round
 from .net import ParamLayout
 
@@ -111,6 +112,13 @@ class LanedTrainer:
         if len(self.lanes) > 1:
             for ln in self.lanes:
                 ln.stream = torch.cuda.Stream(self.device)
+        # split-K fill fraction per lane (ops.set_fill_fraction); FH_LANE_FILL = one value
+        # for every lane or one per lane (diagnostics)
+        self.fill = [1.0] * len(self.lanes)
+        env_fill = os.environ.get("FH_LANE_FILL")
+        if env_fill and len(self.lanes) > 1:
+            vals = [float(v) for v in env_fill.split(",")]
+            self.fill = vals * len(self.lanes) if len(vals) == 1 else vals
         for name in SlotStorage.FIELDS:
             setattr(self, name, getattr(self.storage, name))
         self.seg_offsets = self.lanes[0].seg_offsets
@@ -185,6 +193,7 @@ class LanedTrainer:
         try:
             if probed:  # the probed lane's first step runs alone on the chip
                 i = probed[0]
+                ops.set_fill_fraction(self.fill[i])
                 with torch.cuda.stream(self.lanes[i].stream):
                     self.lanes[i].issue_step(states[i], 0)
                 for j in order:
@@ -194,9 +203,11 @@ class LanedTrainer:
                 for i in order:
                     ln, st, p = self.lanes[i], states[i], plans[i]
                     if g < p["G"] and not (g == 0 and i in probed):
+                        ops.set_fill_fraction(self.fill[i])
                         with torch.cuda.stream(ln.stream):
                             ln.issue_step(st, g)
         finally:
+            ops.set_fill_fraction(1.0)
             for ln in self.lanes:
                 ln.net.seed_dev = None
                 main.wait_stream(ln.stream)

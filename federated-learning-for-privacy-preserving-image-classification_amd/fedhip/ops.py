@@ -109,9 +109,20 @@ def _ws(device) -> Workspace:
 _WS_SIZE: dict = {}
 
 
+_FILL = [1.0]
+
+
+def set_fill_fraction(fraction: float):
+    """Share of the chip the split-K planners aim to fill for launches from this thread
+    (fh_set_fill_fraction); fedhip/lanes.py sets it per lane before issuing its steps."""
+    if fraction != _FILL[0]:
+        call("fh_set_fill_fraction", float(fraction))
+        _FILL[0] = float(fraction)
+
+
 def _ws_for(fn_name, device, *args):
-    """Scratch for a split-K launch; the size query is cached per shape."""
-    key = (fn_name,) + args
+    """Scratch for a split-K launch; the size query is cached per shape (and fill)."""
+    key = (fn_name, _FILL[0]) + args
     need = _WS_SIZE.get(key)
     if need is None:
         need = _WS_SIZE[key] = getattr(load(), fn_name)(*args)

@@ -270,6 +270,13 @@ int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets, int
                   const int32_t* counts, int32_t nclients, int32_t batch, int32_t num_classes,
                   void* stream);
 
+/* ---------------- launch planning ---------------------------------------------
+ * Share of the chip (0, 1] that the split-K planners of the conv / linear entry points
+ * aim to fill, for launches issued by the CALLING THREAD (thread-local; default 1).
+ * A client lane running concurrently with others asks for less (fedhip/lanes.py). */
+int fh_set_fill_fraction(float fraction);
+float fh_get_fill_fraction(void);
+
 /* ---------------- on-device input pipeline (data_loader.py:298-301, 454-458) -----
  * x[z][b] = Normalize(RandomHorizontalFlip(RandomCrop(data[idx[z][b]], pad)))
  * from raw uint8 HWC images (torchvision layout) to fp32 NCHW: (u/255 - mean_c) /

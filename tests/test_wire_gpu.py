@@ -29,9 +29,10 @@ def test_weight_change_metrics_vs_reference(name):
     _, b = _flat(name, g["seeds"][1])
     seg = torch.tensor(L.seg_offsets(), dtype=torch.int64, device=DEV)
     res = wire.weight_change_metrics(a.to(DEV), b.to(DEV), seg)
-    # per-layer norms agree with torch's fp32 norms to one ulp: 1e-6 relative overall
-    assert abs(res["norm"] - g["norm"]) <= 1e-6 * g["norm"]
-    assert abs(res["relative"] - g["relative"]) <= 1e-6 * g["relative"]
+    # the chip accumulates in fp64; torch's CPU fp32 norm accumulates in fp32 (cascade sum
+    # over up to 1M elements): measured 1.6e-6 relative on SimpleCNN.  Tolerance 1e-5.
+    assert abs(res["norm"] - g["norm"]) <= 1e-5 * g["norm"]
+    assert abs(res["relative"] - g["relative"]) <= 1e-5 * g["relative"]
 
 
 def test_packed_edge_round_trip():
