@@ -595,6 +595,8 @@ static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 64);
 static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 256);
 static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 4);
 static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 2);  // tools/tail_sweep.py
+static const int kDconvForceSplits = env_int("FH_DCONV_SPLITS", 0);  // sweeps: force splits
+static const int kDwgradForceSplits = env_int("FH_DWGRAD_SPLITS", 0);
 
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
@@ -610,8 +612,9 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
     p.ck = (p.bm == 128 || Cr <= 4) ? 4 : 8;
     const int64_t blocks = tn * ceil_div(M, p.bm) * nclients;
     const int chunks = (int)ceil_div(Cr, p.ck);
-    if (blocks < fill(512) && chunks > 1) {
+    if ((kDconvForceSplits > 0 || blocks < fill(512)) && chunks > 1) {
         int want = (int)std::min<int64_t>(ceil_div(fill(1024), blocks), chunks);
+        if (kDconvForceSplits > 0) want = std::min(kDconvForceSplits, chunks);
         const int per = (int)ceil_div(chunks, want);
         p.cchunk = per * p.ck;
         p.splits = (int)ceil_div(Cr, p.cchunk);
@@ -705,7 +708,7 @@ static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     // >= 4 stages per split: fewer, longer splits beat a wide slab in the few-client tail
     const int want = (int)std::min<int64_t>(
         std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks), tiles)), std::max(1, nst / kDwgradMinSps));
-    p.sps = (int)ceil_div(nst, want);
+    p.sps = (int)ceil_div(nst, kDwgradForceSplits > 0 ? std::min(kDwgradForceSplits, nst) : want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;
 }
