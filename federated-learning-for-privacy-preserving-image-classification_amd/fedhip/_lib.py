@@ -80,6 +80,12 @@ SIGNATURES = {
     "fh_ce_fwd_bwd": (I32, [P, I64, P, I64, P, I64, P, P, P, P, P, P, I32, I32, I32, P]),
     "fh_set_fill_fraction": (I32, [F32]),
     "fh_get_fill_fraction": (F32, []),
+    "fh_stream_create": (I32, [I32, P, I32, P]),
+    "fh_stream_destroy": (I32, [P]),
+    "fh_program_from_graph": (I32, [P, P, P]),
+    "fh_program_launch": (I32, [P, P]),
+    "fh_program_destroy": (I32, [P]),
+    "fh_copy_bytes": (I32, [P, P, I64, P]),
     "fh_gather_u8": (I32, [P, P, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, P, P, I32,
                            I32, P, P, I64, U64, P, P]),
     "fh_compress_chunk_elems": (I64, []),

@@ -25,8 +25,10 @@ on MI355X for CIFAR10CNN; at most 4 lanes (GPU_MAX_HW_QUEUES is 4).
 """
 from __future__ import annotations
 
+import ctypes
 import itertools
 import os
+import time
 from typing import List, Sequence
 
 import torch
@@ -109,9 +111,11 @@ class LanedTrainer:
         self.lanes = [PackedTrainer(model, cut[i + 1] - cut[i], batch, self.device,
                                     storage=self.storage, row0=cut[i])
                       for i in range(len(cut) - 1)]
+        self._own_streams = []
         if len(self.lanes) > 1:
-            for ln in self.lanes:
-                ln.stream = torch.cuda.Stream(self.device)
+            for i, ln in enumerate(self.lanes):
+                ln.stream = self._lane_stream(i)
+                ln.launch_mode = "program"  # csrc/program.hip: +1.3 % over graph replay
         # split-K fill fraction per lane (ops.set_fill_fraction); FH_LANE_FILL = one value
         # for every lane or one per lane (diagnostics)
         self.fill = [1.0] * len(self.lanes)
@@ -123,6 +127,40 @@ class LanedTrainer:
             setattr(self, name, getattr(self.storage, name))
         self.seg_offsets = self.lanes[0].seg_offsets
         self.net = self.lanes[0].net
+
+    def _lane_stream(self, i):
+        """HIP stream of lane i.  Diagnostics: FH_LANE_PRIO = per-lane dispatch priorities
+        (e.g. "-1,0,0"); FH_LANE_CU = CUs reserved for lane 0 (the others get the rest),
+        FH_LANE_CU_LAYOUT = "spread" (every k-th mask bit) or "block" (the first bits)."""
+        prio_env = os.environ.get("FH_LANE_PRIO")
+        cu_env = os.environ.get("FH_LANE_CU")
+        if not cu_env:  # torch-owned stream; the long lane 0 dispatches first by default
+            prios = [int(v) for v in prio_env.split(",")] if prio_env else [-1, 0]
+            return torch.cuda.Stream(self.device, priority=prios[min(i, len(prios) - 1)])
+        mask_words = None
+        prio = 0
+        if cu_env:
+            ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+            k = int(cu_env)
+            if os.environ.get("FH_LANE_CU_LAYOUT", "spread") == "block":
+                mine = set(range(k))
+            else:
+                step = ncu / k
+                mine = {int(j * step) for j in range(k)}
+            bits = mine if i == 0 else set(range(ncu)) - mine
+            words = [0] * ((ncu + 31) // 32)
+            for b in bits:
+                words[b // 32] |= 1 << (b % 32)
+            mask_words = (ctypes.c_uint32 * len(words))(*words)
+        if prio_env:
+            vals = [int(v) for v in prio_env.split(",")]
+            prio = vals[i] if i < len(vals) else vals[-1]
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            ops.call("fh_stream_create", prio, mask_words,
+                     len(mask_words) if mask_words is not None else 0, ctypes.byref(handle))
+        self._own_streams.append(handle.value)
+        return torch.cuda.ExternalStream(handle.value, device=self.device)
 
     # PackedTrainer surface used by RankRound / bench
     @property
@@ -199,13 +237,48 @@ class LanedTrainer:
                 for j in order:
                     if j != i:
                         self.lanes[j].stream.wait_stream(self.lanes[i].stream)
+            tlog = [] if os.environ.get("FH_HOST_TIMING") else None
             for g in range(G):
                 for i in order:
                     ln, st, p = self.lanes[i], states[i], plans[i]
                     if g < p["G"] and not (g == 0 and i in probed):
                         ops.set_fill_fraction(self.fill[i])
+                        t0 = time.perf_counter() if tlog is not None else 0
                         with torch.cuda.stream(ln.stream):
                             ln.issue_step(st, g)
+                        if tlog is not None:
+                            ev = torch.cuda.Event(enable_timing=True)
+                            ev.record(ln.stream)
+                            tlog.append((g, i, t0, time.perf_counter(), ev))
+            if tlog:
+                import sys
+                torch.cuda.synchronize(self.device)
+                T = tlog[0][2]
+                e0 = tlog[0][4]
+                done = {}
+                for g, i, a, b, ev in tlog:
+                    done.setdefault(i, []).append(e0.elapsed_time(ev))
+                for i, v in done.items():
+                    print(f"lane{i} GPU step ends (ms, every 8th): "
+                          + " ".join(f"{x:.1f}" for x in v[::8]) + f" | last {v[-1]:.1f}",
+                          file=sys.stderr)
+                host = {}
+                for g, i, a, b, ev in tlog:
+                    host.setdefault(i, []).append((b - T) * 1e3)
+                for i, v in host.items():
+                    print(f"lane{i} host issue ends (ms, every 8th): "
+                          + " ".join(f"{x:.1f}" for x in v[::8]), file=sys.stderr)
+                per = {}
+                for g, i, a, b, ev in tlog:
+                    per.setdefault(i, []).append(b - a)
+                print("host issue: " + ", ".join(
+                    f"lane{i} n{len(v)} tot {sum(v)*1e3:.1f}ms max {max(v)*1e3:.2f}ms"
+                    for i, v in per.items()) + f", loop {(tlog[-1][3]-T)*1e3:.1f}ms",
+                    file=sys.stderr)
+                slow = sorted(tlog, key=lambda r: r[2] - r[3])[:5]
+                for g, i, a, b, _ in slow:
+                    print(f"   slow issue g{g} lane{i} {1e3*(b-a):.2f}ms at {1e3*(a-T):.1f}ms",
+                          file=sys.stderr)
         finally:
             ops.set_fill_fraction(1.0)
             for ln in self.lanes:

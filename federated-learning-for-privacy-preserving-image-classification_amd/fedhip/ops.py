@@ -109,6 +109,41 @@ def _ws(device) -> Workspace:
 _WS_SIZE: dict = {}
 
 
+def copy_bytes(src: torch.Tensor, dst: torch.Tensor):
+    """dst <- src (same byte size, contiguous, 16-B multiple) by fh_copy_bytes on the
+    current stream."""
+    nb = src.numel() * src.element_size()
+    if nb != dst.numel() * dst.element_size() or not (src.is_contiguous() and dst.is_contiguous()):
+        raise FedHipError("copy_bytes: size/layout mismatch")
+    call("fh_copy_bytes", ptr(src), ptr(dst), nb, stream_handle(dst.device))
+
+
+class Program:
+    """A captured step as a flat kernel list (csrc/program.hip): built once from a
+    torch.cuda.CUDAGraph(keep_graph=True), launched with hipLaunchKernel on any stream.
+    Keeps the graph (it owns the kernel argument storage) alive."""
+
+    def __init__(self, graph, handle, kernels):
+        self.graph, self.handle, self.kernels = graph, handle, kernels
+
+    @classmethod
+    def from_graph(cls, graph):
+        h, nk = ctypes.c_void_p(), ctypes.c_int32()
+        call("fh_program_from_graph", graph.raw_cuda_graph(), ctypes.byref(h), ctypes.byref(nk))
+        return cls(graph, h.value, nk.value)
+
+    def launch(self, stream):
+        call("fh_program_launch", self.handle, stream.cuda_stream)
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            try:
+                call("fh_program_destroy", self.handle)
+            except Exception:
+                pass
+            self.handle = None
+
+
 _FILL = [1.0]
 
 

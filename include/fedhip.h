@@ -277,6 +277,27 @@ int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets, int
 int fh_set_fill_fraction(float fraction);
 float fh_get_fill_fraction(void);
 
+/* Lane streams (fedhip/lanes.py; replaces the reference's one-thread-per-client
+ * concurrency, federated_simulation.py:309-318).  cu_mask (nullable; mask_words 32-bit
+ * words, bit i = CU i) restricts the stream to those CUs (hipExtStreamCreateWithCUMask);
+ * otherwise the stream gets dispatch priority `priority` (lower = higher, HIP's range).
+ * *stream_out is a hipStream_t; release it with fh_stream_destroy. */
+int fh_stream_create(int32_t priority, const uint32_t* cu_mask, int32_t mask_words,
+                     void** stream_out);
+int fh_stream_destroy(void* stream);
+
+/* Step programs (csrc/program.hip; replaces torch.cuda.CUDAGraph.replay for concurrent
+ * lanes: +1.3 % on KT).  A captured
+ * hipGraph_t's kernel / memset / memcpy nodes in dependency order become a launch list;
+ * fh_program_launch issues it on `stream` (hipLaunchKernel etc.).  The graph must
+ * outlive the program (it owns the kernel argument storage). */
+int fh_program_from_graph(void* graph, void** program_out, int32_t* kernels_out);
+int fh_program_launch(void* program, void* stream);
+int fh_program_destroy(void* program);
+/* dst[0:nbytes) = src[0:nbytes) by a kernel (16-B aligned, nbytes % 16 == 0): the per-step
+ * input row copy of a lane in program mode. */
+int fh_copy_bytes(const void* src, void* dst, int64_t nbytes, void* stream);
+
 /* ---------------- on-device input pipeline (data_loader.py:298-301, 454-458) -----
  * x[z][b] = Normalize(RandomHorizontalFlip(RandomCrop(data[idx[z][b]], pad)))
  * from raw uint8 HWC images (torchvision layout) to fp32 NCHW: (u/255 - mean_c) /
