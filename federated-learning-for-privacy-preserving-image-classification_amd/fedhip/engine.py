@@ -406,20 +406,25 @@ def plan_round(shard_sizes, epochs, batch, generator=None):
         raise FedHipError("slots must be ordered by descending step count")
     T = [epochs * s for s in steps]
     G = T[0] if S else 0
-    counts = torch.zeros(G, S, dtype=torch.int32)
-    reset = torch.zeros(G, S, dtype=torch.int32)
-    index = torch.zeros(G, S, B, dtype=torch.int64)
+    counts = np.zeros((G, S), dtype=np.int32)
+    reset = np.zeros((G, S), dtype=np.int32)
+    index = np.zeros((G, S, B), dtype=np.int64)
     for k, n in enumerate(shard_sizes):
+        st = steps[k]
         for e in range(epochs):
-            perm = torch.randperm(n, generator=generator)
-            for s in range(steps[k]):
-                g = e * steps[k] + s
-                chunk = perm[s * B:(s + 1) * B]
-                counts[g, k] = chunk.numel()
-                reset[g, k] = 1 if s == 0 else 0
-                index[g, k, :chunk.numel()] = chunk
-    active = [sum(1 for t in T if t > g) for g in range(G)]
-    return dict(G=G, steps=steps, T=T, active=active, counts=counts, reset=reset, index=index)
+            perm = torch.randperm(n, generator=generator)  # drawn even for n == 0
+            if not st:
+                continue
+            g0 = e * st
+            blk = np.zeros(st * B, dtype=np.int64)
+            blk[:n] = perm.numpy()
+            index[g0:g0 + st, k, :] = blk.reshape(st, B)  # batch s = perm[s*B:(s+1)*B]
+            counts[g0:g0 + st, k] = B
+            counts[g0 + st - 1, k] = n - (st - 1) * B
+            reset[g0, k] = 1
+    active = (np.asarray(T, dtype=np.int64)[None, :] > np.arange(G)[:, None]).sum(1).tolist()
+    return dict(G=G, steps=steps, T=T, active=active, counts=torch.from_numpy(counts),
+                reset=torch.from_numpy(reset), index=torch.from_numpy(index))
 
 
 def epochs_of(plan):

@@ -217,6 +217,7 @@ class LanedTrainer:
         if len(self.lanes) == 1:
             return self.lanes[0].run_round(data, labels, shard_offsets, plans[0],
                                            optimizer_type, lr, seed)
+        t_r0 = time.perf_counter()
         main = torch.cuda.current_stream(self.device)
         states = []
         for i, ln in enumerate(self.lanes):
@@ -284,7 +285,12 @@ class LanedTrainer:
             for ln in self.lanes:
                 ln.net.seed_dev = None
                 main.wait_stream(ln.stream)
+        t_c = time.perf_counter()
         out = []
         for ln, p in zip(self.lanes, plans):
             out += ln.collect_metrics(p, epochs_of(p))
+        if os.environ.get("FH_HOST_TIMING"):
+            import sys
+            print(f"start_rounds+issue {1e3 * (t_c - t_r0):.1f} ms, collect (sync) "
+                  f"{1e3 * (time.perf_counter() - t_c):.1f} ms", file=sys.stderr)
         return out

@@ -17,6 +17,9 @@ reference's sequential loop, bit for bit.
 from __future__ import annotations
 
 import math
+import os
+import sys
+import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -25,6 +28,9 @@ import torch.distributed as dist
 
 from . import ops
 from .lanes import LanedTrainer
+
+
+_HOST_TIMING = bool(os.environ.get("FH_HOST_TIMING"))  # diagnostics: per-round host split
 
 
 @dataclass
@@ -92,11 +98,16 @@ class RankRound:
         """One round. data/labels: this rank's train shards, slot k's at slot_offsets[k]."""
         tr = self.trainer
         S = len(self.slots)
+        _t = [time.perf_counter()] if _HOST_TIMING else None
         tr.params[:S, :self.P].copy_(self.global_flat.expand(S, -1))  # all start from global
         sizes = [self.all_sizes[k] for k in self.slots]
         plan = tr.make_plan(sizes, self.epochs, generator=generator)
+        if _t:
+            _t.append(time.perf_counter())
         metrics = tr.run_round(data, labels, slot_offsets, plan, optimizer_type=optimizer_type,
                                lr=lr, seed=seed)
+        if _t:
+            _t.append(time.perf_counter())
         if self.dp is not None:
             self._apply_dp(S, seed)
         if self.compression is not None:
@@ -115,6 +126,11 @@ class RankRound:
             if distributed:
                 dist.all_reduce(self.global_bufs, op=dist.ReduceOp.SUM, group=self.group)
         self.round_index += 1
+        if _t:
+            torch.cuda.synchronize(self.device)
+            _t.append(time.perf_counter())
+            print("round host ms: plan %.1f, run_round %.1f, dp/fedavg+sync %.1f" % tuple(
+                1e3 * (b - a) for a, b in zip(_t, _t[1:])), file=sys.stderr)
         return metrics
 
     def evaluate(self, data, labels, template_model=None):

@@ -158,3 +158,37 @@ def test_lane_planner_cuts():
     for steps in ([50, 10], [50, 10, 9], [9, 8, 3, 3, 2, 1, 1]):
         c = plan_lanes(steps)
         assert c[0] == 0 and c[-1] == len(steps) and c == sorted(set(c))
+
+
+def _plan_round_loop(shard_sizes, epochs, B, generator):
+    """The per-step loop form of plan_round (its first implementation): the vectorised
+    plan must reproduce it exactly, randperm draws included."""
+    S = len(shard_sizes)
+    steps = [math.ceil(n / B) for n in shard_sizes]
+    T = [epochs * s for s in steps]
+    G = T[0] if S else 0
+    counts = torch.zeros(G, S, dtype=torch.int32)
+    reset = torch.zeros(G, S, dtype=torch.int32)
+    index = torch.zeros(G, S, B, dtype=torch.int64)
+    for k, n in enumerate(shard_sizes):
+        for e in range(epochs):
+            perm = torch.randperm(n, generator=generator)
+            for s in range(steps[k]):
+                g = e * steps[k] + s
+                chunk = perm[s * B:(s + 1) * B]
+                counts[g, k] = chunk.numel()
+                reset[g, k] = 1 if s == 0 else 0
+                index[g, k, :chunk.numel()] = chunk
+    active = [sum(1 for t in T if t > g) for g in range(G)]
+    return dict(G=G, steps=steps, T=T, active=active, counts=counts, reset=reset, index=index)
+
+
+@pytest.mark.parametrize("epochs", [1, 2])
+def test_plan_round_matches_loop_form(epochs):
+    sizes = [1875, 960, 300, 64, 33, 32, 31, 1, 0]
+    a = plan_round(sizes, epochs, 32, torch.Generator().manual_seed(5))
+    b = _plan_round_loop(sizes, epochs, 32, torch.Generator().manual_seed(5))
+    assert a["G"] == b["G"] and a["steps"] == b["steps"] and a["T"] == b["T"]
+    assert a["active"] == b["active"]
+    for key in ("counts", "reset", "index"):
+        assert a[key].dtype == b[key].dtype and torch.equal(a[key], b[key]), key
