@@ -171,6 +171,38 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const BNArgs a) {
     });
 }
 
+// Train-mode statistics without the apply pass: per (client, channel) the merged moments
+// become save_mean / save_invstd, the running-stat update, and the affine the consumer
+// applies on load (scale = invstd*w, shift = b - mean*scale: bn_apply_kernel's alpha and
+// beta', same operations, so relu(x*scale + shift) is bit-identical to its output).
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const BNArgs a, float* scale,
+                                                          float* shift, int64_t s_cs) {
+    const int c = blockIdx.x * 256 + threadIdx.x, z = blockIdx.y;
+    if (c >= a.C) return;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int64_t n = (int64_t)cnt * a.HW;
+    double sum, sq;
+    merge(a, z, c, sum, sq);
+    const double mean = n > 0 ? sum / (double)n : 0.0;
+    double var = n > 0 ? sq / (double)n - mean * mean : 0.0;
+    if (var < 0.0) var = 0.0;
+    const double invstd = n > 0 ? 1.0 / sqrt(var + (double)a.eps) : 0.0;
+    const float meanf = (float)mean, invstdf = (float)invstd;
+    a.save_mean[z * a.C + c] = meanf;
+    a.save_invstd[z * a.C + c] = invstdf;
+    if (a.rmean && n > 0) {
+        const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+        float* rm = a.rmean + z * a.r_cs + c;
+        float* rv = a.rvar + z * a.r_cs + c;
+        *rm = (float)((double)a.momentum * mean + (1.0 - (double)a.momentum) * (double)*rm);
+        *rv = (float)((double)a.momentum * unb + (1.0 - (double)a.momentum) * (double)*rv);
+    }
+    const float alpha = invstdf * a.gamma[z * a.p_cs + c];
+    const float bconst = a.beta[z * a.p_cs + c] - meanf * alpha;
+    scale[z * s_cs + c] = alpha;
+    shift[z * s_cs + c] = bconst;
+}
+
 // eval mode: running statistics (LocalTrainer._validate_epoch / evaluate_model)
 __global__ void __launch_bounds__(256) bn_eval_kernel(const BNArgs a) {
     const int s = blockIdx.x, c = blockIdx.y, z = blockIdx.z;
@@ -390,6 +422,35 @@ extern "C" int fh_bn_fwd_train(const float* x, int64_t x_cs, float* y, int64_t y
     FH_LAUNCH_CHECK("bn_fwd_train stats");
     hipLaunchKernelGGL(bn_apply_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_fwd_train apply");
+    return FH_OK;
+}
+
+extern "C" int fh_bn_fwd_stats(const float* x, int64_t x_cs, const float* gamma,
+                               const float* beta, int64_t p_cs, float* running_mean,
+                               float* running_var, int64_t r_cs, float* save_mean,
+                               float* save_invstd, float* scale_out, float* shift_out,
+                               int64_t s_cs, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t C, int32_t HW, float eps, float momentum,
+                               void* workspace, size_t ws_bytes, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_stats: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && gamma && beta && save_mean && save_invstd && scale_out && shift_out,
+               "bn_fwd_stats: null pointer");
+    FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "bn_fwd_stats: running stats");
+    const size_t need = fh_bn_workspace(nclients, batch, C, HW);
+    FH_REQUIRE(workspace && ws_bytes >= need, "bn_fwd_stats: workspace %zu < %zu", ws_bytes, need);
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.x = x; a.gamma = gamma; a.beta = beta;
+    a.rmean = running_mean; a.rvar = running_var; a.save_mean = save_mean;
+    a.save_invstd = save_invstd; a.part = (double*)workspace;
+    a.x_cs = x_cs; a.p_cs = p_cs; a.r_cs = r_cs;
+    a.eps = eps; a.momentum = momentum;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(a.S, C, nclients), dim3(256), 0, st, a);
+    FH_LAUNCH_CHECK("bn_fwd_stats stats");
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 256), nclients), dim3(256), 0,
+                       st, a, scale_out, shift_out, s_cs);
+    FH_LAUNCH_CHECK("bn_fwd_stats finalize");
     return FH_OK;
 }
 

@@ -786,24 +786,31 @@ extern "C" size_t fh_conv2d_dgrad_workspace(int32_t nclients, int32_t batch, int
     return mn_ws_bytes(plan_mn(cin, batch * h * w_, cout * kh * kw, nclients), nclients);
 }
 
-extern "C" int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
-                             const float* bias, int64_t b_cs, float* y, int64_t y_cs,
-                             const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
-                             int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
-                             int32_t stride, int32_t pad, int32_t relu, void* workspace,
-                             size_t ws_bytes, void* stream) {
+static int conv2d_fwd_impl(const float* x, int64_t x_cs, const float* in_scale,
+                           const float* in_shift, int64_t aff_cs, const float* w, int64_t w_cs,
+                           const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                           const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
+                           int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
+                           int32_t stride, int32_t pad, int32_t relu, void* workspace,
+                           size_t ws_bytes, void* stream) {
     int oh, ow;
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
     if (rc) return rc;
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && w && y, "conv2d_fwd: null pointer");
+    FH_REQUIRE((in_scale == nullptr) == (in_shift == nullptr), "conv2d_fwd: scale/shift pair");
     if (dconv_supported(h, w_, kh, kw, stride, pad)) {
         DConvArgs d{};
         d.in = x; d.wt = w; d.bias = bias; d.out = y;
         d.in_cs = x_cs; d.w_cs = w_cs; d.b_cs = b_cs; d.out_cs = y_cs;
         d.counts = counts; d.batch = batch; d.Cr = cin; d.M = cout; d.relu = relu;
+        d.in_scale = in_scale; d.in_shift = in_shift; d.aff_cs = aff_cs;
         return run_dconv<OP_FWD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
                                  "conv2d_fwd");
+    }
+    if (in_scale) {
+        set_error("conv2d_fwd_bnrelu: needs the direct 3x3 path (3x3/s1/p1, square 8/16/32)");
+        return FH_E_UNSUPPORTED;
     }
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
     a.x = x; a.wt = w; a.bias = bias; a.out = y;
@@ -812,6 +819,31 @@ extern "C" int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64
     a.M = cout; a.N = batch * oh * ow; a.K = cin * kh * kw;
     return run_mn<OP_FWD>(a, kh, kw, stride, nclients, workspace, ws_bytes, y, y_cs, bias, b_cs,
                           relu, 0, oh * ow, as_stream(stream), "conv2d_fwd");
+}
+
+extern "C" int fh_conv2d_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                             const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                             const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
+                             int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
+                             int32_t stride, int32_t pad, int32_t relu, void* workspace,
+                             size_t ws_bytes, void* stream) {
+    return conv2d_fwd_impl(x, x_cs, nullptr, nullptr, 0, w, w_cs, bias, b_cs, y, y_cs, counts,
+                           nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, relu, workspace,
+                           ws_bytes, stream);
+}
+
+extern "C" int fh_conv2d_fwd_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
+                                    const float* in_shift, int64_t aff_cs, const float* w,
+                                    int64_t w_cs, const float* bias, int64_t b_cs, float* y,
+                                    int64_t y_cs, const int32_t* counts, int32_t nclients,
+                                    int32_t batch, int32_t cin, int32_t h, int32_t w_,
+                                    int32_t cout, int32_t kh, int32_t kw, int32_t stride,
+                                    int32_t pad, int32_t relu, void* workspace, size_t ws_bytes,
+                                    void* stream) {
+    FH_REQUIRE(in_scale && in_shift, "conv2d_fwd_bnrelu: null scale/shift");
+    return conv2d_fwd_impl(x, x_cs, in_scale, in_shift, aff_cs, w, w_cs, bias, b_cs, y, y_cs,
+                           counts, nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, relu,
+                           workspace, ws_bytes, stream);
 }
 
 extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
@@ -856,22 +888,29 @@ extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int
                                            nclients));
 }
 
-extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
-                               float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
-                               size_t ws_bytes, const int32_t* counts, int32_t nclients,
-                               int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
-                               int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream) {
+static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale,
+                             const float* in_shift, int64_t aff_cs, const float* dy,
+                             int64_t dy_cs, float* dw, int64_t dw_cs, float* db, int64_t db_cs,
+                             void* workspace, size_t ws_bytes, const int32_t* counts,
+                             int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
+                             int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad,
+                             void* stream) {
     int oh, ow;
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
     if (rc) return rc;
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && dy && dw, "conv2d_wgrad: null pointer");
+    FH_REQUIRE((in_scale == nullptr) == (in_shift == nullptr), "conv2d_wgrad: scale/shift pair");
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
     a.x = x; a.dy = dy;
     a.x_cs = x_cs; a.dy_cs = dy_cs;
     a.M = cout; a.N = cin * kh * kw; a.K = batch * oh * ow;
     const bool aligned = ((uintptr_t)x % 16 == 0) && ((uintptr_t)dy % 16 == 0) && x_cs % 4 == 0 &&
                          dy_cs % 4 == 0;
+    if (in_scale && !(aligned && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad))) {
+        set_error("conv2d_wgrad_bnrelu: needs the direct 3x3 wgrad (16-B aligned, channels %% 32)");
+        return FH_E_UNSUPPORTED;
+    }
     if (aligned && dwgrad_small_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
         const DWPlan p = plan_dwgrad_small(cout, batch, w_, nclients);
         const size_t need = dwgrad_ws_bytes(p, nclients, a.M, a.N);
@@ -906,6 +945,7 @@ extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, in
         d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
         d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
         d.splits = p.splits; d.stages_per_split = p.sps;
+        d.in_scale = in_scale; d.in_shift = in_shift; d.aff_cs = aff_cs;
         d.part = (float*)workspace;
         const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
         d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
@@ -960,6 +1000,29 @@ extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, in
                        (const float*)a.bias_part, db, db_cs, a.M);
     FH_LAUNCH_CHECK("conv2d_wgrad reduce");
     return FH_OK;
+}
+
+extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                               float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
+                               size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                               int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                               int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream) {
+    return conv2d_wgrad_impl(x, x_cs, nullptr, nullptr, 0, dy, dy_cs, dw, dw_cs, db, db_cs,
+                             workspace, ws_bytes, counts, nclients, batch, cin, h, w_, cout, kh,
+                             kw, stride, pad, stream);
+}
+
+extern "C" int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
+                                      const float* in_shift, int64_t aff_cs, const float* dy,
+                                      int64_t dy_cs, float* dw, int64_t dw_cs, float* db,
+                                      int64_t db_cs, void* workspace, size_t ws_bytes,
+                                      const int32_t* counts, int32_t nclients, int32_t batch,
+                                      int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh,
+                                      int32_t kw, int32_t stride, int32_t pad, void* stream) {
+    FH_REQUIRE(in_scale && in_shift, "conv2d_wgrad_bnrelu: null scale/shift");
+    return conv2d_wgrad_impl(x, x_cs, in_scale, in_shift, aff_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
+                             workspace, ws_bytes, counts, nclients, batch, cin, h, w_, cout, kh,
+                             kw, stride, pad, stream);
 }
 
 // ---- linear layers: a 1x1 convolution over a 1x1 image -------------------

@@ -36,7 +36,22 @@ struct DConvArgs {
     int splits, cchunk;  // reduction channels per split (multiple of CK)
     int Nfull;           // batch * H * W (slab row length)
     int wvec;            // host: weight slices 16-B aligned -> float4 staging instance
+    // FWD only, nullable: the input is a BatchNorm's pre-activation and the kernel stages
+    // relu(x * in_scale[z][c] + in_shift[z][c]) — the BN apply + ReLU done on load
+    const float* in_scale;
+    const float* in_shift;
+    int64_t aff_cs;
 };
+
+// BatchNorm apply + ReLU on a staged float4 of channel c (bn.hip bn_apply_kernel's exact
+// fp32 operations: x * alpha + beta', then max(., 0); contraction is off in this build)
+__device__ __forceinline__ float4 bn_relu4(float4 v, float s, float t) {
+    v.x = fmaxf(v.x * s + t, 0.f);
+    v.y = fmaxf(v.y * s + t, 0.f);
+    v.z = fmaxf(v.z * s + t, 0.f);
+    v.w = fmaxf(v.w * s + t, 0.f);
+    return v;
+}
 
 template <int W>
 struct DGeom {
@@ -96,6 +111,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     constexpr bool wvec = WVEC;  // scalar weight staging (costly in VGPRs) only when needed
 
     float4 rp[NPT], ra[NAV];
+    float bsc[NPT], bsh[NPT];  // BN affine of each staged row (in_scale set)
     auto load = [&](int c0) {
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
@@ -107,6 +123,10 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
             rp[i] = ok ? *reinterpret_cast<const float4*>(
                              inz + ((int64_t)(img * a.Cr + c0 + cl) * G::H + y) * W + px)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (OP == OP_FWD && a.in_scale != nullptr) {  // applied in store(): the loads
+                bsc[i] = ok ? a.in_scale[z * a.aff_cs + c0 + cl] : 1.f;  // stay in flight over
+                bsh[i] = ok ? a.in_shift[z * a.aff_cs + c0 + cl] : 0.f;  // the MFMA loop;
+            }                                                // padding: relu(0*1+0) = 0
         }
         if constexpr (wvec) {
 #pragma unroll
@@ -155,6 +175,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
         for (int i = 0; i < NPT; ++i) {
             const int q = prt + i * RPI;
             if (q < NPR) {
+                if (OP == OP_FWD && a.in_scale != nullptr) rp[i] = bn_relu4(rp[i], bsc[i], bsh[i]);
                 float* d = &Ps[buf][(q / G::PR) * G::CSTR + (q % G::PR) * G::PW + 1 + px];
                 d[0] = rp[i].x;
                 d[1] = rp[i].y;
@@ -325,6 +346,10 @@ struct DWArgs {
     const int32_t* counts;
     int batch, cin, M, N;  // M = cout, N = cin*9
     int splits, stages_per_split;
+    // nullable: x is a BatchNorm pre-activation, staged as relu(x * scale + shift)
+    const float* in_scale;
+    const float* in_shift;
+    int64_t aff_cs;
 };
 
 template <int W, int WCO, int WCI, int WPX, int SR>
@@ -372,6 +397,7 @@ __global__ void __launch_bounds__(256) dconv_wgrad_kernel(const DWArgs a) {
     const int dco = tid / DQ, dp = (tid % DQ) * 4;      // dY: channel row, pixel quad
     const int prt = tid / PQ, px = (tid % PQ) * 4;       // patch: row, column quad
     float4 rd[NDY], rp[NPT];
+    float bsc[NPT], bsh[NPT];  // BN affine of each staged X row (in_scale set)
     auto load = [&](int st) {
         const int R0 = st * SR;
         {
@@ -394,6 +420,10 @@ __global__ void __launch_bounds__(256) dconv_wgrad_kernel(const DWArgs a) {
             rp[i] = ok ? *reinterpret_cast<const float4*>(
                              xz + ((int64_t)(img * a.cin + ci0 + cl) * H + y) * W + px)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.in_scale != nullptr) {  // applied in store() (loads stay in flight)
+                bsc[i] = ok ? a.in_scale[z * a.aff_cs + ci0 + cl] : 1.f;
+                bsh[i] = ok ? a.in_shift[z * a.aff_cs + ci0 + cl] : 0.f;
+            }
         }
     };
     auto store = [&](int bsel) {
@@ -411,6 +441,7 @@ __global__ void __launch_bounds__(256) dconv_wgrad_kernel(const DWArgs a) {
         for (int i = 0; i < NPT; ++i) {
             const int q = prt + i * RPI;
             if (q < NPR) {
+                if (a.in_scale != nullptr) rp[i] = bn_relu4(rp[i], bsc[i], bsh[i]);
                 float* d = P + (q / PR) * CSTR + (q % PR) * PW + 1 + px;
                 d[0] = rp[i].x;
                 d[1] = rp[i].y;

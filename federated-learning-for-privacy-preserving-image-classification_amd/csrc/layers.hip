@@ -25,7 +25,9 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
                     int64_t y_cs, uint8_t* __restrict__ idx, int64_t i_cs,
                     uint8_t* __restrict__ mask, int64_t m_cs, const int32_t* __restrict__ counts,
                     int batch, int C, int H, int W, int drop_mode, float keep_prob, float scale,
-                    uint64_t seed_salt, const uint64_t* __restrict__ seed_dev) {
+                    uint64_t seed_salt, const uint64_t* __restrict__ seed_dev,
+                    const float* __restrict__ in_scale, const float* __restrict__ in_shift,
+                    int64_t aff_cs) {
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
@@ -40,11 +42,20 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
         const int oh = (int)(t % OH);
         const int64_t plane = t / OH;  // img*C + c
         const float* p = xb + plane * H * W + (2 * oh) * W + 2 * ow;
-        float m = p[0];
+        float v0 = p[0], v1 = p[1], v2 = p[W], v3 = p[W + 1];
+        if (in_scale) {  // input = BN pre-activation: relu(x*scale + shift), bn_apply's ops
+            const int c = (int)(plane % C);
+            const float s = in_scale[z * aff_cs + c], t = in_shift[z * aff_cs + c];
+            v0 = fmaxf(v0 * s + t, 0.f);
+            v1 = fmaxf(v1 * s + t, 0.f);
+            v2 = fmaxf(v2 * s + t, 0.f);
+            v3 = fmaxf(v3 * s + t, 0.f);
+        }
+        float m = v0;
         int a = 0;
-        if (p[1] > m) { m = p[1]; a = 1; }
-        if (p[W] > m) { m = p[W]; a = 2; }
-        if (p[W + 1] > m) { m = p[W + 1]; a = 3; }
+        if (v1 > m) { m = v1; a = 1; }
+        if (v2 > m) { m = v2; a = 2; }
+        if (v3 > m) { m = v3; a = 3; }
         idx[z * i_cs + e] = (uint8_t)a;
         if (drop_mode) {
             uint8_t keep;
@@ -371,11 +382,12 @@ static int ew_grid(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(
 
 using namespace fh;
 
-extern "C" int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
-                               int64_t i_cs, uint8_t* mask, int64_t m_cs, const int32_t* counts,
-                               int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
-                               int32_t drop_mode, float p_drop, uint64_t seed,
-                               const uint64_t* seed_dev, void* stream) {
+static int maxpool2_fwd_impl(const float* x, int64_t x_cs, const float* in_scale,
+                             const float* in_shift, int64_t aff_cs, float* y, int64_t y_cs,
+                             uint8_t* idx, int64_t i_cs, uint8_t* mask, int64_t m_cs,
+                             const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
+                             int32_t H, int32_t W, int32_t drop_mode, float p_drop, uint64_t seed,
+                             const uint64_t* seed_dev, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2, "maxpool2_fwd: bad shape");
     FH_REQUIRE((H % 2) == 0 && (W % 2) == 0, "maxpool2_fwd: odd spatial size %dx%d", H, W);
     FH_REQUIRE(drop_mode >= 0 && drop_mode <= 2 && (drop_mode == 0 || mask), "maxpool2_fwd: mask");
@@ -386,9 +398,31 @@ extern "C" int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y
     const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
     hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
                        as_stream(stream), x, x_cs, y, y_cs, idx, i_cs, mask, m_cs, counts, batch, C,
-                       H, W, drop_mode, keep, scale, seed, seed_dev);
+                       H, W, drop_mode, keep, scale, seed, seed_dev, in_scale, in_shift, aff_cs);
     FH_LAUNCH_CHECK("maxpool2_fwd");
     return FH_OK;
+}
+
+extern "C" int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
+                               int64_t i_cs, uint8_t* mask, int64_t m_cs, const int32_t* counts,
+                               int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                               int32_t drop_mode, float p_drop, uint64_t seed,
+                               const uint64_t* seed_dev, void* stream) {
+    return maxpool2_fwd_impl(x, x_cs, nullptr, nullptr, 0, y, y_cs, idx, i_cs, mask, m_cs, counts,
+                             nclients, batch, C, H, W, drop_mode, p_drop, seed, seed_dev, stream);
+}
+
+extern "C" int fh_maxpool2_fwd_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
+                                      const float* in_shift, int64_t aff_cs, float* y,
+                                      int64_t y_cs, uint8_t* idx, int64_t i_cs, uint8_t* mask,
+                                      int64_t m_cs, const int32_t* counts, int32_t nclients,
+                                      int32_t batch, int32_t C, int32_t H, int32_t W,
+                                      int32_t drop_mode, float p_drop, uint64_t seed,
+                                      const uint64_t* seed_dev, void* stream) {
+    FH_REQUIRE(in_scale && in_shift, "maxpool2_fwd_bnrelu: null scale/shift");
+    return maxpool2_fwd_impl(x, x_cs, in_scale, in_shift, aff_cs, y, y_cs, idx, i_cs, mask, m_cs,
+                             counts, nclients, batch, C, H, W, drop_mode, p_drop, seed, seed_dev,
+                             stream);
 }
 
 extern "C" int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,

@@ -58,6 +58,14 @@ SIGNATURES = {
     "fh_bn_workspace": (SZ, [I32, I32, I32, I32]),
     "fh_bn_fwd_train": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, P, P, I32, I32,
                               I32, I32, F32, F32, I32, P, SZ, P]),
+    "fh_bn_fwd_stats": (I32, [P, I64, P, P, I64, P, P, I64, P, P, P, P, I64, P, I32, I32, I32,
+                              I32, F32, F32, P, SZ, P]),
+    "fh_conv2d_fwd_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
+                                   I32, I32, I32, I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_conv2d_wgrad_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32,
+                                     I32, I32, I32, I32, I32, I32, I32, I32, I32, P]),
+    "fh_maxpool2_fwd_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
+                                     I32, I32, I32, F32, U64, P, P]),
     "fh_bn_fwd_eval": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, I32, I32, I32,
                              I32, F32, I32, P]),
     "fh_bn_bwd": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, P, I64, P, I64, P, P, I64, P,

@@ -19,6 +19,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import os
+
 import torch
 
 from . import ops
@@ -126,6 +128,9 @@ class PackedNet:
         self.seed = 0
         self.seed_dev = None  # device uint64 [1] = seed * 1000003 (graph replay)
         self.salt = 0  # per-lane key offset (a lane's slot 0 is not another lane's slot 0)
+        # CIFAR10CNN training: BN apply + ReLU folded into the consumers (FH_FUSE_BN=0: off)
+        self.fuse_bn = os.environ.get("FH_FUSE_BN", "1") != "0"
+        self._fused = False
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -318,25 +323,48 @@ class PackedNet:
                              torch.zeros(self.cap, C, device=self.device))
         return self.A.t[key]
 
+    def _bn_affine(self, name, C):
+        key = f"{name}.affine"
+        if key not in self.A.t:
+            self.A.t[key] = (torch.zeros(self.cap, C, device=self.device),
+                             torch.zeros(self.cap, C, device=self.device))
+        return self.A.t[key]
+
     def _fwd_cifar(self, P_, bufs, n, cnt, train):
+        """conv -> BN -> ReLU (-> pool -> dropout) x6, then the classifier.  Training with
+        fuse_bn: the BN output is never written; bn_fwd_stats leaves the per-(client,
+        channel) affine and the consumer (next conv fwd / its wgrad, or the max-pool)
+        applies relu(x * scale + shift) on load — bit-identical, one pass less each way."""
         A, B, W = self.A, self.batch, self.W
         dm = self._drop_mode(train)
-        xin = self.x
+        fuse = train and self.fuse_bn
+        self._fused = fuse
+        xin, aff = self.x, None
         for i, (cv, ci, co, hw, bn) in enumerate(self._CIFAR_CONVS):
             c = A(f"c_{cv}", co, hw, hw)
-            r = A(f"r_{cv}", co, hw, hw)
             ops.conv2d_fwd(xin, W(P_, f"{cv}.weight"), W(P_, f"{cv}.bias"), c, n, B, ci, hw, hw, co,
-                           3, 1, 1, counts=cnt)
-            self._bn_train(P_, bufs, bn, c, r, n, co, hw * hw, cnt, relu=True, train=train)
-            xin = r
+                           3, 1, 1, counts=cnt, in_affine=aff)
+            if fuse:
+                sm, si = self._bn_save(bn, co)
+                aff = self._bn_affine(bn, co)
+                ops.bn_fwd_stats(c, W(P_, f"{bn}.weight"), W(P_, f"{bn}.bias"),
+                                 self.layout.bview(bufs, f"{bn}.running_mean"),
+                                 self.layout.bview(bufs, f"{bn}.running_var"), sm, si, aff[0],
+                                 aff[1], n, B, co, hw * hw, self.bn_eps, self.bn_momentum,
+                                 counts=cnt)
+                xin = c
+            else:
+                r = A(f"r_{cv}", co, hw, hw)
+                self._bn_train(P_, bufs, bn, c, r, n, co, hw * hw, cnt, relu=True, train=train)
+                xin, aff = r, None
             if i % 2 == 1:
                 q = A(f"q_{cv}", co, hw // 2, hw // 2)
                 idx = A(f"i_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8)
                 msk = A(f"m_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8) if dm else None
-                ops.maxpool2_fwd(r, q, idx, n, B, co, hw, hw, mask=msk, drop_mode=dm,
+                ops.maxpool2_fwd(xin, q, idx, n, B, co, hw, hw, mask=msk, drop_mode=dm,
                                  p_drop=self.dropout_p, seed=self._seed(10 + i), counts=cnt,
-                                 seed_dev=self.seed_dev)
-                xin = q
+                                 seed_dev=self.seed_dev, in_affine=aff)
+                xin, aff = q, None
         # classifier: fc1 -> relu -> drop -> fc2 -> relu -> drop -> fc3
         h1, h2 = A("h1", 512), A("h2", 256)
         ops.linear_fwd(xin, W(P_, "fc1.weight"), W(P_, "fc1.bias"), h1, n, B, 2048, 512, relu=True,
@@ -396,15 +424,19 @@ class PackedNet:
                            W(P_, f"{bn}.weight"), sm, si, dc, W(G, f"{bn}.weight"),
                            W(G, f"{bn}.bias"), n, B, co, hw * hw, relu=True, counts=cnt,
                            beta=W(P_, f"{bn}.bias"))
+            aff = None
             if i == 0:
                 xin = self.x
             elif i % 2 == 0:
                 pcv = convs[i - 1][0]
                 xin = A(f"q_{pcv}", ci, hw, hw)
+            elif self._fused:  # the previous BN's output, applied on load
+                xin = A(f"c_{convs[i - 1][0]}", ci, hw, hw)
+                aff = self._bn_affine(convs[i - 1][4], ci)
             else:
                 xin = A(f"r_{convs[i - 1][0]}", ci, hw, hw)
             ops.conv2d_wgrad(xin, dc, W(G, f"{cv}.weight"), W(G, f"{cv}.bias"), n, B, ci, hw, hw,
-                             co, 3, 1, 1, counts=cnt)
+                             co, 3, 1, 1, counts=cnt, in_affine=aff)
             if i == 0:
                 break
             pcv = convs[i - 1][0]
@@ -537,6 +569,14 @@ class PackedNet:
         if self.family == "SimpleCNN":
             return [A("a1", 32, 28, 28), A("a2", 64, 14, 14), A("h1", 128)]
         if self.family == "CIFAR10CNN":
+            if self._fused:  # BN outputs not materialised: the same fp32 ops on the host side
+                out = []
+                for cv, ci, co, hw, bn in self._CIFAR_CONVS:
+                    sc, sh = self._bn_affine(bn, co)
+                    c = A(f"c_{cv}", co, hw, hw)
+                    out.append(torch.clamp_min(c * sc[:, None, :, None, None]
+                                               + sh[:, None, :, None, None], 0.0))
+                return out + [A("h1", 512), A("h2", 256)]
             return [A(f"r_{cv}", co, hw, hw) for cv, ci, co, hw, bn in self._CIFAR_CONVS] + \
                 [A("h1", 512), A("h2", 256)]
         out = [A("r_stem", 64, 32, 32)]

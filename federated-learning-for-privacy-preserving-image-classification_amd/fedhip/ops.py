@@ -19,7 +19,7 @@ from ._lib import FedHipError, call, load, ptr, require_device, stream_handle
 __all__ = [
     "conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "linear_fwd", "linear_dgrad", "linear_wgrad",
     "fedavg_weighted_sum", "update_stats", "dp_delta_sqnorm", "dp_clip_coef", "dp_apply",
-    "sgd_step", "adam_step", "bn_fwd_train", "bn_fwd_eval", "bn_bwd", "maxpool2_fwd",
+    "sgd_step", "adam_step", "bn_fwd_train", "bn_fwd_stats", "bn_fwd_eval", "bn_bwd", "maxpool2_fwd",
     "maxpool2_bwd", "dropout_fwd", "dropout_bwd", "ce_fwd_bwd", "avgpool_fwd", "avgpool_bwd",
     "gather_batch", "gather_u8", "DataTransform", "eval_metrics", "Workspace",
 ]
@@ -175,14 +175,22 @@ def _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad):
 
 
 def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad, relu=False,
-               counts=None):
+               counts=None, in_affine=None):
+    """in_affine = (scale, shift) [clients, cin]: x is a BatchNorm pre-activation and the
+    kernel convolves relu(x * scale + shift) (fh_conv2d_fwd_bnrelu)."""
     require_device(x, "x")
     ws, nb = _ws_for("fh_conv2d_fwd_workspace", x.device, nclients, batch, cin, h, wd, cout, k, k,
                      stride, pad)
     ev = PROBE.begin(_conv_tag("fwd", cin, h, wd, cout, k, stride))
-    call("fh_conv2d_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y),
-         _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(relu),
-         ptr(ws), nb, stream_handle())
+    if in_affine is not None:
+        sc, sh = in_affine
+        call("fh_conv2d_fwd_bnrelu", ptr(x), _cs(x), ptr(sc), ptr(sh), _cs(sc), ptr(w), _cs(w),
+             ptr(bias), _cs(bias), ptr(y), _cs(y), _counts(counts), nclients, batch, cin, h, wd,
+             cout, k, k, stride, pad, int(relu), ptr(ws), nb, stream_handle())
+    else:
+        call("fh_conv2d_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y),
+             _cs(y), _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
+             int(relu), ptr(ws), nb, stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return y
 
@@ -199,13 +207,21 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
     return dx
 
 
-def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None):
+def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
+                 in_affine=None):
+    """in_affine as in conv2d_fwd (fh_conv2d_wgrad_bnrelu)."""
     ws, nb = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, cin, h, wd, cout, k,
                      k, stride, pad)
     ev = PROBE.begin(_conv_tag("wgrad", cin, h, wd, cout, k, stride))
-    call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
-         ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride,
-         pad, stream_handle())
+    if in_affine is not None:
+        sc, sh = in_affine
+        call("fh_conv2d_wgrad_bnrelu", ptr(x), _cs(x), ptr(sc), ptr(sh), _cs(sc), ptr(dy),
+             _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db), ptr(ws), nb, _counts(counts), nclients,
+             batch, cin, h, wd, cout, k, k, stride, pad, stream_handle())
+    else:
+        call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db),
+             _cs(db), ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k,
+             stride, pad, stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return dw
 
@@ -350,6 +366,17 @@ def bn_fwd_train(x, y, gamma, beta, rmean, rvar, save_mean, save_invstd, nclient
          int(relu), ptr(ws), nb, stream_handle())
 
 
+def bn_fwd_stats(x, gamma, beta, rmean, rvar, save_mean, save_invstd, scale, shift, nclients,
+                 batch, C, HW, eps=1e-5, momentum=0.1, counts=None):
+    """Train-mode BN statistics ending in the consumer's affine (scale, shift [clients, C]):
+    relu(x * scale + shift) == bn_fwd_train(..., relu=True)'s output, bit for bit."""
+    ws, nb = _ws_for("fh_bn_workspace", x.device, nclients, batch, C, HW)
+    call("fh_bn_fwd_stats", ptr(x), _cs(x), ptr(gamma), ptr(beta), _cs(gamma), ptr(rmean),
+         ptr(rvar), _cs(rmean), ptr(save_mean), ptr(save_invstd), ptr(scale), ptr(shift),
+         _cs(scale), _counts(counts), nclients, batch, C, HW, float(eps), float(momentum),
+         ptr(ws), nb, stream_handle())
+
+
 def bn_fwd_eval(x, y, gamma, beta, rmean, rvar, nclients, batch, C, HW, eps=1e-5, relu=False,
                 res=None, counts=None):
     call("fh_bn_fwd_eval", ptr(x), _cs(x), ptr(y), _cs(y), ptr(res), _cs(res), ptr(gamma),
@@ -378,7 +405,14 @@ def bn_bwd_pool(dpool, pidx, yout, x, gamma, save_mean, save_invstd, dx, dgamma,
 
 
 def maxpool2_fwd(x, y, idx, nclients, batch, C, H, W, mask=None, drop_mode=0, p_drop=0.0, seed=0,
-                 counts=None, seed_dev=None):
+                 counts=None, seed_dev=None, in_affine=None):
+    if in_affine is not None:  # x = BN pre-activation: pool relu(x * scale + shift)
+        sc, sh = in_affine
+        call("fh_maxpool2_fwd_bnrelu", ptr(x), _cs(x), ptr(sc), ptr(sh), _cs(sc), ptr(y), _cs(y),
+             ptr(idx), _cs(idx), ptr(mask), _cs(mask), _counts(counts), nclients, batch, C, H, W,
+             int(drop_mode), float(p_drop), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev),
+             stream_handle())
+        return
     call("fh_maxpool2_fwd", ptr(x), _cs(x), ptr(y), _cs(y), ptr(idx), _cs(idx), ptr(mask),
          _cs(mask), _counts(counts), nclients, batch, C, H, W, int(drop_mode), float(p_drop),
          int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), stream_handle())

@@ -270,6 +270,43 @@ int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets, int
                   const int32_t* counts, int32_t nclients, int32_t batch, int32_t num_classes,
                   void* stream);
 
+/* ---------------- BatchNorm apply + ReLU folded into the consumer (CIFAR10CNN) -------
+ * The train-mode BN output relu(x*w*invstd + b - mean*w*invstd) is never written: the
+ * statistics pass ends in a per-(client, channel) affine (scale, shift [z][C], stride
+ * s_cs) and every consumer of the activation — the next conv's forward and weight
+ * gradient, or the 2x2 max-pool — applies relu(x*scale + shift) while loading x.
+ * Same fp32 operations as fh_bn_fwd_train's apply pass, so results are bit-identical.
+ * (models_pytorch.py:128-137: conv -> bn -> relu -> conv / pool.) */
+int fh_bn_fwd_stats(const float* x, int64_t x_cs, const float* gamma, const float* beta,
+                    int64_t p_cs, float* running_mean, float* running_var, int64_t r_cs,
+                    float* save_mean, float* save_invstd, float* scale_out, float* shift_out,
+                    int64_t s_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                    int32_t C, int32_t HW, float eps, float momentum, void* workspace,
+                    size_t ws_bytes, void* stream);
+/* fh_conv2d_fwd / fh_conv2d_wgrad with x = a BN pre-activation (direct 3x3 path only:
+ * 3x3/s1/p1 on 8/16/32 square maps; wgrad also needs cin, cout % 32 == 0; else
+ * FH_E_UNSUPPORTED).  Zero padding is applied after the affine (padding of the ReLU
+ * output, as in the reference). */
+int fh_conv2d_fwd_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
+                         const float* in_shift, int64_t aff_cs, const float* w, int64_t w_cs,
+                         const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                         const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
+                         int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
+                         int32_t stride, int32_t pad, int32_t relu, void* workspace,
+                         size_t ws_bytes, void* stream);
+int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
+                           const float* in_shift, int64_t aff_cs, const float* dy, int64_t dy_cs,
+                           float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
+                           size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                           int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                           int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream);
+int fh_maxpool2_fwd_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
+                           const float* in_shift, int64_t aff_cs, float* y, int64_t y_cs,
+                           uint8_t* idx, int64_t i_cs, uint8_t* mask, int64_t m_cs,
+                           const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
+                           int32_t H, int32_t W, int32_t drop_mode, float p_drop, uint64_t seed,
+                           const uint64_t* seed_dev, void* stream);
+
 /* ---------------- launch planning ---------------------------------------------
  * Share of the chip (0, 1] that the split-K planners of the conv / linear entry points
  * aim to fill, for launches issued by the CALLING THREAD (thread-local; default 1).

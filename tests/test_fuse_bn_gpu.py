@@ -1,0 +1,120 @@
+"""BatchNorm apply + ReLU folded into its consumers (fh_bn_fwd_stats, fh_conv2d_fwd_bnrelu,
+fh_conv2d_wgrad_bnrelu, fh_maxpool2_fwd_bnrelu) is bit-identical to the materialised path
+(fh_bn_fwd_train's apply pass + plain conv / pool): the consumer evaluates the same fp32
+operations on load.  Whole CIFAR10CNN rounds (graph replay, dropout, ragged batches) and
+the single ops on ragged client counts."""
+import pytest
+import torch
+
+from fedhip import ops
+from fedhip.engine import PackedTrainer
+from src.shared import models_pytorch as hm
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _round(fuse, opt, sizes, rounds=2):
+    torch.manual_seed(0)
+    model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.3).to(DEV)
+    S = len(sizes)
+    eng = PackedTrainer(model, capacity=S, batch=32, device=DEV)
+    eng.net.fuse_bn = fuse
+    for k in range(S):
+        eng.load_module_state(k, model)
+    g = torch.Generator().manual_seed(5)
+    data = torch.randn(sum(sizes), 3, 32, 32, generator=g).to(DEV)
+    labels = torch.randint(0, 10, (sum(sizes),), generator=g).to(DEV)
+    offs = [sum(sizes[:k]) for k in range(S)]
+    gen = torch.Generator().manual_seed(11)
+    metrics = []
+    for r in range(rounds):
+        plan = eng.make_plan(sizes, 1, generator=gen)
+        metrics.append(eng.run_round(data, labels, offs, plan, optimizer_type=opt, lr=1e-2,
+                                     seed=r))
+    torch.cuda.synchronize()
+    return eng, metrics
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_fused_bn_rounds_bit_identical(opt):
+    sizes = [130, 70, 33, 9]
+    a, ma = _round(True, opt, sizes)
+    b, mb = _round(False, opt, sizes)
+    assert a.net._fused and not b.net._fused
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.bufs, b.bufs)
+    assert torch.equal(a.state1, b.state1)
+    for ra, rb in zip(ma, mb):
+        for x, y in zip(ra, rb):
+            assert (x.loss, x.accuracy) == (y.loss, y.accuracy)
+
+
+@pytest.mark.parametrize("nc,C,hw", [(1, 32, 32), (3, 64, 16), (5, 128, 8)])
+def test_fused_ops_match_apply_pass(nc, C, hw):
+    B = 32
+    torch.manual_seed(nc + C)
+    cnt = torch.tensor([B] + [int(v) for v in torch.randint(1, B + 1, (nc - 1,))],
+                       dtype=torch.int32, device=DEV)
+    x = torch.randn(nc, B, C, hw, hw, device=DEV) * 1.5 + 0.2
+    gamma = torch.rand(nc, C, device=DEV) + 0.5
+    gamma[:, ::7] *= -1  # negative scales: the ReLU mask is not monotone in x
+    beta = torch.randn(nc, C, device=DEV) * 0.3
+    rm0, rv0 = torch.zeros(nc, C, device=DEV), torch.ones(nc, C, device=DEV)
+    # materialised path
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    sm1, si1 = torch.zeros(nc, C, device=DEV), torch.zeros(nc, C, device=DEV)
+    r = torch.zeros_like(x)
+    ops.bn_fwd_train(x, r, gamma, beta, rm1, rv1, sm1, si1, nc, B, C, hw * hw, relu=True,
+                     counts=cnt)
+    # statistics + affine
+    rm2, rv2 = rm0.clone(), rv0.clone()
+    sm2, si2 = torch.zeros(nc, C, device=DEV), torch.zeros(nc, C, device=DEV)
+    sc, sh = torch.zeros(nc, C, device=DEV), torch.zeros(nc, C, device=DEV)
+    ops.bn_fwd_stats(x, gamma, beta, rm2, rv2, sm2, si2, sc, sh, nc, B, C, hw * hw, counts=cnt)
+    for u, v in ((rm1, rm2), (rv1, rv2), (sm1, sm2), (si1, si2)):
+        assert torch.equal(u, v)
+    # conv forward on r vs on x with the affine
+    co = 64
+    w = torch.randn(nc, co, C, 3, 3, device=DEV) * 0.05
+    bias = torch.randn(nc, co, device=DEV) * 0.1
+    y1 = torch.zeros(nc, B, co, hw, hw, device=DEV)
+    y2 = torch.zeros_like(y1)
+    ops.conv2d_fwd(r, w, bias, y1, nc, B, C, hw, hw, co, 3, 1, 1, counts=cnt)
+    ops.conv2d_fwd(x, w, bias, y2, nc, B, C, hw, hw, co, 3, 1, 1, counts=cnt, in_affine=(sc, sh))
+    for z in range(nc):
+        k = int(cnt[z])
+        assert torch.equal(y1[z, :k], y2[z, :k])
+    # weight gradient with x as the staged input
+    dy = torch.randn(nc, B, co, hw, hw, device=DEV)
+    dw1 = torch.zeros(nc, co, C, 3, 3, device=DEV)
+    db1 = torch.zeros(nc, co, device=DEV)
+    dw2, db2 = torch.zeros_like(dw1), torch.zeros_like(db1)
+    ops.conv2d_wgrad(r, dy, dw1, db1, nc, B, C, hw, hw, co, 3, 1, 1, counts=cnt)
+    ops.conv2d_wgrad(x, dy, dw2, db2, nc, B, C, hw, hw, co, 3, 1, 1, counts=cnt,
+                     in_affine=(sc, sh))
+    assert torch.equal(dw1, dw2) and torch.equal(db1, db2)
+    # max-pool (+ generated dropout mask) on r vs on x with the affine
+    oh = hw // 2
+    q1 = torch.zeros(nc, B, C, oh, oh, device=DEV)
+    q2 = torch.zeros_like(q1)
+    i1 = torch.zeros(nc, B, C, oh, oh, dtype=torch.uint8, device=DEV)
+    i2 = torch.zeros_like(i1)
+    m1, m2 = torch.zeros_like(i1), torch.zeros_like(i1)
+    ops.maxpool2_fwd(r, q1, i1, nc, B, C, hw, hw, mask=m1, drop_mode=1, p_drop=0.3, seed=9,
+                     counts=cnt)
+    ops.maxpool2_fwd(x, q2, i2, nc, B, C, hw, hw, mask=m2, drop_mode=1, p_drop=0.3, seed=9,
+                     counts=cnt, in_affine=(sc, sh))
+    for z in range(nc):
+        k = int(cnt[z])
+        assert torch.equal(q1[z, :k], q2[z, :k]) and torch.equal(i1[z, :k], i2[z, :k])
+        assert torch.equal(m1[z, :k], m2[z, :k])
+
+
+def test_fused_entry_points_refuse_unsupported_shapes():
+    x = torch.zeros(1, 4, 32, 14, 14, device=DEV)  # 14x14: no direct-conv path
+    sc, sh = torch.ones(1, 32, device=DEV), torch.zeros(1, 32, device=DEV)
+    w = torch.zeros(1, 64, 32, 3, 3, device=DEV)
+    y = torch.zeros(1, 4, 64, 14, 14, device=DEV)
+    with pytest.raises(ops.FedHipError):
+        ops.conv2d_fwd(x, w, None, y, 1, 4, 32, 14, 14, 64, 3, 1, 1, in_affine=(sc, sh))
