@@ -11,4 +11,5 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
+python3 $GRAFT_REPO_ROOT/tools/probe_agree.py $OUT/prof/run_kernel_trace.csv $OUT/prof_bench.json > $OUT/probe_agree.txt 2>&1 || true
 echo done
