@@ -368,8 +368,21 @@ splitk_sum_kernel(const float* __restrict__ part, float* __restrict__ dw, int64_
     const int lim = is_w ? MN : Mb;
     const float* src = is_w ? part + (int64_t)z * splits * MN : bpart + (int64_t)z * splits * Mb;
     float s = 0.f;
-    if (e < lim)
-        for (int i = q; i < splits; i += 4) s += src[(int64_t)i * lim + e];
+    if (e < lim) {
+        // loads of 8 splits issued together, then added in split order (same sum, bit for
+        // bit, as the one-at-a-time loop; without this every split is a dependent HBM trip)
+        for (int i0 = q; i0 < splits; i0 += 4 * 8) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = i0 + 4 * j;
+                v[j] = i < splits ? src[(int64_t)i * lim + e] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (i0 + 4 * j < splits) s += v[j];
+        }
+    }
     red[q][l] = s;
     __syncthreads();
     if (q == 0 && e < lim) {
@@ -390,8 +403,16 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
     const int n = blockIdx.x * 256 + threadIdx.x;
     if (n >= cnt * sp) return;
     const float* p = part + ((int64_t)z * splits * M + m) * Nfull + n;
+    const int64_t ss = (int64_t)M * Nfull;
     float s = 0.f;
-    for (int i = 0; i < splits; ++i) s += p[(int64_t)i * M * Nfull];
+    for (int i0 = 0; i0 < splits; i0 += 8) {  // 8 loads in flight, summed in split order
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = i0 + j < splits ? p[(i0 + j) * ss] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (i0 + j < splits) s += v[j];
+    }
     if (bias) s = s + bias[z * b_cs + m];
     if (relu) s = fmaxf(s, 0.f);
     const int img = n / sp, pix = n - img * sp;
