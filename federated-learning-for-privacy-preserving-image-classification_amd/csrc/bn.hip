@@ -83,12 +83,19 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 
 // merge this channel's S partials (fixed order) -> (n, sum0, sum1)
 __device__ __forceinline__ void merge(const BNArgs& a, int z, int c, double& s0, double& s1) {
-    const double* p = a.part + (((int64_t)z * a.C + c) * a.S) * 2;
+    const double2* p = reinterpret_cast<const double2*>(a.part + (((int64_t)z * a.C + c) * a.S) * 2);
     s0 = 0.0;
     s1 = 0.0;
-    for (int i = 0; i < a.S; ++i) {
-        s0 += p[2 * i];
-        s1 += p[2 * i + 1];
+    for (int i0 = 0; i0 < a.S; i0 += 8) {  // 8 partials in flight, added in slice order
+        double2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = i0 + j < a.S ? p[i0 + j] : make_double2(0.0, 0.0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (i0 + j < a.S) {
+                s0 += v[j].x;
+                s1 += v[j].y;
+            }
     }
 }
 

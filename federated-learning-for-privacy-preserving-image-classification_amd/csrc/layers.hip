@@ -157,12 +157,65 @@ ce_kernel(const float* __restrict__ logits, int64_t l_cs, const int64_t* __restr
           const int32_t* __restrict__ counts, int batch, int K) {
     __shared__ double sl[4];
     __shared__ int sc[4];
+    __shared__ double li[256];
+    __shared__ int ci[256];
     const int z = blockIdx.x;
     const int cnt = counts ? counts[z] : batch;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double lsum = 0.0;
     int corr = 0;
     const float inv_n = cnt > 0 ? 1.0f / (float)cnt : 0.f;
+    if (K <= 16 && cnt <= 256) {
+        // 16 lanes per image, 16 images at once (a batch of 32 in two passes instead of
+        // eight wave-serial ones); per-image losses go through LDS so the fp64 sums below
+        // run in exactly the order of the wave-per-image path
+        const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
+        for (int img = g; img < cnt; img += 16) {
+            const float* row = logits + z * l_cs + (int64_t)img * K;
+            const int tgt = (int)targets[z * t_cs + img];
+            const float v = l < K ? row[l] : -INFINITY;
+            float mx = v;
+            int amax = l < K ? l : K;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {  // first index of the max (torch.max tie rule)
+                const float om = __shfl_xor(mx, o, 16);
+                const int oa = __shfl_xor(amax, o, 16);
+                if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+            }
+            float se = l < K ? expf(v - mx) : 0.f;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) se += __shfl_xor(se, o, 16);
+            const float lse = logf(se);
+            if (l == 0) {
+                li[img] = (double)(-((row[tgt] - mx) - lse));
+                ci[img] = amax == tgt;
+            }
+            if (l < K) {
+                const float p = expf((v - mx) - lse);
+                dlogits[z * d_cs + (int64_t)img * K + l] = (p - (l == tgt ? 1.f : 0.f)) * inv_n;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 4) {
+            for (int img = threadIdx.x; img < cnt; img += 4) {
+                lsum += li[img];
+                corr += ci[img];
+            }
+            sl[threadIdx.x] = lsum;
+            sc[threadIdx.x] = corr;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const double tot = sl[0] + sl[1] + sl[2] + sl[3];
+            const float batch_loss = cnt > 0 ? (float)(tot / (double)cnt) : 0.f;
+            const bool rs = reset && reset[z];
+            if (loss_out) loss_out[z] = batch_loss;
+            if (acc_loss) acc_loss[z] = (rs ? 0.0 : acc_loss[z]) + (double)batch_loss;
+            if (acc_correct) acc_correct[z] = (rs ? 0 : acc_correct[z]) + sc[0] + sc[1] + sc[2] + sc[3];
+            if (acc_seen) acc_seen[z] = (rs ? 0 : acc_seen[z]) + cnt;
+        }
+        return;
+    }
     for (int img = wid; img < cnt; img += 4) {
         const float* row = logits + z * l_cs + (int64_t)img * K;
         const int tgt = (int)targets[z * t_cs + img];
