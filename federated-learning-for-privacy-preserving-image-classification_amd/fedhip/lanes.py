@@ -119,6 +119,11 @@ class LanedTrainer:
         # split-K fill fraction per lane (ops.set_fill_fraction); FH_LANE_FILL = one value
         # for every lane or one per lane (diagnostics)
         self.fill = [1.0] * len(self.lanes)
+        if len(self.lanes) > 1 and cut[1] - cut[0] == 1:
+            # an isolated outlier client plans its split-K for a quarter of the chip: fewer,
+            # longer splits (fewer reduction launches) beside the wide lanes (+1 %,
+            # profiles/r01_v10/lane_fill.txt)
+            self.fill[0] = 0.25
         env_fill = os.environ.get("FH_LANE_FILL")
         if env_fill and len(self.lanes) > 1:
             vals = [float(v) for v in env_fill.split(",")]
