@@ -502,10 +502,19 @@ struct Plan {
 
 // FWD/DGRAD: split K only when the output tiling leaves most CUs idle (the
 // latency-bound tail of a round, when few clients are still training).
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+static const int kMnSplitBelow = env_int("FH_MN_SPLIT_BELOW", 192);  // sweeps (fc_bench.py)
+static const int kMnTarget = env_int("FH_MN_TARGET", 768);
+
 static Plan plan_mn(int M, int N, int K, int nclients) {
     Plan p{pick_mn_tile(M, N), 1, K, M, N, K};
     const int64_t tiles = ceil_div(N, p.t.bn) * ceil_div(M, p.t.bm) * (int64_t)nclients;
-    if (tiles < fill(192)) choose_split(tiles, K, p.t.bk, fill(768), 4, p.splits, p.kchunk);
+    if (tiles < fill(kMnSplitBelow))
+        choose_split(tiles, K, p.t.bk, fill(kMnTarget), 4, p.splits, p.kchunk);
     if (p.splits <= 1) {
         p.splits = 1;
         p.kchunk = K;
@@ -604,10 +613,6 @@ static bool dconv_supported(int h, int w, int kh, int kw, int stride, int pad) {
 // still leave (default 1024), FH_DCONV_MAXBM caps BM, FH_DWGRAD_BLOCKS = wgrad split
 // target (default 1024), FH_DWGRAD_WPX forces the pixel-wave count (1, 2 or 4) when the
 // channel counts allow it.
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return (v && *v) ? atoi(v) : dflt;
-}
 // defaults from the MI355X sweeps (tools/conv_sweep.py, CIFAR10CNN layers at 32 clients):
 // BM <= 64 once 512 workgroups are reached; wgrad with four pixel-waves per 32x32
 // (co, ci) tile and ~256 workgroups (one per CU at its 86 KB of LDS)
@@ -1047,6 +1052,68 @@ extern "C" int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float*
 }
 
 // ---- linear layers: a 1x1 convolution over a 1x1 image -------------------
+// Skinny DGRAD (batch <= 32 images per client, the classifier of every reference CNN): a
+// weight stream, so one workgroup owns 32 input features and runs the 32 images as the
+// MFMA's other dimension, the out_f reduction split over its four waves and combined
+// through LDS in wave order; W arrives as 128-B rows, dY as float4 runs.  fc1 dgrad at 32
+// clients: 70 us vs 81 for the implicit GEMM, fc2 12 vs 27 (tools/fc_bench.py).  The same
+// layout for FWD lost (one dependent MFMA chain per wave over K/4: 123 vs 57 us) and
+// stays on the implicit GEMM.
+namespace fh {
+static const int kLinearSkinny = env_int("FH_LINEAR_SKINNY", 1);
+
+__device__ __forceinline__ float f4at(const float4& v, int q) {
+    return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+}
+
+// dX[z][b][k] = sum_m dY[z][b][m] W[z][m][k] for b < cnt; M % 32 == 0, K % 32 == 0
+__global__ void __launch_bounds__(256)
+linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const float* __restrict__ W,
+                           int64_t w_cs, float* __restrict__ dX, int64_t dx_cs,
+                           const int32_t* __restrict__ counts, int batch, int K, int M) {
+    __shared__ float red[3 * 16 * 64];
+    const int z = blockIdx.y, k0 = blockIdx.x * 32;
+    const int cnt = counts ? counts[z] : batch;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    const bool yok = r32 < cnt;
+    const float* yrow = dY + z * dy_cs + (int64_t)(yok ? r32 : 0) * M;   // A: image rows of dY
+    const float* wcol = W + z * w_cs + k0 + r32;                          // B: W[m][k0 + lane]
+    const int mw = M >> 2, mbeg = wid * mw;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int mb = mbeg; mb < mbeg + mw; mb += 8) {
+        const float4 a = yok ? *reinterpret_cast<const float4*>(yrow + mb + 4 * h) : zero;
+        float b[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = wcol[(int64_t)(mb + 4 * h + q) * K];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a, q), b[q], acc, 0, 0, 0);
+    }
+    if (wid > 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[((wid - 1) * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (wid != 0) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int img = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (img >= cnt) continue;
+        const float v = ((acc[r] + red[r * 64 + lane]) + red[(16 + r) * 64 + lane]) +
+                        red[(32 + r) * 64 + lane];
+        dX[z * dx_cs + (int64_t)img * K + k0 + r32] = v;
+    }
+}
+
+static bool skinny_aligned(const void* p, int64_t cs) {
+    return ((uintptr_t)p % 16 == 0) && cs % 4 == 0;
+}
+}  // namespace fh
+
 extern "C" size_t fh_linear_fwd_workspace(int32_t nclients, int32_t batch, int32_t in_f,
                                           int32_t out_f) {
     return fh_conv2d_fwd_workspace(nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0);
@@ -1070,6 +1137,14 @@ extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, i
                                float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
                                int32_t batch, int32_t in_f, int32_t out_f, void* workspace,
                                size_t ws_bytes, void* stream) {
+    if (kLinearSkinny && nclients > 0 && batch <= 32 && in_f % 32 == 0 && out_f % 32 == 0 &&
+        in_f > 0 && out_f > 0 && dy && w && dx && skinny_aligned(dy, dy_cs) && w_cs % 4 == 0) {
+        hipLaunchKernelGGL(linear_dgrad_skinny_kernel, dim3((unsigned)(in_f / 32), nclients),
+                           dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs, counts,
+                           batch, in_f, out_f);
+        FH_LAUNCH_CHECK("linear_dgrad skinny");
+        return FH_OK;
+    }
     return fh_conv2d_dgrad(dy, dy_cs, w, w_cs, dx, dx_cs, counts, nclients, batch, in_f, 1, 1,
                            out_f, 1, 1, 1, 0, 0, workspace, ws_bytes, stream);
 }

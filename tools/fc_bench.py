@@ -1,0 +1,51 @@
+"""Linear-layer (classifier) launch costs per client count: fwd / dgrad / wgrad of
+CIFAR10CNN's fc1-fc3 on packed clients (32 images each), HIP-event timed."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "federated-learning-for-privacy-preserving-image-classification_amd"))
+from fedhip import ops  # noqa: E402
+
+LAYERS = [(2048, 512), (512, 256), (256, 10)]
+
+
+def timeit(fn, it=30):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it * 1e3
+
+
+def main():
+    dev = torch.device("cuda")
+    B = 32
+    for C in [int(v) for v in os.environ.get("FH_BENCH_CLIENTS", "32,23,8,1").split(",")]:
+        tot = 0.0
+        line = f"C={C:2d}"
+        for fi, fo in LAYERS:
+            x = torch.randn(C, B, fi, device=dev)
+            w = torch.randn(C, fo, fi, device=dev) * 0.05
+            b = torch.randn(C, fo, device=dev)
+            y = torch.empty(C, B, fo, device=dev)
+            dy = torch.randn_like(y)
+            dx = torch.empty_like(x)
+            dw, db = torch.empty_like(w), torch.empty_like(b)
+            t1 = timeit(lambda: ops.linear_fwd(x, w, b, y, C, B, fi, fo, relu=True))
+            t2 = timeit(lambda: ops.linear_dgrad(dy, w, dx, C, B, fi, fo))
+            t3 = timeit(lambda: ops.linear_wgrad(x, dy, dw, db, C, B, fi, fo))
+            tot += t1 + t2 + t3
+            line += f" | {fi}->{fo} {t1:6.1f} {t2:6.1f} {t3:6.1f}"
+        print(line + f" | total {tot:7.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
