@@ -1056,7 +1056,7 @@ extern "C" int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float*
 // weight stream, so one workgroup owns 32 input features and runs the 32 images as the
 // MFMA's other dimension, the out_f reduction split over its four waves and combined
 // through LDS in wave order; W arrives as 128-B rows, dY as float4 runs.  fc1 dgrad at 32
-// clients: 70 us vs 81 for the implicit GEMM, fc2 12 vs 27 (tools/fc_bench.py).  The same
+// clients: 44 us vs 81 for the implicit GEMM, fc2 12 vs 27 (tools/fc_bench.py).  The same
 // layout for FWD lost (one dependent MFMA chain per wave over K/4: 123 vs 57 us) and
 // stays on the implicit GEMM.
 namespace fh {
@@ -1066,13 +1066,16 @@ __device__ __forceinline__ float f4at(const float4& v, int q) {
     return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
 }
 
-// dX[z][b][k] = sum_m dY[z][b][m] W[z][m][k] for b < cnt; M % 32 == 0, K % 32 == 0
+// dX[z][b][k] = sum_m dY[z][b][m] W[z][m][k] for b < cnt; M % 32 == 0, K % (32 * KT) == 0.
+// KT 32-feature tiles per workgroup: each W row is read as KT consecutive 128-B pieces
+// (one DRAM page run) and every wave carries KT independent accumulator chains.
+template <int KT>
 __global__ void __launch_bounds__(256)
 linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const float* __restrict__ W,
                            int64_t w_cs, float* __restrict__ dX, int64_t dx_cs,
                            const int32_t* __restrict__ counts, int batch, int K, int M) {
-    __shared__ float red[3 * 16 * 64];
-    const int z = blockIdx.y, k0 = blockIdx.x * 32;
+    __shared__ float red[3 * 16 * 64 * KT];
+    const int z = blockIdx.y, k0 = blockIdx.x * 32 * KT;
     const int cnt = counts ? counts[z] : batch;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r32 = lane & 31, h = lane >> 5;
@@ -1080,33 +1083,44 @@ linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const fl
     const float* yrow = dY + z * dy_cs + (int64_t)(yok ? r32 : 0) * M;   // A: image rows of dY
     const float* wcol = W + z * w_cs + k0 + r32;                          // B: W[m][k0 + lane]
     const int mw = M >> 2, mbeg = wid * mw;
-    f32x16 acc;
+    f32x16 acc[KT];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int mb = mbeg; mb < mbeg + mw; mb += 8) {
         const float4 a = yok ? *reinterpret_cast<const float4*>(yrow + mb + 4 * h) : zero;
-        float b[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) b[q] = wcol[(int64_t)(mb + 4 * h + q) * K];
+        float b[4][KT];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a, q), b[q], acc, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < KT; ++t) b[q][t] = wcol[(int64_t)(mb + 4 * h + q) * K + 32 * t];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a, q), b[q][t], acc[t], 0, 0, 0);
     }
     if (wid > 0) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) red[((wid - 1) * 16 + r) * 64 + lane] = acc[r];
+        for (int t = 0; t < KT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[(((wid - 1) * KT + t) * 16 + r) * 64 + lane] = acc[t][r];
     }
     __syncthreads();
     if (wid != 0) return;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int img = (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (img >= cnt) continue;
-        const float v = ((acc[r] + red[r * 64 + lane]) + red[(16 + r) * 64 + lane]) +
-                        red[(32 + r) * 64 + lane];
-        dX[z * dx_cs + (int64_t)img * K + k0 + r32] = v;
-    }
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int img = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (img >= cnt) continue;
+            const float v = ((acc[t][r] + red[((0 * KT + t) * 16 + r) * 64 + lane]) +
+                             red[((1 * KT + t) * 16 + r) * 64 + lane]) +
+                            red[((2 * KT + t) * 16 + r) * 64 + lane];
+            dX[z * dx_cs + (int64_t)img * K + k0 + 32 * t + r32] = v;
+        }
 }
 
 static bool skinny_aligned(const void* p, int64_t cs) {
@@ -1139,9 +1153,17 @@ extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, i
                                size_t ws_bytes, void* stream) {
     if (kLinearSkinny && nclients > 0 && batch <= 32 && in_f % 32 == 0 && out_f % 32 == 0 &&
         in_f > 0 && out_f > 0 && dy && w && dx && skinny_aligned(dy, dy_cs) && w_cs % 4 == 0) {
-        hipLaunchKernelGGL(linear_dgrad_skinny_kernel, dim3((unsigned)(in_f / 32), nclients),
-                           dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs, counts,
-                           batch, in_f, out_f);
+        // four k-tiles per workgroup once that still fills the chip (fc1 at 32 clients:
+        // 44 us vs 75; with few clients the one-tile form keeps more workgroups)
+        if (in_f % 128 == 0 && kLinearSkinny != 2 &&
+            (int64_t)(in_f / 128) * nclients >= fill(256))
+            hipLaunchKernelGGL(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
+                               dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs,
+                               counts, batch, in_f, out_f);
+        else
+            hipLaunchKernelGGL(linear_dgrad_skinny_kernel<1>, dim3((unsigned)(in_f / 32), nclients),
+                               dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs,
+                               counts, batch, in_f, out_f);
         FH_LAUNCH_CHECK("linear_dgrad skinny");
         return FH_OK;
     }
