@@ -1123,6 +1123,47 @@ linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const fl
         }
 }
 
+// dW[z][m][k] = sum_{b < cnt} dY[z][b][m] X[z][b][k] (and db[z][m] = sum_b dY[z][b][m]):
+// the reduction is only the images, so the layer is a write stream of dW.  One wave = one
+// 32 (m) x 32 (k) tile from 16 MFMAs over the 32 image pairs; a workgroup = 32 m x 128 k.
+// Bias: the k-tile-0 workgroups, one lane per m, images in order.
+__global__ void __launch_bounds__(256)
+linear_wgrad_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float* __restrict__ dY,
+                           int64_t dy_cs, float* __restrict__ dW, int64_t dw_cs,
+                           float* __restrict__ db, int64_t db_cs,
+                           const int32_t* __restrict__ counts, int batch, int K, int M) {
+    const int z = blockIdx.z, m0 = blockIdx.y * 32;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int k0 = blockIdx.x * 128 + wid * 32;
+    const int cnt = counts ? counts[z] : batch;
+    const int r32 = lane & 31, h = lane >> 5;
+    const bool mok = m0 + r32 < M;
+    const float* yz = dY + z * dy_cs + m0 + r32;   // A[i = m][b] = dY[b][m0 + lane]
+    const float* xz = X + z * x_cs + k0 + r32;     // B[b][j = k] = X[b][k0 + lane]
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+        const int b = 2 * p + h;
+        const bool ok = b < cnt;
+        const float av = ok && mok ? yz[(int64_t)b * M] : 0.f;
+        const float bv = ok ? xz[(int64_t)b * K] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+    float* wz = dW + z * dw_cs + k0 + r32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M) wz[(int64_t)m * K] = acc[r];
+    }
+    if (db && blockIdx.x == 0 && wid == 0 && h == 0 && mok) {
+        float v = 0.f;
+        for (int b = 0; b < cnt; ++b) v += yz[(int64_t)b * M];
+        db[z * db_cs + m0 + r32] = v;
+    }
+}
+
 static bool skinny_aligned(const void* p, int64_t cs) {
     return ((uintptr_t)p % 16 == 0) && cs % 4 == 0;
 }
@@ -1180,6 +1221,15 @@ extern "C" int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, in
                                float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
                                size_t ws_bytes, const int32_t* counts, int32_t nclients,
                                int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
+    if (kLinearSkinny && nclients > 0 && batch <= 32 && in_f % 128 == 0 && out_f > 0 && x &&
+        dy && dw) {
+        hipLaunchKernelGGL(linear_wgrad_skinny_kernel,
+                           dim3((unsigned)(in_f / 128), (unsigned)ceil_div(out_f, 32), nclients),
+                           dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
+                           counts, batch, in_f, out_f);
+        FH_LAUNCH_CHECK("linear_wgrad skinny");
+        return FH_OK;
+    }
     return fh_conv2d_wgrad(x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs, workspace, ws_bytes, counts,
                            nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0, stream);
 }
