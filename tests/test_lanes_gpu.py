@@ -9,6 +9,7 @@ the per-step rows, graph pools) shows up as a bit difference."""
 import pytest
 import torch
 
+from fedhip import ops
 from fedhip.engine import PackedTrainer
 from fedhip.lanes import LanedTrainer
 from src.shared import models_pytorch as hm
@@ -57,7 +58,11 @@ def test_lanes_match_standalone(model_name, kw, shape, opt):
         for i, tr in enumerate(alone):
             a, b = cut[i], cut[i + 1]
             plan = tr.make_plan(sizes[a:b], 1, generator=gen)
-            tr.run_round(data, labels, offs[a:b], plan, optimizer_type=opt, lr=1e-3, seed=r)
+            ops.set_fill_fraction(lt.fill[i])  # the lane's split-K plan (1-client lane: 0.25)
+            try:
+                tr.run_round(data, labels, offs[a:b], plan, optimizer_type=opt, lr=1e-3, seed=r)
+            finally:
+                ops.set_fill_fraction(1.0)
     torch.cuda.synchronize()
     for i, tr in enumerate(alone):
         a, b = cut[i], cut[i + 1]
@@ -66,4 +71,5 @@ def test_lanes_match_standalone(model_name, kw, shape, opt):
         assert torch.equal(lt.acc_loss[a:b], tr.acc_loss)
         assert torch.equal(lt.acc_correct[a:b], tr.acc_correct)
     assert len(lt.lanes) == 3 and all(len(ln._graphs) > 0 for ln in lt.lanes[:2])
+    assert lt.fill == [0.25, 1.0, 1.0]
 
