@@ -296,6 +296,19 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     }
     // acc[i][j][r]: row m = (r&3) + 8*(r>>2) + 4*(lane>>5), col n = lane&31.
     const int rbase = 4 * (lane >> 5), col = lane & 31;
+    // FWD bias of this lane's output rows, read once (inside the store loop every store
+    // forces a re-read: `out` may alias `bias`)
+    float bv_r[FM][16];
+    if constexpr (OP == OP_FWD) {
+        const float* bz = (!partial_out && a.bias) ? a.bias + z * a.b_cs : nullptr;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                bv_r[i][r] = (bz && m < M) ? bz[m] : 0.f;
+            }
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
         const int n = n0 + wn * WN + j * 32 + col;
@@ -317,7 +330,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
             if constexpr (OP == OP_FWD) {
                 a.fd_ohw.divmod(n, img, p);
                 float* op = a.out + z * a.out_cs + (int64_t)img * a.cout * ohw + p;
-                const float* bz = a.bias ? a.bias + z * a.b_cs : nullptr;
+                const bool has_bias = a.bias != nullptr;
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -325,7 +338,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
                         const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
                         if (m < M) {
                             float v = acc[i][j][r];
-                            if (bz) v = v + bz[m];
+                            if (has_bias) v = v + bv_r[i][r];
                             if (a.relu) v = fmaxf(v, 0.f);
                             op[(int64_t)m * ohw] = v;
                         }

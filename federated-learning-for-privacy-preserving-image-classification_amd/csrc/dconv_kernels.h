@@ -286,6 +286,19 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 
     // ---- epilogue: lanes = 32 consecutive pixels -> coalesced stores ----
     const int rbase = 4 * h;
+    // the bias of this lane's 16*FM output channels, read once into registers (inside the
+    // store loop the compiler must re-read it after every store: `out` may alias `bias`)
+    float bv_r[FM][16];
+    if (OP == OP_FWD && a.splits == 1) {
+        const float* bz = a.bias ? a.bias + z * a.b_cs : nullptr;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                bv_r[i][r] = (bz && m < M) ? bz[m] : 0.f;
+            }
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
         const int n = n0 + wn * WN + j * 32 + col;
@@ -302,7 +315,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
                 }
         } else {
             float* op = a.out + z * a.out_cs + (int64_t)img * M * G::HW + p;
-            const float* bz = a.bias ? a.bias + z * a.b_cs : nullptr;
+            const bool has_bias = a.bias != nullptr;
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -312,7 +325,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
                         float v = acc[i][j][r];
                         float* q = op + (int64_t)m * G::HW;
                         if (OP == OP_FWD) {
-                            if (bz) v = v + bz[m];
+                            if (has_bias) v = v + bv_r[i][r];
                             if (a.relu) v = fmaxf(v, 0.f);
                         } else if (a.accumulate) {
                             v = *q + v;
