@@ -633,9 +633,12 @@ static const int kDconvBlocks = env_int("FH_DCONV_BLOCKS", 512);
 static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 64);
 static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 256);
 static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 4);
+// RGB-layer wgrad target: 512 workgroups (42 -> 34 us at 32 clients, profiles/r01_v12)
+static const int kDwgradSmallBlocks = env_int("FH_DWGRAD_SMALL_BLOCKS", 512);
 static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 2);  // tools/tail_sweep.py
 static const int kDconvForceSplits = env_int("FH_DCONV_SPLITS", 0);  // sweeps: force splits
 static const int kDwgradForceSplits = env_int("FH_DWGRAD_SPLITS", 0);
+static const int kDconvCk32 = env_int("FH_DCONV_CK32", 8);  // sweeps: CK of the BM=32 tiles
 
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
@@ -648,7 +651,7 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
             break;
         }
     }
-    p.ck = (p.bm == 128 || Cr <= 4) ? 4 : 8;
+    p.ck = (p.bm == 128 || Cr <= 4) ? 4 : (p.bm == 32 && kDconvCk32 == 4) ? 4 : 8;
     const int64_t blocks = tn * ceil_div(M, p.bm) * nclients;
     const int chunks = (int)ceil_div(Cr, p.ck);
     if ((kDconvForceSplits > 0 || blocks < fill(512)) && chunks > 1) {
@@ -744,9 +747,13 @@ static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     else if (ci64) p = {1, 2, 2, 128 / w, 1, 1};
     const int64_t tiles = (int64_t)(cout / (32 * p.wco)) * (cin / (32 * p.wci)) * nclients;
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
+    // one workgroup per CU per resident wave (the 16x16 instance holds two: +3-5 % on those
+    // layers at 512 workgroups; the one-wave instances lose with two rounds of workgroups)
+    const int occ = dwgrad_occ(w, p.wco, p.wci, p.sr);
     // >= 4 stages per split: fewer, longer splits beat a wide slab in the few-client tail
     const int want = (int)std::min<int64_t>(
-        std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks), tiles)), std::max(1, nst / kDwgradMinSps));
+        std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks * occ), tiles)),
+        std::max(1, nst / kDwgradMinSps));
     p.sps = (int)ceil_div(nst, kDwgradForceSplits > 0 ? std::min(kDwgradForceSplits, nst) : want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;
@@ -763,7 +770,8 @@ static DWPlan plan_dwgrad_small(int cout, int batch, int w, int nclients) {
     const int64_t tiles = (int64_t)(cout / 32) * nclients;
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
     const int want = (int)std::min<int64_t>(
-        std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks), tiles)), std::max(1, nst / kDwgradMinSps));
+        std::max<int64_t>(1, ceil_div(fill(kDwgradSmallBlocks), tiles)),
+        std::max(1, nst / kDwgradMinSps));
     p.sps = (int)ceil_div(nst, want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;

@@ -365,8 +365,24 @@ struct DWArgs {
     int64_t aff_cs;
 };
 
+// Two workgroups per CU when the double-buffered staging fits twice in the 160 KB LDS:
+// then ask the allocator for two waves per SIMD (144 accumulator AGPRs + <= 112 VGPRs),
+// so one workgroup's staging + barrier overlaps the other's MFMAs.
+// (host planner: the same formula picks the workgroup target, conv.hip plan_dwgrad)
+constexpr int dwgrad_occ(int W, int WCO, int WCI, int SR) {
+    const int SEGR = SR < W ? SR : W, NI = SR / SEGR;
+    const int PR = NI * (SEGR + 2), CSTR = (PR * (W + 2)) | 1;
+    const int bytes = 4 * 2 * (SR * W * (32 * WCO + 1) + 32 * WCI * CSTR);
+    return 2 * bytes <= 160 * 1024 ? 2 : 1;
+}
+template <int W, int WCO, int WCI, int SR>
+constexpr int dwgrad_occupancy() {
+    constexpr int occ = dwgrad_occ(W, WCO, WCI, SR);
+    return occ;
+}
+
 template <int W, int WCO, int WCI, int WPX, int SR>
-__global__ void __launch_bounds__(256) dconv_wgrad_kernel(const DWArgs a) {
+__global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR>())) dconv_wgrad_kernel(const DWArgs a) {
     constexpr int H = W, HW = H * W;
     constexpr int SPX = SR * W;                     // pixels per stage
     constexpr int SEGR = SR < H ? SR : H;
