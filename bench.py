@@ -27,6 +27,7 @@ import glob
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -187,18 +188,27 @@ def rounds_to_target(dev, target, max_rounds, signal, opt, lr):
                     "MNIST number"}
 
 
-def measured_traffic(probe_tag):
+def measured_traffic(probe_tag, flops_per_launch=None):
     """HBM bytes per launch of the probed kernel, from the newest committed PMC
     measurement (profiles/*/traffic.json, made by tools/traffic.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark), else None."""
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark), else None.
+    The kernel's traffic is per client (each client's own dY, weights and dX), so a
+    measurement taken at another client count is scaled by the FLOP ratio of the two
+    launches when the file records the FLOPs it was measured at."""
     here = os.path.dirname(os.path.abspath(__file__))
-    for f in sorted(glob.glob(os.path.join(here, "profiles", "*", "traffic.json")), reverse=True):
+    def newest_first(f):  # profiles/r01_v13 after r01_v7: compare the digit runs as numbers
+        return [int(p) if p.isdigit() else p for p in re.split(r"(\d+)", f)]
+    for f in sorted(glob.glob(os.path.join(here, "profiles", "*", "traffic.json")),
+                    key=newest_first, reverse=True):
         try:
             t = json.load(open(f))
         except (OSError, ValueError):
             continue
         if t.get("probe") == probe_tag:
-            return int(t["traffic_bytes"])
+            scale = 1.0
+            if flops_per_launch and t.get("flops_per_launch"):
+                scale = flops_per_launch / t["flops_per_launch"]
+            return int(round(t["traffic_bytes"] * scale))
     return None
 
 
@@ -284,7 +294,7 @@ def main():
             roof = {"bound": "mfma", "kernel": probe_tag, "achieved": round(ach, 2),
                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                    "traffic": measured_traffic(probe_tag),
+                    "traffic": measured_traffic(probe_tag, probe["flops_per_launch"]),
                     "launches_timed": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4)}
         out = {
             "metric": "client-images/sec/node", "value": round(value, 1),
