@@ -33,6 +33,37 @@ sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict
     }
 }
 
+// The same update, four parameters per lane (16-B loads/stores; rows are 256-B aligned and
+// padded to 64 floats, so packed slabs always qualify).  Per-element arithmetic is the
+// scalar kernel's, so both give identical bits.
+__device__ __forceinline__ float sgd_elem(float pv, float gv, float bv, float neg_lr, float mom,
+                                          float wd, int first, float& b_out) {
+    if (wd != 0.f) gv = fmaf(pv, wd, gv);
+    float b = gv;
+    if (mom != 0.f) b = first ? gv : (bv * mom + gv);
+    b_out = b;
+    return fmaf(b, neg_lr, pv);
+}
+
+__global__ void __launch_bounds__(256)
+sgd4_kernel(float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ buf,
+            int64_t n4, float neg_lr, float mom, float wd, int first) {
+    const bool use_buf = mom != 0.f;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 pv = p[i];
+        const float4 gv = g[i];
+        const float4 bv = (use_buf && !first) ? buf[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 b, o;
+        o.x = sgd_elem(pv.x, gv.x, bv.x, neg_lr, mom, wd, first, b.x);
+        o.y = sgd_elem(pv.y, gv.y, bv.y, neg_lr, mom, wd, first, b.y);
+        o.z = sgd_elem(pv.z, gv.z, bv.z, neg_lr, mom, wd, first, b.z);
+        o.w = sgd_elem(pv.w, gv.w, bv.w, neg_lr, mom, wd, first, b.w);
+        if (use_buf) buf[i] = b;
+        p[i] = o;
+    }
+}
+
 __global__ void __launch_bounds__(256)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, int64_t n, float wd, float decay_mul, int decoupled,
@@ -71,8 +102,15 @@ extern "C" int fh_sgd_step(float* param, const float* grad, float* momentum_buf,
     FH_REQUIRE(n >= 0, "sgd_step: bad size");
     if (n == 0) return FH_OK;
     FH_REQUIRE(param && grad && (momentum == 0.f || momentum_buf), "sgd_step: null pointer");
-    hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param, grad,
-                       momentum_buf, n, -lr, momentum, weight_decay, first_step);
+    const bool vec = n % 4 == 0 && ((uintptr_t)param | (uintptr_t)grad |
+                                    (momentum != 0.f ? (uintptr_t)momentum_buf : 0)) % 16 == 0;
+    if (vec)
+        hipLaunchKernelGGL(sgd4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream),
+                           (float4*)param, (const float4*)grad, (float4*)momentum_buf, n / 4, -lr,
+                           momentum, weight_decay, first_step);
+    else
+        hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param,
+                           grad, momentum_buf, n, -lr, momentum, weight_decay, first_step);
     FH_LAUNCH_CHECK("sgd_step");
     return FH_OK;
 }

@@ -190,3 +190,29 @@ def test_bn_bwd_recomputed_relu_mask_is_exact(case):
     for z in range(nc):
         assert torch.equal(outs[0][0][z, :cnt[z]], outs[1][0][z, :cnt[z]])
     assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+
+
+@pytest.mark.parametrize("mom,wd,first", [(0.9, 0.0, False), (0.9, 0.0, True), (0.0, 0.0, False),
+                                          (0.9, 0.01, False)])
+def test_sgd_vector_and_scalar_paths_agree(mom, wd, first):
+    """fh_sgd_step takes the float4 kernel for 16-B-aligned, n % 4 == 0 slabs (every packed
+    parameter slab) and the scalar kernel otherwise; both must give the same bits, and the
+    torch.optim.SGD update (training.py:244-255 builds it with momentum 0.9)."""
+    n = 3 * 65536 + 64
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    p0, g0, b0 = (torch.randn(n, generator=gen) for _ in range(3))
+    outs = []
+    for off in (0, 1):  # offset 1 float: misaligned -> scalar kernel
+        p, g, b = (torch.zeros(n + 4, device="cuda") for _ in range(3))
+        p[off:off + n], g[off:off + n], b[off:off + n] = p0.cuda(), g0.cuda(), b0.cuda()
+        ops.sgd_step(p[off:off + n], g[off:off + n], b[off:off + n], 0.01, mom, wd, first)
+        torch.cuda.synchronize()
+        outs.append((p[off:off + n].cpu(), b[off:off + n].cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    gv = g0 + wd * p0
+    bref = gv if (first or mom == 0.0) else b0 * mom + gv
+    torch.testing.assert_close(outs[0][0], p0 - 0.01 * bref, rtol=1e-6, atol=1e-7)
+    if mom != 0.0:
+        torch.testing.assert_close(outs[0][1], bref, rtol=1e-6, atol=1e-7)
+    else:
+        assert torch.equal(outs[0][1], b0)  # no momentum: the buffer is never touched
