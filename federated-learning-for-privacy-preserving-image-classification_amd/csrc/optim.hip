@@ -64,6 +64,24 @@ sgd4_kernel(float4* __restrict__ p, const float4* __restrict__ g, float4* __rest
     }
 }
 
+// One Adam/AdamW element in torch.optim's rounding order; shared by the scalar and the
+// float4 kernel so the two give identical bits.
+__device__ __forceinline__ float adam_elem(float pv, float gv, float& m, float& v, float wd,
+                                          float decay_mul, int decoupled, float one_m_b1,
+                                          float b2, float one_m_b2, float bc2_sqrt, float eps,
+                                          float neg_step_size) {
+    if (wd != 0.f) {
+        if (decoupled) pv = pv * decay_mul;
+        else gv = fmaf(pv, wd, gv);
+    }
+    const float mv = fmaf(one_m_b1, gv - m, m);
+    const float vv = v * b2 + (one_m_b2 * gv) * gv;
+    m = mv;
+    v = vv;
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    return pv + neg_step_size * (mv / denom);
+}
+
 __global__ void __launch_bounds__(256)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, int64_t n, float wd, float decay_mul, int decoupled,
@@ -75,18 +93,32 @@ adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restric
     const float neg_step_size = scal ? scal[1] : neg_step_size_h;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        float pv = p[i];
-        float gv = g[i];
-        if (wd != 0.f) {
-            if (decoupled) pv = pv * decay_mul;
-            else gv = fmaf(pv, wd, gv);
-        }
-        const float mv = fmaf(one_m_b1, gv - m[i], m[i]);
-        const float vv = v[i] * b2 + (one_m_b2 * gv) * gv;
+        float mv = m[i], vv = v[i];
+        p[i] = adam_elem(p[i], g[i], mv, vv, wd, decay_mul, decoupled, one_m_b1, b2, one_m_b2,
+                         bc2_sqrt, eps, neg_step_size);
         m[i] = mv;
         v[i] = vv;
-        const float denom = sqrtf(vv) / bc2_sqrt + eps;
-        p[i] = pv + neg_step_size * (mv / denom);
+    }
+}
+
+__global__ void __launch_bounds__(256)
+adam4_kernel(float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ m,
+             float4* __restrict__ v, int64_t n4, float wd, float decay_mul, int decoupled,
+             float one_m_b1, float b2, float one_m_b2, float bc2_sqrt_h, float eps,
+             float neg_step_size_h, const float* __restrict__ scal) {
+    const float bc2_sqrt = scal ? scal[0] : bc2_sqrt_h;
+    const float neg_step_size = scal ? scal[1] : neg_step_size_h;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 pv = p[i], gv = g[i];
+        float4 mv = m[i], vv = v[i], o;
+#define FH_ADAM_LANE(c) o.c = adam_elem(pv.c, gv.c, mv.c, vv.c, wd, decay_mul, decoupled, \
+                                        one_m_b1, b2, one_m_b2, bc2_sqrt, eps, neg_step_size)
+        FH_ADAM_LANE(x); FH_ADAM_LANE(y); FH_ADAM_LANE(z); FH_ADAM_LANE(w);
+#undef FH_ADAM_LANE
+        m[i] = mv;
+        v[i] = vv;
+        p[i] = o;
     }
 }
 
@@ -123,11 +155,22 @@ extern "C" int fh_adam_step(float* param, const float* grad, float* exp_avg, flo
     if (n == 0) return FH_OK;
     FH_REQUIRE(param && grad && exp_avg && exp_avg_sq, "adam_step: null pointer");
     // Python-double scalars are rounded to fp32 where ATen meets the fp32 tensor.
-    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param, grad,
-                       exp_avg, exp_avg_sq, n, (float)weight_decay,
-                       (float)(1.0 - lr * weight_decay), decoupled, (float)(1.0 - beta1),
-                       (float)beta2, (float)(1.0 - beta2), (float)bc2_sqrt, (float)eps,
-                       (float)(-step_size), scal_dev);
+    const bool vec = n % 4 == 0 &&
+                     ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) %
+                             16 == 0;
+    if (vec)
+        hipLaunchKernelGGL(adam4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream),
+                           (float4*)param, (const float4*)grad, (float4*)exp_avg,
+                           (float4*)exp_avg_sq, n / 4, (float)weight_decay,
+                           (float)(1.0 - lr * weight_decay), decoupled, (float)(1.0 - beta1),
+                           (float)beta2, (float)(1.0 - beta2), (float)bc2_sqrt, (float)eps,
+                           (float)(-step_size), scal_dev);
+    else
+        hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param,
+                           grad, exp_avg, exp_avg_sq, n, (float)weight_decay,
+                           (float)(1.0 - lr * weight_decay), decoupled, (float)(1.0 - beta1),
+                           (float)beta2, (float)(1.0 - beta2), (float)bc2_sqrt, (float)eps,
+                           (float)(-step_size), scal_dev);
     FH_LAUNCH_CHECK("adam_step");
     return FH_OK;
 }

@@ -218,3 +218,24 @@ def test_sgd_vector_and_scalar_paths_agree(mom, wd, first):
         torch.testing.assert_close(outs[0][1], bref, rtol=1e-6, atol=1e-6)
     else:
         assert torch.equal(outs[0][1], b0)  # no momentum: the buffer is never touched
+
+
+@pytest.mark.parametrize("wd,decoupled", [(0.0, False), (0.01, True), (0.01, False)])
+def test_adam_vector_and_scalar_paths_agree(wd, decoupled):
+    """fh_adam_step: float4 kernel on aligned slabs, scalar kernel otherwise — same bits
+    (Adam / AdamW of training.py:244-255; torch parity is test_train_gpu's)."""
+    n = 3 * 65536 + 64
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    p0, g0, m0 = (torch.randn(n, generator=gen) for _ in range(3))
+    v0 = torch.rand(n, generator=gen)
+    outs = []
+    for off in (0, 1):
+        t = [torch.zeros(n + 4, device="cuda") for _ in range(4)]
+        for buf, x in zip(t, (p0, g0, m0, v0)):
+            buf[off:off + n] = x.cuda()
+        ops.adam_step(*(buf[off:off + n] for buf in t), step=3, lr=1e-3, weight_decay=wd,
+                      decoupled=decoupled)
+        torch.cuda.synchronize()
+        outs.append([t[i][off:off + n].cpu() for i in (0, 2, 3)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
