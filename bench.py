@@ -52,14 +52,18 @@ CONFIGS = {
                samples=60000, strategy="iid", alpha=0.5, epochs=1, dp=None),
     "K2": dict(model="simple_cnn", kw={}, shape=(1, 28, 28), classes=10, clients=32,
                samples=60000, strategy="non_iid", alpha=0.5, epochs=1, dp=1.0),
+    # 8-GPU configs: `clients` / `samples` are PER GPU (the config's 1/8 slice: 64/8, 128/8,
+    # 256/8 clients over 50000/8 CIFAR images), so N=8 runs exactly the BASELINE config and
+    # N=1 runs one GPU's share of it (weak scaling)
     "K3": dict(model="federated_resnet", kw={"num_blocks": [1, 1, 1]}, shape=(3, 32, 32),
-               classes=10, clients=64, samples=50000, strategy="non_iid", alpha=0.5, epochs=1,
-               dp=4.0),
-    "K4": dict(model="federated_resnet", kw={}, shape=(3, 32, 32), classes=10, clients=128,
-               samples=50000, strategy="non_iid", alpha=0.5, epochs=5, dp=None),
+               classes=10, clients=8, samples=6250, strategy="non_iid", alpha=0.5, epochs=1,
+               dp=4.0, config_gpus=8),
+    "K4": dict(model="federated_resnet", kw={}, shape=(3, 32, 32), classes=10, clients=16,
+               samples=6250, strategy="non_iid", alpha=0.5, epochs=5, dp=None, config_gpus=8,
+               compression=("topk", 0.9)),
     "K5": dict(model="federated_resnet", kw={"num_classes": 100}, shape=(3, 32, 32),
-               classes=100, clients=256, samples=50000, strategy="non_iid", alpha=0.1, epochs=1,
-               dp=2.0),
+               classes=100, clients=32, samples=6250, strategy="non_iid", alpha=0.1, epochs=1,
+               dp=2.0, config_gpus=8),
 }
 # train FLOPs / image = 6*MACs - 2*MACs(first layer)
 TRAIN_FLOPS = {"simple_cnn": 24_995_328, "cifar10_cnn": 237_124_608,
@@ -74,12 +78,18 @@ def log(msg):
 
 
 def setup(args):
+    """One process per GPU (torchrun env).  --dist-backend gloo / --one-device exist to
+    rehearse the multi-rank path on a one-GPU box (every rank on cuda:0, FedAvg over gloo);
+    the measured configuration is RCCL ("nccl") with one GPU per rank."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     return world, rank, torch.device("cuda", local)
 
 
@@ -228,6 +238,10 @@ def main():
     ap.add_argument("--proxy-signal", type=float, default=0.14)
     ap.add_argument("--fp32-data", action="store_true",
                     help="pre-normalised fp32 shards instead of uint8 images + on-device transform")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (multi-rank path on a 1-GPU box)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="concurrent client lanes per GPU (default: planner / FH_LANES)")
     args = ap.parse_args()
@@ -245,8 +259,13 @@ def main():
     tf = None
     if raw:  # the reference loaders' train transforms (data_loader.py:298-301, 454-458)
         tf = ops.DataTransform.mnist() if cfg["shape"][0] == 1 else ops.DataTransform.cifar10()
+    comp = None
+    if cfg.get("compression"):
+        from fedhip.compress import CompressionConfig
+        algo, ratio = cfg["compression"]
+        comp = CompressionConfig(algorithm=algo, sparsity_ratio=ratio)
     rr = RankRound(template, train, mine, epochs=cfg["epochs"], device=dev, dp=dp,
-                   lanes=args.lanes, transform=tf)
+                   lanes=args.lanes, transform=tf, compression=comp)
     data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, rank, raw=raw)
     my_images = cfg["epochs"] * sum(train[k] for k in mine)
     total_images = cfg["epochs"] * sum(train)
@@ -310,7 +329,12 @@ def main():
                                    f"({cfg['clients']}/GPU), {cfg['strategy']}"
                                    f"{'(a=' + str(cfg['alpha']) + ')' if cfg['strategy'] == 'non_iid' else ''}, "
                                    f"{cfg['epochs']} local epoch(s), batch 32, {args.opt} lr {args.lr}, "
-                                   f"DP eps={cfg['dp']}, FedAvg{' RCCL all-reduce' if world > 1 else ''}",
+                                   f"DP eps={cfg['dp']}, "
+                                   f"{'compression ' + str(cfg['compression']) + ', ' if cfg.get('compression') else ''}"
+                                   f"FedAvg{' RCCL all-reduce' if world > 1 else ''}"
+                                   + (f" [{world}/{cfg['config_gpus']} GPU slice of the "
+                                      f"{cfg['clients'] * cfg['config_gpus']}-client config]"
+                                      if cfg.get('config_gpus') else ""),
                        "clients": C, "images_per_round": total_images, "batch": 32,
                        "parallelism": f"client-packed x{world} GPU",
                        "lanes": rr.trainer.cut},

@@ -425,9 +425,9 @@ extern "C" int fh_bn_fwd_train(const float* x, int64_t x_cs, float* y, int64_t y
     a.eps = eps; a.momentum = momentum; a.relu = relu;
     hipStream_t st = as_stream(stream);
     dim3 grid(a.S, C, nclients);
-    hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH(bn_stats_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_fwd_train stats");
-    hipLaunchKernelGGL(bn_apply_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH(bn_apply_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_fwd_train apply");
     return FH_OK;
 }
@@ -453,9 +453,9 @@ extern "C" int fh_bn_fwd_stats(const float* x, int64_t x_cs, const float* gamma,
     a.x_cs = x_cs; a.p_cs = p_cs; a.r_cs = r_cs;
     a.eps = eps; a.momentum = momentum;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(bn_stats_kernel, dim3(a.S, C, nclients), dim3(256), 0, st, a);
+    FH_LAUNCH(bn_stats_kernel, dim3(a.S, C, nclients), dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_fwd_stats stats");
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 256), nclients), dim3(256), 0,
+    FH_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 256), nclients), dim3(256), 0,
                        st, a, scale_out, shift_out, s_cs);
     FH_LAUNCH_CHECK("bn_fwd_stats finalize");
     return FH_OK;
@@ -475,7 +475,7 @@ extern "C" int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_
     a.rmean = (float*)running_mean; a.rvar = (float*)running_var;
     a.x_cs = x_cs; a.y_cs = y_cs; a.res_cs = res_cs; a.p_cs = p_cs; a.r_cs = r_cs;
     a.eps = eps; a.relu = relu;
-    hipLaunchKernelGGL(bn_eval_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
+    FH_LAUNCH(bn_eval_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
     FH_LAUNCH_CHECK("bn_fwd_eval");
     return FH_OK;
 }
@@ -503,9 +503,9 @@ extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int6
     a.dres_cs = dres_cs; a.g_cs = g_cs; a.relu = relu;
     hipStream_t st = as_stream(stream);
     dim3 grid(a.S, C, nclients);
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH(bn_bwd_reduce_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_bwd reduce");
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH(bn_bwd_apply_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_bwd apply");
     return FH_OK;
 }
@@ -544,9 +544,9 @@ extern "C" int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* 
     a.yo_cs = yo_cs; a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs; a.g_cs = g_cs; a.relu = relu;
     hipStream_t st = as_stream(stream);
     dim3 grid(a.S, C, nclients);
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH(bn_bwd_reduce_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_bwd_pool reduce");
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, st, a);
+    FH_LAUNCH(bn_bwd_apply_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_bwd_pool apply");
     return FH_OK;
 }

@@ -303,10 +303,10 @@ extern "C" int fh_quantize_rows(const float* x, int64_t x_cs, const float* base,
     float2* partial = reinterpret_cast<float2*>(ws);
     hipStream_t st = as_stream(stream);
     dim3 grid(nchunks, nclients);
-    hipLaunchKernelGGL(quant_minmax_kernel, grid, dim3(256), 0, st, x, x_cs, base, base_cs,
+    FH_LAUNCH(quant_minmax_kernel, grid, dim3(256), 0, st, x, x_cs, base, base_cs,
                        seg_offsets, chunk_offsets, nseg, nchunks, partial);
     FH_LAUNCH_CHECK("quantize_rows/minmax");
-    hipLaunchKernelGGL(quant_apply_kernel, grid, dim3(256), 0, st, x, x_cs, base, base_cs, out,
+    FH_LAUNCH(quant_apply_kernel, grid, dim3(256), 0, st, x, x_cs, base, base_cs, out,
                        out_cs, codes, codes_cs, seg_offsets, chunk_offsets, nseg, nchunks,
                        partial, 1 << bits, symmetric, scale_out, zp_out);
     FH_LAUNCH_CHECK("quantize_rows/apply");
@@ -338,15 +338,15 @@ extern "C" int fh_topk_rows(const float* x, int64_t x_cs, const float* base, int
     }
     dim3 grid(nchunks, nclients), sgrid(nseg, nclients);
     for (int r = 0; r < 4; ++r) {
-        hipLaunchKernelGGL(topk_hist_kernel, grid, dim3(256), 0, st, x, x_cs, base, base_cs,
+        FH_LAUNCH(topk_hist_kernel, grid, dim3(256), 0, st, x, x_cs, base, base_cs,
                            seg_offsets, chunk_offsets, nseg, state, hist, r,
                            r == 3 ? chunk_hist : nullptr, nchunks);
         FH_LAUNCH_CHECK("topk_rows/hist");
-        hipLaunchKernelGGL(topk_select_kernel, sgrid, dim3(64), 0, st, seg_k, nseg, state, hist,
+        FH_LAUNCH(topk_select_kernel, sgrid, dim3(64), 0, st, seg_k, nseg, state, hist,
                            r);
         FH_LAUNCH_CHECK("topk_rows/select");
     }
-    hipLaunchKernelGGL(topk_apply_kernel, grid, dim3(256), 0, st, x, x_cs, base, base_cs, out,
+    FH_LAUNCH(topk_apply_kernel, grid, dim3(256), 0, st, x, x_cs, base, base_cs, out,
                        out_cs, keep, keep_cs, seg_offsets, chunk_offsets, nseg, state,
                        chunk_hist, nchunks);
     FH_LAUNCH_CHECK("topk_rows/apply");

@@ -444,7 +444,7 @@ template <int OP, int KH, int KW, int S>
 static int launch_tile(const Tile& t, dim3 grid, const ConvArgs& a, hipStream_t st) {
 #define FH_IG(BM, BN, BK, WMV)                                                               \
     if (t.bm == BM && t.bn == BN && t.bk == BK && t.wavesm == WMV) {                         \
-        hipLaunchKernelGGL((igemm_kernel<OP, KH, KW, S, BM, BN, BK, WMV>), grid, dim3(256), 0, \
+        FH_LAUNCH((igemm_kernel<OP, KH, KW, S, BM, BN, BK, WMV>), grid, dim3(256), 0, \
                            st, a);                                                           \
         return FH_OK;                                                                        \
     }
@@ -606,7 +606,7 @@ static int run_mn(ConvArgs a, int kh, int kw, int stride, int nclients, void* ws
     FH_LAUNCH_CHECK(name);
     if (p.splits > 1) {
         dim3 eg((unsigned)ceil_div(a.N, 256), (unsigned)a.M, (unsigned)nclients);
-        hipLaunchKernelGGL(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
+        FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.N, out, out_cs, bias, b_cs, relu, accum, a.counts, a.batch, sp);
         FH_LAUNCH_CHECK(name);
     }
@@ -676,7 +676,7 @@ template <int OP, int W>
 static int dconv_launch_w(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_t st) {
 #define FH_DC(BM, WMV, CK, VEC)                                                                 \
     if (p.bm == BM && p.ck == CK && (a.wvec != 0) == VEC) {                                     \
-        hipLaunchKernelGGL((dconv_kernel<OP, W, BM, WMV, CK, VEC>), grid, dim3(256), 0, st, a);\
+        FH_LAUNCH((dconv_kernel<OP, W, BM, WMV, CK, VEC>), grid, dim3(256), 0, st, a);\
         return FH_OK;                                                                           \
     }
     FH_DC(32, 1, 8, true)
@@ -718,7 +718,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     FH_LAUNCH_CHECK(name);
     if (p.splits > 1) {
         dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
-        hipLaunchKernelGGL(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
+        FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
                            OP == OP_FWD ? a.relu : 0, OP == OP_FWD ? 0 : a.accumulate, a.counts,
                            a.batch, sp);
@@ -786,7 +786,7 @@ template <int W>
 static int dwgrad_launch_w(const DWPlan& p, dim3 grid, const DWArgs& a, hipStream_t st) {
 #define FH_DW(WCO, WCI, WPX, SPXV)                                                             \
     if (p.wco == WCO && p.wci == WCI && p.wpx == WPX && p.sr * W == SPXV) {                   \
-        hipLaunchKernelGGL((dconv_wgrad_kernel<W, WCO, WCI, WPX, SPXV / W>), grid, dim3(256), 0, \
+        FH_LAUNCH((dconv_wgrad_kernel<W, WCO, WCI, WPX, SPXV / W>), grid, dim3(256), 0, \
                            st, a);                                                            \
         return FH_OK;                                                                         \
     }
@@ -971,14 +971,14 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
         hipStream_t st = as_stream(stream);
         dim3 grid((unsigned)p.splits, (unsigned)(cout / 32), (unsigned)nclients);
-        if (w_ == 32) hipLaunchKernelGGL((dconv_wgrad_small_kernel<32, 3>), grid, dim3(256), 0, st, d);
-        else if (w_ == 16) hipLaunchKernelGGL((dconv_wgrad_small_kernel<16, 3>), grid, dim3(256), 0, st, d);
-        else hipLaunchKernelGGL((dconv_wgrad_small_kernel<8, 3>), grid, dim3(256), 0, st, d);
+        if (w_ == 32) FH_LAUNCH((dconv_wgrad_small_kernel<32, 3>), grid, dim3(256), 0, st, d);
+        else if (w_ == 16) FH_LAUNCH((dconv_wgrad_small_kernel<16, 3>), grid, dim3(256), 0, st, d);
+        else FH_LAUNCH((dconv_wgrad_small_kernel<8, 3>), grid, dim3(256), 0, st, d);
         FH_LAUNCH_CHECK("conv2d_wgrad small-cin");
         const int MN = a.M * a.N;
         const int wblocks = (int)ceil_div(MN, 64);
         const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
-        hipLaunchKernelGGL(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+        FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
                            (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
                            (const float*)d.bias_part, db, db_cs, a.M);
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
@@ -1007,7 +1007,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         const int MN = a.M * a.N;
         const int wblocks = (int)ceil_div(MN, 64);
         const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
-        hipLaunchKernelGGL(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+        FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
                            (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
                            (const float*)d.bias_part, db, db_cs, a.M);
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
@@ -1042,7 +1042,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
     const int MN = a.M * a.N;
     const int wblocks = (int)ceil_div(MN, 64);
     const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
-    hipLaunchKernelGGL(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+    FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
                        (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
                        (const float*)a.bias_part, db, db_cs, a.M);
     FH_LAUNCH_CHECK("conv2d_wgrad reduce");
@@ -1219,11 +1219,11 @@ extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, i
         // 44 us vs 75; with few clients the one-tile form keeps more workgroups)
         if (in_f % 128 == 0 && kLinearSkinny != 2 &&
             (int64_t)(in_f / 128) * nclients >= fill(256))
-            hipLaunchKernelGGL(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
+            FH_LAUNCH(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
                                dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs,
                                counts, batch, in_f, out_f);
         else
-            hipLaunchKernelGGL(linear_dgrad_skinny_kernel<1>, dim3((unsigned)(in_f / 32), nclients),
+            FH_LAUNCH(linear_dgrad_skinny_kernel<1>, dim3((unsigned)(in_f / 32), nclients),
                                dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs,
                                counts, batch, in_f, out_f);
         FH_LAUNCH_CHECK("linear_dgrad skinny");
@@ -1244,7 +1244,7 @@ extern "C" int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, in
                                int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
     if (kLinearSkinny && nclients > 0 && batch <= 32 && in_f % 128 == 0 && out_f > 0 && x &&
         dy && dw) {
-        hipLaunchKernelGGL(linear_wgrad_skinny_kernel,
+        FH_LAUNCH(linear_wgrad_skinny_kernel,
                            dim3((unsigned)(in_f / 128), (unsigned)ceil_div(out_f, 32), nclients),
                            dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
                            counts, batch, in_f, out_f);
@@ -1322,7 +1322,7 @@ extern "C" int fh_conv2d_persample_sqnorm(const float* x, int64_t x_cs, const fl
     if (rc) return rc;
     FH_LAUNCH_CHECK("conv2d_persample_sqnorm");
     const int tiles = (int)(grid.x * grid.y);
-    hipLaunchKernelGGL(conv_sq_reduce_kernel, dim3((unsigned)ceil_div(batch, 256), nclients),
+    FH_LAUNCH(conv_sq_reduce_kernel, dim3((unsigned)ceil_div(batch, 256), nclients),
                        dim3(256), 0, st, (const float*)workspace, tiles, batch, counts, sqnorm);
     FH_LAUNCH_CHECK("conv2d_persample_sqnorm reduce");
     return FH_OK;

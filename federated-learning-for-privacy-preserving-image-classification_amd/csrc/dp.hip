@@ -60,8 +60,11 @@ dp_apply_kernel(const float* __restrict__ local, int64_t ls, const float* __rest
                 int64_t gs, float* __restrict__ out, int64_t os, int64_t P,
                 const float* __restrict__ coef, const int32_t* __restrict__ clipped,
                 const float* __restrict__ sigma, const float* __restrict__ noise, int64_t ns,
-                uint64_t seed) {
+                uint64_t seed, const int64_t* __restrict__ row_ids) {
     const int z = blockIdx.y;
+    // Philox key: the row's global client id when given (ranks / lanes hold different
+    // clients in the same local row z — the noise must never repeat across clients)
+    const uint64_t key = row_ids ? (uint64_t)row_ids[z] : (uint64_t)z;
     const float* l = local + z * ls;
     const float* g = global ? global + z * gs : nullptr;
     float* o = out + z * os;
@@ -73,7 +76,7 @@ dp_apply_kernel(const float* __restrict__ local, int64_t ls, const float* __rest
          q += (int64_t)gridDim.x * blockDim.x) {
         float gauss[4];
         if (!nz) {
-            const uint4 r = Philox::gen(seed, (uint64_t)z, (uint64_t)q);
+            const uint4 r = Philox::gen(seed, key, (uint64_t)q);
             const float u1a = u01(r.x), u2a = u01(r.y), u1b = u01(r.z), u2b = u01(r.w);
             const float ra = sqrtf(-2.0f * logf(u1a)), rb = sqrtf(-2.0f * logf(u1b));
             float sa, ca, sb, cb;
@@ -109,7 +112,7 @@ extern "C" int fh_dp_delta_sqnorm(const float* local, int64_t local_stride, cons
     FH_REQUIRE(num_clients >= 0 && nseg >= 0, "dp_delta_sqnorm: bad sizes");
     if (num_clients == 0 || nseg == 0) return FH_OK;
     FH_REQUIRE(local && seg_offsets && seg_sqnorm, "dp_delta_sqnorm: null pointer");
-    hipLaunchKernelGGL(dp_sqnorm_kernel, dim3(nseg, num_clients), dim3(256), 0, as_stream(stream),
+    FH_LAUNCH(dp_sqnorm_kernel, dim3(nseg, num_clients), dim3(256), 0, as_stream(stream),
                        local, local_stride, global, global_stride, seg_offsets, nseg, seg_sqnorm);
     FH_LAUNCH_CHECK("dp_delta_sqnorm");
     return FH_OK;
@@ -126,7 +129,7 @@ extern "C" int fh_dp_clip_coef(const double* seg_sqnorm, int32_t num_clients, in
     FH_REQUIRE(seg_sqnorm && coef && clipped && sigma, "dp_clip_coef: null pointer");
     // Gaussian mechanism noise scale per unit sensitivity (privacy.py:209), in double.
     const double noise_scale = sqrt(2.0 * log(1.25 / delta)) / epsilon;
-    hipLaunchKernelGGL(dp_coef_kernel, dim3((unsigned)ceil_div(num_clients, 64)), dim3(64), 0,
+    FH_LAUNCH(dp_coef_kernel, dim3((unsigned)ceil_div(num_clients, 64)), dim3(64), 0,
                        as_stream(stream), seg_sqnorm, num_clients, nseg, max_norm, noise_scale,
                        total_norm, coef, clipped, sigma);
     FH_LAUNCH_CHECK("dp_clip_coef");
@@ -137,15 +140,16 @@ extern "C" int fh_dp_apply(const float* local, int64_t local_stride, const float
                            int64_t global_stride, float* out, int64_t out_stride,
                            int32_t num_clients, int64_t P, const float* coef,
                            const int32_t* clipped, const float* sigma, const float* noise_in,
-                           int64_t noise_stride, uint64_t seed, void* stream) {
+                           int64_t noise_stride, uint64_t seed, const int64_t* row_ids,
+                           void* stream) {
     FH_REQUIRE(num_clients >= 0 && P >= 0, "dp_apply: bad sizes");
     if (num_clients == 0 || P == 0) return FH_OK;
     FH_REQUIRE(local && out && coef && clipped && sigma, "dp_apply: null pointer");
     const int64_t nq = (P + 3) / 4;
     const int gx = (int)std::min<int64_t>(ceil_div(nq, 256), 2048);
-    hipLaunchKernelGGL(dp_apply_kernel, dim3(gx, num_clients), dim3(256), 0, as_stream(stream),
+    FH_LAUNCH(dp_apply_kernel, dim3(gx, num_clients), dim3(256), 0, as_stream(stream),
                        local, local_stride, global, global_stride, out, out_stride, P, coef,
-                       clipped, sigma, noise_in, noise_stride, seed);
+                       clipped, sigma, noise_in, noise_stride, seed, row_ids);
     FH_LAUNCH_CHECK("dp_apply");
     return FH_OK;
 }

@@ -103,7 +103,7 @@ extern "C" int fh_linear_persample_sqnorm(const float* x, int64_t x_cs, const fl
     FH_REQUIRE(nclients >= 0 && batch > 0 && in_f > 0 && out_f > 0, "linear_persample_sqnorm: bad shape");
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && dy && sqnorm, "linear_persample_sqnorm: null pointer");
-    hipLaunchKernelGGL(linear_sq_kernel, dim3(batch, nclients), dim3(256), 0, as_stream(stream), x,
+    FH_LAUNCH(linear_sq_kernel, dim3(batch, nclients), dim3(256), 0, as_stream(stream), x,
                        x_cs, dy, dy_cs, with_bias, counts, batch, in_f, out_f, sqnorm);
     FH_LAUNCH_CHECK("linear_persample_sqnorm");
     return FH_OK;
@@ -116,7 +116,7 @@ extern "C" int fh_dpsgd_clip_coef(const double* sqnorm, const int32_t* counts, i
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(sqnorm && coef, "dpsgd_clip_coef: null pointer");
     const int n = nclients * batch;
-    hipLaunchKernelGGL(clip_coef_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+    FH_LAUNCH(clip_coef_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
                        as_stream(stream), sqnorm, counts, nclients, batch, max_norm, coef);
     FH_LAUNCH_CHECK("dpsgd_clip_coef");
     return FH_OK;
@@ -128,7 +128,7 @@ extern "C" int fh_scale_rows(const float* in, int64_t in_cs, const float* coef,
     FH_REQUIRE(nclients >= 0 && batch > 0 && per_img > 0, "scale_rows: bad shape");
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(in && coef && out, "scale_rows: null pointer");
-    hipLaunchKernelGGL(scale_rows_kernel, dim3(ew_blocks((int64_t)batch * per_img), nclients),
+    FH_LAUNCH(scale_rows_kernel, dim3(ew_blocks((int64_t)batch * per_img), nclients),
                        dim3(256), 0, as_stream(stream), in, in_cs, coef, counts, batch, per_img,
                        out, out_cs);
     FH_LAUNCH_CHECK("scale_rows");
@@ -142,7 +142,7 @@ extern "C" int fh_dpsgd_noise(float* grad, int64_t g_cs, int64_t n, const int32_
     FH_REQUIRE(sigma_c >= 0.f, "dpsgd_noise: sigma*C must be >= 0");
     if (nclients == 0 || n == 0 || sigma_c == 0.f) return FH_OK;
     FH_REQUIRE(grad, "dpsgd_noise: null pointer");
-    hipLaunchKernelGGL(dpsgd_noise_kernel, dim3(ew_blocks(ceil_div(n, 4)), nclients), dim3(256), 0,
+    FH_LAUNCH(dpsgd_noise_kernel, dim3(ew_blocks(ceil_div(n, 4)), nclients), dim3(256), 0,
                        as_stream(stream), grad, g_cs, n, counts, batch, sigma_c, seed, seed_dev);
     FH_LAUNCH_CHECK("dpsgd_noise");
     return FH_OK;

@@ -123,14 +123,14 @@ extern "C" int fh_fedavg_weighted_sum(const float* rows, int64_t row_stride,
     if (vec_ok && P >= 4) {
         const int64_t P4 = P / 4;
         const int grid = (int)std::min<int64_t>(ceil_div(P4, 256), 8192);
-        hipLaunchKernelGGL(fedavg_vec4_kernel, dim3(grid), dim3(256), 0, st, rows, row_stride,
+        FH_LAUNCH(fedavg_vec4_kernel, dim3(grid), dim3(256), 0, st, rows, row_stride,
                            row_index, weights, num_clients, P4, out, accumulate);
         FH_LAUNCH_CHECK("fedavg_vec4");
         done = P4 * 4;
     }
     if (done < P) {
         const int grid = (int)std::min<int64_t>(ceil_div(P - done, 256), 8192);
-        hipLaunchKernelGGL(fedavg_scalar_kernel, dim3(grid), dim3(256), 0, st, rows, row_stride,
+        FH_LAUNCH(fedavg_scalar_kernel, dim3(grid), dim3(256), 0, st, rows, row_stride,
                            row_index, weights, num_clients, done, P, out, accumulate);
         FH_LAUNCH_CHECK("fedavg_scalar");
     }
@@ -143,7 +143,7 @@ extern "C" int fh_update_stats(const float* rows, int64_t row_stride, int32_t nu
     FH_REQUIRE(num_clients >= 0 && nseg >= 0, "update_stats: bad sizes");
     if (num_clients == 0 || nseg == 0) return FH_OK;
     FH_REQUIRE(rows && seg_offsets && seg_absmax && seg_nonfinite, "update_stats: null pointer");
-    hipLaunchKernelGGL(update_stats_kernel, dim3(nseg, num_clients), dim3(256), 0,
+    FH_LAUNCH(update_stats_kernel, dim3(nseg, num_clients), dim3(256), 0,
                        as_stream(stream), rows, row_stride, seg_offsets, nseg, seg_absmax,
                        seg_nonfinite);
     FH_LAUNCH_CHECK("update_stats");

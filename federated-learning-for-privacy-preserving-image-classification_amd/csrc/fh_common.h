@@ -12,6 +12,9 @@
 #include <stdint.h>
 #include <algorithm>
 #include <string>
+#include <tuple>
+#include <type_traits>
+#include <utility>
 
 #include "../../include/fedhip.h"
 
@@ -39,6 +42,75 @@ void set_error(const char* fmt, ...);
     } while (0)
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- kernel launches -------------------------------------------------------
+// Every kernel of the library is launched through FH_LAUNCH: the arguments are packed
+// into an owned, typed tuple (the kernel's own parameter types) and issued with
+// hipLaunchKernel.  While a step program is being recorded on this thread (program.hip,
+// fh_record_begin) the launch is also appended to it with its own copy of the argument
+// bytes, so a program never borrows storage from a HIP graph or the runtime.  The launch
+// geometry is validated before anything reaches the queue (an empty grid would be a
+// malformed dispatch packet).
+struct KernelArgs {
+    virtual ~KernelArgs() = default;
+    void** params = nullptr;
+};
+
+template <typename... P>
+struct KernelArgsT final : KernelArgs {
+    std::tuple<P...> vals;
+    void* ptrs[sizeof...(P) > 0 ? sizeof...(P) : 1];
+    explicit KernelArgsT(P... p) : vals(p...) { bind(std::index_sequence_for<P...>{}); }
+    KernelArgsT(const KernelArgsT&) = delete;
+    KernelArgsT& operator=(const KernelArgsT&) = delete;
+
+   private:
+    template <size_t... I>
+    void bind(std::index_sequence<I...>) {
+        ((ptrs[I] = (void*)&std::get<I>(vals)), ...);
+        params = ptrs;
+    }
+};
+
+struct Recorder;                            // program.hip
+extern thread_local Recorder* g_recorder;   // non-null while recording a step program
+void record_kernel(Recorder* r, const void* func, dim3 grid, dim3 block, size_t shmem,
+                   KernelArgs* args /* ownership passes */);
+
+inline bool launch_geometry_ok(dim3 grid, dim3 block) {
+    return grid.x && grid.y && grid.z && block.x && block.y && block.z &&
+           block.x * block.y * block.z <= 1024 && grid.y <= 65535u && grid.z <= 65535u;
+}
+
+template <typename... P, typename... A>
+inline hipError_t launch_kernel(void (*k)(P...), dim3 grid, dim3 block, size_t shmem,
+                                hipStream_t st, A&&... a) {
+    static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+    if (!launch_geometry_ok(grid, block)) return hipErrorInvalidConfiguration;
+    if (g_recorder) {
+        auto* owned = new KernelArgsT<std::decay_t<P>...>(static_cast<std::decay_t<P>>(a)...);
+        const hipError_t e = hipLaunchKernel((const void*)k, grid, block, owned->params, shmem, st);
+        if (e != hipSuccess) {
+            delete owned;
+            return e;
+        }
+        record_kernel(g_recorder, (const void*)k, grid, block, shmem, owned);
+        return e;
+    }
+    KernelArgsT<std::decay_t<P>...> args(static_cast<std::decay_t<P>>(a)...);
+    return hipLaunchKernel((const void*)k, grid, block, args.params, shmem, st);
+}
+
+#define FH_LAUNCH(kernel, grid, block, shmem, stream, ...)                                  \
+    do {                                                                                    \
+        const hipError_t _le = ::fh::launch_kernel(kernel, grid, block, shmem, stream,      \
+                                                   __VA_ARGS__);                            \
+        if (_le != hipSuccess) {                                                            \
+            ::fh::set_error("%s: launch of %s failed: %s", __func__, #kernel,               \
+                            hipGetErrorString(_le));                                        \
+            return FH_E_LAUNCH;                                                             \
+        }                                                                                   \
+    } while (0)
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -449,7 +449,7 @@ static int maxpool2_fwd_impl(const float* x, int64_t x_cs, const float* in_scale
     FH_REQUIRE(x && y && idx, "maxpool2_fwd: null pointer");
     const float keep = 1.0f - p_drop, scale = 1.0f / keep;
     const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
-    hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
+    FH_LAUNCH(maxpool2_fwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
                        as_stream(stream), x, x_cs, y, y_cs, idx, i_cs, mask, m_cs, counts, batch, C,
                        H, W, drop_mode, keep, scale, seed, seed_dev, in_scale, in_shift, aff_cs);
     FH_LAUNCH_CHECK("maxpool2_fwd");
@@ -489,7 +489,7 @@ extern "C" int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* id
     FH_REQUIRE(dy && idx && dx, "maxpool2_bwd: null pointer");
     const float scale = 1.0f / (1.0f - p_drop);
     const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
-    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
+    FH_LAUNCH(maxpool2_bwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
                        as_stream(stream), dy, dy_cs, idx, i_cs, mask, m_cs, xin, x_cs, dx, dx_cs,
                        counts, batch, C, H, W, scale);
     FH_LAUNCH_CHECK("maxpool2_bwd");
@@ -506,7 +506,7 @@ extern "C" int fh_dropout_fwd(const float* x, int64_t x_cs, float* y, int64_t y_
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && y, "dropout_fwd: null pointer");
     const float keep = 1.0f - p_drop, scale = 1.0f / keep;
-    hipLaunchKernelGGL(dropout_fwd_kernel, dim3(ew_grid(batch * per_img), nclients), dim3(256), 0,
+    FH_LAUNCH(dropout_fwd_kernel, dim3(ew_grid(batch * per_img), nclients), dim3(256), 0,
                        as_stream(stream), x, x_cs, y, y_cs, mask, m_cs, counts, batch, per_img,
                        drop_mode, keep, scale, seed, seed_dev);
     FH_LAUNCH_CHECK("dropout_fwd");
@@ -521,7 +521,7 @@ extern "C" int fh_dropout_bwd(const float* dy, int64_t dy_cs, const uint8_t* mas
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(dy && dx, "dropout_bwd: null pointer");
     const float scale = 1.0f / (1.0f - p_drop);
-    hipLaunchKernelGGL(dropout_bwd_kernel, dim3(ew_grid(batch * per_img), nclients), dim3(256), 0,
+    FH_LAUNCH(dropout_bwd_kernel, dim3(ew_grid(batch * per_img), nclients), dim3(256), 0,
                        as_stream(stream), dy, dy_cs, mask, m_cs, relu_out, r_cs, dx, dx_cs, counts,
                        batch, per_img, scale);
     FH_LAUNCH_CHECK("dropout_bwd");
@@ -536,7 +536,7 @@ extern "C" int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* t
     FH_REQUIRE(nclients >= 0 && batch > 0 && num_classes > 0, "ce_fwd_bwd: bad shape");
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(logits && targets && dlogits, "ce_fwd_bwd: null pointer");
-    hipLaunchKernelGGL(ce_kernel, dim3(nclients), dim3(256), 0, as_stream(stream), logits, l_cs,
+    FH_LAUNCH(ce_kernel, dim3(nclients), dim3(256), 0, as_stream(stream), logits, l_cs,
                        targets, t_cs, dlogits, d_cs, loss_out, acc_loss, acc_correct, acc_seen,
                        reset, counts, batch, num_classes);
     FH_LAUNCH_CHECK("ce_fwd_bwd");
@@ -553,7 +553,7 @@ extern "C" int fh_eval_metrics(const float* logits, int64_t l_cs, const int64_t*
     FH_REQUIRE(logits && targets, "eval_metrics: null pointer");
     FH_REQUIRE((class_correct == nullptr) == (class_total == nullptr),
                "eval_metrics: class_correct and class_total go together");
-    hipLaunchKernelGGL(eval_metrics_kernel, dim3(nclients), dim3(256), 0, as_stream(stream),
+    FH_LAUNCH(eval_metrics_kernel, dim3(nclients), dim3(256), 0, as_stream(stream),
                        logits, l_cs, targets, t_cs, counts, batch, num_classes, loss_sum, correct,
                        reinterpret_cast<unsigned long long*>(class_correct),
                        reinterpret_cast<unsigned long long*>(class_total));
@@ -568,7 +568,7 @@ extern "C" int fh_avgpool_fwd(const float* x, int64_t x_cs, float* y, int64_t y_
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && y, "avgpool_fwd: null pointer");
     const int64_t planes = (int64_t)batch * C;
-    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(ew_grid(planes * 64), nclients), dim3(256), 0,
+    FH_LAUNCH(avgpool_fwd_kernel, dim3(ew_grid(planes * 64), nclients), dim3(256), 0,
                        as_stream(stream), x, x_cs, y, y_cs, counts, batch, C, HW);
     FH_LAUNCH_CHECK("avgpool_fwd");
     return FH_OK;
@@ -580,7 +580,7 @@ extern "C" int fh_avgpool_bwd(const float* dy, int64_t dy_cs, float* dx, int64_t
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "avgpool_bwd: bad shape");
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(dy && dx, "avgpool_bwd: null pointer");
-    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(ew_grid((int64_t)batch * C * HW), nclients),
+    FH_LAUNCH(avgpool_bwd_kernel, dim3(ew_grid((int64_t)batch * C * HW), nclients),
                        dim3(256), 0, as_stream(stream), dy, dy_cs, dx, dx_cs, counts, batch, C, HW);
     FH_LAUNCH_CHECK("avgpool_bwd");
     return FH_OK;
@@ -593,7 +593,7 @@ extern "C" int fh_gather_batch(const float* data, const int64_t* labels, const i
     FH_REQUIRE(nclients >= 0 && batch > 0 && sample_elems > 0, "gather_batch: bad shape");
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(data && idx && x && (!y || labels), "gather_batch: null pointer");
-    hipLaunchKernelGGL(gather_kernel, dim3(ew_grid(batch * sample_elems), nclients), dim3(256), 0,
+    FH_LAUNCH(gather_kernel, dim3(ew_grid(batch * sample_elems), nclients), dim3(256), 0,
                        as_stream(stream), data, labels, idx, idx_cs, x, x_cs, y, y_cs, sample_elems,
                        counts, batch);
     FH_LAUNCH_CHECK("gather_batch");
@@ -617,7 +617,7 @@ extern "C" int fh_gather_u8(const uint8_t* data, const int64_t* labels, const in
         np.mean[c] = c < C ? mean[c] : 0.f;
         np.stdv[c] = c < C ? stdv[c] : 1.f;
     }
-    hipLaunchKernelGGL(gather_u8_kernel, dim3(ew_grid((int64_t)batch * C * H * W), nclients),
+    FH_LAUNCH(gather_u8_kernel, dim3(ew_grid((int64_t)batch * C * H * W), nclients),
                        dim3(256), 0, as_stream(stream), data, labels, idx, idx_cs, x, x_cs, y, y_cs,
                        counts, batch, C, H, W, np, pad, flip,
                        reinterpret_cast<const uchar4*>(aug_in), reinterpret_cast<uchar4*>(aug_out),

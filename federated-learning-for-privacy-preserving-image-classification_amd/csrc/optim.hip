@@ -137,11 +137,11 @@ extern "C" int fh_sgd_step(float* param, const float* grad, float* momentum_buf,
     const bool vec = n % 4 == 0 && ((uintptr_t)param | (uintptr_t)grad |
                                     (momentum != 0.f ? (uintptr_t)momentum_buf : 0)) % 16 == 0;
     if (vec)
-        hipLaunchKernelGGL(sgd4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream),
+        FH_LAUNCH(sgd4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream),
                            (float4*)param, (const float4*)grad, (float4*)momentum_buf, n / 4, -lr,
                            momentum, weight_decay, first_step);
     else
-        hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param,
+        FH_LAUNCH(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param,
                            grad, momentum_buf, n, -lr, momentum, weight_decay, first_step);
     FH_LAUNCH_CHECK("sgd_step");
     return FH_OK;
@@ -159,14 +159,14 @@ extern "C" int fh_adam_step(float* param, const float* grad, float* exp_avg, flo
                      ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) %
                              16 == 0;
     if (vec)
-        hipLaunchKernelGGL(adam4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream),
+        FH_LAUNCH(adam4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream),
                            (float4*)param, (const float4*)grad, (float4*)exp_avg,
                            (float4*)exp_avg_sq, n / 4, (float)weight_decay,
                            (float)(1.0 - lr * weight_decay), decoupled, (float)(1.0 - beta1),
                            (float)beta2, (float)(1.0 - beta2), (float)bc2_sqrt, (float)eps,
                            (float)(-step_size), scal_dev);
     else
-        hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param,
+        FH_LAUNCH(adam_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), param,
                            grad, exp_avg, exp_avg_sq, n, (float)weight_decay,
                            (float)(1.0 - lr * weight_decay), decoupled, (float)(1.0 - beta1),
                            (float)beta2, (float)(1.0 - beta2), (float)bc2_sqrt, (float)eps,

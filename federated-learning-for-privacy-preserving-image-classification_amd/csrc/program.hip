@@ -1,37 +1,52 @@
-// program.hip — step programs: a captured training step replayed as plain kernel
-// launches on the lane's own stream.
+// program.hip — step programs: a training step recorded once as a flat list of kernel
+// launches and re-issued with hipLaunchKernel on the lane's own stream.
 //
-// Why.  Concurrent client lanes (fedhip/lanes.py) each replay one captured step per
-// global step on their own stream.  Replaying the kernel list with hipLaunchKernel
-// instead of hipGraphLaunch, with the per-step input row moved by a kernel instead of a
-// device-to-device hipMemcpyAsync, measured +1.3 % client-images/s on KT (3 lanes,
+// Why.  Concurrent client lanes (fedhip/lanes.py) each issue one step per global step on
+// their own stream.  Re-issuing the step's kernels with hipLaunchKernel instead of
+// hipGraphLaunch, with the per-step input row moved by a kernel instead of a device-to-
+// device hipMemcpyAsync, measured +1.3 % client-images/s on KT (3 lanes,
 // profiles/r01_v10/launch_modes.txt) at ~2-3 us of host time per kernel, which the host
-// hides (it runs tens of steps ahead).  The kernels, arguments and order are the graph's,
-// so results are identical by construction.  (Under rocprofv3 --kernel-trace, lanes
-// replaying graphs or programs appear to advance in lockstep; HIP-event timelines
-// without the profiler show them overlapping — trust the events.)
+// hides (it runs tens of steps ahead).
+//
+// Ownership.  The program is recorded by the library's own launch path (FH_LAUNCH in
+// fh_common.h): while a recorder is active on the calling thread every kernel launch
+// appends {kernel, grid, block, LDS bytes, a private typed copy of its arguments}.  Nothing
+// is borrowed from a HIP graph node or from runtime storage, so the program stays valid
+// for exactly as long as the device buffers its arguments point at (the caller keeps
+// those alive — fedhip/engine.py holds them with the program).  The host side records
+// while the same step is captured into a HIP graph and compares the two: a step that
+// contains anything the recorder cannot see (a memset, a copy, a kernel launched outside
+// libfedhip) makes the recording invalid and the caller replays the graph instead.
+#include <memory>
 #include <vector>
 
 #include "fh_common.h"
 
 namespace fh {
 
-struct ProgOp {
-    int kind;  // 0 kernel, 1 memset, 2 memcpy
-    hipKernelNodeParams k;
-    hipMemsetParams ms;
-    hipMemcpy3DParms mc;
+struct RecordedKernel {
+    const void* func;
+    dim3 grid, block;
+    size_t shmem;
+    std::unique_ptr<KernelArgs> args;
 };
 
-struct Program {
-    std::vector<ProgOp> ops;
-    int kernels = 0;
+struct Recorder {
+    std::vector<RecordedKernel> kernels;
+    Recorder* prev = nullptr;  // recorders nest per thread (never in practice)
 };
+
+thread_local Recorder* g_recorder = nullptr;
+
+void record_kernel(Recorder* r, const void* func, dim3 grid, dim3 block, size_t shmem,
+                   KernelArgs* args) {
+    r->kernels.push_back(RecordedKernel{func, grid, block, shmem,
+                                        std::unique_ptr<KernelArgs>(args)});
+}
 
 }  // namespace fh
 
-using fh::ProgOp;
-using fh::Program;
+using fh::Recorder;
 
 #define FH_HIPCHK(expr, what)                                                  \
     do {                                                                       \
@@ -42,9 +57,35 @@ using fh::Program;
         }                                                                      \
     } while (0)
 
-extern "C" int fh_program_from_graph(void* graph, void** program_out, int32_t* kernels_out) {
-    if (!graph || !program_out) {
-        fh::set_error("fh_program_from_graph: null argument");
+extern "C" int fh_record_begin(void** program_out) {
+    if (!program_out) {
+        fh::set_error("fh_record_begin: null argument");
+        return FH_E_INVALID;
+    }
+    auto* r = new Recorder();
+    r->prev = fh::g_recorder;
+    fh::g_recorder = r;
+    *program_out = r;
+    return FH_OK;
+}
+
+extern "C" int fh_record_end(void* program, int32_t* kernels_out) {
+    auto* r = (Recorder*)program;
+    if (!r || fh::g_recorder != r) {
+        fh::set_error("fh_record_end: not the active recorder of this thread");
+        return FH_E_INVALID;
+    }
+    fh::g_recorder = r->prev;
+    r->prev = nullptr;
+    if (kernels_out) *kernels_out = (int32_t)r->kernels.size();
+    return FH_OK;
+}
+
+// Kernel / other node counts of a captured graph (the host compares them with a
+// recording of the same step: equal kernel counts and no other work node = complete).
+extern "C" int fh_graph_node_counts(void* graph, int32_t* kernels_out, int32_t* others_out) {
+    if (!graph || !kernels_out || !others_out) {
+        fh::set_error("fh_graph_node_counts: null argument");
         return FH_E_INVALID;
     }
     hipGraph_t g = (hipGraph_t)graph;
@@ -52,110 +93,32 @@ extern "C" int fh_program_from_graph(void* graph, void** program_out, int32_t* k
     FH_HIPCHK(hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
     std::vector<hipGraphNode_t> nodes(n);
     if (n) FH_HIPCHK(hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
-    size_t ne = 0;
-    FH_HIPCHK(hipGraphGetEdges(g, nullptr, nullptr, &ne), "hipGraphGetEdges");
-    std::vector<hipGraphNode_t> from(ne), to(ne);
-    if (ne) FH_HIPCHK(hipGraphGetEdges(g, from.data(), to.data(), &ne), "hipGraphGetEdges");
-    // Kahn's order (ties by capture order): one serial stream honours every edge
-    auto idx = [&](hipGraphNode_t x) {
-        for (size_t i = 0; i < n; ++i)
-            if (nodes[i] == x) return (int)i;
-        return -1;
-    };
-    std::vector<int> indeg(n, 0);
-    std::vector<std::vector<int>> succ(n);
-    for (size_t e = 0; e < ne; ++e) {
-        const int a = idx(from[e]), b = idx(to[e]);
-        if (a < 0 || b < 0) {
-            fh::set_error("fh_program_from_graph: edge to an unknown node");
-            return FH_E_INVALID;
-        }
-        succ[a].push_back(b);
-        ++indeg[b];
-    }
-    std::vector<int> order, ready;
-    for (size_t i = 0; i < n; ++i)
-        if (!indeg[i]) ready.push_back((int)i);
-    while (!ready.empty()) {
-        auto it = std::min_element(ready.begin(), ready.end());
-        const int v = *it;
-        ready.erase(it);
-        order.push_back(v);
-        for (int s : succ[v])
-            if (--indeg[s] == 0) ready.push_back(s);
-    }
-    if (order.size() != n) {
-        fh::set_error("fh_program_from_graph: graph has a cycle");
-        return FH_E_INVALID;
-    }
-    auto* prog = new Program();
-    for (int v : order) {
+    int32_t k = 0, o = 0;
+    for (size_t i = 0; i < n; ++i) {
         hipGraphNodeType t;
-        hipError_t e = hipGraphNodeGetType(nodes[v], &t);
-        ProgOp op{};
-        if (e == hipSuccess && t == hipGraphNodeTypeKernel) {
-            e = hipGraphKernelNodeGetParams(nodes[v], &op.k);
-            if (e == hipSuccess && (!op.k.kernelParams || op.k.extra)) {
-                delete prog;
-                fh::set_error("fh_program_from_graph: kernel node without kernelParams");
-                return FH_E_UNSUPPORTED;
-            }
-            op.kind = 0;
-            ++prog->kernels;
-        } else if (e == hipSuccess && t == hipGraphNodeTypeMemset) {
-            e = hipGraphMemsetNodeGetParams(nodes[v], &op.ms);
-            op.kind = 1;
-        } else if (e == hipSuccess && t == hipGraphNodeTypeMemcpy) {
-            e = hipGraphMemcpyNodeGetParams(nodes[v], &op.mc);
-            op.kind = 2;
-        } else if (e == hipSuccess && t == hipGraphNodeTypeEmpty) {
-            continue;
-        } else if (e == hipSuccess) {
-            delete prog;
-            fh::set_error("fh_program_from_graph: unsupported node type %d", (int)t);
-            return FH_E_UNSUPPORTED;
-        }
-        if (e != hipSuccess) {
-            delete prog;
-            fh::set_error("fh_program_from_graph: %s", hipGetErrorString(e));
-            return FH_E_LAUNCH;
-        }
-        prog->ops.push_back(op);
+        FH_HIPCHK(hipGraphNodeGetType(nodes[i], &t), "hipGraphNodeGetType");
+        if (t == hipGraphNodeTypeKernel) ++k;
+        else if (t != hipGraphNodeTypeEmpty) ++o;
     }
-    *program_out = prog;
-    if (kernels_out) *kernels_out = prog->kernels;
+    *kernels_out = k;
+    *others_out = o;
     return FH_OK;
 }
 
 extern "C" int fh_program_launch(void* program, void* stream) {
-    auto* prog = (Program*)program;
-    if (!prog) {
+    auto* r = (Recorder*)program;
+    if (!r) {
         fh::set_error("fh_program_launch: null program");
         return FH_E_INVALID;
     }
-    hipStream_t st = (hipStream_t)stream;
-    for (const ProgOp& op : prog->ops) {
-        if (op.kind == 0) {
-            FH_HIPCHK(hipLaunchKernel(op.k.func, op.k.gridDim, op.k.blockDim, op.k.kernelParams,
-                                      op.k.sharedMemBytes, st),
-                      "fh_program_launch kernel");
-        } else if (op.kind == 1) {
-            const hipMemsetParams& m = op.ms;
-            if (m.elementSize == 4 && m.height <= 1) {
-                FH_HIPCHK(hipMemsetD32Async((hipDeviceptr_t)m.dst, m.value, m.width, st),
-                          "fh_program_launch memset");
-            } else if (m.elementSize == 1) {
-                FH_HIPCHK(hipMemset2DAsync(m.dst, m.pitch ? m.pitch : m.width, (int)m.value,
-                                           m.width, m.height ? m.height : 1, st),
-                          "fh_program_launch memset");
-            } else {
-                fh::set_error("fh_program_launch: memset element size %u", m.elementSize);
-                return FH_E_UNSUPPORTED;
-            }
-        } else {
-            FH_HIPCHK(hipMemcpy3DAsync(&op.mc, st), "fh_program_launch memcpy");
-        }
+    if (fh::g_recorder == r) {
+        fh::set_error("fh_program_launch: program is still recording");
+        return FH_E_INVALID;
     }
+    hipStream_t st = (hipStream_t)stream;
+    for (const auto& k : r->kernels)
+        FH_HIPCHK(hipLaunchKernel(k.func, k.grid, k.block, k.args->params, k.shmem, st),
+                  "fh_program_launch");
     return FH_OK;
 }
 
@@ -176,13 +139,17 @@ extern "C" int fh_copy_bytes(const void* src, void* dst, int64_t nbytes, void* s
     if (!nbytes) return FH_OK;
     const int64_t n16 = nbytes / 16;
     const int blocks = (int)std::min<int64_t>((n16 + 255) / 256, 1024);
-    hipLaunchKernelGGL(copy_bytes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                       (const uint4*)src, (uint4*)dst, n16);
-    FH_HIPCHK(hipGetLastError(), "fh_copy_bytes");
+    FH_LAUNCH(copy_bytes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+              (const uint4*)src, (uint4*)dst, n16);
     return FH_OK;
 }
 
 extern "C" int fh_program_destroy(void* program) {
-    delete (Program*)program;
+    auto* r = (Recorder*)program;
+    if (r && fh::g_recorder == r) {
+        fh::set_error("fh_program_destroy: program is still recording");
+        return FH_E_INVALID;
+    }
+    delete r;
     return FH_OK;
 }

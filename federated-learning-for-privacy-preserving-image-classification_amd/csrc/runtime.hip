@@ -52,4 +52,4 @@ extern "C" int fh_stream_destroy(void* stream) {
 }
 
 // 0xMMmmpp
-extern "C" int fh_version(void) { return 0x000100; }
+extern "C" int fh_version(void) { return 0x000200; }

@@ -37,7 +37,7 @@ SIGNATURES = {
     "fh_update_stats": (I32, [P, I64, I32, P, I32, P, P, P]),
     "fh_dp_delta_sqnorm": (I32, [P, I64, P, I64, I32, P, I32, P, P]),
     "fh_dp_clip_coef": (I32, [P, I32, I32, F64, F64, F64, P, P, P, P, P]),
-    "fh_dp_apply": (I32, [P, I64, P, I64, P, I64, I32, I64, P, P, P, P, I64, U64, P]),
+    "fh_dp_apply": (I32, [P, I64, P, I64, P, I64, I32, I64, P, P, P, P, I64, U64, P, P]),
     "fh_sgd_step": (I32, [P, P, P, I64, F32, F32, F32, I32, P]),
     "fh_adam_step": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, I32, F64, F64, P, P]),
     "fh_conv2d_fwd_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
@@ -90,7 +90,9 @@ SIGNATURES = {
     "fh_get_fill_fraction": (F32, []),
     "fh_stream_create": (I32, [I32, P, I32, P]),
     "fh_stream_destroy": (I32, [P]),
-    "fh_program_from_graph": (I32, [P, P, P]),
+    "fh_record_begin": (I32, [P]),
+    "fh_record_end": (I32, [P, P]),
+    "fh_graph_node_counts": (I32, [P, P, P]),
     "fh_program_launch": (I32, [P, P]),
     "fh_program_destroy": (I32, [P]),
     "fh_copy_bytes": (I32, [P, P, I64, P]),

@@ -26,8 +26,10 @@ a round.
 """
 from __future__ import annotations
 
+import atexit
 import math
 import os
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -38,8 +40,23 @@ from ._lib import FedHipError, load
 from .net import PackedNet
 
 
-# FH_LAUNCH=graph|program overrides how captured steps are replayed (diagnostics)
+# FH_LAUNCH=graph|program|eager overrides how steps after the first are issued
+# (diagnostics; "eager" = no capture at all, e.g. under rocprofv3 --pmc)
 _LAUNCH_ENV = os.environ.get("FH_LAUNCH", "")
+
+# Every trainer's captured steps are released at exit, programs before graphs and
+# after a device sync, while the HIP runtime is still up (destroying captured graphs
+# during interpreter teardown aborted a profiled run in round 1).
+_TRAINERS = weakref.WeakSet()
+
+
+@atexit.register
+def _release_all():
+    for t in list(_TRAINERS):
+        try:
+            t.release_graphs()
+        except Exception:
+            pass
 
 
 @dataclass
@@ -136,6 +153,7 @@ class PackedTrainer:
         self.probe_first_only = False  # lanes: probe only the (serialised) first step
         self._graphs = {}
         self._graph_pool = None
+        _TRAINERS.add(self)
 
     # ------------------------------------------------------------ state I/O
     def load_module_state(self, slot, model):
@@ -236,8 +254,8 @@ class PackedTrainer:
                        counts=counts)
 
     # ------------------------------------------------------------ a local-training round
-    def make_plan(self, shard_sizes, epochs, generator=None):
-        return plan_round(shard_sizes, epochs, self.batch, generator)
+    def make_plan(self, shard_sizes, epochs, generator=None, client_seeds=None):
+        return plan_round(shard_sizes, epochs, self.batch, generator, client_seeds)
 
     def run_round(self, data, labels, shard_offsets, plan, optimizer_type="sgd", lr=0.01,
                   seed=0):
@@ -261,8 +279,8 @@ class PackedTrainer:
         return dict(data=data, labels=labels, plan=plan, seed=seed, rows=rows, cur=cur,
                     views=views, sample_elems=int(math.prod(self.net.in_shape)),
                     full_batch=(plan["counts"] == self.batch).all(dim=1).tolist(),
-                    graphs=(self.use_graphs and self.on_step is None and self.pre_step is None
-                            and not ops.PROBE.enabled))
+                    graphs=(self.use_graphs and _LAUNCH_ENV != "eager" and self.on_step is None
+                            and self.pre_step is None and not ops.PROBE.enabled))
 
     def issue_step(self, st, g):
         """Launch global step g of the round (eager or graph replay) on the current stream."""
@@ -345,8 +363,10 @@ class PackedTrainer:
 
     def _replay(self, n, data, labels, views, sample_elems):
         """Replay the captured step for n active clients: as a HIP graph, or (launch_mode
-        "program", concurrent lanes) as its kernel list issued on this trainer's stream
-        (csrc/program.hip; measured +1.3 % on KT with three lanes)."""
+        "program", concurrent lanes) as its recorded kernel list issued on this trainer's
+        stream (csrc/program.hip; measured +1.3 % on KT with three lanes).  The program is
+        recorded by libfedhip during the same capture; if it did not see every node of the
+        graph (a non-libfedhip op inside the step) the graph is replayed instead."""
         key = (n, self.opt_type, self.lr, self.transform, data.data_ptr(), labels.data_ptr(),
                views["gidx"].data_ptr(), tuple(views["gidx"].shape))
         mode = _LAUNCH_ENV or self.launch_mode
@@ -357,22 +377,38 @@ class PackedTrainer:
             if self._graph_pool is None:
                 self._graph_pool = torch.cuda.graph_pool_handle()
             graph = torch.cuda.CUDAGraph(keep_graph=(mode == "program"))
+            prog = None
             # capture on this trainer's own stream when it has one, so the split-K scratch
             # (keyed by stream) is the lane's, never shared with a concurrently running lane
             with torch.cuda.graph(graph, pool=self._graph_pool, stream=self.stream):
-                self._gather(data, labels, views, n, sample_elems)
-                self._step_launches(n, views["counts"], views["reset"], first=False,
-                                    adam_dev=views["adam"])
+                rec = ops.Program.record_begin() if mode == "program" else None
+                try:
+                    self._gather(data, labels, views, n, sample_elems)
+                    self._step_launches(n, views["counts"], views["reset"], first=False,
+                                        adam_dev=views["adam"])
+                finally:
+                    if rec is not None:
+                        prog = ops.Program.record_end(rec)
             net.seed_dev = None
-            prog = None
-            if mode == "program":
-                prog = ops.Program.from_graph(graph)
+            if prog is not None and not prog.complete_for(graph):
+                prog.release()  # fail closed: replay the graph
+                prog = None
             entry = self._graphs[key] = (graph, prog)
         graph, prog = entry
         if prog is not None:
             prog.launch(torch.cuda.current_stream(self.device))
         else:
             graph.replay()
+
+    def release_graphs(self):
+        """Drop step programs, then graphs (programs reference the graphs' pool memory);
+        called before interpreter teardown (fedhip/engine.py atexit) and on demand."""
+        if self._graphs:
+            torch.cuda.synchronize(self.device)
+        for graph, prog in self._graphs.values():
+            if prog is not None:
+                prog.release()
+        self._graphs.clear()
 
     def collect_metrics(self, plan, epochs):
         loss = self.acc_loss.cpu()
@@ -387,7 +423,7 @@ class PackedTrainer:
         return out
 
 
-def plan_round(shard_sizes, epochs, batch, generator=None):
+def plan_round(shard_sizes, epochs, batch, generator=None, client_seeds=None):
     """Host-side schedule for one round (integer bookkeeping only).
 
     shard_sizes[k] = train samples of slot k; slots must be ordered so that
@@ -398,7 +434,10 @@ def plan_round(shard_sizes, epochs, batch, generator=None):
       counts[g,k] valid images of slot k at step g (last batch partial, 0 when done)
       reset[g,k]  1 at the first batch of each of slot k's epochs
       index[g,k,:] positions inside slot k's shard: a fresh torch.randperm per
-               client per epoch, as DataLoader(shuffle=True) draws them."""
+               client per epoch, as DataLoader(shuffle=True) draws them — from
+               `generator` in slot order, or (client_seeds[k] given) from slot k's own
+               generator, so a client's batches do not depend on which other clients
+               share its GPU / rank (each reference client shuffles with its own RNG)."""
     B = batch
     S = len(shard_sizes)
     steps = [math.ceil(n / B) for n in shard_sizes]
@@ -409,10 +448,15 @@ def plan_round(shard_sizes, epochs, batch, generator=None):
     counts = np.zeros((G, S), dtype=np.int32)
     reset = np.zeros((G, S), dtype=np.int32)
     index = np.zeros((G, S, B), dtype=np.int64)
+    if client_seeds is not None and len(client_seeds) != S:
+        raise FedHipError("plan_round: one client seed per slot")
     for k, n in enumerate(shard_sizes):
         st = steps[k]
+        gk = generator
+        if client_seeds is not None:
+            gk = torch.Generator().manual_seed(int(client_seeds[k]) & 0x7FFFFFFFFFFFFFFF)
         for e in range(epochs):
-            perm = torch.randperm(n, generator=generator)  # drawn even for n == 0
+            perm = torch.randperm(n, generator=gk)  # drawn even for n == 0
             if not st:
                 continue
             g0 = e * st

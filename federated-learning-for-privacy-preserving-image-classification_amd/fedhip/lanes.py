@@ -84,7 +84,7 @@ class LanedTrainer:
     """PackedTrainer-compatible round driver over L concurrent lanes (see module doc)."""
 
     def __init__(self, model, slot_steps: Sequence[int], batch=32, device="cuda",
-                 lanes=None, cut=None):
+                 lanes=None, cut=None, salt=0):
         self.device = torch.device(device)
         S = len(slot_steps)
         if lanes is None:
@@ -111,6 +111,10 @@ class LanedTrainer:
         self.lanes = [PackedTrainer(model, cut[i + 1] - cut[i], batch, self.device,
                                     storage=self.storage, row0=cut[i])
                       for i in range(len(cut) - 1)]
+        # dropout / augmentation Philox keys: per lane (row0) and per rank (salt), so no
+        # two clients anywhere in the job share a stream
+        for ln in self.lanes:
+            ln.net.salt = (ln.net.salt + salt * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
         self._own_streams = []
         if len(self.lanes) > 1:
             for i, ln in enumerate(self.lanes):
@@ -212,10 +216,12 @@ class LanedTrainer:
                 return ln, slot - self.cut[i]
         raise IndexError(slot)
 
-    def make_plan(self, shard_sizes, epochs, generator=None):
-        """One plan per lane; randperms are drawn in slot order, as for a single lane."""
+    def make_plan(self, shard_sizes, epochs, generator=None, client_seeds=None):
+        """One plan per lane; randperms are drawn in slot order, as for a single lane (or
+        per client from client_seeds, see plan_round)."""
+        cs = lambda i: None if client_seeds is None else client_seeds[self.cut[i]:self.cut[i + 1]]
         return [plan_round(shard_sizes[self.cut[i]:self.cut[i + 1]], epochs, self.batch,
-                           generator) for i in range(len(self.lanes))]
+                           generator, cs(i)) for i in range(len(self.lanes))]
 
     def run_round(self, data, labels, shard_offsets, plans, optimizer_type="sgd", lr=0.01,
                   seed=0):

@@ -119,29 +119,47 @@ def copy_bytes(src: torch.Tensor, dst: torch.Tensor):
 
 
 class Program:
-    """A captured step as a flat kernel list (csrc/program.hip): built once from a
-    torch.cuda.CUDAGraph(keep_graph=True), launched with hipLaunchKernel on any stream.
-    Keeps the graph (it owns the kernel argument storage) alive."""
+    """A training step as a flat kernel list (csrc/program.hip), recorded by libfedhip's
+    own launch path while the step is captured into a HIP graph, re-issued with
+    hipLaunchKernel on any stream.  The program owns its kernel handles and argument bytes;
+    the device buffers the arguments point at belong to the trainer (and to the graph's
+    memory pool, so the graph is kept alive beside the program)."""
 
-    def __init__(self, graph, handle, kernels):
-        self.graph, self.handle, self.kernels = graph, handle, kernels
+    def __init__(self, handle, kernels):
+        self.handle, self.kernels = handle, kernels
+
+    @staticmethod
+    def record_begin():
+        h = ctypes.c_void_p()
+        call("fh_record_begin", ctypes.byref(h))
+        return h.value
 
     @classmethod
-    def from_graph(cls, graph):
-        h, nk = ctypes.c_void_p(), ctypes.c_int32()
-        call("fh_program_from_graph", graph.raw_cuda_graph(), ctypes.byref(h), ctypes.byref(nk))
-        return cls(graph, h.value, nk.value)
+    def record_end(cls, handle):
+        nk = ctypes.c_int32()
+        call("fh_record_end", handle, ctypes.byref(nk))
+        return cls(handle, nk.value)
+
+    def complete_for(self, graph) -> bool:
+        """True when the recording saw every work node of `graph` (captured in the same
+        pass): the same number of kernels and no memset / copy / foreign node."""
+        k, o = ctypes.c_int32(), ctypes.c_int32()
+        call("fh_graph_node_counts", graph.raw_cuda_graph(), ctypes.byref(k), ctypes.byref(o))
+        return o.value == 0 and k.value == self.kernels
 
     def launch(self, stream):
         call("fh_program_launch", self.handle, stream.cuda_stream)
 
-    def __del__(self):
+    def release(self):
         if getattr(self, "handle", None):
-            try:
-                call("fh_program_destroy", self.handle)
-            except Exception:
-                pass
+            call("fh_program_destroy", self.handle)
             self.handle = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
 
 
 _FILL = [1.0]
@@ -322,12 +340,16 @@ def dp_clip_coef(seg_sqnorm, max_norm, epsilon, delta):
     return total, coef, clipped, sigma
 
 
-def dp_apply(local, global_, out, coef, clipped, sigma, noise=None, seed=0, P=None):
+def dp_apply(local, global_, out, coef, clipped, sigma, noise=None, seed=0, P=None, row_ids=None):
+    """row_ids: int64 [C] global client id of each row — the Philox key of its noise (None:
+    the local row index; only safe when one engine holds every client)."""
     C = coef.numel()
+    if row_ids is not None and (row_ids.dtype != torch.int64 or row_ids.numel() != C):
+        raise FedHipError("dp_apply: row_ids must be int64 with one id per row")
     P = local.shape[1] if P is None else P
     call("fh_dp_apply", ptr(local), local.stride(0), ptr(global_), _cs(global_), ptr(out),
          out.stride(0), C, P, ptr(coef), ptr(clipped), ptr(sigma), ptr(noise), _cs(noise),
-         int(seed) & 0xFFFFFFFFFFFFFFFF, stream_handle())
+         int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(row_ids), stream_handle())
     return out
 
 

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import math
 import os
+import secrets
 import sys
 import time
 from dataclasses import dataclass
@@ -43,7 +44,8 @@ class DPConfig:
 class RankRound:
     def __init__(self, template_model, all_train_sizes: Sequence[int], my_clients: Sequence[int],
                  epochs: int = 1, batch: int = 32, device="cuda", dp: Optional[DPConfig] = None,
-                 group=None, lanes=None, compression=None, transform=None):
+                 group=None, lanes=None, compression=None, transform=None, dp_seed=None,
+                 shuffle_seed=None):
         self.device = torch.device(device)
         self._template = template_model
         self.B, self.epochs, self.dp, self.group = batch, epochs, dp, group
@@ -53,8 +55,10 @@ class RankRound:
         self.slots = sorted(self.clients, key=lambda k: (-math.ceil(self.all_sizes[k] / batch), k))
         self.slot_of = {k: i for i, k in enumerate(self.slots)}
         steps = [epochs * math.ceil(self.all_sizes[k] / batch) for k in self.slots]
+        self.distributed = group is not None or (dist.is_available() and dist.is_initialized())
+        self.rank = dist.get_rank(group) if self.distributed else 0
         self.trainer = LanedTrainer(template_model, steps or [0], batch=batch, device=self.device,
-                                    lanes=lanes)
+                                    lanes=lanes, salt=self.rank)
         self.transform = transform  # ops.DataTransform when the shards are raw uint8 images
         self.trainer.transform = transform
         L = self.trainer.layout
@@ -72,6 +76,17 @@ class RankRound:
                                 device=self.device)
         self.rows = torch.tensor([self.slot_of[k] for k in self.clients], dtype=torch.int32,
                                  device=self.device)
+        # update-level DP noise: Philox keyed by (round key, global client id, element), so
+        # no two clients — on any rank or lane — ever draw the same noise; the round key
+        # comes from a secret base seed (os.urandom) unless the caller fixes one (tests /
+        # reproducible benchmarks: a public seed makes the noise recomputable, i.e. no
+        # privacy)
+        self.slot_ids = torch.tensor(list(self.slots), dtype=torch.int64, device=self.device)
+        self.dp_seed = secrets.randbits(63) if dp_seed is None else int(dp_seed)
+        # data shuffling when run() gets no generator: every client draws its epochs'
+        # permutations from its own generator keyed by (shuffle seed, round seed, client
+        # id) — independent of the rank / lane / slot it lands on
+        self.shuffle_seed = secrets.randbits(62) if shuffle_seed is None else int(shuffle_seed)
         self.partial = torch.zeros(self.P, device=self.device)
         # global BN running statistics for evaluation (f-1; divergence D13): FedAvg of the
         # clients' buffers with the same weights.  Clients keep their own buffers (D4).
@@ -101,7 +116,11 @@ class RankRound:
         _t = [time.perf_counter()] if _HOST_TIMING else None
         tr.params[:S, :self.P].copy_(self.global_flat.expand(S, -1))  # all start from global
         sizes = [self.all_sizes[k] for k in self.slots]
-        plan = tr.make_plan(sizes, self.epochs, generator=generator)
+        cseeds = None
+        if generator is None:
+            cseeds = [(self.shuffle_seed * 0x9E3779B97F4A7C15 + seed * 0xBF58476D1CE4E5B9
+                       + k * 0x94D049BB133111EB) & 0x7FFFFFFFFFFFFFFF for k in self.slots]
+        plan = tr.make_plan(sizes, self.epochs, generator=generator, client_seeds=cseeds)
         if _t:
             _t.append(time.perf_counter())
         metrics = tr.run_round(data, labels, slot_offsets, plan, optimizer_type=optimizer_type,
@@ -116,7 +135,7 @@ class RankRound:
                           base=self.global_flat.view(1, -1).expand(S, -1))
         # FedAvg: this rank's partial sum in client-list order, then RCCL all-reduce.
         ops.fedavg_weighted_sum(tr.params, self.w32, self.partial, row_index=self.rows, P=self.P)
-        distributed = self.group is not None or (dist.is_available() and dist.is_initialized())
+        distributed = self.distributed
         if distributed:
             dist.all_reduce(self.partial, op=dist.ReduceOp.SUM, group=self.group)
         self.global_flat.copy_(self.partial)
@@ -150,6 +169,8 @@ class RankRound:
                                  tr.seg_offsets, S)
         total, coef, clipped, sigma = ops.dp_clip_coef(sq, dp.max_grad_norm, dp.epsilon, dp.delta)
         g = self.global_flat.view(1, -1).expand(S, -1)
-        ops.dp_apply(tr.params, g, tr.params, coef, clipped, sigma, P=self.P,
-                     seed=(seed * 6364136223846793005 + 1442695040888963407) & ((1 << 64) - 1))
+        key = (self.dp_seed * 6364136223846793005 + seed * 1442695040888963407
+               + self.round_index) & ((1 << 64) - 1)
+        ops.dp_apply(tr.params, g, tr.params, coef, clipped, sigma, P=self.P, seed=key,
+                     row_ids=self.slot_ids[:S])
         self.last_dp = (total, clipped, sigma)

@@ -25,6 +25,7 @@ import torch
 
 from fedhip import ops
 
+from ..shared.interfaces import AggregationServiceInterface
 from ..shared.models import GlobalModel, ModelUpdate, ModelWeights
 from ..shared.validation import ModelUpdateValidator, validate_model_compatibility
 
@@ -35,7 +36,7 @@ class FedAvgError(Exception):
     """Any aggregation failure (reference :20-22)."""
 
 
-class FedAvgAggregator:
+class FedAvgAggregator(AggregationServiceInterface):
     def __init__(self, min_clients: int = 2, max_clients: Optional[int] = None,
                  validate_updates: bool = True, device: Optional[torch.device] = None):
         self.min_clients, self.max_clients = min_clients, max_clients
@@ -77,6 +78,8 @@ class FedAvgAggregator:
         """Weighted FedAvg of client rows already on the device ([clients, P] fp32).
         Rows are summed in the order of `row_index` (default: row order)."""
         C = len(num_samples)
+        if C == 0:
+            raise FedAvgError("No updates to aggregate")
         w = self._calculate_sample_weights_n(list(num_samples))
         dev = packed.device
         w32 = torch.tensor(w, dtype=torch.float32, device=dev)
@@ -84,8 +87,6 @@ class FedAvgAggregator:
                                                           device=dev)
         if out is None:
             out = torch.empty(packed.shape[1], dtype=torch.float32, device=dev)
-        if C == 0:
-            raise FedAvgError("No updates to aggregate")
         ops.fedavg_weighted_sum(packed, w32, out, row_index=idx)
         return out
 

@@ -45,12 +45,3 @@ class PrivacyEngineInterface(ABC):
     def clip_gradients(self, gradients: ModelWeights, max_norm: float) -> ModelWeights:
         ...
 
-
-def _register():
-    """Declare the HIP implementations as virtual subclasses of the contracts."""
-    from ..aggregation.fedavg import FedAvgAggregator
-    from .models_pytorch import FederatedCNNBase
-    from .privacy import DifferentialPrivacyEngine
-    AggregationServiceInterface.register(FedAvgAggregator)
-    ModelInterface.register(FederatedCNNBase)
-    PrivacyEngineInterface.register(DifferentialPrivacyEngine)

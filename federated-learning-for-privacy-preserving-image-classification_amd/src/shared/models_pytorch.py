@@ -16,12 +16,13 @@ from typing import Any, Dict, List
 import torch
 import torch.nn as nn
 
+from .interfaces import ModelInterface
 from .models import ModelWeights
 
 logger = logging.getLogger(__name__)
 
 
-class FederatedCNNBase(nn.Module):
+class FederatedCNNBase(nn.Module, ModelInterface):
     """get/set weights over named_parameters (reference :18-56)."""
 
     model_name = "base_cnn"

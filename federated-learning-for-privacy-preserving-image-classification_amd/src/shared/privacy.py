@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import logging
 import math
+import secrets
 from datetime import datetime
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -27,6 +28,7 @@ import torch
 
 from fedhip import ops
 
+from .interfaces import PrivacyEngineInterface
 from .models import ModelWeights, PrivacyConfig
 
 logger = logging.getLogger(__name__)
@@ -136,11 +138,16 @@ class GradientClipper:
 
 
 class GaussianNoiseGenerator:
-    """Gaussian mechanism noise, generated on the device."""
+    """Gaussian mechanism noise, generated on the device.
 
-    def __init__(self, device: Optional[torch.device] = None, seed: int = 0):
+    seed None (default) draws a secret 64-bit Philox key from os.urandom, as the
+    reference's torch.normal draws from an RNG state nobody else holds (privacy.py:212).
+    A fixed seed is for tests and replay only: anyone who knows it can regenerate the
+    noise and subtract it, which removes the privacy guarantee."""
+
+    def __init__(self, device: Optional[torch.device] = None, seed: Optional[int] = None):
         self.device = device
-        self._seed = seed
+        self._seed = secrets.randbits(64) if seed is None else int(seed)
         self._calls = 0
 
     @staticmethod
@@ -192,11 +199,12 @@ class GaussianNoiseGenerator:
             raise PrivacyError(f"Adding noise to gradients failed: {e}") from e
 
 
-class DifferentialPrivacyEngine:
+class DifferentialPrivacyEngine(PrivacyEngineInterface):
     """PrivacyEngineInterface implementation (reference :257-417)."""
 
     def __init__(self, privacy_config: PrivacyConfig, device: Optional[torch.device] = None,
-                 seed: int = 0):
+                 seed: Optional[int] = None):
+        """seed: see GaussianNoiseGenerator (None = secret key from os.urandom)."""
         self.config = privacy_config
         self.device = device
         self.clipper = GradientClipper(privacy_config.max_grad_norm, device)

@@ -90,7 +90,8 @@ int fh_dp_clip_coef(const double* seg_sqnorm, int32_t num_clients, int32_t nseg,
 int fh_dp_apply(const float* local, int64_t local_stride, const float* global,
                 int64_t global_stride, float* out, int64_t out_stride, int32_t num_clients,
                 int64_t P, const float* coef, const int32_t* clipped, const float* sigma,
-                const float* noise_in, int64_t noise_stride, uint64_t seed, void* stream);
+                const float* noise_in, int64_t noise_stride, uint64_t seed,
+                const int64_t* row_ids, void* stream);
 
 /* ---------------- optimizers (torch.optim single-tensor semantics) -------- */
 /* SGD(momentum, dampening=0, nesterov=False): buf = first ? g : m*buf + g; p -= lr*buf */
@@ -324,11 +325,15 @@ int fh_stream_create(int32_t priority, const uint32_t* cu_mask, int32_t mask_wor
 int fh_stream_destroy(void* stream);
 
 /* Step programs (csrc/program.hip; replaces torch.cuda.CUDAGraph.replay for concurrent
- * lanes: +1.3 % on KT).  A captured
- * hipGraph_t's kernel / memset / memcpy nodes in dependency order become a launch list;
- * fh_program_launch issues it on `stream` (hipLaunchKernel etc.).  The graph must
- * outlive the program (it owns the kernel argument storage). */
-int fh_program_from_graph(void* graph, void** program_out, int32_t* kernels_out);
+ * lanes: +1.3 % on KT).  fh_record_begin makes this thread's libfedhip launches ALSO append
+ * to a new program (kernel, geometry, LDS bytes and a private copy of the arguments);
+ * fh_record_end stops it.  fh_program_launch re-issues the list on `stream`.  A program
+ * owns everything it launches with except the device buffers its arguments point at.
+ * fh_graph_node_counts: kernel / non-kernel work nodes of a captured hipGraph_t, so the
+ * caller can verify a recording made during that capture saw the whole step. */
+int fh_record_begin(void** program_out);
+int fh_record_end(void* program, int32_t* kernels_out);
+int fh_graph_node_counts(void* graph, int32_t* kernels_out, int32_t* others_out);
 int fh_program_launch(void* program, void* stream);
 int fh_program_destroy(void* program);
 /* dst[0:nbytes) = src[0:nbytes) by a kernel (16-B aligned, nbytes % 16 == 0): the per-step

@@ -96,6 +96,35 @@ def test_dp_philox_noise_statistics():
     assert not torch.equal(out[0], out[1])
 
 
+def test_dp_noise_keyed_by_client_id():
+    """row_ids: the noise of a client depends on its global id, not on the row it occupies
+    (two ranks both have a row 0; their clients must not draw the same noise)."""
+    P = 4099
+    seg_off = torch.tensor([0, P], dtype=torch.int64, device=DEV)
+    ld = torch.zeros(4, P, device=DEV)
+    sq = ops.dp_delta_sqnorm(ld, None, seg_off, 4)
+    _, coef, clipped, sigma = ops.dp_clip_coef(sq, 1.0, 1.0, 1e-5)
+    sigma.fill_(1.0)
+    ids = torch.tensor([7, 3, 12, 0], dtype=torch.int64, device=DEV)
+    full = torch.empty_like(ld)
+    ops.dp_apply(ld, None, full, coef, clipped, sigma, seed=99, row_ids=ids)
+    # "rank 1" holds clients 12 and 3 in its rows 0 and 1: same noise as above
+    part = torch.empty(2, P, device=DEV)
+    ops.dp_apply(ld[:2], None, part, coef[:2], clipped[:2], sigma[:2], seed=99,
+                 row_ids=ids[[2, 1]].contiguous())
+    assert torch.equal(part[0], full[2]) and torch.equal(part[1], full[1])
+    # without ids the key is the row: row 0 of both launches would collide
+    plain = torch.empty(2, P, device=DEV)
+    ops.dp_apply(ld[:2], None, plain, coef[:2], clipped[:2], sigma[:2], seed=99)
+    assert not torch.equal(plain[0], full[0]) or int(ids[0]) == 0
+    for i in range(4):
+        for j in range(i + 1, 4):
+            assert not torch.equal(full[i], full[j])
+    with pytest.raises(Exception):
+        ops.dp_apply(ld[:2], None, plain, coef[:2], clipped[:2], sigma[:2], seed=99,
+                     row_ids=ids[:3])
+
+
 def _torch_opt_steps(kind, p0, grads, lr):
     p = torch.nn.Parameter(p0.clone())
     if kind == "sgd":

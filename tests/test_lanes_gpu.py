@@ -72,4 +72,38 @@ def test_lanes_match_standalone(model_name, kw, shape, opt):
         assert torch.equal(lt.acc_correct[a:b], tr.acc_correct)
     assert len(lt.lanes) == 3 and all(len(ln._graphs) > 0 for ln in lt.lanes[:2])
     assert lt.fill == [0.25, 1.0, 1.0]
+    # the lanes replayed libfedhip-recorded step programs (csrc/program.hip), each one
+    # verified complete against its captured graph — not the graph fallback
+    for ln in lt.lanes:
+        assert ln.launch_mode == "program"
+        for graph, prog in ln._graphs.values():
+            assert prog is not None and prog.kernels > 20 and prog.complete_for(graph)
+    for ln in lt.lanes:
+        ln.release_graphs()
+    assert all(not ln._graphs for ln in lt.lanes)
+
+
+def test_program_replays_graph_bit_for_bit():
+    """One trainer, every step after the first replayed as a recorded program vs as the
+    captured graph: same kernels, same arguments -> identical parameters / buffers."""
+    sizes = [96, 70, 40]
+    torch.manual_seed(0)
+    model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.3).to(DEV)
+    data, labels, offs = _data(sizes, (3, 32, 32))
+    out = []
+    for mode in ("graph", "program"):
+        tr = PackedTrainer(model, len(sizes), batch=32, device=DEV)
+        tr.launch_mode = mode
+        for k in range(len(sizes)):
+            tr.load_module_state(k, model)
+        gen = torch.Generator().manual_seed(3)
+        plan = tr.make_plan(sizes, 1, generator=gen)
+        tr.run_round(data, labels, offs, plan, optimizer_type="adam", lr=1e-3, seed=4)
+        torch.cuda.synchronize()
+        progs = [p for _, p in tr._graphs.values()]
+        assert progs and all((p is not None) == (mode == "program") for p in progs)
+        out.append((tr.params.clone(), tr.bufs.clone(), tr.acc_loss.clone()))
+        tr.release_graphs()
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
 

@@ -209,13 +209,17 @@ def test_sgd_vector_and_scalar_paths_agree(mom, wd, first):
         torch.cuda.synchronize()
         outs.append((p[off:off + n].cpu(), b[off:off + n].cpu()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    # the kernels fuse g + wd*p and b*mom + g into FMAs (one rounding): 1-ulp tolerance
-    # against the two-rounding torch formula, on O(1) values
-    gv = g0 + wd * p0
+    # ATen's rounding, exactly: the add-with-alpha steps (g + wd*p, p - lr*b) are single-
+    # rounding fmadds (emulated in fp64: the fp32 product is exact there), the momentum
+    # update b*mom + g is two fp32 roundings (optim.hip builds with -ffp-contract=off)
+    def fmadd(a, b, alpha):  # fl32(a + alpha*b) with one rounding
+        return (a.double() + b.double() * torch.tensor(alpha, dtype=torch.float32).double()
+                ).float()
+    gv = fmadd(g0, p0, wd) if wd != 0.0 else g0
     bref = gv if (first or mom == 0.0) else b0 * mom + gv
-    torch.testing.assert_close(outs[0][0], p0 - 0.01 * bref, rtol=1e-6, atol=1e-6)
+    assert torch.equal(outs[0][0], fmadd(p0, bref, -0.01))
     if mom != 0.0:
-        torch.testing.assert_close(outs[0][1], bref, rtol=1e-6, atol=1e-6)
+        assert torch.equal(outs[0][1], bref)
     else:
         assert torch.equal(outs[0][1], b0)  # no momentum: the buffer is never touched
 
