@@ -175,7 +175,7 @@ class PackedTrainer:
             sd = dict(model.named_parameters())
             for n in self.layout.names:
                 p = sd[n]
-                p.data.copy_(self.layout.view(self.params, n)[slot].reshape(p.shape))
+                p.copy_(self.layout.view(self.params, n)[slot].reshape(p.shape))
             bd = dict(model.named_buffers())
             for n in self.layout.buf_names:
                 b = bd[n]
@@ -416,6 +416,13 @@ class PackedTrainer:
         seen = self.acc_seen.cpu()
         out = []
         for k, st in enumerate(plan["steps"]):
+            if st == 0:
+                # an empty shard: the reference LocalTrainer fails on it (running_loss /
+                # len(loader), training.py:209) and the client uploads nothing; here it
+                # trains nothing, reports no epoch and carries FedAvg weight 0
+                out.append(ClientMetrics(loss=float("nan"), accuracy=0.0, epochs_completed=0,
+                                         samples_processed=0))
+                continue
             n_k = int(plan["counts"][:st, k].sum())
             out.append(ClientMetrics(loss=float(loss[k]) / st,
                                      accuracy=int(corr[k]) / max(1, int(seen[k])),

@@ -98,6 +98,11 @@ class RankRound:
                     L.bview(self.global_bufs.view(1, -1), n)[0].copy_(b.detach().reshape(-1))
         self.round_index = 0
         self._evaluator = None
+        # test / diagnostic hooks: on_trained(params, S) sees the trained rows before DP /
+        # compression / FedAvg; dp_noise [S, P] replaces the Philox draw (exact replay)
+        self.on_trained = None
+        self.dp_noise = None
+        self.last_plan = None
         # update compression before FedAvg (f-3; insertion point D14): delta vs the global
         self.compression = compression
         self._cplan = None
@@ -121,12 +126,15 @@ class RankRound:
             cseeds = [(self.shuffle_seed * 0x9E3779B97F4A7C15 + seed * 0xBF58476D1CE4E5B9
                        + k * 0x94D049BB133111EB) & 0x7FFFFFFFFFFFFFFF for k in self.slots]
         plan = tr.make_plan(sizes, self.epochs, generator=generator, client_seeds=cseeds)
+        self.last_plan = plan
         if _t:
             _t.append(time.perf_counter())
         metrics = tr.run_round(data, labels, slot_offsets, plan, optimizer_type=optimizer_type,
                                lr=lr, seed=seed)
         if _t:
             _t.append(time.perf_counter())
+        if self.on_trained is not None:
+            self.on_trained(tr.params, S)
         if self.dp is not None:
             self._apply_dp(S, seed)
         if self.compression is not None:
@@ -172,5 +180,5 @@ class RankRound:
         key = (self.dp_seed * 6364136223846793005 + seed * 1442695040888963407
                + self.round_index) & ((1 << 64) - 1)
         ops.dp_apply(tr.params, g, tr.params, coef, clipped, sigma, P=self.P, seed=key,
-                     row_ids=self.slot_ids[:S])
+                     row_ids=self.slot_ids[:S], noise=self.dp_noise)
         self.last_dp = (total, clipped, sigma)

@@ -23,6 +23,7 @@ from typing import Any, Dict, List, Optional
 import torch
 import torch.nn as nn
 
+from fedhip import infer
 from fedhip._lib import FedHipError
 from fedhip.engine import PackedTrainer
 
@@ -182,16 +183,17 @@ class LocalTrainer:
             correct = total = 0
             cls_ok: Dict[int, int] = {}
             cls_n: Dict[int, int] = {}
-            for data, targets in test_loader:
-                out = self.model(data.to(self.device))
-                pred = out.argmax(dim=1).cpu()
-                t = targets.cpu()
-                total += t.numel()
-                hit = pred == t
-                correct += int(hit.sum())
-                for lab, h in zip(t.tolist(), hit.tolist()):
-                    cls_ok[lab] = cls_ok.get(lab, 0) + int(h)
-                    cls_n[lab] = cls_n.get(lab, 0) + 1
+            with infer.frozen(self.model):  # weights loaded into the engine once
+                for data, targets in test_loader:
+                    out = self.model(data.to(self.device))
+                    pred = out.argmax(dim=1).cpu()
+                    t = targets.cpu()
+                    total += t.numel()
+                    hit = pred == t
+                    correct += int(hit.sum())
+                    for lab, h in zip(t.tolist(), hit.tolist()):
+                        cls_ok[lab] = cls_ok.get(lab, 0) + int(h)
+                        cls_n[lab] = cls_n.get(lab, 0) + 1
             res = {"overall_accuracy": correct / total, "total_samples": total,
                    "correct_predictions": correct}
             for c in cls_n:

@@ -173,7 +173,11 @@ class FederatedResNet(nn.Module):
     def forward(self, x, drop=None):
         drop = drop or _Dropout(0.0)
         x = drop.relu(self.bn1(self.conv1(x)))
-        x = self.layer3(self.layer2(self.layer1(x)))
+        # blocks one by one with the step context, so a replay reaches their ReLUs too
+        # (the same ops as layer3(layer2(layer1(x))) when nothing is replayed)
+        for layer in (self.layer1, self.layer2, self.layer3):
+            for blk in layer:
+                x = blk(x, drop)
         x = self.avg_pool(x).view(x.size(0), -1)
         return self.fc(x)
 
