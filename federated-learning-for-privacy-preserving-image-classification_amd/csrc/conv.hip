@@ -27,7 +27,12 @@ namespace fh {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-enum { OP_FWD = 0, OP_DGRAD = 1, OP_WGRAD = 2 };
+// OP_DGRAD_S2: DGRAD of a stride-2 convolution (3x3/p1 or 1x1/p0) split into the four
+// output-pixel parity phases (ih % 2, iw % 2).  A phase's pixels receive only the taps whose
+// (ih + pad - kh) is even: 1, 2, 2 and 4 of the 3x3 kernel's 9 (the 1x1 kernel: its one tap
+// in phase (0,0), none elsewhere), so each phase is a dense implicit GEMM with
+// K = cout * taps instead of the generic DGRAD's cout * 9 with 3 of every 4 terms zero.
+enum { OP_FWD = 0, OP_DGRAD = 1, OP_WGRAD = 2, OP_DGRAD_S2 = 3 };
 
 struct ConvArgs {
     const float* x;     // FWD/WGRAD: input activations; DGRAD: unused
@@ -65,9 +70,16 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WAVES_N, wn = wid % WAVES_N;
 
-    // blockIdx.z = client * splits + split (split-K: WGRAD always, FWD/DGRAD on small grids)
-    const int z = blockIdx.z / a.splits;
-    const int split = blockIdx.z - z * a.splits;
+    // blockIdx.z = client * splits + split (split-K: WGRAD always, FWD/DGRAD on small grids);
+    // OP_DGRAD_S2: (client * 4 + phase) * splits + split
+    constexpr bool DG2 = (OP == OP_DGRAD_S2);
+    const int zz = blockIdx.z / a.splits;
+    const int split = blockIdx.z - zz * a.splits;
+    const int z = DG2 ? (zz >> 2) : zz;
+    const int py = DG2 ? ((zz >> 1) & 1) : 0, px = DG2 ? (zz & 1) : 0;
+    // taps of this phase per dimension (3x3/p1: 1 even, 2 odd; 1x1/p0: 1 even, 0 odd)
+    const int nth = KH == 3 ? 1 + py : 1 - py, ntw = KW == 3 ? 1 + px : 1 - px;
+    const int lg_tw = ntw == 2, lg_t = (nth == 2) + lg_tw;
     const bool partial_out = (OP == OP_WGRAD) || a.splits > 1;
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int ohw = a.oh * a.ow, hw = a.h * a.w;
@@ -75,7 +87,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
 
     // GEMM extents for this client (partial last batch shrinks the pixel dim).
     int M = a.M, N = a.N, kbeg = 0, kend = a.K;
-    if constexpr (OP == OP_FWD) N = cnt * ohw;
+    if constexpr (OP == OP_FWD || DG2) N = cnt * ohw;
     if constexpr (OP == OP_DGRAD) N = cnt * hw;
     if constexpr (OP == OP_WGRAD) {
         const int kv = cnt * ohw;
@@ -84,7 +96,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     } else {
         if (n0 >= N) return;
         kbeg = split * a.kchunk;
-        kend = min(a.K, kbeg + a.kchunk);
+        kend = min(DG2 ? a.cout * nth * ntw : a.K, kbeg + a.kchunk);
     }
 
     // ---------------- per-thread fixed coordinates -----------------------
@@ -93,11 +105,17 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     bool bcol_ok = false;
     const float* bcol_base = nullptr;
     int bi0 = 0, bj0 = 0;  // FWD: ih0/iw0 of the output pixel; DGRAD: ih/iw of the input pixel
-    if constexpr (OP == OP_FWD || OP == OP_DGRAD) {
+    if constexpr (OP == OP_FWD || OP == OP_DGRAD || DG2) {
         const int n = n0 + nb;
         bcol_ok = n < N;
         uint32_t img, p, r, c;
-        if constexpr (OP == OP_FWD) {
+        if constexpr (DG2) {  // n = (img, oy', ox') of the phase grid -> dX pixel (2oy'+py, 2ox'+px)
+            a.fd_ohw.divmod(bcol_ok ? n : 0, img, p);
+            a.fd_ow.divmod(p, r, c);
+            bi0 = 2 * (int)r + py;
+            bj0 = 2 * (int)c + px;
+            bcol_base = a.dy + z * a.dy_cs + (int64_t)img * a.cout * ohw;
+        } else if constexpr (OP == OP_FWD) {
             a.fd_ohw.divmod(bcol_ok ? n : 0, img, p);
             a.fd_ow.divmod(p, r, c);
             bi0 = (int)r * S - a.pad;
@@ -136,6 +154,30 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
                 const bool ok = bcol_ok && k < kend && (unsigned)ih < (unsigned)a.h &&
                                 (unsigned)iw < (unsigned)a.w;
                 rb[i] = ok ? bcol_base[(int64_t)ci * hw + ih * a.w + iw] : 0.f;
+            }
+        } else if constexpr (DG2) {
+            // k = (co, tap): tap -> (kh, kw) of this phase; odd phases take kh in {0, 2}
+#pragma unroll
+            for (int i = 0; i < NA; ++i) {
+                const int e = tid + i * 256, mm = e / BK, kk = e % BK;
+                const int m = m0 + mm, k = k0 + kk;
+                const int co = k >> lg_t, t = k & ((1 << lg_t) - 1);
+                const int kh = KH == 3 ? (py ? 2 * (t >> lg_tw) : 1) : 0;
+                const int kw = KW == 3 ? (px ? 2 * (t & ((1 << lg_tw) - 1)) : 1) : 0;
+                ra[i] = (m < M && k < kend) ? wz[((int64_t)co * a.cin + m) * KHW + kh * KW + kw]
+                                            : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int e = tid + i * 256, kk = e / BN;
+                const int k = k0 + kk;
+                const int co = k >> lg_t, t = k & ((1 << lg_t) - 1);
+                const int kh = KH == 3 ? (py ? 2 * (t >> lg_tw) : 1) : 0;
+                const int kw = KW == 3 ? (px ? 2 * (t & ((1 << lg_tw) - 1)) : 1) : 0;
+                const int oy = (bi0 + a.pad - kh) >> 1, ox = (bj0 + a.pad - kw) >> 1;  // exact
+                const bool ok = bcol_ok && k < kend && (unsigned)oy < (unsigned)a.oh &&
+                                (unsigned)ox < (unsigned)a.ow;
+                rb[i] = ok ? bcol_base[(int64_t)co * ohw + oy * a.ow + ox] : 0.f;
             }
         } else if constexpr (OP == OP_DGRAD) {
             // A[m=ci][k=(co,kh,kw)] = W[co][ci][kh][kw], k-fast.
@@ -343,6 +385,22 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
                             op[(int64_t)m * ohw] = v;
                         }
                     }
+            } else if constexpr (DG2) {
+                uint32_t r, c;
+                a.fd_ohw.divmod(n, img, p);
+                a.fd_ow.divmod(p, r, c);
+                float* op = a.out + z * a.out_cs + (int64_t)img * a.cin * hw +
+                            (2 * (int)r + py) * a.w + 2 * (int)c + px;
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r2 = 0; r2 < 16; ++r2) {
+                        const int m = m0 + wm * WM + i * 32 + (r2 & 3) + 8 * (r2 >> 2) + rbase;
+                        if (m < M) {
+                            float* q = op + (int64_t)m * hw;
+                            *q = a.accumulate ? (*q + acc[i][j][r2]) : acc[i][j][r2];
+                        }
+                    }
             } else {
                 a.fd_hw.divmod(n, img, p);
                 float* op = a.out + z * a.out_cs + (int64_t)img * a.cin * hw + p;
@@ -433,6 +491,33 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
     *o = accumulate ? (*o + s) : s;
 }
 
+// OP_DGRAD_S2 split-K epilogue: slab part[(client*4 + phase)][split][m][n over the phase
+// grid] summed in split order into dX[client][img][m][2oy'+py][2ox'+px] (=|+=).
+__global__ void __launch_bounds__(256)
+splitk_epilogue_s2_kernel(const float* __restrict__ part, int splits, int M, int Nfull,
+                          float* __restrict__ out, int64_t out_cs, int accumulate,
+                          const int32_t* __restrict__ counts, int batch, int oh, int ow, int w) {
+    const int zz = blockIdx.z, z = zz >> 2, py = (zz >> 1) & 1, px = zz & 1, m = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int ohw = oh * ow;
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= cnt * ohw) return;
+    const float* p = part + ((int64_t)zz * splits * M + m) * Nfull + n;
+    const int64_t ss = (int64_t)M * Nfull;
+    float s = 0.f;
+    for (int i0 = 0; i0 < splits; i0 += 8) {  // 8 loads in flight, summed in split order
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = i0 + j < splits ? p[(i0 + j) * ss] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (i0 + j < splits) s += v[j];
+    }
+    const int img = n / ohw, q = n - img * ohw, r = q / ow, c = q - r * ow;
+    float* o = out + z * out_cs + ((int64_t)img * M + m) * (4 * ohw) + (2 * r + py) * w + 2 * c + px;
+    *o = accumulate ? (*o + s) : s;
+}
+
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
@@ -466,6 +551,12 @@ static int launch_tile(const Tile& t, dim3 grid, const ConvArgs& a, hipStream_t 
 template <int OP>
 static int launch_shape(int kh, int kw, int s, const Tile& t, dim3 grid, const ConvArgs& a,
                         hipStream_t st) {
+    if constexpr (OP == OP_DGRAD_S2) {
+        if (kh == 3 && kw == 3 && s == 2) return launch_tile<OP, 3, 3, 2>(t, grid, a, st);
+        if (kh == 1 && kw == 1 && s == 2) return launch_tile<OP, 1, 1, 2>(t, grid, a, st);
+        set_error("conv dgrad s2: unsupported kernel %dx%d stride %d", kh, kw, s);
+        return FH_E_UNSUPPORTED;
+    }
     if (kh == 3 && kw == 3 && s == 1) return launch_tile<OP, 3, 3, 1>(t, grid, a, st);
     if (kh == 3 && kw == 3 && s == 2) return launch_tile<OP, 3, 3, 2>(t, grid, a, st);
     if (kh == 1 && kw == 1 && s == 1) return launch_tile<OP, 1, 1, 1>(t, grid, a, st);
@@ -521,6 +612,8 @@ static int env_int(const char* name, int dflt) {
 }
 
 static const int kMnSplitBelow = env_int("FH_MN_SPLIT_BELOW", 192);  // sweeps (fc_bench.py)
+// diagnostics / A-B: FH_DGRAD_S2=0 sends stride-2 DGRAD back to the generic igemm
+static const int g_dgrad_s2_off = env_int("FH_DGRAD_S2", 1) == 0;
 static const int kMnTarget = env_int("FH_MN_TARGET", 768);
 
 static Plan plan_mn(int M, int N, int K, int nclients) {
@@ -609,6 +702,44 @@ static int run_mn(ConvArgs a, int kh, int kw, int stride, int nclients, void* ws
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.N, out, out_cs, bias, b_cs, relu, accum, a.counts, a.batch, sp);
         FH_LAUNCH_CHECK(name);
+    }
+    return FH_OK;
+}
+
+// ---- stride-2 DGRAD by parity phases (OP_DGRAD_S2) -------------------------
+static bool dgrad_s2_supported(int h, int w, int kh, int kw, int stride, int pad) {
+    return stride == 2 && h % 2 == 0 && w % 2 == 0 &&
+           ((kh == 3 && kw == 3 && pad == 1) || (kh == 1 && kw == 1 && pad == 0));
+}
+
+// GEMM per (client, phase): M = cin, N = batch * oh * ow, K <= cout * 4 (3x3) or cout (1x1)
+static Plan plan_dgrad_s2(int cin, int cout, int kh, int batch, int oh, int ow, int nclients) {
+    return plan_mn(cin, batch * oh * ow, cout * (kh == 3 ? 4 : 1), nclients * 4);
+}
+
+static int run_dgrad_s2(ConvArgs a, int kh, int nclients, void* ws, size_t ws_bytes, float* out,
+                        int64_t out_cs, int accum, hipStream_t st) {
+    Plan p = plan_dgrad_s2(a.cin, a.cout, kh, a.batch, a.oh, a.ow, nclients);
+    if (p.splits > 1 && (!ws || ws_bytes < mn_ws_bytes(p, nclients * 4))) {
+        p.splits = 1;
+        p.kchunk = p.K;
+    }
+    a.M = p.M;
+    a.N = p.N;
+    a.K = p.K;
+    a.splits = p.splits;
+    a.kchunk = p.kchunk;
+    if (p.splits > 1) a.out = (float*)ws;
+    dim3 grid((unsigned)ceil_div(a.N, p.t.bn), (unsigned)ceil_div(a.M, p.t.bm),
+              (unsigned)(nclients * 4 * p.splits));
+    int rc = launch_shape<OP_DGRAD_S2>(kh, kh, 2, p.t, grid, a, st);
+    if (rc) return rc;
+    FH_LAUNCH_CHECK("conv2d_dgrad s2");
+    if (p.splits > 1) {
+        dim3 eg((unsigned)ceil_div(a.N, 256), (unsigned)a.M, (unsigned)(nclients * 4));
+        FH_LAUNCH(splitk_epilogue_s2_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
+                  a.M, a.N, out, out_cs, accum, a.counts, a.batch, a.oh, a.ow, a.w);
+        FH_LAUNCH_CHECK("conv2d_dgrad s2 epilogue");
     }
     return FH_OK;
 }
@@ -830,6 +961,8 @@ extern "C" size_t fh_conv2d_dgrad_workspace(int32_t nclients, int32_t batch, int
     if (dconv_supported(h, w_, kh, kw, stride, pad))
         return dconv_ws_bytes(plan_dconv(cin, cout, batch, h * w_, nclients), nclients, cin, batch,
                               h * w_);
+    if (dgrad_s2_supported(h, w_, kh, kw, stride, pad) && !g_dgrad_s2_off)
+        return mn_ws_bytes(plan_dgrad_s2(cin, cout, kh, batch, oh, ow, nclients), nclients * 4);
     return mn_ws_bytes(plan_mn(cin, batch * h * w_, cout * kh * kw, nclients), nclients);
 }
 
@@ -916,6 +1049,9 @@ extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, i
     a.dy = dy; a.wt = w; a.out = dx;
     a.dy_cs = dy_cs; a.w_cs = w_cs; a.out_cs = dx_cs;
     a.accumulate = accumulate;
+    if (dgrad_s2_supported(h, w_, kh, kw, stride, pad) && !g_dgrad_s2_off)
+        return run_dgrad_s2(a, kh, nclients, workspace, ws_bytes, dx, dx_cs, accumulate,
+                            as_stream(stream));
     a.M = cin; a.N = batch * h * w_; a.K = cout * kh * kw;
     return run_mn<OP_DGRAD>(a, kh, kw, stride, nclients, workspace, ws_bytes, dx, dx_cs, nullptr, 0,
                             0, accumulate, h * w_, as_stream(stream), "conv2d_dgrad");

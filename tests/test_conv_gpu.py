@@ -104,6 +104,30 @@ def test_conv_relu_and_accumulate(case):
     assert torch.equal(acc, base + dx)
 
 
+@pytest.mark.parametrize("C,B,cin,h,cout,k,pad", [(8, 32, 64, 32, 128, 3, 1),
+                                                   (1, 32, 128, 16, 256, 3, 1),
+                                                   (2, 11, 64, 16, 128, 1, 0)])
+def test_dgrad_s2_accumulate(C, B, cin, h, cout, k, pad):
+    """Stride-2 DGRAD (parity phases) into a residual gradient: dx += result equals
+    base + (the written result), and untouched images (past counts) keep their values
+    (ResNet adds the conv1 dgrad onto the shortcut's, models_pytorch.py:182-194)."""
+    g = torch.Generator().manual_seed(5)
+    oh = h // 2
+    wt = (torch.randn(C, cout, cin, k, k, generator=g) / math.sqrt(cin * k * k)).to(DEV)
+    dy = torch.randn(C, B, cout, oh, oh, generator=g).to(DEV)
+    base = torch.randn(C, B, cin, h, h, generator=g).to(DEV)
+    counts = torch.tensor([B - (i % 3) for i in range(C)], dtype=torch.int32, device=DEV)
+    dx = torch.zeros_like(base)
+    ops.conv2d_dgrad(dy, wt, dx, C, B, cin, h, h, cout, k, 2, pad, counts=counts)
+    acc = base.clone()
+    ops.conv2d_dgrad(dy, wt, acc, C, B, cin, h, h, cout, k, 2, pad, counts=counts, accumulate=True)
+    torch.cuda.synchronize()
+    for z in range(C):
+        n = int(counts[z])
+        assert torch.equal(acc[z, :n], base[z, :n] + dx[z, :n])
+        assert torch.equal(acc[z, n:], base[z, n:])
+
+
 @pytest.mark.parametrize("C,B,inf,outf", [(3, 32, 3136, 128), (2, 17, 128, 10), (2, 32, 2048, 512)])
 def test_linear_fwd_bwd(C, B, inf, outf):
     g = torch.Generator().manual_seed(7)
@@ -146,6 +170,13 @@ EXACT = [  # nclients, batch, cin, h, cout, k, stride, pad (square maps)
     (2, 8, 64, 16, 128, 3, 2, 1),
     (2, 8, 64, 16, 128, 1, 2, 0),
     (3, 6, 32, 28, 64, 3, 1, 1),
+    # stride-2 DGRAD by parity phases (ResNet down-sampling: 3x3/p1 and the 1x1 shortcut),
+    # full-width (no split-K) and one-client (split-K + phase epilogue) grids
+    (8, 32, 64, 32, 128, 3, 2, 1),
+    (8, 32, 64, 32, 128, 1, 2, 0),
+    (1, 32, 128, 16, 256, 3, 2, 1),
+    (1, 32, 128, 16, 256, 1, 2, 0),
+    (3, 19, 32, 8, 48, 3, 2, 1),
 ]
 
 
