@@ -40,7 +40,7 @@ PKG = os.path.join(REPO, "federated-learning-for-privacy-preserving-image-classi
 sys.path[:0] = [REPO, PKG]
 
 from fedhip import ops  # noqa: E402
-from fedhip.partition import lpt_assign, partition, train_split_sizes  # noqa: E402
+from fedhip.partition import lpt_assign, partition, train_split, train_split_sizes  # noqa: E402
 from fedhip.round import DPConfig, RankRound  # noqa: E402
 from src.shared import models_pytorch as hm  # noqa: E402
 
@@ -131,71 +131,188 @@ def flops_key(cfg):
     return cfg["model"]
 
 
-def cpu_baseline(cfg, seconds=12.0):
-    """Reference algorithm (oracle restatement, bit-exact with the reference LocalTrainer)
-    on host cores: one client's local SGD steps at batch 32 for ~`seconds`."""
-    from oracle import train_ref
+def cpu_baseline(cfg, train_sizes, opt="sgd", lr=0.01, seconds=12.0):
+    """The reference's client round on the host cores — oracle/ (the CPU restatement pinned
+    bit-exact to the reference LocalTrainer / privacy / compression / FedAvg): clients of
+    this workload in order, each its whole shard of synthetic uint8 images through the
+    reference loaders' per-sample transforms (data_loader.py:298-306, 454-458), batches of 32
+    in a shuffled order with the partial last one, a fresh optimizer (training.py:89), the
+    config's local epochs, then its update DP (privacy.py:284-311, torch.normal noise) and
+    compression when the config has them, and the FedAvg of the sampled clients
+    (fedavg.py:267-289).  Clients are taken median shard size first (a representative
+    sample) until ~`seconds` of this work; the sample's client-images / its wall time is
+    the baseline.  Data generation is not timed."""
+    from oracle import compress_ref, data_ref, fedavg_ref, privacy_ref, train_ref
     threads = torch.get_num_threads()
+    rng = np.random.default_rng(0)
+    c, h, w = cfg["shape"]
+    tf = ops.DataTransform.mnist() if c == 1 else ops.DataTransform.cifar10()
     model = train_ref.make_model(cfg["model"], 0, **cfg["kw"])
-    opt = train_ref.make_optimizer(model, "sgd", 0.01)
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(32, *cfg["shape"], generator=g)
-    y = torch.randint(0, cfg["classes"], (32,), generator=g)
-    train_ref.train_step(model, opt, x, y)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        train_ref.train_step(model, opt, x, y)
-        n += 32
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "client-images/s", "cores": threads, "kind": "port",
-            "sample": f"{cfg['model']} local SGD steps, batch 32, {n} images in {dt:.1f}s "
-                      f"(oracle/train_ref.py, torch CPU, {threads} threads)"}
+    gsd = {k: v.clone() for k, v in model.state_dict().items()}
+    gvec = [p.detach().numpy().copy() for p in model.parameters()]
+    rows, ns, imgs, busy, nclients = [], [], 0, 0.0, 0
+    med = float(np.median(train_sizes))
+    for n in sorted(train_sizes, key=lambda v: (abs(v - med), v)):
+        if busy > seconds:
+            break
+        if n == 0:
+            continue
+        raw = rng.integers(0, 256, (n, h, w) if c == 1 else (n, h, w, c), dtype=np.uint8)
+        labels = torch.from_numpy(rng.integers(0, cfg["classes"], n))
+        draws = rng.integers(0, 2 * tf.pad + 1, (cfg["epochs"], n, 2))
+        flips = rng.integers(0, 2, (cfg["epochs"], n)).astype(bool) & tf.flip
+        perms = [rng.permutation(n) for _ in range(cfg["epochs"])]
+        t0 = time.perf_counter()
+        m = train_ref.make_model(cfg["model"], None, **cfg["kw"])
+        m.load_state_dict(gsd)
+        optm = train_ref.make_optimizer(m, opt, lr)
+        for e in range(cfg["epochs"]):
+            for j in range(0, n, 32):
+                idx = perms[e][j:j + 32]
+                x = np.ascontiguousarray(np.stack([data_ref.transform(raw[i], tf.mean, tf.std, tf.pad,
+                                                 int(draws[e, i, 0]), int(draws[e, i, 1]),
+                                                 bool(flips[e, i])) for i in idx]))
+                train_ref.train_step(m, optm, torch.from_numpy(x), labels[idx])
+                imgs += len(idx)
+        local = [p.detach().numpy() for p in m.parameters()]
+        if cfg["dp"]:
+            deltas = [(lp - gp).astype(np.float32) for lp, gp in zip(local, gvec)]
+            clipped, sens, _, _ = privacy_ref.clip(deltas, 1.0)
+            sig = privacy_ref.sigma(sens, cfg["dp"], 1e-5)
+            noisy = privacy_ref.add_noise(clipped, [torch.normal(0.0, sig, t.shape).numpy()
+                                                    for t in clipped])
+            local = [(gp + d).astype(np.float32) for gp, d in zip(gvec, noisy)]
+        if cfg.get("compression"):
+            _, ratio = cfg["compression"]
+            local = [(gp + compress_ref.topk_dense((lp - gp).astype(np.float32), ratio))
+                     .astype(np.float32) for lp, gp in zip(local, gvec)]
+        rows.append(np.concatenate([v.reshape(-1) for v in local]))
+        ns.append(cfg["epochs"] * n)
+        nclients += 1
+        busy += time.perf_counter() - t0
+    t0 = time.perf_counter()
+    fedavg_ref.weighted_average(rows, fedavg_ref.calculate_sample_weights(ns))
+    busy += time.perf_counter() - t0
+    extras = ", update DP" if cfg["dp"] else ""
+    extras += ", top-k compression" if cfg.get("compression") else ""
+    return {"value": imgs / busy, "unit": "client-images/s", "cores": threads, "kind": "port",
+            "sample": f"{nclients} clients of this workload ({imgs} client-images: whole "
+                      f"shards, {cfg['epochs']} local epoch(s), per-sample host transforms, "
+                      f"batch 32, {opt} lr {lr}{extras}, FedAvg of the sample) in "
+                      f"{busy:.1f}s (oracle/*.py, torch CPU, {threads} threads)"}
 
 
-def mnist_proxy(n, signal, seed, device, classes=10):
-    """Learnable synthetic MNIST-shaped data (no dataset download is possible here):
-    x = signal * P[y] + N(0, 1), with ten fixed class prototypes P (N(0,1) images smoothed
-    by a 5x5 box filter and rescaled to unit std).  Labels uniform."""
+def proxy_prototypes(classes=10):
+    """Ten fixed class prototypes: N(0,1) images smoothed by a 5x5 box filter, unit std."""
     g = torch.Generator(device="cpu").manual_seed(4242)
     proto = torch.randn(classes, 1, 28, 28, generator=g)
     proto = torch.nn.functional.avg_pool2d(proto, 5, stride=1, padding=2)
-    proto = (proto / proto.std(dim=(1, 2, 3), keepdim=True)).to(device)
-    gd = torch.Generator(device=device).manual_seed(seed)
-    y = torch.randint(0, classes, (n,), generator=gd, device=device)
-    x = torch.randn(n, 1, 28, 28, generator=gd, device=device) + signal * proto[y]
-    return x, y
+    return proto / proto.std(dim=(1, 2, 3), keepdim=True)
 
 
-def rounds_to_target(dev, target, max_rounds, signal, opt, lr):
+def mnist_proxy(labels, signal, seed):
+    """Learnable synthetic MNIST-shaped images for given labels (no dataset download is
+    possible here): x = signal * P[y] + N(0, 1).  CPU tensor."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(len(labels), 1, 28, 28, generator=g) + signal * proxy_prototypes()[labels]
+
+
+RTT_CONFIG = "K2"        # 32 Dirichlet(0.5) MNIST clients: FedAvg needs several rounds
+RTT_SIGNAL = 0.135       # proxy difficulty, fixed: HIP needs 5 rounds (tools/rtt_calibrate.py)
+
+
+def rtt_data(cfg_key=RTT_CONFIG, signal=RTT_SIGNAL, seed=0):
+    """The reference's partition of a 60k-label MNIST-shaped proxy (data_loader.py:139-177,
+    90/10 random_split :343-351) + a 10k test split.  Returns (train index lists per client,
+    X [60k], labels [60k], Xt, yt) on the CPU."""
+    cfg = CONFIGS[cfg_key]
+    labels = np.random.default_rng(seed).integers(0, 10, size=cfg["samples"])
+    import random
+    random.seed(seed)
+    np.random.seed(seed)
+    parts = partition(labels, cfg["clients"], cfg["strategy"], cfg["alpha"])
+    g = torch.Generator().manual_seed(seed + 5)
+    train_idx = [train_split(parts.get(c, []), 0.1, g)[0] for c in range(cfg["clients"])]
+    lab = torch.from_numpy(labels)
+    X = mnist_proxy(lab, signal, seed + 1)
+    yt = torch.from_numpy(np.random.default_rng(seed + 2).integers(0, 10, size=10000))
+    Xt = mnist_proxy(yt, signal, seed + 3)
+    return train_idx, X, lab, Xt, yt
+
+
+def rounds_to_target(dev, target, max_rounds, opt, lr, oracle_budget_s=150.0, signal=RTT_SIGNAL,
+                     cfg_key=RTT_CONFIG):
     """Second half of the BASELINE metric: FedAvg rounds until the global model's test
-    accuracy reaches `target` on config K1 (MNIST SimpleCNN, 4 IID clients, 1 local epoch),
-    on the learnable MNIST proxy (60k train / 10k test), global model evaluated after every
-    aggregation by fedhip.evaluate (eval-mode forward on the chip)."""
-    cfg = CONFIGS["K1"]
-    labels, train = build_clients(cfg, 1)
+    accuracy reaches `target`, on the K2 client partition (MNIST SimpleCNN, 32 Dirichlet(0.5)
+    clients, 1 local epoch, no DP — at the reference's DP semantics eps=1 noise has
+    sigma ~4.8 per weight and no model trains) of a learnable MNIST proxy,
+    global model evaluated after every aggregation.  Run twice on the same data, partition,
+    initial model and per-client batch order: by the HIP path, and by the oracle (the
+    reference LocalTrainer + FedAvg restated on the host CPU)."""
+    cfg = CONFIGS[cfg_key]
+    train_idx, X, lab, Xt, yt = rtt_data(cfg_key, signal)
+    sizes = [len(t) for t in train_idx]
     torch.manual_seed(0)
-    template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
-    rr = RankRound(template, train, list(range(len(train))), epochs=cfg["epochs"], device=dev)
-    xs, ys = mnist_proxy(sum(train), signal, 1, dev)
-    offs = np.cumsum([0] + [train[k] for k in rr.slots][:-1]).tolist()
-    xt, yt = mnist_proxy(10000, signal, 2, dev)
-    gen = torch.Generator().manual_seed(3)
+    template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"])
+    init = {k: v.clone() for k, v in template.state_dict().items()}
+    rr = RankRound(template.to(dev), sizes, list(range(len(sizes))), epochs=cfg["epochs"],
+                   device=dev, shuffle_seed=11)
+    order = torch.cat([torch.tensor(train_idx[k], dtype=torch.int64) for k in rr.slots])
+    xs, ys = X[order].to(dev), lab[order].to(dev)
+    offs = np.cumsum([0] + [sizes[k] for k in rr.slots][:-1]).tolist()
+    xt_d, yt_d = Xt.to(dev), yt.to(dev)
     curve, hit = [], None
     t0 = time.perf_counter()
     for r in range(max_rounds):
-        rr.run(xs, ys, offs, opt, lr, seed=r, generator=gen)
-        acc = rr.evaluate(xt, yt)["overall_accuracy"]
+        rr.run(xs, ys, offs, opt, lr, seed=r)  # client-keyed batch order
+        acc = rr.evaluate(xt_d, yt_d)["overall_accuracy"]
         curve.append(round(acc, 4))
         if acc >= target:
             hit = r + 1
             break
-    return {"target": target, "rounds": hit, "max_rounds": max_rounds, "accuracy_curve": curve,
-            "seconds": round(time.perf_counter() - t0, 2),
-            "config": f"K1: simple_cnn, 4 IID clients, 1 local epoch, batch 32, {opt} lr {lr}, "
-                      f"MNIST proxy (signal {signal}, 60k train / 10k test), no DP",
+    hip_s = time.perf_counter() - t0
+    # the oracle, same data / partition / init / batch order, until it hits or the budget ends
+    from oracle import fedavg_ref, train_ref
+    w = fedavg_ref.calculate_sample_weights([cfg["epochs"] * n for n in sizes])
+    ref = train_ref.make_model(cfg["model"], None, **cfg["kw"])
+    ref.load_state_dict(init)
+    glob = train_ref.param_vector(ref).numpy()
+    ocurve, ohit, t1 = [], None, time.perf_counter()
+    torch.manual_seed(1)  # the oracle's dropout masks (torch CPU stream)
+    for r in range((hit or max_rounds) + 1):
+        if time.perf_counter() - t1 > oracle_budget_s:
+            break
+        rows = []
+        for k in range(len(sizes)):
+            m = train_ref.make_model(cfg["model"], None, **cfg["kw"])
+            torch.nn.utils.vector_to_parameters(torch.from_numpy(glob.copy()), m.parameters())
+            gk = torch.Generator().manual_seed(rr.client_shuffle_seed(r, k))
+            opt_k = train_ref.make_optimizer(m, opt, lr)
+            idx = torch.tensor(train_idx[k], dtype=torch.int64)
+            for _ in range(cfg["epochs"]):
+                perm = idx[torch.randperm(len(idx), generator=gk)]
+                for j in range(0, len(perm), 32):
+                    train_ref.train_step(m, opt_k, X[perm[j:j + 32]], lab[perm[j:j + 32]])
+            rows.append(train_ref.param_vector(m).numpy())
+        glob = fedavg_ref.weighted_average(rows, w)
+        m = train_ref.make_model(cfg["model"], None, **cfg["kw"])
+        torch.nn.utils.vector_to_parameters(torch.from_numpy(glob.copy()), m.parameters())
+        oacc = train_ref.evaluate_model(m, Xt, yt, batch=1000)[0]["overall_accuracy"]
+        ocurve.append(round(oacc, 4))
+        if oacc >= target:
+            ohit = r + 1
+            break
+    return {"target": target, "rounds": hit, "oracle_rounds": ohit, "max_rounds": max_rounds,
+            "accuracy_curve": curve, "oracle_accuracy_curve": ocurve,
+            "seconds": round(hip_s, 2), "oracle_seconds": round(time.perf_counter() - t1, 1),
+            "config": f"{cfg_key} partition: {cfg['model']}, {len(sizes)} {cfg['strategy']}"
+                      f"(a={cfg['alpha']}) clients, {cfg['epochs']} local epoch, batch 32, "
+                      f"{opt} lr {lr}, no DP; MNIST proxy signal {signal} (60k train / 10k test)",
             "data": "synthetic learnable MNIST proxy (class prototypes + N(0,1) noise); the "
                     "real MNIST is not available offline: parity unpinned vs the reference's "
-                    "MNIST number"}
+                    "MNIST number.  oracle_rounds: the same rounds by oracle/train_ref.py + "
+                    "oracle/fedavg_ref.py on the host (dropout masks from torch's CPU stream, "
+                    "the HIP run's from Philox: equal in distribution only)"}
 
 
 def measured_traffic(probe_tag, flops_per_launch=None):
@@ -232,10 +349,11 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--probe", default=None, help="conv launch tag to time (default: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-instances", action="store_true",
+                    help="skip the instrumented per-launch-shape round")
     ap.add_argument("--rounds-target", type=float, default=0.91,
                     help="rounds-to-accuracy half of the metric (K1 MNIST proxy); 0 disables")
     ap.add_argument("--rounds-max", type=int, default=30)
-    ap.add_argument("--proxy-signal", type=float, default=0.14)
     ap.add_argument("--fp32-data", action="store_true",
                     help="pre-normalised fp32 shards instead of uint8 images + on-device transform")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -303,18 +421,52 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     probe = ops.PROBE.summary()
+    # one instrumented round (untimed, every step eager, the lanes one after another so a
+    # launch never shares the chip with another lane's): HIP events around EVERY conv /
+    # linear launch — every client count, ragged and tail steps included
+    inst = None
+    if not args.no_instances:
+        ops.PROBE.reset()
+        ops.PROBE.tag, ops.PROBE.enabled = "*", True
+        rr.run(data, lab, offs, args.opt, args.lr, seed=999, generator=gen, serialize_lanes=True)
+        ops.PROBE.enabled = False
+        inst = ops.PROBE.by_tag()
 
     if rank == 0:
         value = total_images * args.steps / elapsed
         fl = TRAIN_FLOPS[flops_key(cfg)]
-        roof = None
+        peak = FP32_MFMA_PEAK_TFLOPS
+        roof, full = None, None
         if probe:
             ach = probe["flops_per_launch"] / (probe["avg_ms"] * 1e-3) / 1e12
-            roof = {"bound": "mfma", "kernel": probe_tag, "achieved": round(ach, 2),
-                    "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                    "traffic": measured_traffic(probe_tag, probe["flops_per_launch"]),
-                    "launches_timed": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4)}
+            full = {"kernel": probe_tag, "achieved": round(ach, 2), "frac": round(ach / peak, 4),
+                    "launches_timed": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4),
+                    "note": "full-width full-batch launches of the timed rounds only"}
+        instances, conv_all = None, None
+        if inst:
+            rows = sorted(inst.items(), key=lambda kv: -kv[1][1])
+            instances = [{"launch": tag, "launches": n, "total_ms": round(t, 3),
+                          "avg_us": round(1e3 * t / n, 2),
+                          "tflops": round(f / (t * 1e-3) / 1e12, 2),
+                          "frac": round(f / (t * 1e-3) / 1e12 / peak, 4)} for tag, (n, t, f) in rows]
+            T = sum(t for _, t, _ in inst.values())
+            F = sum(f for _, _, f in inst.values())
+            conv_all = {"tflops": round(F / (T * 1e-3) / 1e12, 2),
+                        "frac": round(F / (T * 1e-3) / 1e12 / peak, 4), "total_ms": round(T, 2),
+                        "launches": sum(n for n, _, _ in inst.values())}
+            # the roofline kernel: the launch shape with the largest share of the round's
+            # conv/linear time, averaged over ALL its launches (every client count, ragged
+            # batches, tail steps)
+            tag, (n, t, f) = rows[0]
+            ach = f / (t * 1e-3) / 1e12
+            roof = {"bound": "mfma", "kernel": tag, "achieved": round(ach, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                    "traffic": measured_traffic(tag, f / n),
+                    "launches_timed": n, "avg_launch_ms": round(t / n, 4),
+                    "flops_per_launch": round(f / n),
+                    "measured": "HIP events on the launch stream around every launch of one "
+                                "instrumented round of this workload (eager, lanes serialised); "
+                                "small tail launches include host issue gaps (conservative)"}
         out = {
             "metric": "client-images/sec/node", "value": round(value, 1),
             "unit": "client-images/s", "n_gpus": world, "steps": args.steps,
@@ -339,13 +491,18 @@ def main():
                        "parallelism": f"client-packed x{world} GPU",
                        "lanes": rr.trainer.cut},
             "achieved_tflops_step": round(value * fl / 1e12, 2),
+            "round_frac": round(value * fl / 1e12 / peak, 4),
             "roofline": roof,
+            "roofline_full_width_probe": full,
+            "conv_linear_all_launches": conv_all,
+            "instances": instances,
         }
         if world == 1 and args.rounds_target > 0:
             out["rounds_to_target"] = rounds_to_target(dev, args.rounds_target, args.rounds_max,
-                                                       args.proxy_signal, args.opt, args.lr)
+                                                       args.opt, args.lr)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cfg)
+            out["cpu_baseline"] = cpu_baseline(cfg, [train[k] for k in rr.slots], args.opt,
+                                               args.lr)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

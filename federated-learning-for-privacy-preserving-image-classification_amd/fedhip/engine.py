@@ -298,13 +298,14 @@ class PackedTrainer:
             self._replay(n, st["data"], st["labels"], views, st["sample_elems"])
         else:
             arm = self.probe_full and full and bool(st["full_batch"][g])
-            ops.PROBE.enabled = arm
+            if not ops.PROBE.all:  # "*": an instrumented round, every launch timed
+                ops.PROBE.enabled = arm
             net.seed = (st["seed"] * 1000003 + g) & 0x7FFFFFFF
             net.seed_dev = None
             self._gather(st["data"], st["labels"], views, n, st["sample_elems"])
             self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
                                 adam_dev=views["adam"])
-            if arm:
+            if arm and not ops.PROBE.all:
                 ops.PROBE.enabled = False
         self._after_step(n)
 

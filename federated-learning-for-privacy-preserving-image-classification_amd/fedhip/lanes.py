@@ -224,10 +224,20 @@ class LanedTrainer:
                            generator, cs(i)) for i in range(len(self.lanes))]
 
     def run_round(self, data, labels, shard_offsets, plans, optimizer_type="sgd", lr=0.01,
-                  seed=0):
-        if len(self.lanes) == 1:
-            return self.lanes[0].run_round(data, labels, shard_offsets, plans[0],
-                                           optimizer_type, lr, seed)
+                  seed=0, serialize=False):
+        """serialize: run the lanes one after another on the current stream (bench.py's
+        instrumented round: every launch timed alone, without other lanes beside it)."""
+        if len(self.lanes) == 1 or serialize:
+            out = []
+            for i, ln in enumerate(self.lanes):
+                ops.set_fill_fraction(self.fill[i])
+                try:
+                    out += ln.run_round(data, labels,
+                                        shard_offsets[self.cut[i]:self.cut[i + 1]], plans[i],
+                                        optimizer_type, lr, seed)
+                finally:
+                    ops.set_fill_fraction(1.0)
+            return out
         t_r0 = time.perf_counter()
         main = torch.cuda.current_stream(self.device)
         states = []

@@ -54,10 +54,12 @@ _WS: dict = {}
 
 
 class LaunchProbe:
-    """Times one chosen kernel launch with HIP events on the launch stream.
+    """Times libfedhip conv / linear launches with HIP events on the launch stream.
 
-    bench.py points ``tag`` at the dominant kernel (e.g. "conv_wgrad:c32x32x32->32k3s1");
-    every matching launch while ``enabled`` records (start, end, algorithmic flops)."""
+    bench.py points ``tag`` at one kernel launch shape (e.g.
+    "conv_wgrad:c32x32x32->32k3s1") and every matching launch while ``enabled`` records
+    (start, end, algorithmic flops); tag "*" records every tagged launch (one instrumented
+    round: the per-instance table of bench.py)."""
 
     def __init__(self):
         self.tag = None
@@ -65,30 +67,54 @@ class LaunchProbe:
         self.records = []
         self.seen = {}
 
+    @property
+    def all(self):
+        return self.tag == "*"
+
+    # instrumented rounds issue eagerly from Python, which is slower than the small kernels
+    # of a few-client step: a GPU spin of this many cycles ahead of each timed launch keeps
+    # the stream busy while the host queues the launch and its end event, so the window is
+    # the launch itself, not the host's issue time (the spin is outside the window)
+    lead_cycles = 120_000
+
     def begin(self, tag):
         if not self.enabled:
             return None
         self.seen[tag] = self.seen.get(tag, 0) + 1
-        if tag != self.tag:
+        if tag != self.tag and not self.all:
             return None
+        if self.all:
+            torch.cuda._sleep(self.lead_cycles)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        return ev
+        return (tag, ev)
 
-    def end(self, ev, flops):
-        if ev is None:
+    def end(self, h, flops):
+        if h is None:
             return
         e2 = torch.cuda.Event(enable_timing=True)
         e2.record()
-        self.records.append((ev, e2, flops))
+        self.records.append((h[0], h[1], e2, flops))
+
+    def reset(self):
+        self.records, self.seen = [], {}
 
     def summary(self):
         torch.cuda.synchronize()
         if not self.records:
             return None
-        ms = [a.elapsed_time(b) for a, b, _ in self.records]
-        fl = [f for _, _, f in self.records]
+        ms = [a.elapsed_time(b) for _, a, b, _ in self.records]
+        fl = [f for _, _, _, f in self.records]
         return {"launches": len(ms), "avg_ms": sum(ms) / len(ms), "flops_per_launch": sum(fl) / len(fl)}
+
+    def by_tag(self):
+        """{tag: (launches, total ms, total flops)} over every recorded launch."""
+        torch.cuda.synchronize()
+        out = {}
+        for tag, a, b, f in self.records:
+            n, t, fl = out.get(tag, (0, 0.0, 0.0))
+            out[tag] = (n + 1, t + a.elapsed_time(b), fl + f)
+        return out
 
 
 PROBE = LaunchProbe()
@@ -247,22 +273,28 @@ def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pa
 def linear_fwd(x, w, bias, y, nclients, batch, in_f, out_f, relu=False, counts=None):
     require_device(x, "x")
     ws, nb = _ws_for("fh_linear_fwd_workspace", x.device, nclients, batch, in_f, out_f)
+    ev = PROBE.begin(f"linear_fwd:{in_f}->{out_f}")
     call("fh_linear_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y),
          _counts(counts), nclients, batch, in_f, out_f, int(relu), ptr(ws), nb, stream_handle())
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f)
     return y
 
 
 def linear_dgrad(dy, w, dx, nclients, batch, in_f, out_f, counts=None):
     ws, nb = _ws_for("fh_linear_dgrad_workspace", dy.device, nclients, batch, in_f, out_f)
+    ev = PROBE.begin(f"linear_dgrad:{in_f}->{out_f}")
     call("fh_linear_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
          nclients, batch, in_f, out_f, ptr(ws), nb, stream_handle())
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f)
     return dx
 
 
 def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
     ws, nb = _ws_for("fh_linear_wgrad_workspace", x.device, nclients, batch, in_f, out_f)
+    ev = PROBE.begin(f"linear_wgrad:{in_f}->{out_f}")
     call("fh_linear_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
          ptr(ws), nb, _counts(counts), nclients, batch, in_f, out_f, stream_handle())
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f)
     return dw
 
 

@@ -110,11 +110,17 @@ class RankRound:
             from .compress import SegmentPlan
             self._cplan = SegmentPlan(L.seg_offsets(), self.device)
 
+    def client_shuffle_seed(self, seed: int, client: int) -> int:
+        """Seed of the torch.Generator client `client` draws its round-`seed` batch
+        permutations from (one torch.randperm per local epoch, fedhip/engine.plan_round)."""
+        return (self.shuffle_seed * 0x9E3779B97F4A7C15 + seed * 0xBF58476D1CE4E5B9
+                + client * 0x94D049BB133111EB) & 0x7FFFFFFFFFFFFFFF
+
     def set_global(self, flat: torch.Tensor):
         self.global_flat.copy_(flat)
 
     def run(self, data, labels, slot_offsets: Sequence[int], optimizer_type="sgd", lr=0.01,
-            seed=0, generator=None):
+            seed=0, generator=None, serialize_lanes=False):
         """One round. data/labels: this rank's train shards, slot k's at slot_offsets[k]."""
         tr = self.trainer
         S = len(self.slots)
@@ -123,14 +129,13 @@ class RankRound:
         sizes = [self.all_sizes[k] for k in self.slots]
         cseeds = None
         if generator is None:
-            cseeds = [(self.shuffle_seed * 0x9E3779B97F4A7C15 + seed * 0xBF58476D1CE4E5B9
-                       + k * 0x94D049BB133111EB) & 0x7FFFFFFFFFFFFFFF for k in self.slots]
+            cseeds = [self.client_shuffle_seed(seed, k) for k in self.slots]
         plan = tr.make_plan(sizes, self.epochs, generator=generator, client_seeds=cseeds)
         self.last_plan = plan
         if _t:
             _t.append(time.perf_counter())
         metrics = tr.run_round(data, labels, slot_offsets, plan, optimizer_type=optimizer_type,
-                               lr=lr, seed=seed)
+                               lr=lr, seed=seed, serialize=serialize_lanes)
         if _t:
             _t.append(time.perf_counter())
         if self.on_trained is not None:
