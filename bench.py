@@ -332,6 +332,8 @@ def measured_traffic(probe_tag, flops_per_launch=None):
         except (OSError, ValueError):
             continue
         if t.get("probe") == probe_tag:
+            if t.get("bytes_per_flop") and flops_per_launch:  # per-client traffic x clients
+                return int(round(t["bytes_per_flop"] * flops_per_launch))
             scale = 1.0
             if flops_per_launch and t.get("flops_per_launch"):
                 scale = flops_per_launch / t["flops_per_launch"]

@@ -123,11 +123,16 @@ class LanedTrainer:
         # split-K fill fraction per lane (ops.set_fill_fraction); FH_LANE_FILL = one value
         # for every lane or one per lane (diagnostics)
         self.fill = [1.0] * len(self.lanes)
-        if len(self.lanes) > 1 and cut[1] - cut[0] == 1:
-            # an isolated outlier client plans its split-K for a quarter of the chip: fewer,
-            # longer splits (fewer reduction launches) beside the wide lanes (+1 %,
-            # profiles/r01_v10/lane_fill.txt)
-            self.fill[0] = 0.25
+        if len(self.lanes) > 1:
+            # concurrent lanes share the chip, so each plans its split-K for part of it:
+            # fewer, longer splits and fewer reduction launches.  Measured on KT
+            # (profiles/r02_fill/, r02_fill2/: 247.6k -> 255.9k client-images/s): an isolated
+            # outlier client a quarter, the widest lane three quarters, the others half
+            # (round 1 had only the first rule, profiles/r01_v10/lane_fill.txt)
+            sizes = [cut[i + 1] - cut[i] for i in range(len(self.lanes))]
+            widest = max(range(len(sizes)), key=lambda i: (sizes[i], -i))
+            for i, n in enumerate(sizes):
+                self.fill[i] = 0.25 if n == 1 else (0.75 if i == widest else 0.5)
         env_fill = os.environ.get("FH_LANE_FILL")
         if env_fill and len(self.lanes) > 1:
             vals = [float(v) for v in env_fill.split(",")]

@@ -71,7 +71,7 @@ def test_lanes_match_standalone(model_name, kw, shape, opt):
         assert torch.equal(lt.acc_loss[a:b], tr.acc_loss)
         assert torch.equal(lt.acc_correct[a:b], tr.acc_correct)
     assert len(lt.lanes) == 3 and all(len(ln._graphs) > 0 for ln in lt.lanes[:2])
-    assert lt.fill == [0.25, 1.0, 1.0]
+    assert lt.fill == [0.25, 0.75, 0.5]  # isolated client, widest lane, the rest
     # the lanes replayed libfedhip-recorded step programs (csrc/program.hip), each one
     # verified complete against its captured graph — not the graph fallback
     for ln in lt.lanes:
