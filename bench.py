@@ -315,13 +315,14 @@ def rounds_to_target(dev, target, max_rounds, opt, lr, oracle_budget_s=150.0, si
                     "the HIP run's from Philox: equal in distribution only)"}
 
 
-def measured_traffic(probe_tag, flops_per_launch=None):
-    """HBM bytes per launch of the probed kernel, from the newest committed PMC
-    measurement (profiles/*/traffic.json, made by tools/traffic.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark), else None.
-    The kernel's traffic is per client (each client's own dY, weights and dX), so a
-    measurement taken at another client count is scaled by the FLOP ratio of the two
-    launches when the file records the FLOPs it was measured at."""
+def measured_traffic(tag, flops_per_launch=None):
+    """HBM bytes per launch of a conv launch shape, from the newest committed PMC
+    measurement (profiles/*/traffic.json, tools/traffic3.py: separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of tools/traffic_probe.py, x2 FETCH correction), else
+    None.  A launch's bytes are linear in its client count (each client's own activations,
+    weights and split-K partials), so the file's per-shape fit bytes = a + b * FLOPs over
+    the measured client counts (32, 8, 1) is evaluated at the roofline launch's average
+    FLOPs.  (Round-1 files hold one probed launch, scaled by FLOPs.)"""
     here = os.path.dirname(os.path.abspath(__file__))
     def newest_first(f):  # profiles/r01_v13 after r01_v7: compare the digit runs as numbers
         return [int(p) if p.isdigit() else p for p in re.split(r"(\d+)", f)]
@@ -331,7 +332,10 @@ def measured_traffic(probe_tag, flops_per_launch=None):
             t = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if t.get("probe") == probe_tag:
+        fit = t.get("shapes", {}).get(tag, {}).get("fit")
+        if fit and flops_per_launch:
+            return int(round(fit["bytes_at_zero_flops"] + fit["bytes_per_flop"] * flops_per_launch))
+        if t.get("probe") == tag:
             if t.get("bytes_per_flop") and flops_per_launch:  # per-client traffic x clients
                 return int(round(t["bytes_per_flop"] * flops_per_launch))
             scale = 1.0
@@ -401,6 +405,9 @@ def main():
     rr.trainer.probe_full = False
 
     gen = torch.Generator().manual_seed(7)
+    if os.environ.get("FH_DUMP_MAPS"):  # diagnostics: where libraries live (profiler crashes)
+        with open("/proc/self/maps") as src, open(os.environ["FH_DUMP_MAPS"], "w") as dst:
+            dst.write(src.read())
     for w in range(args.warmup):
         rr.run(data, lab, offs, args.opt, args.lr, seed=w, generator=gen)
     torch.cuda.synchronize()

@@ -461,6 +461,37 @@ extern "C" int fh_bn_fwd_stats(const float* x, int64_t x_cs, const float* gamma,
     return FH_OK;
 }
 
+// Train-mode statistics from partials a convolution epilogue already wrote
+// (fh_conv2d_fwd_bnstats: one fp64 (sum, sum of squares) pair per (client, channel,
+// 256-pixel tile), zeros past a client's count): bn_finalize_kernel merges the tiles in
+// order -> save_mean / save_invstd, running statistics, and the consumer's affine.
+extern "C" int fh_bn_finalize_tiles(const double* part, const float* gamma, const float* beta,
+                                    int64_t p_cs, float* running_mean, float* running_var,
+                                    int64_t r_cs, float* save_mean, float* save_invstd,
+                                    float* scale_out, float* shift_out, int64_t s_cs,
+                                    const int32_t* counts, int32_t nclients, int32_t batch,
+                                    int32_t C, int32_t HW, float eps, float momentum,
+                                    void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_finalize_tiles: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(part && gamma && beta && save_mean && save_invstd && scale_out && shift_out,
+               "bn_finalize_tiles: null pointer");
+    FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr),
+               "bn_finalize_tiles: running stats");
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.S = (int)ceil_div((int64_t)batch * HW, 256);
+    a.part = (double*)part;
+    a.gamma = gamma; a.beta = beta;
+    a.rmean = running_mean; a.rvar = running_var; a.save_mean = save_mean;
+    a.save_invstd = save_invstd;
+    a.p_cs = p_cs; a.r_cs = r_cs;
+    a.eps = eps; a.momentum = momentum;
+    FH_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 256), nclients), dim3(256), 0,
+              as_stream(stream), a, scale_out, shift_out, s_cs);
+    FH_LAUNCH_CHECK("bn_finalize_tiles");
+    return FH_OK;
+}
+
 extern "C" int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_cs,
                               const float* res, int64_t res_cs, const float* gamma,
                               const float* beta, int64_t p_cs, const float* running_mean,

@@ -464,31 +464,56 @@ splitk_sum_kernel(const float* __restrict__ part, float* __restrict__ dw, int64_
 }
 
 // FWD/DGRAD split-K epilogue: out[z][img][m][p] (=|+=) sum_s part[z][s][m][n] (+bias, relu).
+// bn_part (FWD, nullable): the BatchNorm statistics of the stored values of this block's
+// 256 pixels of channel m, one fp64 (sum, sum of squares) pair per (client, channel, tile)
+// as the unsplit dconv epilogue writes them (dconv_kernels.h DConvArgs::bn_part).
 __global__ void __launch_bounds__(256)
 splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nfull,
                        float* __restrict__ out, int64_t out_cs, const float* __restrict__ bias,
                        int64_t b_cs, int relu, int accumulate, const int32_t* __restrict__ counts,
-                       int batch, int sp) {
+                       int batch, int sp, double* __restrict__ bn_part, int bn_tiles) {
     const int z = blockIdx.z, m = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int n = blockIdx.x * 256 + threadIdx.x;
-    if (n >= cnt * sp) return;
-    const float* p = part + ((int64_t)z * splits * M + m) * Nfull + n;
-    const int64_t ss = (int64_t)M * Nfull;
+    const bool valid = n < cnt * sp;
+    if (!valid && bn_part == nullptr) return;
     float s = 0.f;
-    for (int i0 = 0; i0 < splits; i0 += 8) {  // 8 loads in flight, summed in split order
-        float v[8];
+    if (valid) {
+        const float* p = part + ((int64_t)z * splits * M + m) * Nfull + n;
+        const int64_t ss = (int64_t)M * Nfull;
+        for (int i0 = 0; i0 < splits; i0 += 8) {  // 8 loads in flight, summed in split order
+            float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = i0 + j < splits ? p[(i0 + j) * ss] : 0.f;
+            for (int j = 0; j < 8; ++j) v[j] = i0 + j < splits ? p[(i0 + j) * ss] : 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (i0 + j < splits) s += v[j];
+            for (int j = 0; j < 8; ++j)
+                if (i0 + j < splits) s += v[j];
+        }
+        if (bias) s = s + bias[z * b_cs + m];
+        if (relu) s = fmaxf(s, 0.f);
+        const int img = n / sp, pix = n - img * sp;
+        float* o = out + z * out_cs + ((int64_t)img * M + m) * sp + pix;
+        if (accumulate) s = *o + s;
+        *o = s;
     }
-    if (bias) s = s + bias[z * b_cs + m];
-    if (relu) s = fmaxf(s, 0.f);
-    const int img = n / sp, pix = n - img * sp;
-    float* o = out + z * out_cs + ((int64_t)img * M + m) * sp + pix;
-    *o = accumulate ? (*o + s) : s;
+    if (bn_part != nullptr) {  // block-uniform
+        __shared__ double red[2][4];
+        double d0 = valid ? (double)s : 0.0;
+        double d1 = d0 * d0;
+        d0 = wave_sum(d0);
+        d1 = wave_sum(d1);
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        if (lane == 0) {
+            red[0][wid] = d0;
+            red[1][wid] = d1;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double* q = bn_part + (((int64_t)z * M + m) * bn_tiles + blockIdx.x) * 2;
+            q[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+            q[1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        }
+    }
 }
 
 // OP_DGRAD_S2 split-K epilogue: slab part[(client*4 + phase)][split][m][n over the phase
@@ -700,7 +725,8 @@ static int run_mn(ConvArgs a, int kh, int kw, int stride, int nclients, void* ws
     if (p.splits > 1) {
         dim3 eg((unsigned)ceil_div(a.N, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
-                           a.M, a.N, out, out_cs, bias, b_cs, relu, accum, a.counts, a.batch, sp);
+                           a.M, a.N, out, out_cs, bias, b_cs, relu, accum, a.counts, a.batch, sp,
+                           (double*)nullptr, 0);
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -852,7 +878,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
                            OP == OP_FWD ? a.relu : 0, OP == OP_FWD ? 0 : a.accumulate, a.counts,
-                           a.batch, sp);
+                           a.batch, sp, OP == OP_FWD ? a.bn_part : nullptr, a.bn_tiles);
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -972,7 +998,7 @@ static int conv2d_fwd_impl(const float* x, int64_t x_cs, const float* in_scale,
                            const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
                            int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
                            int32_t stride, int32_t pad, int32_t relu, void* workspace,
-                           size_t ws_bytes, void* stream) {
+                           size_t ws_bytes, void* stream, double* bn_part = nullptr) {
     int oh, ow;
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
     if (rc) return rc;
@@ -985,11 +1011,13 @@ static int conv2d_fwd_impl(const float* x, int64_t x_cs, const float* in_scale,
         d.in_cs = x_cs; d.w_cs = w_cs; d.b_cs = b_cs; d.out_cs = y_cs;
         d.counts = counts; d.batch = batch; d.Cr = cin; d.M = cout; d.relu = relu;
         d.in_scale = in_scale; d.in_shift = in_shift; d.aff_cs = aff_cs;
+        d.bn_part = bn_part; d.bn_tiles = (int)ceil_div((int64_t)batch * h * w_, 256);
         return run_dconv<OP_FWD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
                                  "conv2d_fwd");
     }
-    if (in_scale) {
-        set_error("conv2d_fwd_bnrelu: needs the direct 3x3 path (3x3/s1/p1, square 8/16/32)");
+    if (in_scale || bn_part) {
+        set_error("conv2d_fwd_bnrelu / _bnstats: need the direct 3x3 path (3x3/s1/p1, square "
+                  "8/16/32)");
         return FH_E_UNSUPPORTED;
     }
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
@@ -1024,6 +1052,32 @@ extern "C" int fh_conv2d_fwd_bnrelu(const float* x, int64_t x_cs, const float* i
     return conv2d_fwd_impl(x, x_cs, in_scale, in_shift, aff_cs, w, w_cs, bias, b_cs, y, y_cs,
                            counts, nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, relu,
                            workspace, ws_bytes, stream);
+}
+
+// BatchNorm partial statistics of a direct-conv FWD output: bytes of the fp64 (sum, sum of
+// squares) pairs per (client, channel, 256-pixel tile) that fh_conv2d_fwd_bnstats writes.
+extern "C" size_t fh_conv_bnstats_bytes(int32_t nclients, int32_t batch, int32_t cout, int32_t h,
+                                        int32_t w_) {
+    if (nclients <= 0 || batch <= 0 || cout <= 0 || h <= 0 || w_ <= 0) return 0;
+    return (size_t)nclients * cout * ceil_div((int64_t)batch * h * w_, 256) * 2 * sizeof(double);
+}
+
+// fh_conv2d_fwd_bnrelu (in_scale / in_shift nullable) that also leaves the BatchNorm
+// statistics of y in bn_part (fh_conv_bnstats_bytes; merged by fh_bn_finalize_tiles), so the
+// BN layer after this conv never re-reads y.  Direct 3x3 path only; no ReLU on y.
+extern "C" int fh_conv2d_fwd_bnstats(const float* x, int64_t x_cs, const float* in_scale,
+                                     const float* in_shift, int64_t aff_cs, const float* w,
+                                     int64_t w_cs, const float* bias, int64_t b_cs, float* y,
+                                     int64_t y_cs, double* bn_part, const int32_t* counts,
+                                     int32_t nclients, int32_t batch, int32_t cin, int32_t h,
+                                     int32_t w_, int32_t cout, void* workspace, size_t ws_bytes,
+                                     void* stream) {
+    FH_REQUIRE(bn_part, "conv2d_fwd_bnstats: null statistics buffer");
+    FH_REQUIRE(dconv_supported(h, w_, 3, 3, 1, 1), "conv2d_fwd_bnstats: needs a 3x3/s1/p1 conv "
+               "on a square 8/16/32 map (got %dx%d)", h, w_);
+    return conv2d_fwd_impl(x, x_cs, in_scale, in_shift, aff_cs, w, w_cs, bias, b_cs, y, y_cs,
+                           counts, nclients, batch, cin, h, w_, cout, 3, 3, 1, 1, 0, workspace,
+                           ws_bytes, stream, bn_part);
 }
 
 extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
@@ -1226,13 +1280,23 @@ __device__ __forceinline__ float f4at(const float4& v, int q) {
 // dX[z][b][k] = sum_m dY[z][b][m] W[z][m][k] for b < cnt; M % 32 == 0, K % (32 * KT) == 0.
 // KT 32-feature tiles per workgroup: each W row is read as KT consecutive 128-B pieces
 // (one DRAM page run) and every wave carries KT independent accumulator chains.
+// Epilogue (fused linear backward): the gradient of the layer's input through the Dropout
+// and ReLU in front of it, g = dX * keep(mask) / (1 - p) if the input (relu_ref) > 0, else 0
+// (dropout_bwd_kernel's operations).
+struct SkinnyBwdEpi {
+    const uint8_t* mask;   // dropout keep-mask [z][b][K] (nullable)
+    int64_t m_cs;
+    float scale;           // 1 / (1 - p)
+    const float* relu_ref; // the layer input [z][b][K]: zero where it is not > 0 (nullable)
+    int64_t r_cs;
+};
+
 template <int KT>
-__global__ void __launch_bounds__(256)
-linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const float* __restrict__ W,
-                           int64_t w_cs, float* __restrict__ dX, int64_t dx_cs,
-                           const int32_t* __restrict__ counts, int batch, int K, int M) {
-    __shared__ float red[3 * 16 * 64 * KT];
-    const int z = blockIdx.y, k0 = blockIdx.x * 32 * KT;
+__device__ __forceinline__ void linear_dgrad_skinny_body(
+        const float* __restrict__ dY, int64_t dy_cs, const float* __restrict__ W, int64_t w_cs,
+        float* __restrict__ dX, int64_t dx_cs, const int32_t* __restrict__ counts, int batch,
+        int K, int M, int z, int kblock, float* red, const SkinnyBwdEpi& ep) {
+    const int k0 = kblock * 32 * KT;
     const int cnt = counts ? counts[z] : batch;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r32 = lane & 31, h = lane >> 5;
@@ -1273,25 +1337,39 @@ linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const fl
         for (int r = 0; r < 16; ++r) {
             const int img = (r & 3) + 8 * (r >> 2) + 4 * h;
             if (img >= cnt) continue;
-            const float v = ((acc[t][r] + red[((0 * KT + t) * 16 + r) * 64 + lane]) +
-                             red[((1 * KT + t) * 16 + r) * 64 + lane]) +
-                            red[((2 * KT + t) * 16 + r) * 64 + lane];
-            dX[z * dx_cs + (int64_t)img * K + k0 + 32 * t + r32] = v;
+            float v = ((acc[t][r] + red[((0 * KT + t) * 16 + r) * 64 + lane]) +
+                       red[((1 * KT + t) * 16 + r) * 64 + lane]) +
+                      red[((2 * KT + t) * 16 + r) * 64 + lane];
+            const int64_t e = (int64_t)img * K + k0 + 32 * t + r32;
+            if (ep.mask) v = ep.mask[z * ep.m_cs + e] ? v * ep.scale : 0.f;
+            if (ep.relu_ref && !(ep.relu_ref[z * ep.r_cs + e] > 0.f)) v = 0.f;
+            dX[z * dx_cs + e] = v;
         }
+}
+
+template <int KT>
+__global__ void __launch_bounds__(256)
+linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const float* __restrict__ W,
+                           int64_t w_cs, float* __restrict__ dX, int64_t dx_cs,
+                           const int32_t* __restrict__ counts, int batch, int K, int M) {
+    __shared__ float red[3 * 16 * 64 * KT];
+    const SkinnyBwdEpi ep{nullptr, 0, 1.f, nullptr, 0};
+    linear_dgrad_skinny_body<KT>(dY, dy_cs, W, w_cs, dX, dx_cs, counts, batch, K, M, blockIdx.y,
+                                 blockIdx.x, red, ep);
 }
 
 // dW[z][m][k] = sum_{b < cnt} dY[z][b][m] X[z][b][k] (and db[z][m] = sum_b dY[z][b][m]):
 // the reduction is only the images, so the layer is a write stream of dW.  One wave = one
 // 32 (m) x 32 (k) tile from 16 MFMAs over the 32 image pairs; a workgroup = 32 m x 128 k.
 // Bias: the k-tile-0 workgroups, one lane per m, images in order.
-__global__ void __launch_bounds__(256)
-linear_wgrad_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float* __restrict__ dY,
-                           int64_t dy_cs, float* __restrict__ dW, int64_t dw_cs,
-                           float* __restrict__ db, int64_t db_cs,
-                           const int32_t* __restrict__ counts, int batch, int K, int M) {
-    const int z = blockIdx.z, m0 = blockIdx.y * 32;
+__device__ __forceinline__ void linear_wgrad_skinny_body(
+        const float* __restrict__ X, int64_t x_cs, const float* __restrict__ dY, int64_t dy_cs,
+        float* __restrict__ dW, int64_t dw_cs, float* __restrict__ db, int64_t db_cs,
+        const int32_t* __restrict__ counts, int batch, int K, int M, int z, int kblock,
+        int mblock) {
+    const int m0 = mblock * 32;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int k0 = blockIdx.x * 128 + wid * 32;
+    const int k0 = kblock * 128 + wid * 32;
     const int cnt = counts ? counts[z] : batch;
     const int r32 = lane & 31, h = lane >> 5;
     const bool mok = m0 + r32 < M;
@@ -1314,10 +1392,42 @@ linear_wgrad_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const floa
         const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (m < M) wz[(int64_t)m * K] = acc[r];
     }
-    if (db && blockIdx.x == 0 && wid == 0 && h == 0 && mok) {
+    if (db && kblock == 0 && wid == 0 && h == 0 && mok) {
         float v = 0.f;
         for (int b = 0; b < cnt; ++b) v += yz[(int64_t)b * M];
         db[z * db_cs + m0 + r32] = v;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+linear_wgrad_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float* __restrict__ dY,
+                           int64_t dy_cs, float* __restrict__ dW, int64_t dw_cs,
+                           float* __restrict__ db, int64_t db_cs,
+                           const int32_t* __restrict__ counts, int batch, int K, int M) {
+    linear_wgrad_skinny_body(X, x_cs, dY, dy_cs, dW, dw_cs, db, db_cs, counts, batch, K, M,
+                             blockIdx.z, blockIdx.x, blockIdx.y);
+}
+
+// A whole linear backward in one launch: workgroups [0, nw) of each client are the skinny
+// WGRAD tiles (in_f/128 x ceil(out_f/32)), the rest the skinny DGRAD tiles with the Dropout /
+// ReLU backward of the layer's input fused into the epilogue — three launches (wgrad, dgrad,
+// dropout_bwd) become one.  grid = (nw + nd, clients).
+template <int KT>
+__global__ void __launch_bounds__(256)
+linear_bwd_fused_kernel(const float* __restrict__ X, int64_t x_cs, const float* __restrict__ dY,
+                        int64_t dy_cs, const float* __restrict__ W, int64_t w_cs,
+                        float* __restrict__ dW, int64_t dw_cs, float* __restrict__ db,
+                        int64_t db_cs, float* __restrict__ dX, int64_t dx_cs, SkinnyBwdEpi ep,
+                        const int32_t* __restrict__ counts, int batch, int K, int M, int nw) {
+    __shared__ float red[3 * 16 * 64 * KT];
+    const int z = blockIdx.y, bx = blockIdx.x;
+    if (bx < nw) {
+        const int kt = K / 128;
+        linear_wgrad_skinny_body(X, x_cs, dY, dy_cs, dW, dw_cs, db, db_cs, counts, batch, K, M,
+                                 z, bx % kt, bx / kt);
+    } else {
+        linear_dgrad_skinny_body<KT>(dY, dy_cs, W, w_cs, dX, dx_cs, counts, batch, K, M, z,
+                                     bx - nw, red, ep);
     }
 }
 
@@ -1367,6 +1477,41 @@ extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, i
     }
     return fh_conv2d_dgrad(dy, dy_cs, w, w_cs, dx, dx_cs, counts, nclients, batch, in_f, 1, 1,
                            out_f, 1, 1, 1, 0, 0, workspace, ws_bytes, stream);
+}
+
+// Fused linear backward (fh_linear_wgrad + fh_linear_dgrad + the Dropout/ReLU backward of
+// the layer input, fh_dropout_bwd) in one launch: batch <= 32, in_f % 128 == 0,
+// out_f % 32 == 0, 16-B aligned dY rows; FH_E_UNSUPPORTED otherwise (the caller then issues
+// the three entry points).  mask / relu_ref nullable; db nullable.
+extern "C" int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                                   const float* w, int64_t w_cs, float* dw, int64_t dw_cs,
+                                   float* db, int64_t db_cs, float* dx, int64_t dx_cs,
+                                   const uint8_t* mask, int64_t m_cs, float p_drop,
+                                   const float* relu_ref, int64_t r_cs, const int32_t* counts,
+                                   int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f,
+                                   void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && in_f > 0 && out_f > 0, "linear_bwd_fused: bad shape");
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_bwd_fused: p=%g", p_drop);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && dy && w && dw && dx, "linear_bwd_fused: null pointer");
+    if (!(batch <= 32 && in_f % 128 == 0 && out_f % 32 == 0 && skinny_aligned(dy, dy_cs) &&
+          w_cs % 4 == 0)) {
+        set_error("linear_bwd_fused: needs batch <= 32, in_f %% 128 == 0, out_f %% 32 == 0 and "
+                  "aligned dY (got %d, %d, %d)", batch, in_f, out_f);
+        return FH_E_UNSUPPORTED;
+    }
+    const SkinnyBwdEpi ep{mask, m_cs, 1.0f / (1.0f - p_drop), relu_ref, r_cs};
+    const int nw = (in_f / 128) * (int)ceil_div(out_f, 32);
+    if (kLinearSkinny != 2 && (int64_t)(in_f / 128) * nclients >= fill(256))
+        FH_LAUNCH(linear_bwd_fused_kernel<4>, dim3((unsigned)(nw + in_f / 128), nclients),
+                  dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, w, w_cs, dw, dw_cs, db,
+                  db_cs, dx, dx_cs, ep, counts, batch, in_f, out_f, nw);
+    else
+        FH_LAUNCH(linear_bwd_fused_kernel<1>, dim3((unsigned)(nw + in_f / 32), nclients),
+                  dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, w, w_cs, dw, dw_cs, db,
+                  db_cs, dx, dx_cs, ep, counts, batch, in_f, out_f, nw);
+    FH_LAUNCH_CHECK("linear_bwd_fused");
+    return FH_OK;
 }
 
 extern "C" size_t fh_linear_wgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f,

@@ -41,7 +41,19 @@ struct DConvArgs {
     const float* in_scale;
     const float* in_shift;
     int64_t aff_cs;
+    // FWD only, nullable: BatchNorm statistics of the stored output, taken from the
+    // accumulators instead of a second pass over y: one fp64 (sum, sum of squares) pair per
+    // (client, channel, 256-pixel tile) -> bn_part[((z * M + m) * bn_tiles + t) * 2]
+    // (tiles past the client's count hold zeros).  Unsplit launches only; with split-K the
+    // epilogue kernel takes the statistics (conv.hip splitk_epilogue_kernel).
+    double* bn_part;
+    int bn_tiles;
 };
+
+// Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
+// mod 64, so the epilogue's writes (32 pixels x 2 channel halves 4 apart) hit 64 distinct
+// banks and the per-channel strided reads at most 2-way conflicts.
+constexpr int kStatPitch = 264;
 
 // BatchNorm apply + ReLU on a staged float4 of channel c (bn.hip bn_apply_kernel's exact
 // fp32 operations: x * alpha + beta', then max(., 0); contraction is off in this build)
@@ -81,8 +93,13 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     constexpr int NAV = (BM * KS / 4 + 255) / 256;   // float4 weight slots per thread
     static_assert(FM >= 1 && FN >= 1 && (CK % 2) == 0, "dconv tile");
 
-    __shared__ float As[2][KS * BMP];
-    __shared__ float Ps[2][PE];
+    // one LDS block: the double-buffered weight / patch stages, reused after the K loop as
+    // the statistics image (FWD with bn_part)
+    constexpr int LDS_MAIN = 2 * KS * BMP + 2 * PE;
+    constexpr int LDS_N = (OP == OP_FWD && BM * kStatPitch > LDS_MAIN) ? BM * kStatPitch : LDS_MAIN;
+    __shared__ float smem[LDS_N];
+    float (*As)[KS * BMP] = reinterpret_cast<float (*)[KS * BMP]>(smem);
+    float (*Ps)[PE] = reinterpret_cast<float (*)[PE]>(smem + 2 * KS * BMP);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -92,7 +109,15 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int t = blockIdx.x, m0 = blockIdx.y * BM;
     const int n0 = t * 256;
-    if (n0 >= cnt * G::HW) return;
+    const bool stats = OP == OP_FWD && a.bn_part != nullptr && a.splits == 1;  // block-uniform
+    if (n0 >= cnt * G::HW) {  // a tile past this client's images: zero statistics
+        if (stats && tid < BM && m0 + tid < a.M) {
+            double* q = a.bn_part + (((int64_t)z * a.M + m0 + tid) * a.bn_tiles + t) * 2;
+            q[0] = 0.0;
+            q[1] = 0.0;
+        }
+        return;
+    }
     const int cbeg = split * a.cchunk;
     const int cend = min(a.Cr, cbeg + a.cchunk);
     const int M = a.M;
@@ -299,11 +324,24 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
                 bv_r[i][r] = (bz && m < M) ? bz[m] : 0.f;
             }
     }
+    // statistics image (FWD with bn_part): the stored value of every (channel, pixel) of
+    // the tile, [BM][kStatPitch] fp32 in the LDS the K loop has finished with
+    float* red = smem;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
         const int n = n0 + wn * WN + j * 32 + col;
         const int img = n / G::HW, p = n % G::HW;
-        if (img >= cnt) continue;
+        if (img >= cnt) {
+            if (OP == OP_FWD && stats) {  // past the client's images: contributes zero
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        red[(wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase) * kStatPitch +
+                            n - n0] = 0.f;
+            }
+            continue;
+        }
         if (a.splits > 1) {
             float* op = a.out + ((int64_t)blockIdx.z * M) * a.Nfull + n;
 #pragma unroll
@@ -320,19 +358,49 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
             for (int i = 0; i < FM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                    const int ml = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                    const int m = m0 + ml;
                     if (m < M) {
                         float v = acc[i][j][r];
                         float* q = op + (int64_t)m * G::HW;
                         if (OP == OP_FWD) {
                             if (has_bias) v = v + bv_r[i][r];
                             if (a.relu) v = fmaxf(v, 0.f);
+                            if (stats) red[ml * kStatPitch + n - n0] = v;
                         } else if (a.accumulate) {
                             v = *q + v;
                         }
                         *q = v;
                     }
                 }
+        }
+    }
+    if constexpr (OP == OP_FWD) {
+        if (stats) {
+            // BatchNorm statistics of the tile's stored values per output channel, in a
+            // fixed order: TPC threads per channel each add 256/TPC pixels (stride TPC) in
+            // fp64 (x and x*x, as bn_stats_kernel), then combine by xor-shuffles.
+            constexpr int TPC = 256 / BM;
+            __syncthreads();
+            const int c = tid / TPC, q = tid % TPC;
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll 8
+            for (int k = 0; k < 256 / TPC; ++k) {
+                const double v = red[c * kStatPitch + q + TPC * k];
+                s0 += v;
+                s1 += v * v;
+            }
+#pragma unroll
+            for (int o = 1; o < TPC; o <<= 1) {
+                s0 += __shfl_xor(s0, o, 64);
+                s1 += __shfl_xor(s1, o, 64);
+            }
+            const int m = m0 + c;
+            if (q == 0 && m < M) {
+                double* d = a.bn_part + (((int64_t)z * M + m) * a.bn_tiles + t) * 2;
+                d[0] = s0;
+                d[1] = s1;
+            }
         }
     }
 }

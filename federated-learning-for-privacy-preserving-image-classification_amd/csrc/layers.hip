@@ -263,6 +263,193 @@ ce_kernel(const float* __restrict__ logits, int64_t l_cs, const int64_t* __restr
     }
 }
 
+// ------------------------------------------------------------------ classifier head
+// The end of a training step's forward and the start of its backward in ONE launch (S
+// blocks per client): the last linear layer (logits = x W^T + b: CIFAR10CNN fc3
+// models_pytorch.py:159-165, SimpleCNN fc2 :96-97, FederatedResNet fc :241-246), the
+// cross-entropy forward + backward with ce_kernel's arithmetic and accumulators
+// (training.py:193-203), the layer's weight and bias gradients, and the gradient of its
+// input through the Dropout (keep-mask, scale 1/(1-p)) and ReLU in front of it — ReLU
+// decided on the layer input itself (x > 0 <=> the pre-dropout ReLU output > 0 wherever
+// the keep-mask is 1; elsewhere the gradient is 0 anyway).  Replaces the layer's forward
+// (+ split-K epilogue), ce, its wgrad, its dgrad and dropout_bwd.  batch <= 32.
+// Every block of a client stages x [cnt][F] (and, SMALLK, W [K][F]) in LDS with a +1 pitch,
+// recomputes the logits and the loss (a few hundred dot products), and then owns 1/S of the
+// dW and dX outputs; block 0 publishes logits, dlogits and the loss accumulators.  Dot
+// products are sequential fmaf chains (one thread per output), images / classes in order.
+constexpr int kHeadBlocks = 4;
+template <bool SMALLK>
+__global__ void __launch_bounds__(256)
+linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ w,
+                      int64_t w_cs, const float* __restrict__ bias, int64_t b_cs,
+                      const int64_t* __restrict__ targets, int64_t t_cs, float* __restrict__ logits,
+                      int64_t l_cs, float* __restrict__ dlogits, int64_t d_cs,
+                      float* __restrict__ loss_out, double* __restrict__ acc_loss,
+                      int64_t* __restrict__ acc_correct, int64_t* __restrict__ acc_seen,
+                      const int32_t* __restrict__ reset, float* __restrict__ dw, int64_t dw_cs,
+                      float* __restrict__ db, int64_t db_cs, float* __restrict__ dx,
+                      int64_t dx_cs, const uint8_t* __restrict__ mask, int64_t m_cs, float scale,
+                      int relu_in, const int32_t* __restrict__ counts, int batch, int F, int K) {
+    constexpr int KMAX = SMALLK ? 16 : 128;
+    constexpr int FMAX = 256;                      // SMALLK: staged x / W width (F <= 256)
+    constexpr int XS = SMALLK ? 32 * (FMAX + 1) : 1;
+    constexpr int WS = SMALLK ? KMAX * (FMAX + 1) : 1;
+    __shared__ float Xs[XS];
+    __shared__ float Ws[WS];
+    __shared__ float L[32 * KMAX];   // logits [img][K]
+    __shared__ float D[32 * KMAX];   // dlogits [img][K]
+    __shared__ double li[32];
+    __shared__ int ci[32];
+    __shared__ double sl[4];
+    __shared__ int sc[4];
+    const int z = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
+    const int cnt = counts ? counts[z] : batch;
+    const float* xz = x + z * x_cs;
+    const float* wz = w + z * w_cs;
+    const int FP = F + 1;
+    if constexpr (SMALLK) {
+        for (int e = tid; e < cnt * F; e += 256) {
+            const int b = e / F;
+            Xs[b * FP + (e - b * F)] = xz[e];
+        }
+        for (int e = tid; e < K * F; e += 256) {
+            const int k = e / F;
+            Ws[k * FP + (e - k * F)] = wz[e];
+        }
+        __syncthreads();
+    }
+    auto X = [&](int b, int f) -> float { return SMALLK ? Xs[b * FP + f] : xz[(int64_t)b * F + f]; };
+    auto Wt = [&](int k, int f) -> float { return SMALLK ? Ws[k * FP + f] : wz[(int64_t)k * F + f]; };
+    // 1. logits
+    for (int o = tid; o < cnt * K; o += 256) {
+        const int img = o / K, k = o - img * K;
+        float acc = 0.f;
+        for (int f = 0; f < F; ++f) acc = fmaf(X(img, f), Wt(k, f), acc);
+        L[img * K + k] = bias ? acc + bias[z * b_cs + k] : acc;
+    }
+    __syncthreads();
+    // 2. cross-entropy (ce_kernel's operations and fp64 sum order)
+    const int lane = tid & 63, wid = tid >> 6;
+    const float inv_n = cnt > 0 ? 1.0f / (float)cnt : 0.f;
+    double lsum = 0.0;
+    int corr = 0;
+    if (K <= 16) {
+        const int g = tid >> 4, l = tid & 15;
+        for (int img = g; img < cnt; img += 16) {
+            const float* row = L + img * K;
+            const int tgt = (int)targets[z * t_cs + img];
+            const float v = l < K ? row[l] : -INFINITY;
+            float mx = v;
+            int amax = l < K ? l : K;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+                const float om = __shfl_xor(mx, o, 16);
+                const int oa = __shfl_xor(amax, o, 16);
+                if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+            }
+            float se = l < K ? expf(v - mx) : 0.f;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) se += __shfl_xor(se, o, 16);
+            const float lse = logf(se);
+            if (l == 0) {
+                li[img] = (double)(-((row[tgt] - mx) - lse));
+                ci[img] = amax == tgt;
+            }
+            if (l < K) {
+                const float p = expf((v - mx) - lse);
+                D[img * K + l] = (p - (l == tgt ? 1.f : 0.f)) * inv_n;
+            }
+        }
+        __syncthreads();
+        if (tid < 4) {
+            for (int img = tid; img < cnt; img += 4) {
+                lsum += li[img];
+                corr += ci[img];
+            }
+            sl[tid] = lsum;
+            sc[tid] = corr;
+        }
+    } else {
+        for (int img = wid; img < cnt; img += 4) {
+            const float* row = L + img * K;
+            const int tgt = (int)targets[z * t_cs + img];
+            float mx = -INFINITY;
+            int amax = 0;
+            for (int k = lane; k < K; k += 64) {
+                const float v = row[k];
+                if (v > mx) { mx = v; amax = k; }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const float om = __shfl_xor(mx, o, 64);
+                const int oa = __shfl_xor(amax, o, 64);
+                if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+            }
+            float se = 0.f;
+            for (int k = lane; k < K; k += 64) se += expf(row[k] - mx);
+            se = wave_sum(se);
+            const float lse = logf(se);
+            if (lane == 0) {
+                lsum += (double)(-((row[tgt] - mx) - lse));
+                corr += (amax == tgt);
+            }
+            for (int k = lane; k < K; k += 64) {
+                const float p = expf((row[k] - mx) - lse);
+                D[img * K + k] = (p - (k == tgt ? 1.f : 0.f)) * inv_n;
+            }
+        }
+        if (lane == 0) {
+            sl[wid] = lsum;
+            sc[wid] = corr;
+        }
+    }
+    __syncthreads();
+    if (part == 0) {
+        if (tid == 0) {
+            const double tot = sl[0] + sl[1] + sl[2] + sl[3];
+            const float batch_loss = cnt > 0 ? (float)(tot / (double)cnt) : 0.f;
+            const bool rs = reset && reset[z];
+            if (loss_out) loss_out[z] = batch_loss;
+            if (acc_loss) acc_loss[z] = (rs ? 0.0 : acc_loss[z]) + (double)batch_loss;
+            if (acc_correct)
+                acc_correct[z] = (rs ? 0 : acc_correct[z]) + sc[0] + sc[1] + sc[2] + sc[3];
+            if (acc_seen) acc_seen[z] = (rs ? 0 : acc_seen[z]) + cnt;
+        }
+        for (int o = tid; o < cnt * K; o += 256) {
+            logits[z * l_cs + o] = L[o];
+            dlogits[z * d_cs + o] = D[o];
+        }
+        if (db && tid < K) {
+            float v = 0.f;
+            for (int b = 0; b < cnt; ++b) v += D[b * K + tid];
+            db[z * db_cs + tid] = v;
+        }
+    }
+    const int S = gridDim.x;
+    // 3. weight gradient, this block's share: dW[k][f] = sum_b D[b][k] x[b][f]
+    {
+        const int per = (K * F + S - 1) / S, e0 = part * per, e1 = min(K * F, e0 + per);
+        for (int e = e0 + tid; e < e1; e += 256) {
+            const int k = e / F, f = e - k * F;
+            float acc = 0.f;
+            for (int b = 0; b < cnt; ++b) acc = fmaf(D[b * K + k], X(b, f), acc);
+            dw[z * dw_cs + e] = acc;
+        }
+    }
+    // 4. input gradient through Dropout + ReLU, this block's share: dx[b][f] = sum_k D[b][k] W[k][f]
+    if (dx) {
+        const int per = (cnt * F + S - 1) / S, e0 = part * per, e1 = min(cnt * F, e0 + per);
+        for (int e = e0 + tid; e < e1; e += 256) {
+            const int img = e / F, f = e - img * F;
+            float acc = 0.f;
+            for (int k = 0; k < K; ++k) acc = fmaf(D[img * K + k], Wt(k, f), acc);
+            if (mask) acc = mask[z * m_cs + e] ? acc * scale : 0.f;
+            if (relu_in && !(X(img, f) > 0.f)) acc = 0.f;
+            dx[z * dx_cs + e] = acc;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ evaluation metrics
 // LocalTrainer.evaluate_model (training.py:307-360) / _validate_epoch (:214-242): per image
 // the first-index argmax (torch.max) and the CE loss; per slot the fp64 loss sum and correct
@@ -540,6 +727,37 @@ extern "C" int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* t
                        targets, t_cs, dlogits, d_cs, loss_out, acc_loss, acc_correct, acc_seen,
                        reset, counts, batch, num_classes);
     FH_LAUNCH_CHECK("ce_fwd_bwd");
+    return FH_OK;
+}
+
+extern "C" int fh_linear_head_ce(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                                 const float* bias, int64_t b_cs, const int64_t* targets,
+                                 int64_t t_cs, float* logits, int64_t l_cs, float* dlogits,
+                                 int64_t d_cs, float* loss_out, double* acc_loss,
+                                 int64_t* acc_correct, int64_t* acc_seen, const int32_t* reset,
+                                 float* dw, int64_t dw_cs, float* db, int64_t db_cs, float* dx,
+                                 int64_t dx_cs, const uint8_t* mask, int64_t m_cs, float p_drop,
+                                 int32_t relu_in, const int32_t* counts, int32_t nclients,
+                                 int32_t batch, int32_t in_f, int32_t num_classes, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && in_f > 0 && num_classes > 0, "linear_head_ce: bad shape");
+    FH_REQUIRE(batch <= 32 && num_classes <= 128, "linear_head_ce: needs batch <= 32 and <= 128 "
+               "classes (got %d, %d)", batch, num_classes);
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_head_ce: p=%g", p_drop);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && w && targets && logits && dlogits && dw, "linear_head_ce: null pointer");
+    const dim3 grid(kHeadBlocks, nclients);
+    const float scale = 1.0f / (1.0f - p_drop);
+    if (num_classes <= 16 && in_f <= 256)
+        FH_LAUNCH(linear_head_ce_kernel<true>, grid, dim3(256), 0, as_stream(stream), x, x_cs, w,
+                  w_cs, bias, b_cs, targets, t_cs, logits, l_cs, dlogits, d_cs, loss_out,
+                  acc_loss, acc_correct, acc_seen, reset, dw, dw_cs, db, db_cs, dx, dx_cs, mask,
+                  m_cs, scale, relu_in, counts, batch, in_f, num_classes);
+    else
+        FH_LAUNCH(linear_head_ce_kernel<false>, grid, dim3(256), 0, as_stream(stream), x, x_cs, w,
+                  w_cs, bias, b_cs, targets, t_cs, logits, l_cs, dlogits, d_cs, loss_out,
+                  acc_loss, acc_correct, acc_seen, reset, dw, dw_cs, db, db_cs, dx, dx_cs, mask,
+                  m_cs, scale, relu_in, counts, batch, in_f, num_classes);
+    FH_LAUNCH_CHECK("linear_head_ce");
     return FH_OK;
 }
 

@@ -55,11 +55,21 @@ SIGNATURES = {
     "fh_linear_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, P, SZ, P]),
     "fh_linear_wgrad_workspace": (SZ, [I32, I32, I32, I32]),
     "fh_linear_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32, P]),
+    "fh_linear_bwd_fused": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, F32,
+                                  P, I64, P, I32, I32, I32, I32, P]),
+    "fh_linear_head_ce": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, P, P, P, P,
+                                P, I64, P, I64, P, I64, P, I64, F32, I32, P, I32, I32, I32, I32,
+                                P]),
     "fh_bn_workspace": (SZ, [I32, I32, I32, I32]),
     "fh_bn_fwd_train": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, P, P, I32, I32,
                               I32, I32, F32, F32, I32, P, SZ, P]),
     "fh_bn_fwd_stats": (I32, [P, I64, P, P, I64, P, P, I64, P, P, P, P, I64, P, I32, I32, I32,
                               I32, F32, F32, P, SZ, P]),
+    "fh_conv_bnstats_bytes": (SZ, [I32, I32, I32, I32, I32]),
+    "fh_conv2d_fwd_bnstats": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, P, I32, I32,
+                                    I32, I32, I32, I32, P, SZ, P]),
+    "fh_bn_finalize_tiles": (I32, [P, P, P, I64, P, P, I64, P, P, P, P, I64, P, I32, I32, I32,
+                                   I32, F32, F32, P]),
     "fh_conv2d_fwd_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
                                    I32, I32, I32, I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_conv2d_wgrad_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32,
@@ -142,8 +152,16 @@ def stream_handle(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+# Diagnostics only (timing ablations, tools/r02_ablate.sh): entry points named in
+# FH_ABLATE are not called at all, so a benchmark measures what the round would cost
+# without them.  The results are wrong by construction; never set it outside a timing probe.
+_ABLATE = frozenset(v for v in os.environ.get("FH_ABLATE", "").split(",") if v)
+
+
 def call(name: str, *args):
     """Invoke a status-returning entry point; raise FedHipError on failure."""
+    if name in _ABLATE:
+        return 0
     lib = load()
     rc = getattr(lib, name)(*args)
     if rc != 0:

@@ -216,11 +216,18 @@ class PackedTrainer:
     def _step_launches(self, n, counts, reset, first, adam_dev=None):
         """The kernel sequence of one packed step (no host bookkeeping: graph-capturable)."""
         net = self.net
+        ce = dict(loss_out=self.loss_out, acc_loss=self.acc_loss, acc_correct=self.acc_correct,
+                  acc_seen=self.acc_seen, reset=reset)
+        if self.dpsgd is None and net.fused_head and self.batch <= 32 and net.num_classes <= 128:
+            # the last linear layer, the loss and that layer's backward: one launch
+            net.forward(self.params, self.bufs, n, counts, train=True, head=False)
+            net.head_ce(self.params, self.grads, n, counts, **ce)
+            net.backward(self.params, self.grads, n, counts)
+            self._optimizer_launch(n, first, adam_dev)
+            return
         net.forward(self.params, self.bufs, n, counts, train=True)
         ops.ce_fwd_bwd(net.logits, net.y, net.dlogits, n, self.batch, net.num_classes,
-                       loss_out=self.loss_out, acc_loss=self.acc_loss,
-                       acc_correct=self.acc_correct, acc_seen=self.acc_seen, reset=reset,
-                       counts=counts)
+                       counts=counts, **ce)
         if self.dpsgd is None:
             net.backward(self.params, self.grads, n, counts)
         else:

@@ -130,7 +130,18 @@ class PackedNet:
         self.salt = 0  # per-lane key offset (a lane's slot 0 is not another lane's slot 0)
         # CIFAR10CNN training: BN apply + ReLU folded into the consumers (FH_FUSE_BN=0: off)
         self.fuse_bn = os.environ.get("FH_FUSE_BN", "1") != "0"
+        # ... and the BN statistics taken by the producing conv's epilogue instead of a
+        # second pass over its output (FH_BN_EPILOGUE=0: the separate statistics pass)
+        self.bn_epilogue = os.environ.get("FH_BN_EPILOGUE", "1") != "0"
         self._fused = False
+        # training step: the last linear layer, the cross-entropy and that layer's backward
+        # in one launch (fh_linear_head_ce; FH_FUSED_HEAD=0: separate launches)
+        self.fused_head = os.environ.get("FH_FUSED_HEAD", "1") != "0"
+        # classifier backward: wgrad + dgrad + dropout/ReLU backward in one launch where
+        # the layer shape allows (fh_linear_bwd_fused; FH_FUSED_LINEAR_BWD=0: off)
+        self.fused_linear_bwd = os.environ.get("FH_FUSED_LINEAR_BWD", "1") != "0"
+        self._head_done = False
+        self._head = True
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -162,7 +173,9 @@ class PackedNet:
         return self.mask_mode
 
     # -------------------------------------------------------------- forward
-    def forward(self, params, bufs, n, counts, train=True):
+    def forward(self, params, bufs, n, counts, train=True, head=True):
+        """head=False: stop before the last linear layer (its forward runs inside head_ce)."""
+        self._head = head
         if n == 0:
             return self.logits
         fam = self.family
@@ -174,8 +187,34 @@ class PackedNet:
             self._fwd_resnet(params, bufs, n, counts, train)
         return self.logits
 
-    def backward(self, params, grads, n, counts):
+    def head_ce(self, params, grads, n, counts, **ce):
+        """Last linear layer + cross-entropy + its backward + the dropout/ReLU backward of
+        its input, one launch (after forward(head=False)); ce: ce_fwd_bwd's outputs."""
+        self._head_done = True
         if n == 0:
+            return
+        A, B, W, K, P_, G = self.A, self.batch, self.W, self.num_classes, params, grads
+        fam = self.family
+        if fam == "CIFAR10CNN":
+            x, F, wname, dx = self._e2, 256, "fc3", A("dh2", 256)
+            mask = A("m_fc2", 256, dtype=torch.uint8) if self._dm else None
+            relu = True
+        elif fam == "SimpleCNN":
+            x, F, wname, dx = self._fc_in, 128, "fc2", A("dh1", 128)
+            mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
+            relu = True
+        else:
+            x, F, wname, dx = A("feat", 256), 256, "fc", A("dfeat", 256)
+            mask, relu = None, False
+        ops.linear_head_ce(x, W(P_, f"{wname}.weight"), W(P_, f"{wname}.bias"), self.y,
+                           self.logits, self.dlogits, W(G, f"{wname}.weight"),
+                           W(G, f"{wname}.bias"), dx, n, B, F, K, mask=mask,
+                           p_drop=self.dropout_p, relu_in=relu, counts=counts, **ce)
+
+    def backward(self, params, grads, n, counts):
+        """After head_ce the last layer's backward is already done."""
+        if n == 0:
+            self._head_done = False
             return
         fam = self.family
         if fam == "SimpleCNN":
@@ -184,6 +223,7 @@ class PackedNet:
             self._bwd_cifar(params, grads, n, counts)
         else:
             self._bwd_resnet(params, grads, n, counts)
+        self._head_done = False
 
     # ---------------- SimpleCNN (models_pytorch.py:82-97)
     def _fwd_simple(self, P_, n, cnt, train):
@@ -208,20 +248,22 @@ class PackedNet:
                             seed_dev=self.seed_dev)
             x3 = d1
         self._fc_in = x3
-        ops.linear_fwd(x3, W(P_, "fc2.weight"), W(P_, "fc2.bias"), self.logits, n, B, 128,
-                       self.num_classes, counts=cnt)
+        if self._head:
+            ops.linear_fwd(x3, W(P_, "fc2.weight"), W(P_, "fc2.bias"), self.logits, n, B, 128,
+                           self.num_classes, counts=cnt)
 
     def _bwd_simple(self, P_, G, n, cnt):
         A, B, W = self.A, self.batch, self.W
         K = self.num_classes
-        ops.linear_wgrad(self._fc_in, self.dlogits, W(G, "fc2.weight"), W(G, "fc2.bias"), n, B,
-                         128, K, counts=cnt)
-        dd1 = A("dd1", 128)
-        ops.linear_dgrad(self.dlogits, W(P_, "fc2.weight"), dd1, n, B, 128, K, counts=cnt)
         dh1 = A("dh1", 128)
-        mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
-        ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
-                        relu_out=A("h1", 128), counts=cnt)
+        if not self._head_done:
+            ops.linear_wgrad(self._fc_in, self.dlogits, W(G, "fc2.weight"), W(G, "fc2.bias"), n,
+                             B, 128, K, counts=cnt)
+            dd1 = A("dd1", 128)
+            ops.linear_dgrad(self.dlogits, W(P_, "fc2.weight"), dd1, n, B, 128, K, counts=cnt)
+            mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
+            ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
+                            relu_out=A("h1", 128), counts=cnt)
         ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136,
                          128, counts=cnt)
         dp2 = A("dp2", 64, 7, 7)
@@ -323,6 +365,15 @@ class PackedNet:
                              torch.zeros(self.cap, C, device=self.device))
         return self.A.t[key]
 
+    def _bn_part(self, name, C, hw):
+        """fp64 [cap, C, tiles, 2]: the per-tile BN statistics a conv epilogue writes."""
+        key = f"{name}.part"
+        if key not in self.A.t:
+            tiles = ops.bnstats_tiles(self.batch, hw, hw)
+            self.A.t[key] = torch.zeros(self.cap, C, tiles, 2, dtype=torch.float64,
+                                        device=self.device)
+        return self.A.t[key]
+
     def _bn_affine(self, name, C):
         key = f"{name}.affine"
         if key not in self.A.t:
@@ -342,16 +393,22 @@ class PackedNet:
         xin, aff = self.x, None
         for i, (cv, ci, co, hw, bn) in enumerate(self._CIFAR_CONVS):
             c = A(f"c_{cv}", co, hw, hw)
+            part = None
+            if fuse and self.bn_epilogue:
+                part = self._bn_part(bn, co, hw)
             ops.conv2d_fwd(xin, W(P_, f"{cv}.weight"), W(P_, f"{cv}.bias"), c, n, B, ci, hw, hw, co,
-                           3, 1, 1, counts=cnt, in_affine=aff)
+                           3, 1, 1, counts=cnt, in_affine=aff, bn_stats=part)
             if fuse:
                 sm, si = self._bn_save(bn, co)
                 aff = self._bn_affine(bn, co)
-                ops.bn_fwd_stats(c, W(P_, f"{bn}.weight"), W(P_, f"{bn}.bias"),
-                                 self.layout.bview(bufs, f"{bn}.running_mean"),
-                                 self.layout.bview(bufs, f"{bn}.running_var"), sm, si, aff[0],
-                                 aff[1], n, B, co, hw * hw, self.bn_eps, self.bn_momentum,
-                                 counts=cnt)
+                stat_args = (W(P_, f"{bn}.weight"), W(P_, f"{bn}.bias"),
+                             self.layout.bview(bufs, f"{bn}.running_mean"),
+                             self.layout.bview(bufs, f"{bn}.running_var"), sm, si, aff[0],
+                             aff[1], n, B, co, hw * hw, self.bn_eps, self.bn_momentum)
+                if part is not None:
+                    ops.bn_finalize_tiles(part, *stat_args, counts=cnt)
+                else:
+                    ops.bn_fwd_stats(c, *stat_args, counts=cnt)
                 xin = c
             else:
                 r = A(f"r_{cv}", co, hw, hw)
@@ -382,30 +439,43 @@ class PackedNet:
             ops.dropout_fwd(h2, e2, A("m_fc2", 256, dtype=torch.uint8), n, B, 256, self.dropout_p,
                             dm, self._seed(22), counts=cnt, seed_dev=self.seed_dev)
         self._e1, self._e2, self._dm = e1, e2, dm
-        ops.linear_fwd(e2, W(P_, "fc3.weight"), W(P_, "fc3.bias"), self.logits, n, B, 256,
-                       self.num_classes, counts=cnt)
+        if self._head:
+            ops.linear_fwd(e2, W(P_, "fc3.weight"), W(P_, "fc3.bias"), self.logits, n, B, 256,
+                           self.num_classes, counts=cnt)
 
     def _bwd_cifar(self, P_, G, n, cnt):
         A, B, W = self.A, self.batch, self.W
         K, dm, p = self.num_classes, self._dm, self.dropout_p
-        ops.linear_wgrad(self._e2, self.dlogits, W(G, "fc3.weight"), W(G, "fc3.bias"), n, B, 256, K,
-                         counts=cnt)
-        de2 = A("de2", 256)
-        ops.linear_dgrad(self.dlogits, W(P_, "fc3.weight"), de2, n, B, 256, K, counts=cnt)
         dh2 = A("dh2", 256)
-        ops.dropout_bwd(de2, dh2, n, B, 256, mask=A("m_fc2", 256, dtype=torch.uint8) if dm else None,
-                        p_drop=p, relu_out=A("h2", 256), counts=cnt)
-        ops.linear_wgrad(self._e1, dh2, W(G, "fc2.weight"), W(G, "fc2.bias"), n, B, 512, 256,
-                         counts=cnt)
-        de1 = A("de1", 512)
-        ops.linear_dgrad(dh2, W(P_, "fc2.weight"), de1, n, B, 512, 256, counts=cnt)
+        if not self._head_done:
+            ops.linear_wgrad(self._e2, self.dlogits, W(G, "fc3.weight"), W(G, "fc3.bias"), n, B,
+                             256, K, counts=cnt)
+            de2 = A("de2", 256)
+            ops.linear_dgrad(self.dlogits, W(P_, "fc3.weight"), de2, n, B, 256, K, counts=cnt)
+            ops.dropout_bwd(de2, dh2, n, B, 256,
+                            mask=A("m_fc2", 256, dtype=torch.uint8) if dm else None,
+                            p_drop=p, relu_out=A("h2", 256), counts=cnt)
         dh1 = A("dh1", 512)
-        ops.dropout_bwd(de1, dh1, n, B, 512, mask=A("m_fc1", 512, dtype=torch.uint8) if dm else None,
-                        p_drop=p, relu_out=A("h1", 512), counts=cnt)
+        # fc2 backward + the dropout/ReLU backward of its input e1 (e1 > 0 <=> h1 > 0 where
+        # the keep-mask is 1): one launch, else three
+        m1 = A("m_fc1", 512, dtype=torch.uint8) if dm else None
+        if not (self.fused_linear_bwd and ops.linear_bwd_fused(
+                self._e1, dh2, W(P_, "fc2.weight"), W(G, "fc2.weight"), W(G, "fc2.bias"), dh1, n,
+                B, 512, 256, mask=m1, p_drop=p, relu_ref=self._e1, counts=cnt)):
+            ops.linear_wgrad(self._e1, dh2, W(G, "fc2.weight"), W(G, "fc2.bias"), n, B, 512, 256,
+                             counts=cnt)
+            de1 = A("de1", 512)
+            ops.linear_dgrad(dh2, W(P_, "fc2.weight"), de1, n, B, 512, 256, counts=cnt)
+            ops.dropout_bwd(de1, dh1, n, B, 512, mask=m1, p_drop=p, relu_out=A("h1", 512),
+                            counts=cnt)
         q3 = A("q_conv6", 128, 4, 4)
-        ops.linear_wgrad(q3, dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 2048, 512, counts=cnt)
         dq = A("dq_conv6", 128, 4, 4)
-        ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dq, n, B, 2048, 512, counts=cnt)
+        if not (self.fused_linear_bwd and ops.linear_bwd_fused(
+                q3, dh1, W(P_, "fc1.weight"), W(G, "fc1.weight"), W(G, "fc1.bias"), dq, n, B,
+                2048, 512, counts=cnt)):
+            ops.linear_wgrad(q3, dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 2048, 512,
+                             counts=cnt)
+            ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dq, n, B, 2048, 512, counts=cnt)
         convs = self._CIFAR_CONVS
         for i in range(len(convs) - 1, -1, -1):
             cv, ci, co, hw, bn = convs[i]
@@ -482,17 +552,19 @@ class PackedNet:
         f = A("feat", 256)
         ho = self.blocks[-1]["hout"]
         ops.avgpool_fwd(xin, f, n, B, 256, ho * ho, counts=cnt)
-        ops.linear_fwd(f, W(P_, "fc.weight"), W(P_, "fc.bias"), self.logits, n, B, 256,
-                       self.num_classes, counts=cnt)
+        if self._head:
+            ops.linear_fwd(f, W(P_, "fc.weight"), W(P_, "fc.bias"), self.logits, n, B, 256,
+                           self.num_classes, counts=cnt)
 
     def _bwd_resnet(self, P_, G, n, cnt):
         A, B, W = self.A, self.batch, self.W
         K = self.num_classes
         f = A("feat", 256)
-        ops.linear_wgrad(f, self.dlogits, W(G, "fc.weight"), W(G, "fc.bias"), n, B, 256, K,
-                         counts=cnt)
         df = A("dfeat", 256)
-        ops.linear_dgrad(self.dlogits, W(P_, "fc.weight"), df, n, B, 256, K, counts=cnt)
+        if not self._head_done:
+            ops.linear_wgrad(f, self.dlogits, W(G, "fc.weight"), W(G, "fc.bias"), n, B, 256, K,
+                             counts=cnt)
+            ops.linear_dgrad(self.dlogits, W(P_, "fc.weight"), df, n, B, 256, K, counts=cnt)
         last = self.blocks[-1]
         dout = A(f"{last['pfx']}.dout", last["cout"], last["hout"], last["hout"])
         ops.avgpool_bwd(df, dout, n, B, 256, last["hout"] ** 2, counts=cnt)

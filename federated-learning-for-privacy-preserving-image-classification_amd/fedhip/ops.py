@@ -212,6 +212,11 @@ def _ws_for(fn_name, device, *args):
 
 
 # ------------------------------------------------------------------ conv / linear
+# diagnostics only (timing ablations): linear layers with these input widths are skipped
+_ABLATE_LINEAR = frozenset(int(v) for v in __import__("os").environ.get("FH_ABLATE_LINEAR", "")
+                           .split(",") if v)
+
+
 def _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad):
     oh = (h + 2 * pad - k) // stride + 1
     ow = (wd + 2 * pad - k) // stride + 1
@@ -219,14 +224,24 @@ def _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad):
 
 
 def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad, relu=False,
-               counts=None, in_affine=None):
+               counts=None, in_affine=None, bn_stats=None):
     """in_affine = (scale, shift) [clients, cin]: x is a BatchNorm pre-activation and the
-    kernel convolves relu(x * scale + shift) (fh_conv2d_fwd_bnrelu)."""
+    kernel convolves relu(x * scale + shift) (fh_conv2d_fwd_bnrelu).  bn_stats: fp64
+    [clients, cout, tiles, 2] (bnstats_tiles) that receives the BatchNorm statistics of y
+    from the epilogue (fh_conv2d_fwd_bnstats; direct 3x3 path, relu off)."""
     require_device(x, "x")
     ws, nb = _ws_for("fh_conv2d_fwd_workspace", x.device, nclients, batch, cin, h, wd, cout, k, k,
                      stride, pad)
     ev = PROBE.begin(_conv_tag("fwd", cin, h, wd, cout, k, stride))
-    if in_affine is not None:
+    if bn_stats is not None:
+        if relu or k != 3 or stride != 1 or pad != 1:
+            raise FedHipError("conv2d_fwd(bn_stats=...): 3x3/s1/p1 without ReLU only")
+        sc, sh = in_affine if in_affine is not None else (None, None)
+        call("fh_conv2d_fwd_bnstats", ptr(x), _cs(x), ptr(sc), ptr(sh),
+             _cs(sc) if sc is not None else 0, ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y),
+             _cs(y), ptr(bn_stats), _counts(counts), nclients, batch, cin, h, wd, cout, ptr(ws),
+             nb, stream_handle())
+    elif in_affine is not None:
         sc, sh = in_affine
         call("fh_conv2d_fwd_bnrelu", ptr(x), _cs(x), ptr(sc), ptr(sh), _cs(sc), ptr(w), _cs(w),
              ptr(bias), _cs(bias), ptr(y), _cs(y), _counts(counts), nclients, batch, cin, h, wd,
@@ -271,6 +286,8 @@ def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pa
 
 
 def linear_fwd(x, w, bias, y, nclients, batch, in_f, out_f, relu=False, counts=None):
+    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
+        return None
     require_device(x, "x")
     ws, nb = _ws_for("fh_linear_fwd_workspace", x.device, nclients, batch, in_f, out_f)
     ev = PROBE.begin(f"linear_fwd:{in_f}->{out_f}")
@@ -281,6 +298,8 @@ def linear_fwd(x, w, bias, y, nclients, batch, in_f, out_f, relu=False, counts=N
 
 
 def linear_dgrad(dy, w, dx, nclients, batch, in_f, out_f, counts=None):
+    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
+        return None
     ws, nb = _ws_for("fh_linear_dgrad_workspace", dy.device, nclients, batch, in_f, out_f)
     ev = PROBE.begin(f"linear_dgrad:{in_f}->{out_f}")
     call("fh_linear_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
@@ -290,6 +309,8 @@ def linear_dgrad(dy, w, dx, nclients, batch, in_f, out_f, counts=None):
 
 
 def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
+    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
+        return None
     ws, nb = _ws_for("fh_linear_wgrad_workspace", x.device, nclients, batch, in_f, out_f)
     ev = PROBE.begin(f"linear_wgrad:{in_f}->{out_f}")
     call("fh_linear_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
@@ -299,6 +320,42 @@ def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
 
 
 # ------------------------------------------------------------------ DP-SGD (per-sample clip)
+def linear_bwd_fused(x, dy, w, dw, db, dx, nclients, batch, in_f, out_f, mask=None, p_drop=0.0,
+                     relu_ref=None, counts=None):
+    """linear_wgrad + linear_dgrad + dropout_bwd(dx, mask, relu_out) in one launch
+    (fh_linear_bwd_fused).  Returns False (nothing issued) when the shape is outside the
+    fused kernel (the caller then issues the three ops)."""
+    if not (batch <= 32 and in_f % 128 == 0 and out_f % 32 == 0 and dy.data_ptr() % 16 == 0
+            and dy.stride(0) % 4 == 0 and w.stride(0) % 4 == 0):
+        return False
+    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
+        return True
+    ev = PROBE.begin(f"linear_bwd:{in_f}->{out_f}")
+    call("fh_linear_bwd_fused", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dw),
+         _cs(dw), ptr(db), _cs(db), ptr(dx), _cs(dx), ptr(mask), _cs(mask), float(p_drop),
+         ptr(relu_ref), _cs(relu_ref), _counts(counts), nclients, batch, in_f, out_f,
+         stream_handle())
+    PROBE.end(ev, 4.0 * nclients * batch * in_f * out_f)
+    return True
+
+
+def linear_head_ce(x, w, bias, targets, logits, dlogits, dw, db, dx, nclients, batch, in_f,
+                   num_classes, loss_out=None, acc_loss=None, acc_correct=None, acc_seen=None,
+                   reset=None, mask=None, p_drop=0.0, relu_in=False, counts=None):
+    """Last linear layer forward + cross-entropy (ce_fwd_bwd's outputs) + that layer's
+    backward + the dropout/ReLU backward of its input, one launch per client
+    (fh_linear_head_ce)."""
+    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
+        return
+    ev = PROBE.begin(f"linear_head:{in_f}->{num_classes}")
+    call("fh_linear_head_ce", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(targets),
+         _cs(targets), ptr(logits), _cs(logits), ptr(dlogits), _cs(dlogits), ptr(loss_out),
+         ptr(acc_loss), ptr(acc_correct), ptr(acc_seen), ptr(reset), ptr(dw), _cs(dw), ptr(db),
+         _cs(db), ptr(dx), _cs(dx), ptr(mask), _cs(mask), float(p_drop), int(bool(relu_in)),
+         _counts(counts), nclients, batch, in_f, num_classes, stream_handle())
+    PROBE.end(ev, 6.0 * nclients * batch * in_f * num_classes)
+
+
 def conv2d_persample_sqnorm(x, dy, sqnorm, nclients, batch, cin, h, wd, cout, k, stride, pad,
                             with_bias=True, counts=None):
     ws, nb = _ws_for("fh_conv2d_persample_sqnorm_workspace", x.device, nclients, batch, cin, h,
@@ -418,6 +475,21 @@ def bn_fwd_train(x, y, gamma, beta, rmean, rvar, save_mean, save_invstd, nclient
          ptr(beta), _cs(gamma), ptr(rmean), ptr(rvar), _cs(rmean), ptr(save_mean),
          ptr(save_invstd), _counts(counts), nclients, batch, C, HW, float(eps), float(momentum),
          int(relu), ptr(ws), nb, stream_handle())
+
+
+def bnstats_tiles(batch, h, w):
+    """256-pixel tiles per client of a [batch, h, w] map (fh_conv2d_fwd_bnstats layout)."""
+    return (batch * h * w + 255) // 256
+
+
+def bn_finalize_tiles(part, gamma, beta, rmean, rvar, save_mean, save_invstd, scale, shift,
+                      nclients, batch, C, HW, eps=1e-5, momentum=0.1, counts=None):
+    """bn_fwd_stats' outputs from the per-tile statistics a conv epilogue wrote (part, see
+    conv2d_fwd(bn_stats=...))."""
+    call("fh_bn_finalize_tiles", ptr(part), ptr(gamma), ptr(beta), _cs(gamma), ptr(rmean),
+         ptr(rvar), _cs(rmean), ptr(save_mean), ptr(save_invstd), ptr(scale), ptr(shift),
+         _cs(scale), _counts(counts), nclients, batch, C, HW, float(eps), float(momentum),
+         stream_handle())
 
 
 def bn_fwd_stats(x, gamma, beta, rmean, rvar, save_mean, save_invstd, scale, shift, nclients,

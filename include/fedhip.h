@@ -154,6 +154,17 @@ int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs
                     int64_t dw_cs, float* db, int64_t db_cs, void* workspace, size_t ws_bytes,
                     const int32_t* counts, int32_t nclients, int32_t batch, int32_t in_f,
                     int32_t out_f, void* stream);
+/* One launch for a classifier layer's whole backward (nn.Linear.backward + the
+ * F.dropout / ReLU backward of its input, models_pytorch.py:153-163): dw, db (nullable) as
+ * fh_linear_wgrad, and dx = (dy W) * keep(mask)/(1-p) where relu_ref > 0 (mask, relu_ref
+ * nullable: that factor is skipped).  batch <= 32, in_f % 128 == 0, out_f % 32 == 0, dy
+ * rows 16-B aligned; FH_E_UNSUPPORTED otherwise. */
+int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                        const float* w, int64_t w_cs, float* dw, int64_t dw_cs, float* db,
+                        int64_t db_cs, float* dx, int64_t dx_cs, const uint8_t* mask,
+                        int64_t m_cs, float p_drop, const float* relu_ref, int64_t r_cs,
+                        const int32_t* counts, int32_t nclients, int32_t batch, int32_t in_f,
+                        int32_t out_f, void* stream);
 
 /* ---------------- BatchNorm2d (+ReLU, +residual add) ----------------------
  * x/y/res: [clients][batch][C][HW]; gamma/beta live in the per-client param
@@ -270,6 +281,21 @@ int fh_ce_fwd_bwd(const float* logits, int64_t l_cs, const int64_t* targets, int
                   int64_t* acc_correct, int64_t* acc_seen, const int32_t* reset,
                   const int32_t* counts, int32_t nclients, int32_t batch, int32_t num_classes,
                   void* stream);
+/* The classifier head of a training step in one launch per client (replaces the last
+ * nn.Linear forward, fh_ce_fwd_bwd, that layer's wgrad / dgrad and the dropout backward in
+ * front of it: CIFAR10CNN fc3 models_pytorch.py:159-165, SimpleCNN fc2 :96-97,
+ * FederatedResNet fc :241-246, with LocalTrainer's criterion training.py:193-203):
+ * logits = x W^T + b (also stored), CE outputs exactly as fh_ce_fwd_bwd, dw / db (nullable),
+ * and dx (nullable) = (dlogits W) * keep(mask)/(1-p), zeroed where relu_in and x <= 0.
+ * batch <= 32, num_classes <= 128. */
+int fh_linear_head_ce(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                      const float* bias, int64_t b_cs, const int64_t* targets, int64_t t_cs,
+                      float* logits, int64_t l_cs, float* dlogits, int64_t d_cs, float* loss_out,
+                      double* acc_loss, int64_t* acc_correct, int64_t* acc_seen,
+                      const int32_t* reset, float* dw, int64_t dw_cs, float* db, int64_t db_cs,
+                      float* dx, int64_t dx_cs, const uint8_t* mask, int64_t m_cs, float p_drop,
+                      int32_t relu_in, const int32_t* counts, int32_t nclients, int32_t batch,
+                      int32_t in_f, int32_t num_classes, void* stream);
 
 /* ---------------- BatchNorm apply + ReLU folded into the consumer (CIFAR10CNN) -------
  * The train-mode BN output relu(x*w*invstd + b - mean*w*invstd) is never written: the
@@ -307,6 +333,27 @@ int fh_maxpool2_fwd_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
                            const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
                            int32_t H, int32_t W, int32_t drop_mode, float p_drop, uint64_t seed,
                            const uint64_t* seed_dev, void* stream);
+/* BatchNorm statistics from the producing convolution (models_pytorch.py:128-137 conv ->
+ * bn; replaces the statistics pass of nn.BatchNorm2d's train forward): the direct-conv
+ * forward (fh_conv2d_fwd_bnrelu semantics, in_scale/in_shift nullable, no ReLU on y) also
+ * writes one fp64 (sum of y, sum of y^2) pair per (client, channel, 256-pixel tile of the
+ * client's [batch*H*W] pixels) into bn_part (fh_conv_bnstats_bytes; tiles past a client's
+ * count are zero), and fh_bn_finalize_tiles merges them in tile order into fh_bn_fwd_stats'
+ * outputs — y is never re-read for its statistics. */
+size_t fh_conv_bnstats_bytes(int32_t nclients, int32_t batch, int32_t cout, int32_t h,
+                             int32_t w_);
+int fh_conv2d_fwd_bnstats(const float* x, int64_t x_cs, const float* in_scale,
+                          const float* in_shift, int64_t aff_cs, const float* w, int64_t w_cs,
+                          const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                          double* bn_part, const int32_t* counts, int32_t nclients,
+                          int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                          void* workspace, size_t ws_bytes, void* stream);
+int fh_bn_finalize_tiles(const double* part, const float* gamma, const float* beta,
+                         int64_t p_cs, float* running_mean, float* running_var, int64_t r_cs,
+                         float* save_mean, float* save_invstd, float* scale_out,
+                         float* shift_out, int64_t s_cs, const int32_t* counts,
+                         int32_t nclients, int32_t batch, int32_t C, int32_t HW, float eps,
+                         float momentum, void* stream);
 
 /* ---------------- launch planning ---------------------------------------------
  * Share of the chip (0, 1] that the split-K planners of the conv / linear entry points

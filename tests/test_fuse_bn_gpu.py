@@ -14,14 +14,16 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _round(fuse, opt, sizes, rounds=2):
+def _round(fuse, opt, sizes, rounds=2, bn_epilogue=False):
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.3).to(DEV)
     S = len(sizes)
     eng = PackedTrainer(model, capacity=S, batch=32, device=DEV)
     eng.net.fuse_bn = fuse
+    eng.net.bn_epilogue = bn_epilogue
     for k in range(S):
         eng.load_module_state(k, model)
+    eng.init_params = eng.params.clone()
     g = torch.Generator().manual_seed(5)
     data = torch.randn(sum(sizes), 3, 32, 32, generator=g).to(DEV)
     labels = torch.randint(0, 10, (sum(sizes),), generator=g).to(DEV)
@@ -109,6 +111,92 @@ def test_fused_ops_match_apply_pass(nc, C, hw):
         k = int(cnt[z])
         assert torch.equal(q1[z, :k], q2[z, :k]) and torch.equal(i1[z, :k], i2[z, :k])
         assert torch.equal(m1[z, :k], m2[z, :k])
+
+
+def _ulps(a, b):
+    """Largest distance in units in the last place between two fp32 tensors."""
+    ia = a.contiguous().view(torch.int32).to(torch.int64)
+    ib = b.contiguous().view(torch.int32).to(torch.int64)
+    ia = torch.where(ia < 0, -(ia & 0x7FFFFFFF), ia)
+    ib = torch.where(ib < 0, -(ib & 0x7FFFFFFF), ib)
+    return int((ia - ib).abs().max())
+
+
+# client counts that take the unsplit epilogue (many clients) and the split-K epilogue
+# kernel (one client: the planner splits the input channels), every map width, with and
+# without a BN-on-load input, ragged counts
+@pytest.mark.parametrize("nc,ci,co,hw,affine", [(1, 32, 32, 32, True), (1, 3, 32, 32, False),
+                                                (1, 64, 128, 8, True), (3, 32, 64, 16, True),
+                                                (32, 32, 32, 32, True), (32, 64, 64, 16, False),
+                                                (24, 128, 128, 8, True), (9, 64, 128, 8, False)])
+def test_epilogue_bn_stats_match_separate_pass(nc, ci, co, hw, affine):
+    """fh_conv2d_fwd_bnstats + fh_bn_finalize_tiles vs fh_conv2d_fwd_bnrelu + fh_bn_fwd_stats:
+    y bit-identical; the per-tile fp64 partials equal fp64 sums of the stored y; the BN
+    outputs (save_mean/invstd, running stats, the consumer's affine) within 1 ulp (the two
+    paths add the same fp64 terms in different orders)."""
+    B = 32
+    torch.manual_seed(nc * 7 + co)
+    cnt = torch.tensor([B] + [int(v) for v in torch.randint(1, B + 1, (nc - 1,))],
+                       dtype=torch.int32, device=DEV)
+    x = torch.randn(nc, B, ci, hw, hw, device=DEV)
+    w = torch.randn(nc, co, ci, 3, 3, device=DEV) * 0.1
+    bias = torch.randn(nc, co, device=DEV) * 0.2 + 0.5
+    aff = None
+    if affine:
+        aff = (torch.rand(nc, ci, device=DEV) + 0.5, torch.randn(nc, ci, device=DEV) * 0.2)
+    y1 = torch.zeros(nc, B, co, hw, hw, device=DEV)
+    y2 = torch.zeros_like(y1)
+    part = torch.full((nc, co, ops.bnstats_tiles(B, hw, hw), 2), float("nan"),
+                      dtype=torch.float64, device=DEV)
+    ops.conv2d_fwd(x, w, bias, y1, nc, B, ci, hw, hw, co, 3, 1, 1, counts=cnt, in_affine=aff)
+    ops.conv2d_fwd(x, w, bias, y2, nc, B, ci, hw, hw, co, 3, 1, 1, counts=cnt, in_affine=aff,
+                   bn_stats=part)
+    torch.cuda.synchronize()
+    for z in range(nc):
+        k = int(cnt[z])
+        assert torch.equal(y1[z, :k], y2[z, :k])
+    # partials: fp64 sums of the stored values of each 256-pixel tile (zeros past the count)
+    T = part.shape[2]
+    yz = y2.double().permute(0, 2, 1, 3, 4).reshape(nc, co, B * hw * hw)
+    for z in range(nc):
+        yz[z, :, int(cnt[z]) * hw * hw:] = 0.0
+    yt = torch.nn.functional.pad(yz, (0, T * 256 - B * hw * hw)).reshape(nc, co, T, 256)
+    assert not torch.isnan(part).any()
+    torch.testing.assert_close(part[..., 0], yt.sum(-1), rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(part[..., 1], (yt * yt).sum(-1), rtol=1e-12, atol=1e-9)
+    # BN outputs
+    gamma = torch.rand(nc, co, device=DEV) + 0.5
+    beta = torch.randn(nc, co, device=DEV) * 0.3
+    outs = []
+    for use_part in (False, True):
+        rm, rv = torch.zeros(nc, co, device=DEV), torch.ones(nc, co, device=DEV)
+        sm, si = torch.zeros(nc, co, device=DEV), torch.zeros(nc, co, device=DEV)
+        sc, sh = torch.zeros(nc, co, device=DEV), torch.zeros(nc, co, device=DEV)
+        if use_part:
+            ops.bn_finalize_tiles(part, gamma, beta, rm, rv, sm, si, sc, sh, nc, B, co, hw * hw,
+                                  counts=cnt)
+        else:
+            ops.bn_fwd_stats(y1, gamma, beta, rm, rv, sm, si, sc, sh, nc, B, co, hw * hw,
+                             counts=cnt)
+        outs.append((rm, rv, sm, si, sc, sh))
+    for u, v in zip(*outs):
+        assert _ulps(u, v) <= 1
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_epilogue_bn_stats_rounds_match(opt):
+    """Whole CIFAR10CNN rounds with the statistics from the conv epilogues vs the separate
+    statistics pass: the same training up to the fp64 summation order of the statistics."""
+    sizes = [130, 70, 33, 9]
+    a, ma = _round(True, opt, sizes, bn_epilogue=True)
+    b, mb = _round(True, opt, sizes, bn_epilogue=False)
+    P = a.layout.P
+    d = (a.params[:, :P] - b.params[:, :P]).norm(dim=1)
+    upd = (b.params[:, :P] - b.init_params[:, :P]).norm(dim=1)
+    assert bool((d <= 1e-3 * upd).all()), (d, upd)
+    for ra, rb in zip(ma, mb):
+        for x, y in zip(ra, rb):
+            assert abs(x.loss - y.loss) <= 1e-4 * max(1.0, abs(y.loss))
 
 
 def test_fused_entry_points_refuse_unsupported_shapes():
