@@ -81,22 +81,21 @@ __device__ __forceinline__ void for_slice(const BNArgs& a, int z, int c, int s, 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
-// merge this channel's S partials (fixed order) -> (n, sum0, sum1)
+// Merge channel c's S partials -> (sum0, sum1), wave-cooperative: lane l adds partials
+// l, l+64, ... in order, then an xor-shuffle tree; a fixed order, the same result in every
+// lane.  Every lane of the calling wave must call it with the same (z, c).  (A sequential
+// merge by one thread was S/8 dependent L2 round trips: the finalize on the critical path.)
 __device__ __forceinline__ void merge(const BNArgs& a, int z, int c, double& s0, double& s1) {
     const double2* p = reinterpret_cast<const double2*>(a.part + (((int64_t)z * a.C + c) * a.S) * 2);
     s0 = 0.0;
     s1 = 0.0;
-    for (int i0 = 0; i0 < a.S; i0 += 8) {  // 8 partials in flight, added in slice order
-        double2 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = i0 + j < a.S ? p[i0 + j] : make_double2(0.0, 0.0);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (i0 + j < a.S) {
-                s0 += v[j].x;
-                s1 += v[j].y;
-            }
+    for (int i = threadIdx.x & 63; i < a.S; i += 64) {
+        const double2 v = p[i];
+        s0 += v.x;
+        s1 += v.y;
     }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
 }
 
 __global__ void __launch_bounds__(256) bn_stats_kernel(const BNArgs a) {
@@ -184,12 +183,14 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const BNArgs a) {
 // beta', same operations, so relu(x*scale + shift) is bit-identical to its output).
 __global__ void __launch_bounds__(256) bn_finalize_kernel(const BNArgs a, float* scale,
                                                           float* shift, int64_t s_cs) {
-    const int c = blockIdx.x * 256 + threadIdx.x, z = blockIdx.y;
+    // one wave per channel (merge() is wave-cooperative)
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6), z = blockIdx.y;
     if (c >= a.C) return;
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int64_t n = (int64_t)cnt * a.HW;
     double sum, sq;
     merge(a, z, c, sum, sq);
+    if ((threadIdx.x & 63) != 0) return;
     const double mean = n > 0 ? sum / (double)n : 0.0;
     double var = n > 0 ? sq / (double)n - mean * mean : 0.0;
     if (var < 0.0) var = 0.0;
@@ -208,6 +209,91 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const BNArgs a, float*
     const float bconst = a.beta[z * a.p_cs + c] - meanf * alpha;
     scale[z * s_cs + c] = alpha;
     shift[z * s_cs + c] = bconst;
+}
+
+// BatchNorm finalize fused into the 2x2 max-pool (+dropout) that consumes the BN-ReLU output
+// (CIFAR10CNN bn2/bn4/bn6 -> relu -> pool -> dropout, models_pytorch.py:139-155): one launch
+// instead of fh_bn_finalize_tiles + fh_maxpool2_fwd_bnrelu.  Blocks own one channel of one
+// client (BPC blocks per channel split its pooled elements); each merges the channel's
+// per-tile partials from the producing conv's epilogue (lane-strided fp64 sums combined by
+// xor-shuffles: a fixed order, the same in every block of the channel), derives the affine
+// with bn_finalize_kernel's operations, and pools relu(x*alpha + beta') exactly as
+// maxpool2_fwd_kernel (window argmax, Philox keep-mask keyed by the pooled element index).
+// Block 0 of the channel writes save_mean / save_invstd, the running statistics and the
+// affine.
+__global__ void __launch_bounds__(256)
+maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __restrict__ shift_out,
+                      int64_t s_cs, const float* __restrict__ x, int64_t x_cs,
+                      float* __restrict__ y, int64_t y_cs, uint8_t* __restrict__ idx, int64_t i_cs,
+                      uint8_t* __restrict__ mask, int64_t m_cs, int H, int W, int drop_mode,
+                      float keep_prob, float dscale, uint64_t seed_salt,
+                      const uint64_t* __restrict__ seed_dev, int bpc) {
+    __shared__ float s_aff[2];
+    const int z = blockIdx.y, c = blockIdx.x / bpc, sb = blockIdx.x - c * bpc;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int64_t n = (int64_t)cnt * a.HW;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        double s0, s1;
+        merge(a, z, c, s0, s1);
+        if (lane == 0) {
+            const double mean = n > 0 ? s0 / (double)n : 0.0;
+            double var = n > 0 ? s1 / (double)n - mean * mean : 0.0;
+            if (var < 0.0) var = 0.0;
+            const double invstd = n > 0 ? 1.0 / sqrt(var + (double)a.eps) : 0.0;
+            const float meanf = (float)mean, invstdf = (float)invstd;
+            const float alpha = invstdf * a.gamma[z * a.p_cs + c];
+            const float bconst = a.beta[z * a.p_cs + c] - meanf * alpha;
+            s_aff[0] = alpha;
+            s_aff[1] = bconst;
+            if (sb == 0) {
+                a.save_mean[z * a.C + c] = meanf;
+                a.save_invstd[z * a.C + c] = invstdf;
+                if (a.rmean && n > 0) {
+                    const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+                    float* rm = a.rmean + z * a.r_cs + c;
+                    float* rv = a.rvar + z * a.r_cs + c;
+                    *rm = (float)((double)a.momentum * mean + (1.0 - (double)a.momentum) * (double)*rm);
+                    *rv = (float)((double)a.momentum * unb + (1.0 - (double)a.momentum) * (double)*rv);
+                }
+                scale_out[z * s_cs + c] = alpha;
+                shift_out[z * s_cs + c] = bconst;
+            }
+        }
+    }
+    __syncthreads();
+    const float s = s_aff[0], t = s_aff[1];
+    const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
+    const int OH = H / 2, OW = W / 2, ohw = OH * OW;
+    const float* xb = x + z * x_cs;
+    const int64_t per_ch = (int64_t)cnt * ohw;
+    for (int64_t q = (int64_t)sb * 256 + threadIdx.x; q < per_ch; q += (int64_t)bpc * 256) {
+        const int img = (int)(q / ohw), r = (int)(q - (int64_t)img * ohw);
+        const int oh = r / OW, ow = r - oh * OW;
+        const int64_t plane = (int64_t)img * a.C + c;
+        const int64_t e = plane * ohw + r;  // maxpool2_fwd_kernel's element index
+        const float* pp = xb + plane * H * W + (2 * oh) * W + 2 * ow;
+        const float v0 = fmaxf(pp[0] * s + t, 0.f), v1 = fmaxf(pp[1] * s + t, 0.f);
+        const float v2 = fmaxf(pp[W] * s + t, 0.f), v3 = fmaxf(pp[W + 1] * s + t, 0.f);
+        float m = v0;
+        int am = 0;
+        if (v1 > m) { m = v1; am = 1; }
+        if (v2 > m) { m = v2; am = 2; }
+        if (v3 > m) { m = v3; am = 3; }
+        idx[z * i_cs + e] = (uint8_t)am;
+        if (drop_mode) {
+            uint8_t keep;
+            if (drop_mode == 1) {
+                const uint4 rr = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
+                keep = u01(rr.x) <= keep_prob ? 1 : 0;
+                mask[z * m_cs + e] = keep;
+            } else {
+                keep = mask[z * m_cs + e];
+            }
+            m = keep ? m * dscale : 0.f;
+        }
+        y[z * y_cs + e] = m;
+    }
 }
 
 // eval mode: running statistics (LocalTrainer._validate_epoch / evaluate_model)
@@ -455,7 +541,7 @@ extern "C" int fh_bn_fwd_stats(const float* x, int64_t x_cs, const float* gamma,
     hipStream_t st = as_stream(stream);
     FH_LAUNCH(bn_stats_kernel, dim3(a.S, C, nclients), dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_fwd_stats stats");
-    FH_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 256), nclients), dim3(256), 0,
+    FH_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 4), nclients), dim3(256), 0,
                        st, a, scale_out, shift_out, s_cs);
     FH_LAUNCH_CHECK("bn_fwd_stats finalize");
     return FH_OK;
@@ -486,9 +572,46 @@ extern "C" int fh_bn_finalize_tiles(const double* part, const float* gamma, cons
     a.save_invstd = save_invstd;
     a.p_cs = p_cs; a.r_cs = r_cs;
     a.eps = eps; a.momentum = momentum;
-    FH_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 256), nclients), dim3(256), 0,
+    FH_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 4), nclients), dim3(256), 0,
               as_stream(stream), a, scale_out, shift_out, s_cs);
     FH_LAUNCH_CHECK("bn_finalize_tiles");
+    return FH_OK;
+}
+
+// fh_bn_finalize_tiles + fh_maxpool2_fwd_bnrelu in one launch (maxpool2_bnfin_kernel).
+extern "C" int fh_maxpool2_fwd_bnfinalize(
+        const double* part, const float* gamma, const float* beta, int64_t p_cs,
+        float* running_mean, float* running_var, int64_t r_cs, float* save_mean,
+        float* save_invstd, float* scale_out, float* shift_out, int64_t s_cs, const float* x,
+        int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx, int64_t i_cs, uint8_t* mask,
+        int64_t m_cs, const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
+        int32_t H, int32_t W, float eps, float momentum, int32_t drop_mode, float p_drop,
+        uint64_t seed, const uint64_t* seed_dev, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2 && !(H & 1) && !(W & 1),
+               "maxpool2_fwd_bnfinalize: bad shape");
+    FH_REQUIRE(drop_mode >= 0 && drop_mode <= 2 && (drop_mode == 0 || mask),
+               "maxpool2_fwd_bnfinalize: mask");
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "maxpool2_fwd_bnfinalize: p=%g", p_drop);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(part && gamma && beta && save_mean && save_invstd && scale_out && shift_out && x &&
+               y && idx, "maxpool2_fwd_bnfinalize: null pointer");
+    FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr),
+               "maxpool2_fwd_bnfinalize: running stats");
+    BNArgs a = bn_args(nclients, batch, C, H * W, counts);
+    a.S = (int)ceil_div((int64_t)batch * H * W, 256);
+    a.part = (double*)part;
+    a.gamma = gamma; a.beta = beta;
+    a.rmean = running_mean; a.rvar = running_var; a.save_mean = save_mean;
+    a.save_invstd = save_invstd;
+    a.p_cs = p_cs; a.r_cs = r_cs;
+    a.eps = eps; a.momentum = momentum;
+    const int64_t per_ch = (int64_t)batch * (H / 2) * (W / 2);
+    const int bpc = (int)std::max<int64_t>(1, ceil_div(per_ch, 256));  // one element per thread
+    const float keep = 1.0f - p_drop;
+    FH_LAUNCH(maxpool2_bnfin_kernel, dim3((unsigned)(C * bpc), nclients), dim3(256), 0,
+              as_stream(stream), a, scale_out, shift_out, s_cs, x, x_cs, y, y_cs, idx, i_cs,
+              mask, m_cs, H, W, drop_mode, keep, 1.0f / keep, seed, seed_dev, bpc);
+    FH_LAUNCH_CHECK("maxpool2_fwd_bnfinalize");
     return FH_OK;
 }
 

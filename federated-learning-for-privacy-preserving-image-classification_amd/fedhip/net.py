@@ -137,6 +137,8 @@ class PackedNet:
         # training step: the last linear layer, the cross-entropy and that layer's backward
         # in one launch (fh_linear_head_ce; FH_FUSED_HEAD=0: separate launches)
         self.fused_head = os.environ.get("FH_FUSED_HEAD", "1") != "0"
+        # the BN finalize of a pooled layer inside the max-pool launch (FH_POOL_FINALIZE=0: off)
+        self.pool_finalize = os.environ.get("FH_POOL_FINALIZE", "1") != "0"
         # classifier backward: wgrad + dgrad + dropout/ReLU backward in one launch where
         # the layer shape allows (fh_linear_bwd_fused; FH_FUSED_LINEAR_BWD=0: off)
         self.fused_linear_bwd = os.environ.get("FH_FUSED_LINEAR_BWD", "1") != "0"
@@ -398,29 +400,42 @@ class PackedNet:
                 part = self._bn_part(bn, co, hw)
             ops.conv2d_fwd(xin, W(P_, f"{cv}.weight"), W(P_, f"{cv}.bias"), c, n, B, ci, hw, hw, co,
                            3, 1, 1, counts=cnt, in_affine=aff, bn_stats=part)
+            pooled = i % 2 == 1
+            fin_in_pool = False
             if fuse:
                 sm, si = self._bn_save(bn, co)
                 aff = self._bn_affine(bn, co)
                 stat_args = (W(P_, f"{bn}.weight"), W(P_, f"{bn}.bias"),
                              self.layout.bview(bufs, f"{bn}.running_mean"),
                              self.layout.bview(bufs, f"{bn}.running_var"), sm, si, aff[0],
-                             aff[1], n, B, co, hw * hw, self.bn_eps, self.bn_momentum)
-                if part is not None:
-                    ops.bn_finalize_tiles(part, *stat_args, counts=cnt)
+                             aff[1])
+                if part is not None and pooled and self.pool_finalize:
+                    fin_in_pool = True  # the finalize runs inside the pool launch below
+                elif part is not None:
+                    ops.bn_finalize_tiles(part, *stat_args, n, B, co, hw * hw, self.bn_eps,
+                                          self.bn_momentum, counts=cnt)
                 else:
-                    ops.bn_fwd_stats(c, *stat_args, counts=cnt)
+                    ops.bn_fwd_stats(c, *stat_args, n, B, co, hw * hw, self.bn_eps,
+                                     self.bn_momentum, counts=cnt)
                 xin = c
             else:
                 r = A(f"r_{cv}", co, hw, hw)
                 self._bn_train(P_, bufs, bn, c, r, n, co, hw * hw, cnt, relu=True, train=train)
                 xin, aff = r, None
-            if i % 2 == 1:
+            if pooled:
                 q = A(f"q_{cv}", co, hw // 2, hw // 2)
                 idx = A(f"i_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8)
                 msk = A(f"m_{cv}", co, hw // 2, hw // 2, dtype=torch.uint8) if dm else None
-                ops.maxpool2_fwd(xin, q, idx, n, B, co, hw, hw, mask=msk, drop_mode=dm,
-                                 p_drop=self.dropout_p, seed=self._seed(10 + i), counts=cnt,
-                                 seed_dev=self.seed_dev, in_affine=aff)
+                if fin_in_pool:
+                    ops.maxpool2_fwd_bnfinalize(part, *stat_args, c, q, idx, n, B, co, hw, hw,
+                                                self.bn_eps, self.bn_momentum, mask=msk,
+                                                drop_mode=dm, p_drop=self.dropout_p,
+                                                seed=self._seed(10 + i), counts=cnt,
+                                                seed_dev=self.seed_dev)
+                else:
+                    ops.maxpool2_fwd(xin, q, idx, n, B, co, hw, hw, mask=msk, drop_mode=dm,
+                                     p_drop=self.dropout_p, seed=self._seed(10 + i), counts=cnt,
+                                     seed_dev=self.seed_dev, in_affine=aff)
                 xin, aff = q, None
         # classifier: fc1 -> relu -> drop -> fc2 -> relu -> drop -> fc3
         h1, h2 = A("h1", 512), A("h2", 256)

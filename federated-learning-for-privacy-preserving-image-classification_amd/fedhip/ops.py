@@ -492,6 +492,18 @@ def bn_finalize_tiles(part, gamma, beta, rmean, rvar, save_mean, save_invstd, sc
          stream_handle())
 
 
+def maxpool2_fwd_bnfinalize(part, gamma, beta, rmean, rvar, save_mean, save_invstd, scale,
+                            shift, x, y, idx, nclients, batch, C, H, W, eps=1e-5, momentum=0.1,
+                            mask=None, drop_mode=0, p_drop=0.0, seed=0, counts=None,
+                            seed_dev=None):
+    """bn_finalize_tiles + maxpool2_fwd(in_affine=(scale, shift)) in one launch."""
+    call("fh_maxpool2_fwd_bnfinalize", ptr(part), ptr(gamma), ptr(beta), _cs(gamma), ptr(rmean),
+         ptr(rvar), _cs(rmean), ptr(save_mean), ptr(save_invstd), ptr(scale), ptr(shift),
+         _cs(scale), ptr(x), _cs(x), ptr(y), _cs(y), ptr(idx), _cs(idx), ptr(mask), _cs(mask),
+         _counts(counts), nclients, batch, C, H, W, float(eps), float(momentum), int(drop_mode),
+         float(p_drop), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), stream_handle())
+
+
 def bn_fwd_stats(x, gamma, beta, rmean, rvar, save_mean, save_invstd, scale, shift, nclients,
                  batch, C, HW, eps=1e-5, momentum=0.1, counts=None):
     """Train-mode BN statistics ending in the consumer's affine (scale, shift [clients, C]):

@@ -348,6 +348,19 @@ int fh_conv2d_fwd_bnstats(const float* x, int64_t x_cs, const float* in_scale,
                           double* bn_part, const int32_t* counts, int32_t nclients,
                           int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
                           void* workspace, size_t ws_bytes, void* stream);
+/* fh_bn_finalize_tiles fused into the 2x2 max-pool (+dropout, drop_mode as fh_maxpool2_fwd)
+ * of the BN-ReLU output (CIFAR10CNN conv -> bn -> relu -> pool -> dropout,
+ * models_pytorch.py:139-155): the same outputs as fh_bn_finalize_tiles followed by
+ * fh_maxpool2_fwd_bnrelu, one launch. */
+int fh_maxpool2_fwd_bnfinalize(const double* part, const float* gamma, const float* beta,
+                               int64_t p_cs, float* running_mean, float* running_var,
+                               int64_t r_cs, float* save_mean, float* save_invstd,
+                               float* scale_out, float* shift_out, int64_t s_cs, const float* x,
+                               int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx, int64_t i_cs,
+                               uint8_t* mask, int64_t m_cs, const int32_t* counts,
+                               int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                               float eps, float momentum, int32_t drop_mode, float p_drop,
+                               uint64_t seed, const uint64_t* seed_dev, void* stream);
 int fh_bn_finalize_tiles(const double* part, const float* gamma, const float* beta,
                          int64_t p_cs, float* running_mean, float* running_var, int64_t r_cs,
                          float* save_mean, float* save_invstd, float* scale_out,

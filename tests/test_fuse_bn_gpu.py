@@ -206,3 +206,57 @@ def test_fused_entry_points_refuse_unsupported_shapes():
     y = torch.zeros(1, 4, 64, 14, 14, device=DEV)
     with pytest.raises(ops.FedHipError):
         ops.conv2d_fwd(x, w, None, y, 1, 4, 32, 14, 14, 64, 3, 1, 1, in_affine=(sc, sh))
+
+
+@pytest.mark.parametrize("nc,C,hw,dm", [(1, 32, 32, 1), (5, 64, 16, 1), (3, 128, 8, 0),
+                                        (24, 32, 32, 1)])
+def test_pool_finalize_matches_separate_launches(nc, C, hw, dm):
+    """fh_maxpool2_fwd_bnfinalize == fh_bn_finalize_tiles + fh_maxpool2_fwd_bnrelu: the BN
+    outputs within 1 ulp (tree vs sequential merge of the same fp64 partials); the pooled
+    values, window argmax and dropout keep-mask bit-identical to the separate pool launch
+    given the affine the fused kernel publishes."""
+    B = 32
+    torch.manual_seed(nc * 11 + C)
+    cnt = torch.tensor([B] + [int(v) for v in torch.randint(1, B + 1, (nc - 1,))],
+                       dtype=torch.int32, device=DEV)
+    ci = 16
+    x = torch.randn(nc, B, ci, hw, hw, device=DEV)
+    w = torch.randn(nc, C, ci, 3, 3, device=DEV) * 0.1
+    bias = torch.randn(nc, C, device=DEV) * 0.2
+    c = torch.zeros(nc, B, C, hw, hw, device=DEV)
+    part = torch.zeros(nc, C, ops.bnstats_tiles(B, hw, hw), 2, dtype=torch.float64, device=DEV)
+    ops.conv2d_fwd(x, w, bias, c, nc, B, ci, hw, hw, C, 3, 1, 1, counts=cnt, bn_stats=part)
+    gamma = torch.rand(nc, C, device=DEV) + 0.5
+    gamma[:, ::5] *= -1
+    beta = torch.randn(nc, C, device=DEV) * 0.3
+    outs = []
+    for fused in (False, True):
+        rm, rv = torch.zeros(nc, C, device=DEV), torch.ones(nc, C, device=DEV)
+        sm, si = torch.zeros(nc, C, device=DEV), torch.zeros(nc, C, device=DEV)
+        sc, sh = torch.zeros(nc, C, device=DEV), torch.zeros(nc, C, device=DEV)
+        q = torch.zeros(nc, B, C, hw // 2, hw // 2, device=DEV)
+        idx = torch.zeros(nc, B, C, hw // 2, hw // 2, dtype=torch.uint8, device=DEV)
+        msk = torch.zeros_like(idx)
+        if fused:
+            ops.maxpool2_fwd_bnfinalize(part, gamma, beta, rm, rv, sm, si, sc, sh, c, q, idx, nc,
+                                        B, C, hw, hw, mask=msk, drop_mode=dm, p_drop=0.3, seed=5,
+                                        counts=cnt)
+        else:
+            ops.bn_finalize_tiles(part, gamma, beta, rm, rv, sm, si, sc, sh, nc, B, C, hw * hw,
+                                  counts=cnt)
+            ops.maxpool2_fwd(c, q, idx, nc, B, C, hw, hw, mask=msk, drop_mode=dm, p_drop=0.3,
+                             seed=5, counts=cnt, in_affine=(sc, sh))
+        outs.append((rm, rv, sm, si, sc, sh, q, idx, msk))
+    for u, v in zip(outs[0][:6], outs[1][:6]):
+        assert _ulps(u, v) <= 1
+    # the pool given the fused kernel's own affine
+    rm, rv, sm, si, sc, sh, q2, i2, m2 = outs[1]
+    q3 = torch.zeros_like(q2)
+    i3, m3 = torch.zeros_like(i2), torch.zeros_like(m2)
+    ops.maxpool2_fwd(c, q3, i3, nc, B, C, hw, hw, mask=m3, drop_mode=dm, p_drop=0.3, seed=5,
+                     counts=cnt, in_affine=(sc, sh))
+    for z in range(nc):
+        k = int(cnt[z])
+        assert torch.equal(q2[z, :k], q3[z, :k]) and torch.equal(i2[z, :k], i3[z, :k])
+        if dm:
+            assert torch.equal(m2[z, :k], m3[z, :k]) and torch.equal(m2[z, :k], outs[0][8][z, :k])
