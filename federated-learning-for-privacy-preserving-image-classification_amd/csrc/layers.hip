@@ -27,7 +27,10 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
                     int batch, int C, int H, int W, int drop_mode, float keep_prob, float scale,
                     uint64_t seed_salt, const uint64_t* __restrict__ seed_dev,
                     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
-                    int64_t aff_cs) {
+                    int64_t aff_cs, int xh, int xw, int yh, int yw) {
+    // x planes are xh x xw (row pitch xw) holding the H x W map in their top-left corner,
+    // y planes yh x yw holding the pooled map likewise (a map embedded in a wider zero
+    // ring for the direct-conv kernels); idx / mask stay dense [img][C][H/2][W/2]
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
@@ -41,8 +44,8 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
         const int64_t t = e / OW;
         const int oh = (int)(t % OH);
         const int64_t plane = t / OH;  // img*C + c
-        const float* p = xb + plane * H * W + (2 * oh) * W + 2 * ow;
-        float v0 = p[0], v1 = p[1], v2 = p[W], v3 = p[W + 1];
+        const float* p = xb + plane * xh * xw + (2 * oh) * xw + 2 * ow;
+        float v0 = p[0], v1 = p[1], v2 = p[xw], v3 = p[xw + 1];
         if (in_scale) {  // input = BN pre-activation: relu(x*scale + shift), bn_apply's ops
             const int c = (int)(plane % C);
             const float s = in_scale[z * aff_cs + c], t = in_shift[z * aff_cs + c];
@@ -68,7 +71,7 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
             }
             m = keep ? m * scale : 0.f;
         }
-        y[z * y_cs + e] = m;
+        y[z * y_cs + plane * yh * yw + oh * yw + ow] = m;
     }
 }
 
@@ -79,7 +82,9 @@ maxpool2_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const uint8_t* 
                     int64_t i_cs, const uint8_t* __restrict__ mask, int64_t m_cs,
                     const float* __restrict__ xin, int64_t x_cs, float* __restrict__ dx,
                     int64_t dx_cs, const int32_t* __restrict__ counts, int batch, int C, int H,
-                    int W, float scale) {
+                    int W, float scale, int gh, int gw, int xh, int xw) {
+    // dy planes gh x gw, dx / xin planes xh x xw (maps in the top-left corner, see
+    // maxpool2_fwd_kernel); idx / mask dense
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int OH = H / 2, OW = W / 2;
@@ -90,11 +95,11 @@ maxpool2_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const uint8_t* 
         const int64_t t = e / OW;
         const int oh = (int)(t % OH);
         const int64_t plane = t / OH;
-        float g = dy[z * dy_cs + e];
+        float g = dy[z * dy_cs + plane * gh * gw + oh * gw + ow];
         if (mask) g = mask[z * m_cs + e] ? g * scale : 0.f;
         const int a = idx[z * i_cs + e];
-        const int64_t base = plane * H * W + (2 * oh) * W + 2 * ow;
-        const int64_t off[4] = {0, 1, W, W + 1};
+        const int64_t base = plane * xh * xw + (2 * oh) * xw + 2 * ow;
+        const int64_t off[4] = {0, 1, xw, xw + 1};
         if (xin && !(xin[z * x_cs + base + off[a]] > 0.f)) g = 0.f;
         float* d = dx + z * dx_cs + base;
 #pragma unroll
@@ -627,8 +632,12 @@ static int maxpool2_fwd_impl(const float* x, int64_t x_cs, const float* in_scale
                              uint8_t* idx, int64_t i_cs, uint8_t* mask, int64_t m_cs,
                              const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
                              int32_t H, int32_t W, int32_t drop_mode, float p_drop, uint64_t seed,
-                             const uint64_t* seed_dev, void* stream) {
+                             const uint64_t* seed_dev, void* stream, int32_t xh = 0,
+                             int32_t xw = 0, int32_t yh = 0, int32_t yw = 0) {
+    if (xh == 0) { xh = H; xw = W; yh = H / 2; yw = W / 2; }
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2, "maxpool2_fwd: bad shape");
+    FH_REQUIRE(xh >= H && xw >= W && yh >= H / 2 && yw >= W / 2, "maxpool2_fwd: plane %dx%d / "
+               "%dx%d smaller than the map %dx%d", xh, xw, yh, yw, H, W);
     FH_REQUIRE((H % 2) == 0 && (W % 2) == 0, "maxpool2_fwd: odd spatial size %dx%d", H, W);
     FH_REQUIRE(drop_mode >= 0 && drop_mode <= 2 && (drop_mode == 0 || mask), "maxpool2_fwd: mask");
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "maxpool2_fwd: p=%g", p_drop);
@@ -638,7 +647,8 @@ static int maxpool2_fwd_impl(const float* x, int64_t x_cs, const float* in_scale
     const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
     FH_LAUNCH(maxpool2_fwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
                        as_stream(stream), x, x_cs, y, y_cs, idx, i_cs, mask, m_cs, counts, batch, C,
-                       H, W, drop_mode, keep, scale, seed, seed_dev, in_scale, in_shift, aff_cs);
+                       H, W, drop_mode, keep, scale, seed, seed_dev, in_scale, in_shift, aff_cs,
+                       xh, xw, yh, yw);
     FH_LAUNCH_CHECK("maxpool2_fwd");
     return FH_OK;
 }
@@ -665,22 +675,60 @@ extern "C" int fh_maxpool2_fwd_bnrelu(const float* x, int64_t x_cs, const float*
                              stream);
 }
 
-extern "C" int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,
-                               const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin,
-                               int64_t x_cs, float* dx, int64_t dx_cs, const int32_t* counts,
-                               int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
-                               void* stream) {
+static int maxpool2_bwd_impl(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,
+                             const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin,
+                             int64_t x_cs, float* dx, int64_t dx_cs, const int32_t* counts,
+                             int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                             void* stream, int32_t gh, int32_t gw, int32_t xh, int32_t xw) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2 && !(H & 1) && !(W & 1),
                "maxpool2_bwd: bad shape");
+    FH_REQUIRE(gh >= H / 2 && gw >= W / 2 && xh >= H && xw >= W, "maxpool2_bwd: plane %dx%d / "
+               "%dx%d smaller than the map %dx%d", gh, gw, xh, xw, H, W);
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(dy && idx && dx, "maxpool2_bwd: null pointer");
     const float scale = 1.0f / (1.0f - p_drop);
     const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
     FH_LAUNCH(maxpool2_bwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
                        as_stream(stream), dy, dy_cs, idx, i_cs, mask, m_cs, xin, x_cs, dx, dx_cs,
-                       counts, batch, C, H, W, scale);
+                       counts, batch, C, H, W, scale, gh, gw, xh, xw);
     FH_LAUNCH_CHECK("maxpool2_bwd");
     return FH_OK;
+}
+
+extern "C" int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,
+                               const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin,
+                               int64_t x_cs, float* dx, int64_t dx_cs, const int32_t* counts,
+                               int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                               void* stream) {
+    return maxpool2_bwd_impl(dy, dy_cs, idx, i_cs, mask, m_cs, p_drop, xin, x_cs, dx, dx_cs,
+                             counts, nclients, batch, C, H, W, stream, H / 2, W / 2, H, W);
+}
+
+// The same max-pools on maps embedded in larger planes (top-left corner; the direct-conv
+// path runs SimpleCNN's 14x14 conv on 16x16 planes with a zero ring): fwd x planes
+// xh x xw, y planes yh x yw; bwd dy planes gh x gw, dx / xin planes xh x xw.  The pool
+// never writes outside the map, so a zero ring stays zero.
+extern "C" int fh_maxpool2_fwd_pitched(const float* x, int64_t x_cs, float* y, int64_t y_cs,
+                                       uint8_t* idx, int64_t i_cs, uint8_t* mask, int64_t m_cs,
+                                       const int32_t* counts, int32_t nclients, int32_t batch,
+                                       int32_t C, int32_t H, int32_t W, int32_t drop_mode,
+                                       float p_drop, uint64_t seed, const uint64_t* seed_dev,
+                                       int32_t xh, int32_t xw, int32_t yh, int32_t yw,
+                                       void* stream) {
+    FH_REQUIRE(xh > 0 && xw > 0 && yh > 0 && yw > 0, "maxpool2_fwd_pitched: bad planes");
+    return maxpool2_fwd_impl(x, x_cs, nullptr, nullptr, 0, y, y_cs, idx, i_cs, mask, m_cs, counts,
+                             nclients, batch, C, H, W, drop_mode, p_drop, seed, seed_dev, stream,
+                             xh, xw, yh, yw);
+}
+
+extern "C" int fh_maxpool2_bwd_pitched(const float* dy, int64_t dy_cs, const uint8_t* idx,
+                                       int64_t i_cs, const uint8_t* mask, int64_t m_cs,
+                                       float p_drop, const float* xin, int64_t x_cs, float* dx,
+                                       int64_t dx_cs, const int32_t* counts, int32_t nclients,
+                                       int32_t batch, int32_t C, int32_t H, int32_t W, int32_t gh,
+                                       int32_t gw, int32_t xh, int32_t xw, void* stream) {
+    return maxpool2_bwd_impl(dy, dy_cs, idx, i_cs, mask, m_cs, p_drop, xin, x_cs, dx, dx_cs,
+                             counts, nclients, batch, C, H, W, stream, gh, gw, xh, xw);
 }
 
 extern "C" int fh_dropout_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* mask,

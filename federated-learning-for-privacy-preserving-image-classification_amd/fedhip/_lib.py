@@ -77,6 +77,10 @@ SIGNATURES = {
                                    I32, I32, I32, I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_conv2d_wgrad_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32,
                                      I32, I32, I32, I32, I32, I32, I32, I32, I32, P]),
+    "fh_maxpool2_fwd_pitched": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32,
+                                      I32, F32, U64, P, I32, I32, I32, I32, P]),
+    "fh_maxpool2_bwd_pitched": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, I32, I32,
+                                      I32, I32, I32, I32, I32, I32, I32, P]),
     "fh_maxpool2_fwd_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
                                      I32, I32, I32, F32, U64, P, P]),
     "fh_bn_fwd_eval": (I32, [P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, I32, I32, I32,

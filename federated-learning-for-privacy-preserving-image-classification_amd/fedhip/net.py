@@ -144,6 +144,10 @@ class PackedNet:
         self.fused_linear_bwd = os.environ.get("FH_FUSED_LINEAR_BWD", "1") != "0"
         self._head_done = False
         self._head = True
+        # SimpleCNN: the 14x14 conv runs on 16x16 planes (the map in the top-left corner,
+        # a zero ring around it) so the direct 3x3 kernels take it instead of the implicit
+        # GEMM; the max-pools read / write the embedded maps (FH_PAD_MAPS=0: dense 14x14)
+        self.pad_maps = os.environ.get("FH_PAD_MAPS", "1") != "0"
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -228,17 +232,28 @@ class PackedNet:
         self._head_done = False
 
     # ---------------- SimpleCNN (models_pytorch.py:82-97)
+    def _simple_maps(self):
+        """(p1, a2, da2, dp1, plane) of SimpleCNN's 14x14 conv: 16x16 planes on the direct
+        path (pad_maps; rings of p1 / da2 stay zero: nothing writes them), else dense."""
+        A = self.A
+        if self.pad_maps:
+            return (A("p1_16", 32, 16, 16), A("a2_16", 64, 16, 16), A("da2_16", 64, 16, 16),
+                    A("dp1_16", 32, 16, 16), 16)
+        return (A("p1", 32, 14, 14), A("a2", 64, 14, 14), A("da2", 64, 14, 14),
+                A("dp1", 32, 14, 14), 14)
+
     def _fwd_simple(self, P_, n, cnt, train):
         A, B, W = self.A, self.batch, self.W
-        a1, p1 = A("a1", 32, 28, 28), A("p1", 32, 14, 14)
-        a2, p2 = A("a2", 64, 14, 14), A("p2", 64, 7, 7)
+        a1 = A("a1", 32, 28, 28)
+        p1, a2, _, _, hp = self._simple_maps()
+        p2 = A("p2", 64, 7, 7)
         i1, i2 = A("i1", 32, 14, 14, dtype=torch.uint8), A("i2", 64, 7, 7, dtype=torch.uint8)
         h1, d1 = A("h1", 128), A("d1", 128)
         m1 = A("m1", 128, dtype=torch.uint8)
         ops.conv2d_fwd(self.x, W(P_, "conv1.weight"), W(P_, "conv1.bias"), a1, n, B, 1, 28, 28,
                        32, 3, 1, 1, relu=True, counts=cnt)
         ops.maxpool2_fwd(a1, p1, i1, n, B, 32, 28, 28, counts=cnt)
-        ops.conv2d_fwd(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, n, B, 32, 14, 14, 64,
+        ops.conv2d_fwd(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, n, B, 32, hp, hp, 64,
                        3, 1, 1, relu=True, counts=cnt)
         ops.maxpool2_fwd(a2, p2, i2, n, B, 64, 14, 14, counts=cnt)
         ops.linear_fwd(p2, W(P_, "fc1.weight"), W(P_, "fc1.bias"), h1, n, B, 3136, 128, relu=True,
@@ -270,13 +285,12 @@ class PackedNet:
                          128, counts=cnt)
         dp2 = A("dp2", 64, 7, 7)
         ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
-        da2 = A("da2", 64, 14, 14)
+        p1, a2, da2, dp1, hp = self._simple_maps()
         ops.maxpool2_bwd(dp2, A("i2", 64, 7, 7, dtype=torch.uint8), da2, n, B, 64, 14, 14,
-                         xin=A("a2", 64, 14, 14), counts=cnt)
-        ops.conv2d_wgrad(A("p1", 32, 14, 14), da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B,
-                         32, 14, 14, 64, 3, 1, 1, counts=cnt)
-        dp1 = A("dp1", 32, 14, 14)
-        ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, 14, 14, 64, 3, 1, 1,
+                         xin=a2, counts=cnt)
+        ops.conv2d_wgrad(p1, da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, hp, hp, 64,
+                         3, 1, 1, counts=cnt)
+        ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt)
         da1 = A("da1", 32, 28, 28)
         ops.maxpool2_bwd(dp1, A("i1", 32, 14, 14, dtype=torch.uint8), da1, n, B, 32, 28, 28,
@@ -654,7 +668,8 @@ class PackedNet:
         """Post-ReLU activations in forward order (their > 0 pattern is the ReLU mask)."""
         A = self.A
         if self.family == "SimpleCNN":
-            return [A("a1", 32, 28, 28), A("a2", 64, 14, 14), A("h1", 128)]
+            a2 = self._simple_maps()[1][..., :14, :14]
+            return [A("a1", 32, 28, 28), a2, A("h1", 128)]
         if self.family == "CIFAR10CNN":
             if self._fused:  # BN outputs not materialised: the same fp32 ops on the host side
                 out = []

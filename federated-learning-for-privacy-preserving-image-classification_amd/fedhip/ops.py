@@ -544,6 +544,17 @@ def bn_bwd_pool(dpool, pidx, yout, x, gamma, save_mean, save_invstd, dx, dgamma,
 
 def maxpool2_fwd(x, y, idx, nclients, batch, C, H, W, mask=None, drop_mode=0, p_drop=0.0, seed=0,
                  counts=None, seed_dev=None, in_affine=None):
+    """x [clients, batch, C, xh, xw], y [clients, batch, C, yh, yw]: planes larger than the
+    H x W map / its pooled map (the map in their top-left corner) go to the pitched entry."""
+    xh, xw, yh, yw = x.shape[-2], x.shape[-1], y.shape[-2], y.shape[-1]
+    if (xh, xw, yh, yw) != (H, W, H // 2, W // 2):
+        if in_affine is not None:
+            raise FedHipError("maxpool2_fwd: in_affine needs dense planes")
+        call("fh_maxpool2_fwd_pitched", ptr(x), _cs(x), ptr(y), _cs(y), ptr(idx), _cs(idx),
+             ptr(mask), _cs(mask), _counts(counts), nclients, batch, C, H, W, int(drop_mode),
+             float(p_drop), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), xh, xw, yh, yw,
+             stream_handle())
+        return
     if in_affine is not None:  # x = BN pre-activation: pool relu(x * scale + shift)
         sc, sh = in_affine
         call("fh_maxpool2_fwd_bnrelu", ptr(x), _cs(x), ptr(sc), ptr(sh), _cs(sc), ptr(y), _cs(y),
@@ -558,6 +569,16 @@ def maxpool2_fwd(x, y, idx, nclients, batch, C, H, W, mask=None, drop_mode=0, p_
 
 def maxpool2_bwd(dy, idx, dx, nclients, batch, C, H, W, mask=None, p_drop=0.0, xin=None,
                  counts=None):
+    """dy [.., gh, gw], dx / xin [.., xh, xw]: planes larger than the pooled / full map go to
+    the pitched entry (the maps in their top-left corners)."""
+    gh, gw, xh, xw = dy.shape[-2], dy.shape[-1], dx.shape[-2], dx.shape[-1]
+    if (gh, gw, xh, xw) != (H // 2, W // 2, H, W):
+        if xin is not None and tuple(xin.shape[-2:]) != (xh, xw):
+            raise FedHipError("maxpool2_bwd: xin and dx planes differ")
+        call("fh_maxpool2_bwd_pitched", ptr(dy), _cs(dy), ptr(idx), _cs(idx), ptr(mask),
+             _cs(mask), float(p_drop), ptr(xin), _cs(xin), ptr(dx), _cs(dx), _counts(counts),
+             nclients, batch, C, H, W, gh, gw, xh, xw, stream_handle())
+        return
     call("fh_maxpool2_bwd", ptr(dy), _cs(dy), ptr(idx), _cs(idx), ptr(mask), _cs(mask),
          float(p_drop), ptr(xin), _cs(xin), ptr(dx), _cs(dx), _counts(counts), nclients, batch, C,
          H, W, stream_handle())

@@ -258,6 +258,21 @@ int fh_maxpool2_bwd(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t 
                     const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin, int64_t x_cs,
                     float* dx, int64_t dx_cs, const int32_t* counts, int32_t nclients,
                     int32_t batch, int32_t C, int32_t H, int32_t W, void* stream);
+/* The same pools on H x W maps embedded in the top-left corner of larger planes (SimpleCNN's
+ * 14x14 conv runs on 16x16 planes with a zero ring on the direct-conv path): fwd x planes
+ * xh x xw and y planes yh x yw; bwd dy planes gh x gw, dx / xin planes xh x xw; idx / mask
+ * stay dense [img][C][H/2][W/2].  Nothing outside the map is written. */
+int fh_maxpool2_fwd_pitched(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
+                            int64_t i_cs, uint8_t* mask, int64_t m_cs, const int32_t* counts,
+                            int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                            int32_t drop_mode, float p_drop, uint64_t seed,
+                            const uint64_t* seed_dev, int32_t xh, int32_t xw, int32_t yh,
+                            int32_t yw, void* stream);
+int fh_maxpool2_bwd_pitched(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,
+                            const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin,
+                            int64_t x_cs, float* dx, int64_t dx_cs, const int32_t* counts,
+                            int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
+                            int32_t gh, int32_t gw, int32_t xh, int32_t xw, void* stream);
 
 /* ---------------- Dropout (F.dropout: x * bernoulli(1-p)/(1-p)) ------------
  * drop_mode 1 generate mask (uint8), 2 use the caller's mask.  Backward:

@@ -243,3 +243,41 @@ def test_adam_vector_and_scalar_paths_agree(wd, decoupled):
         outs.append([t[i][off:off + n].cpu() for i in (0, 2, 3)])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.25])
+def test_pitched_maxpool_matches_dense(p_drop):
+    """Max-pool fwd / bwd on 14x14 maps embedded in 16x16 planes (SimpleCNN's direct-conv
+    layout) == the dense kernels, bit for bit, and nothing outside the maps is written."""
+    nc, B, C, H = 3, 32, 32, 14
+    torch.manual_seed(2)
+    counts = torch.tensor([32, 17, 5], dtype=torch.int32, device=DEV)
+    x = torch.randn(nc, B, C, H, H, device=DEV)
+    xp = torch.full((nc, B, C, 16, 16), 7.0, device=DEV)
+    xp[..., :H, :H] = x
+    q = torch.zeros(nc, B, C, 7, 7, device=DEV)
+    qp = torch.full((nc, B, C, 16, 16), -3.0, device=DEV)  # pooled map into a 16x16 plane
+    i1, i2 = (torch.zeros(nc, B, C, 7, 7, dtype=torch.uint8, device=DEV) for _ in range(2))
+    m1, m2 = (torch.zeros_like(i1) if p_drop else None for _ in range(2))
+    dm = 1 if p_drop else 0
+    ops.maxpool2_fwd(x, q, i1, nc, B, C, H, H, mask=m1, drop_mode=dm, p_drop=p_drop, seed=4,
+                     counts=counts)
+    ops.maxpool2_fwd(xp, qp, i2, nc, B, C, H, H, mask=m2, drop_mode=dm, p_drop=p_drop, seed=4,
+                     counts=counts)
+    dq = torch.randn(nc, B, C, 7, 7, device=DEV)
+    dqp = torch.full((nc, B, C, 16, 16), 5.0, device=DEV)
+    dqp[..., :7, :7] = dq
+    dx = torch.zeros(nc, B, C, H, H, device=DEV)
+    dxp = torch.zeros(nc, B, C, 16, 16, device=DEV)
+    ops.maxpool2_bwd(dq, i1, dx, nc, B, C, H, H, mask=m1, p_drop=p_drop, xin=x, counts=counts)
+    ops.maxpool2_bwd(dqp, i2, dxp, nc, B, C, H, H, mask=m2, p_drop=p_drop, xin=xp, counts=counts)
+    torch.cuda.synchronize()
+    for z in range(nc):
+        k = int(counts[z])
+        assert torch.equal(q[z, :k], qp[z, :k, :, :7, :7])
+        assert torch.equal(i1[z, :k], i2[z, :k])
+        if p_drop:
+            assert torch.equal(m1[z, :k], m2[z, :k])
+        assert torch.equal(dx[z, :k], dxp[z, :k, :, :H, :H])
+    assert bool((qp[..., 7:] == -3.0).all()) and bool((qp[..., 7:, :] == -3.0).all())
+    assert bool((dxp[..., H:] == 0).all()) and bool((dxp[..., H:, :] == 0).all())

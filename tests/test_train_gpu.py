@@ -266,3 +266,38 @@ def test_packed_clients_match_independent_oracles(name, kw, shape, ncls, opt, lr
         check_loss(mk.loss, running / st, r64 / st)
         assert abs(mk.accuracy - correct / seen) <= 1.0 / seen + 1e-12
         check_params(eng.weights_dict(k), ref, ref64, init, epochs * st, lr, opt)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_simplecnn_padded_maps_match_dense(opt):
+    """SimpleCNN rounds with the 14x14 conv on zero-ringed 16x16 planes (direct kernels) vs
+    the dense 14x14 layout (implicit GEMM): the same training up to fp32 summation order."""
+    def run(pad):
+        torch.manual_seed(0)
+        model = hm.ModelFactory.create_model("simple_cnn").to(DEV)
+        sizes = [90, 40, 7]
+        eng = PackedTrainer(model, capacity=3, batch=32, device=DEV)
+        eng.net.pad_maps = pad
+        for k in range(3):
+            eng.load_module_state(k, model)
+        init = eng.params.clone()
+        g = torch.Generator().manual_seed(3)
+        data = torch.randn(sum(sizes), 1, 28, 28, generator=g).to(DEV)
+        labels = torch.randint(0, 10, (sum(sizes),), generator=g).to(DEV)
+        offs = [0, 90, 130]
+        gen = torch.Generator().manual_seed(1)
+        ms = []
+        for r in range(2):
+            plan = eng.make_plan(sizes, 1, generator=gen)
+            ms.append(eng.run_round(data, labels, offs, plan, optimizer_type=opt, lr=0.01, seed=r))
+        torch.cuda.synchronize()
+        return eng, init, ms
+    a, ia, ma = run(True)
+    b, ib, mb = run(False)
+    P = a.layout.P
+    d = (a.params[:, :P] - b.params[:, :P]).norm(dim=1)
+    upd = (b.params[:, :P] - ib[:, :P]).norm(dim=1)
+    assert bool((d <= 2e-3 * upd).all()), (d, upd)
+    for ra, rb in zip(ma, mb):
+        for x, y in zip(ra, rb):
+            assert abs(x.loss - y.loss) <= 1e-3 * max(1.0, abs(y.loss))
