@@ -220,7 +220,9 @@ class PackedTrainer:
         net = self.net
         ce = dict(loss_out=self.loss_out, acc_loss=self.acc_loss, acc_correct=self.acc_correct,
                   acc_seen=self.acc_seen, reset=reset)
-        if self.dpsgd is None and net.fused_head and self.batch <= 32 and net.num_classes <= 128:
+        # (<= 16 classes: the head kernel stages W in LDS; CIFAR-100's 100-class head is
+        # faster as separate launches, measured on K5)
+        if self.dpsgd is None and net.fused_head and self.batch <= 32 and net.num_classes <= 16:
             # the last linear layer, the loss and that layer's backward: one launch
             net.forward(self.params, self.bufs, n, counts, train=True, head=False)
             net.head_ce(self.params, self.grads, n, counts, **ce)
