@@ -34,6 +34,32 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // K = cout * taps instead of the generic DGRAD's cout * 9 with 3 of every 4 terms zero.
 enum { OP_FWD = 0, OP_DGRAD = 1, OP_WGRAD = 2, OP_DGRAD_S2 = 3 };
 
+// Dropout fused into a FWD epilogue (F.dropout after the ReLU of a classifier layer,
+// models_pytorch.py:153-163): element e of a client's output [img][cout][oh][ow] is kept with
+// probability keep (Philox keyed by (seed + *seed_dev, client, e), dropout_fwd_kernel's draw)
+// and scaled by 1/keep; mode 1 writes the keep-mask, mode 2 reads an injected one.
+struct DropArgs {
+    uint8_t* mask;
+    int64_t m_cs;
+    int mode;  // 0: off
+    float keep, scale;
+    uint64_t seed;
+    const uint64_t* seed_dev;
+};
+
+__device__ __forceinline__ float apply_dropout(const DropArgs& d, int z, int64_t e, float v) {
+    uint8_t keep;
+    if (d.mode == 1) {
+        const uint64_t seed = d.seed + (d.seed_dev ? *d.seed_dev : 0ull);
+        const uint4 r = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
+        keep = u01(r.x) <= d.keep ? 1 : 0;
+        d.mask[z * d.m_cs + e] = keep;
+    } else {
+        keep = d.mask[z * d.m_cs + e];
+    }
+    return keep ? v * d.scale : 0.f;
+}
+
 struct ConvArgs {
     const float* x;     // FWD/WGRAD: input activations; DGRAD: unused
     const float* wt;    // FWD/DGRAD: weights
@@ -51,6 +77,7 @@ struct ConvArgs {
     int sq_bias;         //   ... including the conv-bias gradient (first n-tile)
     int M, N, K;         // GEMM extents at full batch
     FastDiv fd_ohw, fd_ow, fd_hw, fd_w;
+    DropArgs drop;       // FWD: dropout after bias / ReLU (unsplit launches; else the epilogue)
 };
 
 template <int OP, int KH, int KW, int S, int BM, int BN, int BK, int WAVES_M>
@@ -382,6 +409,8 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
                             float v = acc[i][j][r];
                             if (has_bias) v = v + bv_r[i][r];
                             if (a.relu) v = fmaxf(v, 0.f);
+                            if (a.drop.mode)
+                                v = apply_dropout(a.drop, z, ((int64_t)img * a.cout + m) * ohw + p, v);
                             op[(int64_t)m * ohw] = v;
                         }
                     }
@@ -471,7 +500,8 @@ __global__ void __launch_bounds__(256)
 splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nfull,
                        float* __restrict__ out, int64_t out_cs, const float* __restrict__ bias,
                        int64_t b_cs, int relu, int accumulate, const int32_t* __restrict__ counts,
-                       int batch, int sp, double* __restrict__ bn_part, int bn_tiles) {
+                       int batch, int sp, double* __restrict__ bn_part, int bn_tiles,
+                       DropArgs drop) {
     const int z = blockIdx.z, m = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int n = blockIdx.x * 256 + threadIdx.x;
@@ -492,6 +522,7 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
         if (bias) s = s + bias[z * b_cs + m];
         if (relu) s = fmaxf(s, 0.f);
         const int img = n / sp, pix = n - img * sp;
+        if (drop.mode) s = apply_dropout(drop, z, ((int64_t)img * M + m) * sp + pix, s);
         float* o = out + z * out_cs + ((int64_t)img * M + m) * sp + pix;
         if (accumulate) s = *o + s;
         *o = s;
@@ -726,7 +757,7 @@ static int run_mn(ConvArgs a, int kh, int kw, int stride, int nclients, void* ws
         dim3 eg((unsigned)ceil_div(a.N, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.N, out, out_cs, bias, b_cs, relu, accum, a.counts, a.batch, sp,
-                           (double*)nullptr, 0);
+                           (double*)nullptr, 0, a.drop);
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -878,7 +909,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
                            OP == OP_FWD ? a.relu : 0, OP == OP_FWD ? 0 : a.accumulate, a.counts,
-                           a.batch, sp, OP == OP_FWD ? a.bn_part : nullptr, a.bn_tiles);
+                           a.batch, sp, OP == OP_FWD ? a.bn_part : nullptr, a.bn_tiles, DropArgs{});
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -1453,6 +1484,34 @@ extern "C" int fh_linear_fwd(const float* x, int64_t x_cs, const float* w, int64
                              void* stream) {
     return fh_conv2d_fwd(x, x_cs, w, w_cs, bias, b_cs, y, y_cs, counts, nclients, batch, in_f, 1, 1,
                          out_f, 1, 1, 1, 0, relu, workspace, ws_bytes, stream);
+}
+
+// fh_linear_fwd + fh_dropout_fwd (F.dropout after the layer's ReLU) in one product: the
+// dropout runs in the FWD epilogue (or the split-K epilogue), same keep-mask draws and
+// element order as fh_dropout_fwd, so y equals dropout_fwd(linear_fwd(x)).
+extern "C" int fh_linear_fwd_dropout(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                                     const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                                     uint8_t* mask, int64_t m_cs, const int32_t* counts,
+                                     int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f,
+                                     int32_t relu, int32_t drop_mode, float p_drop,
+                                     uint64_t seed, const uint64_t* seed_dev, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+    int oh, ow;
+    int rc = conv_common_check(nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0, oh, ow);
+    if (rc) return rc;
+    FH_REQUIRE((drop_mode == 1 || drop_mode == 2) && mask, "linear_fwd_dropout: mask mode");
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_fwd_dropout: p=%g", p_drop);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && w && y, "linear_fwd_dropout: null pointer");
+    ConvArgs a = make_args(batch, in_f, 1, 1, out_f, 1, 1, 0, counts);
+    a.x = x; a.wt = w; a.bias = bias; a.out = y;
+    a.x_cs = x_cs; a.w_cs = w_cs; a.b_cs = b_cs; a.out_cs = y_cs;
+    a.relu = relu;
+    a.M = out_f; a.N = batch; a.K = in_f;
+    const float keep = 1.0f - p_drop;
+    a.drop = DropArgs{mask, m_cs, drop_mode, keep, 1.0f / keep, seed, seed_dev};
+    return run_mn<OP_FWD>(a, 1, 1, 1, nclients, workspace, ws_bytes, y, y_cs, bias, b_cs, relu, 0,
+                          1, as_stream(stream), "linear_fwd_dropout");
 }
 
 extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,

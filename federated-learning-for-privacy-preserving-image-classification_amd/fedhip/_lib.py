@@ -52,6 +52,8 @@ SIGNATURES = {
     "fh_linear_fwd_workspace": (SZ, [I32, I32, I32, I32]),
     "fh_linear_dgrad_workspace": (SZ, [I32, I32, I32, I32]),
     "fh_linear_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_linear_fwd_dropout": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
+                                    I32, I32, I32, F32, U64, P, P, SZ, P]),
     "fh_linear_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, P, SZ, P]),
     "fh_linear_wgrad_workspace": (SZ, [I32, I32, I32, I32]),
     "fh_linear_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32, P]),

@@ -148,6 +148,10 @@ class PackedNet:
         # a zero ring around it) so the direct 3x3 kernels take it instead of the implicit
         # GEMM; the max-pools read / write the embedded maps (FH_PAD_MAPS=0: dense 14x14)
         self.pad_maps = os.environ.get("FH_PAD_MAPS", "1") != "0"
+        # classifier dropout in the linear layer's forward epilogue (FH_FUSED_DROPOUT=0: its
+        # own launch); the pre-dropout ReLU output is then never written — every backward
+        # decides the ReLU on the dropped output (equal wherever the keep-mask is 1)
+        self.fused_dropout = os.environ.get("FH_FUSED_DROPOUT", "1") != "0"
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -256,14 +260,20 @@ class PackedNet:
         ops.conv2d_fwd(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, n, B, 32, hp, hp, 64,
                        3, 1, 1, relu=True, counts=cnt)
         ops.maxpool2_fwd(a2, p2, i2, n, B, 64, 14, 14, counts=cnt)
-        ops.linear_fwd(p2, W(P_, "fc1.weight"), W(P_, "fc1.bias"), h1, n, B, 3136, 128, relu=True,
-                       counts=cnt)
         dm = self._drop_mode(train)
         x3 = h1
-        if dm:
-            ops.dropout_fwd(h1, d1, m1, n, B, 128, self.dropout_p, dm, self._seed(1), counts=cnt,
-                            seed_dev=self.seed_dev)
+        if dm and self.fused_dropout:
+            ops.linear_fwd_dropout(p2, W(P_, "fc1.weight"), W(P_, "fc1.bias"), d1, m1, n, B, 3136,
+                                   128, self.dropout_p, drop_mode=dm, seed=self._seed(1),
+                                   counts=cnt, seed_dev=self.seed_dev)
             x3 = d1
+        else:
+            ops.linear_fwd(p2, W(P_, "fc1.weight"), W(P_, "fc1.bias"), h1, n, B, 3136, 128,
+                           relu=True, counts=cnt)
+            if dm:
+                ops.dropout_fwd(h1, d1, m1, n, B, 128, self.dropout_p, dm, self._seed(1),
+                                counts=cnt, seed_dev=self.seed_dev)
+                x3 = d1
         self._fc_in = x3
         if self._head:
             ops.linear_fwd(x3, W(P_, "fc2.weight"), W(P_, "fc2.bias"), self.logits, n, B, 128,
@@ -280,7 +290,7 @@ class PackedNet:
             ops.linear_dgrad(self.dlogits, W(P_, "fc2.weight"), dd1, n, B, 128, K, counts=cnt)
             mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
             ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
-                            relu_out=A("h1", 128), counts=cnt)
+                            relu_out=self._fc_in, counts=cnt)
         ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136,
                          128, counts=cnt)
         dp2 = A("dp2", 64, 7, 7)
@@ -452,25 +462,34 @@ class PackedNet:
                                      seed_dev=self.seed_dev, in_affine=aff)
                 xin, aff = q, None
         # classifier: fc1 -> relu -> drop -> fc2 -> relu -> drop -> fc3
-        h1, h2 = A("h1", 512), A("h2", 256)
-        ops.linear_fwd(xin, W(P_, "fc1.weight"), W(P_, "fc1.bias"), h1, n, B, 2048, 512, relu=True,
-                       counts=cnt)
-        e1 = h1
-        if dm:
-            e1 = A("e1", 512)
-            ops.dropout_fwd(h1, e1, A("m_fc1", 512, dtype=torch.uint8), n, B, 512, self.dropout_p,
-                            dm, self._seed(21), counts=cnt, seed_dev=self.seed_dev)
-        ops.linear_fwd(e1, W(P_, "fc2.weight"), W(P_, "fc2.bias"), h2, n, B, 512, 256, relu=True,
-                       counts=cnt)
-        e2 = h2
-        if dm:
-            e2 = A("e2", 256)
-            ops.dropout_fwd(h2, e2, A("m_fc2", 256, dtype=torch.uint8), n, B, 256, self.dropout_p,
-                            dm, self._seed(22), counts=cnt, seed_dev=self.seed_dev)
+        e1 = self._linear_relu_drop(P_, "fc1", xin, "h1", "e1", "m_fc1", 2048, 512, dm, 21, n,
+                                    cnt)
+        e2 = self._linear_relu_drop(P_, "fc2", e1, "h2", "e2", "m_fc2", 512, 256, dm, 22, n, cnt)
         self._e1, self._e2, self._dm = e1, e2, dm
         if self._head:
             ops.linear_fwd(e2, W(P_, "fc3.weight"), W(P_, "fc3.bias"), self.logits, n, B, 256,
                            self.num_classes, counts=cnt)
+
+    def _linear_relu_drop(self, P_, name, x, hname, ename, mname, in_f, out_f, dm, site, n, cnt):
+        """relu(x W^T + b) then (dm) dropout: one fused launch, or linear + dropout_fwd."""
+        A, B, W = self.A, self.batch, self.W
+        if not dm:
+            h = A(hname, out_f)
+            ops.linear_fwd(x, W(P_, f"{name}.weight"), W(P_, f"{name}.bias"), h, n, B, in_f, out_f,
+                           relu=True, counts=cnt)
+            return h
+        e, m = A(ename, out_f), A(mname, out_f, dtype=torch.uint8)
+        if self.fused_dropout:
+            ops.linear_fwd_dropout(x, W(P_, f"{name}.weight"), W(P_, f"{name}.bias"), e, m, n, B,
+                                   in_f, out_f, self.dropout_p, drop_mode=dm,
+                                   seed=self._seed(site), counts=cnt, seed_dev=self.seed_dev)
+            return e
+        h = A(hname, out_f)
+        ops.linear_fwd(x, W(P_, f"{name}.weight"), W(P_, f"{name}.bias"), h, n, B, in_f, out_f,
+                       relu=True, counts=cnt)
+        ops.dropout_fwd(h, e, m, n, B, out_f, self.dropout_p, dm, self._seed(site), counts=cnt,
+                        seed_dev=self.seed_dev)
+        return e
 
     def _bwd_cifar(self, P_, G, n, cnt):
         A, B, W = self.A, self.batch, self.W
@@ -483,7 +502,7 @@ class PackedNet:
             ops.linear_dgrad(self.dlogits, W(P_, "fc3.weight"), de2, n, B, 256, K, counts=cnt)
             ops.dropout_bwd(de2, dh2, n, B, 256,
                             mask=A("m_fc2", 256, dtype=torch.uint8) if dm else None,
-                            p_drop=p, relu_out=A("h2", 256), counts=cnt)
+                            p_drop=p, relu_out=self._e2, counts=cnt)
         dh1 = A("dh1", 512)
         # fc2 backward + the dropout/ReLU backward of its input e1 (e1 > 0 <=> h1 > 0 where
         # the keep-mask is 1): one launch, else three
@@ -495,7 +514,7 @@ class PackedNet:
                              counts=cnt)
             de1 = A("de1", 512)
             ops.linear_dgrad(dh2, W(P_, "fc2.weight"), de1, n, B, 512, 256, counts=cnt)
-            ops.dropout_bwd(de1, dh1, n, B, 512, mask=m1, p_drop=p, relu_out=A("h1", 512),
+            ops.dropout_bwd(de1, dh1, n, B, 512, mask=m1, p_drop=p, relu_out=self._e1,
                             counts=cnt)
         q3 = A("q_conv6", 128, 4, 4)
         dq = A("dq_conv6", 128, 4, 4)
@@ -669,7 +688,7 @@ class PackedNet:
         A = self.A
         if self.family == "SimpleCNN":
             a2 = self._simple_maps()[1][..., :14, :14]
-            return [A("a1", 32, 28, 28), a2, A("h1", 128)]
+            return [A("a1", 32, 28, 28), a2, self._fc_in]  # dropped fc1 output: see fused_dropout
         if self.family == "CIFAR10CNN":
             if self._fused:  # BN outputs not materialised: the same fp32 ops on the host side
                 out = []
@@ -678,9 +697,9 @@ class PackedNet:
                     c = A(f"c_{cv}", co, hw, hw)
                     out.append(torch.clamp_min(c * sc[:, None, :, None, None]
                                                + sh[:, None, :, None, None], 0.0))
-                return out + [A("h1", 512), A("h2", 256)]
+                return out + [self._e1, self._e2]
             return [A(f"r_{cv}", co, hw, hw) for cv, ci, co, hw, bn in self._CIFAR_CONVS] + \
-                [A("h1", 512), A("h2", 256)]
+                [self._e1, self._e2]
         out = [A("r_stem", 64, 32, 32)]
         for b in self.blocks:
             pf, co, ho = b["pfx"], b["cout"], b["hout"]

@@ -297,6 +297,23 @@ def linear_fwd(x, w, bias, y, nclients, batch, in_f, out_f, relu=False, counts=N
     return y
 
 
+def linear_fwd_dropout(x, w, bias, y, mask, nclients, batch, in_f, out_f, p_drop, drop_mode=1,
+                       relu=True, seed=0, counts=None, seed_dev=None):
+    """linear_fwd + dropout_fwd in one product (fh_linear_fwd_dropout): y is the dropped
+    output, mask the keep-mask (drop_mode 1 generates it, 2 reads it)."""
+    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
+        return None
+    require_device(x, "x")
+    ws, nb = _ws_for("fh_linear_fwd_workspace", x.device, nclients, batch, in_f, out_f)
+    ev = PROBE.begin(f"linear_fwd:{in_f}->{out_f}")
+    call("fh_linear_fwd_dropout", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y),
+         _cs(y), ptr(mask), _cs(mask), _counts(counts), nclients, batch, in_f, out_f, int(relu),
+         int(drop_mode), float(p_drop), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), ptr(ws), nb,
+         stream_handle())
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f)
+    return y
+
+
 def linear_dgrad(dy, w, dx, nclients, batch, in_f, out_f, counts=None):
     if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
         return None

@@ -146,6 +146,16 @@ int fh_linear_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs, co
                   int64_t b_cs, float* y, int64_t y_cs, const int32_t* counts, int32_t nclients,
                   int32_t batch, int32_t in_f, int32_t out_f, int32_t relu, void* workspace,
                   size_t ws_bytes, void* stream);
+/* fh_linear_fwd followed by fh_dropout_fwd (F.dropout after the layer's ReLU,
+ * models_pytorch.py:153-163) as one product: the dropout runs in the forward epilogue
+ * with fh_dropout_fwd's keep-mask draws and element order (drop_mode 1 generate / 2 use
+ * mask), so y == dropout_fwd(linear_fwd(x)). */
+int fh_linear_fwd_dropout(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                          const float* bias, int64_t b_cs, float* y, int64_t y_cs, uint8_t* mask,
+                          int64_t m_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                          int32_t in_f, int32_t out_f, int32_t relu, int32_t drop_mode,
+                          float p_drop, uint64_t seed, const uint64_t* seed_dev, void* workspace,
+                          size_t ws_bytes, void* stream);
 int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs, float* dx,
                     int64_t dx_cs, const int32_t* counts, int32_t nclients, int32_t batch,
                     int32_t in_f, int32_t out_f, void* workspace, size_t ws_bytes, void* stream);

@@ -137,3 +137,31 @@ def test_linear_bwd_fused_declines_unsupported_shapes():
     w = torch.zeros(1, 128, 3136, device=DEV)
     assert not ops.linear_bwd_fused(x, dy, w, torch.zeros(1, 128, 3136, device=DEV), None,
                                     torch.zeros_like(x), 1, 32, 3136, 128)
+
+
+@pytest.mark.parametrize("nc,in_f,out_f", [(1, 2048, 512), (32, 2048, 512), (5, 512, 256),
+                                           (3, 3136, 128)])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_linear_fwd_dropout_equals_two_launches(nc, in_f, out_f, mode):
+    """fh_linear_fwd_dropout == fh_dropout_fwd(fh_linear_fwd(x)), bit for bit, unsplit and
+    split-K plans (1 client splits K), generated and injected keep-masks."""
+    B, p = 32, 0.3
+    cnt = _counts(nc, B, in_f + out_f)
+    g = torch.Generator(device=DEV).manual_seed(nc + in_f)
+    x = torch.randn(nc, B, in_f, generator=g, device=DEV)
+    w = torch.randn(nc, out_f, in_f, generator=g, device=DEV) * 0.05
+    b = torch.randn(nc, out_f, generator=g, device=DEV) * 0.1
+    h = torch.zeros(nc, B, out_f, device=DEV)
+    e1, e2 = torch.zeros_like(h), torch.zeros_like(h)
+    m1 = torch.zeros(nc, B, out_f, dtype=torch.uint8, device=DEV)
+    if mode == 2:
+        m1 = (torch.rand(nc, B, out_f, generator=g, device=DEV) > p).to(torch.uint8)
+    m2 = m1.clone()
+    ops.linear_fwd(x, w, b, h, nc, B, in_f, out_f, relu=True, counts=cnt)
+    ops.dropout_fwd(h, e1, m1, nc, B, out_f, p, mode, seed=77, counts=cnt)
+    ops.linear_fwd_dropout(x, w, b, e2, m2, nc, B, in_f, out_f, p, drop_mode=mode, seed=77,
+                           counts=cnt)
+    torch.cuda.synchronize()
+    for z in range(nc):
+        n = int(cnt[z])
+        assert torch.equal(e1[z, :n], e2[z, :n]) and torch.equal(m1[z, :n], m2[z, :n])
