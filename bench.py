@@ -117,6 +117,8 @@ def make_rank_data(cfg, train_sizes, my_slots, device, seed, raw=True):
         c, h, w = cfg["shape"]
         shp = (total, h, w) if c == 1 else (total, h, w, c)
         data = torch.randint(0, 256, shp, generator=g, device=device, dtype=torch.uint8)
+        if os.environ.get("FH_BENCH_CONST_DATA"):  # diagnostics: power / clock sensitivity
+            data.fill_(int(os.environ["FH_BENCH_CONST_DATA"]))
     else:
         data = torch.randn(total, *cfg["shape"], generator=g, device=device)
     labels = torch.randint(0, cfg["classes"], (total,), generator=g, device=device)
@@ -378,6 +380,10 @@ def main():
     mine = assign[rank]
     torch.manual_seed(0)
     template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
+    if os.environ.get("FH_BENCH_ZERO_WEIGHTS"):  # diagnostics: power / clock sensitivity
+        with torch.no_grad():
+            for prm in template.parameters():
+                prm.zero_()
     dp = DPConfig(epsilon=cfg["dp"]) if cfg["dp"] else None
     raw = not args.fp32_data
     tf = None
