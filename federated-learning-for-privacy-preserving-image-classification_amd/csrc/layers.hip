@@ -328,8 +328,14 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     // 1. logits
     for (int o = tid; o < cnt * K; o += 256) {
         const int img = o / K, k = o - img * K;
-        float acc = 0.f;
-        for (int f = 0; f < F; ++f) acc = fmaf(X(img, f), Wt(k, f), acc);
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four chains: LDS latency overlaps
+        for (int f = 0; f < F; f += 4) {
+            a0 = fmaf(X(img, f), Wt(k, f), a0);
+            a1 = fmaf(X(img, f + 1), Wt(k, f + 1), a1);
+            a2 = fmaf(X(img, f + 2), Wt(k, f + 2), a2);
+            a3 = fmaf(X(img, f + 3), Wt(k, f + 3), a3);
+        }
+        const float acc = (a0 + a1) + (a2 + a3);
         L[img * K + k] = bias ? acc + bias[z * b_cs + k] : acc;
     }
     __syncthreads();
@@ -436,9 +442,14 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         const int per = (K * F + S - 1) / S, e0 = part * per, e1 = min(K * F, e0 + per);
         for (int e = e0 + tid; e < e1; e += 256) {
             const int k = e / F, f = e - k * F;
-            float acc = 0.f;
-            for (int b = 0; b < cnt; ++b) acc = fmaf(D[b * K + k], X(b, f), acc);
-            dw[z * dw_cs + e] = acc;
+            float a0 = 0.f, a1 = 0.f;
+            int b = 0;
+            for (; b + 1 < cnt; b += 2) {
+                a0 = fmaf(D[b * K + k], X(b, f), a0);
+                a1 = fmaf(D[(b + 1) * K + k], X(b + 1, f), a1);
+            }
+            if (b < cnt) a0 = fmaf(D[b * K + k], X(b, f), a0);
+            dw[z * dw_cs + e] = a0 + a1;
         }
     }
     // 4. input gradient through Dropout + ReLU, this block's share: dx[b][f] = sum_k D[b][k] W[k][f]
@@ -788,8 +799,9 @@ extern "C" int fh_linear_head_ce(const float* x, int64_t x_cs, const float* w, i
                                  int32_t relu_in, const int32_t* counts, int32_t nclients,
                                  int32_t batch, int32_t in_f, int32_t num_classes, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && in_f > 0 && num_classes > 0, "linear_head_ce: bad shape");
-    FH_REQUIRE(batch <= 32 && num_classes <= 128, "linear_head_ce: needs batch <= 32 and <= 128 "
-               "classes (got %d, %d)", batch, num_classes);
+    FH_REQUIRE(batch <= 32 && num_classes <= 128 && in_f % 4 == 0, "linear_head_ce: needs batch "
+               "<= 32, <= 128 classes and in_f %% 4 == 0 (got %d, %d, %d)", batch, num_classes,
+               in_f);
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_head_ce: p=%g", p_drop);
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && w && targets && logits && dlogits && dw, "linear_head_ce: null pointer");
