@@ -828,7 +828,8 @@ static const int kDconvForceSplits = env_int("FH_DCONV_SPLITS", 0);  // sweeps: 
 static const int kDwgradForceSplits = env_int("FH_DWGRAD_SPLITS", 0);
 static const int kDconvCk32 = env_int("FH_DCONV_CK32", 8);  // sweeps: CK of the BM=32 tiles
 
-static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false) {
+static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false,
+                        bool ck4 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
     DPlan p{32, 8, 1, Cr};
     for (int bm : {128, 64}) {
@@ -839,7 +840,7 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
             break;
         }
     }
-    p.ck = (p.bm == 128 || Cr <= 4) ? 4 : (p.bm == 32 && kDconvCk32 == 4) ? 4 : 8;
+    p.ck = (ck4 || p.bm == 128 || Cr <= 4) ? 4 : (p.bm == 32 && kDconvCk32 == 4) ? 4 : 8;
     const int64_t blocks = tn * ceil_div(M, p.bm) * nclients;
     const int chunks = (int)ceil_div(Cr, p.ck);
     if ((kDconvForceSplits > 0 || blocks < fill(512)) && chunks > 1) {
@@ -860,31 +861,38 @@ static size_t dconv_ws_bytes(const DPlan& p, int nclients, int M, int batch, int
     return p.splits > 1 ? (size_t)nclients * p.splits * M * batch * hw * sizeof(float) : 0;
 }
 
-template <int OP, int W>
+template <int OP, int W, int S = 1>
 static int dconv_launch_w(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_t st) {
 #define FH_DC(BM, WMV, CK, VEC)                                                                 \
     if (p.bm == BM && p.ck == CK && (a.wvec != 0) == VEC) {                                     \
-        FH_LAUNCH((dconv_kernel<OP, W, BM, WMV, CK, VEC>), grid, dim3(256), 0, st, a);\
+        FH_LAUNCH((dconv_kernel<OP, W, BM, WMV, CK, VEC, S>), grid, dim3(256), 0, st, a);     \
         return FH_OK;                                                                           \
     }
-    FH_DC(32, 1, 8, true)
-    FH_DC(32, 1, 4, true)
-    FH_DC(64, 2, 8, true)
-    FH_DC(128, 2, 4, true)
-    FH_DC(32, 1, 8, false)
-    FH_DC(32, 1, 4, false)
+    if constexpr (S == 1) {
+        FH_DC(32, 1, 8, true)
+        FH_DC(32, 1, 4, true)
+        FH_DC(64, 2, 8, true)
+        FH_DC(128, 2, 4, true)
+        FH_DC(32, 1, 8, false)
+        FH_DC(32, 1, 4, false)
+    } else {  // stride 2 (forward): CK = 4 keeps the 2*SEGR+1-row patch at two stages in LDS
+        FH_DC(32, 1, 4, true)
+        FH_DC(64, 2, 4, true)
+        FH_DC(128, 2, 4, true)
+        FH_DC(32, 1, 4, false)
+    }
 #undef FH_DC
-    set_error("dconv: no instantiation bm=%d ck=%d", p.bm, p.ck);
+    set_error("dconv: no instantiation bm=%d ck=%d s=%d", p.bm, p.ck, S);
     return FH_E_UNSUPPORTED;
 }
 
-template <int OP>
+template <int OP, int S = 1>
 static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes, int sp,
                      hipStream_t st, const char* name) {
-    DPlan p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients);
+    DPlan p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients, false, S == 2);
     const bool aligned = ((uintptr_t)a.wt % 16 == 0) && a.w_cs % 4 == 0;
     if (!(aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0)) && p.bm != 32) {
-        p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients, /*force_bm32=*/true);  // scalar staging
+        p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients, /*force_bm32=*/true, S == 2);  // scalar
     }
     if (p.splits > 1 && (!ws || ws_bytes < dconv_ws_bytes(p, nclients, a.M, a.batch, sp))) {
         p.splits = 1;
@@ -899,9 +907,14 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     if (p.splits > 1) a.out = (float*)ws;
     dim3 grid((unsigned)ceil_div(a.Nfull, 256), (unsigned)ceil_div(a.M, p.bm),
               (unsigned)(nclients * p.splits));
-    int rc = w == 32 ? dconv_launch_w<OP, 32>(p, grid, a, st)
+    int rc;
+    if constexpr (S == 1)
+        rc = w == 32 ? dconv_launch_w<OP, 32>(p, grid, a, st)
            : w == 16 ? dconv_launch_w<OP, 16>(p, grid, a, st)
                      : dconv_launch_w<OP, 8>(p, grid, a, st);
+    else
+        rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
+                     : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
     if (rc) return rc;
     FH_LAUNCH_CHECK(name);
     if (p.splits > 1) {
@@ -913,6 +926,14 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
+}
+
+// 3x3 / stride 2 / pad 1 forward on square maps with an 8x8 or 16x16 output (ResNet
+// down-sampling blocks, 32->16 and 16->8): dconv_kernel<FWD, W_out, ..., S=2>
+static const int g_dconv_s2_off = env_int("FH_DCONV_S2", 1) == 0;  // A/B: back to igemm
+static bool dconv_s2_supported(int h, int w, int kh, int kw, int stride, int pad) {
+    return !g_dconv_s2_off && kh == 3 && kw == 3 && stride == 2 && pad == 1 && h == w &&
+           (w == 16 || w == 32);
 }
 
 // ---- direct 3x3 wgrad planning -------------------------------------------
@@ -1007,6 +1028,13 @@ extern "C" size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32
     if (dconv_supported(h, w_, kh, kw, stride, pad))
         return dconv_ws_bytes(plan_dconv(cout, cin, batch, h * w_, nclients), nclients, cout, batch,
                               h * w_);
+    if (dconv_s2_supported(h, w_, kh, kw, stride, pad)) {
+        size_t b = dconv_ws_bytes(plan_dconv(cout, cin, batch, oh * ow, nclients, false, true),
+                                  nclients, cout, batch, oh * ow);
+        size_t b32 = dconv_ws_bytes(plan_dconv(cout, cin, batch, oh * ow, nclients, true, true),
+                                    nclients, cout, batch, oh * ow);  // scalar-staging plan
+        return b > b32 ? b : b32;
+    }
     return mn_ws_bytes(plan_mn(cout, batch * oh * ow, cin * kh * kw, nclients), nclients);
 }
 
@@ -1045,6 +1073,14 @@ static int conv2d_fwd_impl(const float* x, int64_t x_cs, const float* in_scale,
         d.bn_part = bn_part; d.bn_tiles = (int)ceil_div((int64_t)batch * h * w_, 256);
         return run_dconv<OP_FWD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
                                  "conv2d_fwd");
+    }
+    if (!in_scale && !bn_part && dconv_s2_supported(h, w_, kh, kw, stride, pad)) {
+        DConvArgs d{};
+        d.in = x; d.wt = w; d.bias = bias; d.out = y;
+        d.in_cs = x_cs; d.w_cs = w_cs; d.b_cs = b_cs; d.out_cs = y_cs;
+        d.counts = counts; d.batch = batch; d.Cr = cin; d.M = cout; d.relu = relu;
+        return run_dconv<OP_FWD, 2>(d, ow, nclients, workspace, ws_bytes, oh * ow,
+                                    as_stream(stream), "conv2d_fwd_s2");
     }
     if (in_scale || bn_part) {
         set_error("conv2d_fwd_bnrelu / _bnstats: need the direct 3x3 path (3x3/s1/p1, square "

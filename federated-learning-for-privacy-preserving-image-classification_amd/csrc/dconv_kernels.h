@@ -78,25 +78,37 @@ struct DGeom {
     static_assert(256 % W == 0 && (TR % H == 0 || H % TR == 0), "tile geometry");
 };
 
-template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC>
+// S = 2 (FWD only): the 3x3 / stride-2 / pad-1 convolution of the ResNet down-sampling
+// blocks (models_pytorch.py:176-181) on the same machinery: the tile is 256 OUTPUT pixels
+// (W = output width), the staged patch covers the 2*SEGR+1 input rows those pixels read
+// (2W + 2 columns with the halo), and a lane's operand address strides by 2 — the 3x3
+// shifts stay LDS immediates.  The channel stride of the patch is odd, so the two lane
+// halves (channel pair) fall on opposite bank parities.
+template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC, int S = 1>
 __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     using G = DGeom<W>;
+    static_assert(S == 1 || (S == 2 && OP == OP_FWD), "stride 2: forward only");
+    constexpr int WI = S * W, HI = S * G::H;               // input map
+    constexpr int PRS = S == 1 ? G::SEGR + 2 : 2 * G::SEGR + 1;  // input rows per segment
+    constexpr int PW = WI + 2, PR = G::NI * PRS;
+    constexpr int CSTR = S == 1 ? PR * PW : ((PR * PW) | 1);
     constexpr int WAVES_N = 4 / WAVES_M;
     constexpr int WM = BM / WAVES_M, WN = 256 / WAVES_N;
     constexpr int FM = WM / 32, FN = WN / 32;
     constexpr int BMP = BM + 1;                 // As row pitch (staging writes spread banks)
     constexpr int KS = 9 * CK;                  // k-values per stage
-    constexpr int PE = CK * G::CSTR;            // patch elements per stage
+    constexpr int PE = CK * CSTR;               // patch elements per stage
     // staging: patch interior rows as float4 (halo columns are constant zeros), weights
     // as float4 runs of the contiguous [ch][3][3] (FWD) / [m][3][3] (DGRAD) slices
-    constexpr int PQ = W / 4, RPI = 256 / PQ, NPR = CK * G::PR, NPT = (NPR + RPI - 1) / RPI;
+    constexpr int PQ = WI / 4, RPI = 256 / PQ, NPR = CK * PR, NPT = (NPR + RPI - 1) / RPI;
     constexpr int NAV = (BM * KS / 4 + 255) / 256;   // float4 weight slots per thread
     static_assert(FM >= 1 && FN >= 1 && (CK % 2) == 0, "dconv tile");
 
     // one LDS block: the double-buffered weight / patch stages, reused after the K loop as
     // the statistics image (FWD with bn_part)
     constexpr int LDS_MAIN = 2 * KS * BMP + 2 * PE;
-    constexpr int LDS_N = (OP == OP_FWD && BM * kStatPitch > LDS_MAIN) ? BM * kStatPitch : LDS_MAIN;
+    constexpr int LDS_N = (OP == OP_FWD && S == 1 && BM * kStatPitch > LDS_MAIN) ? BM * kStatPitch
+                                                                      : LDS_MAIN;
     __shared__ float smem[LDS_N];
     float (*As)[KS * BMP] = reinterpret_cast<float (*)[KS * BMP]>(smem);
     float (*Ps)[PE] = reinterpret_cast<float (*)[PE]>(smem + 2 * KS * BMP);
@@ -109,7 +121,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int t = blockIdx.x, m0 = blockIdx.y * BM;
     const int n0 = t * 256;
-    const bool stats = OP == OP_FWD && a.bn_part != nullptr && a.splits == 1;  // block-uniform
+    const bool stats = OP == OP_FWD && S == 1 && a.bn_part != nullptr && a.splits == 1;  // block-uniform
     if (n0 >= cnt * G::HW) {  // a tile past this client's images: zero statistics
         if (stats && tid < BM && m0 + tid < a.M) {
             double* q = a.bn_part + (((int64_t)z * a.M + m0 + tid) * a.bn_tiles + t) * 2;
@@ -124,9 +136,9 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 
     for (int q = tid; q < 2 * NPR; q += 256) {  // zero halo columns of both buffers
         const int bsel = q / NPR, row = q % NPR;
-        float* r = &Ps[bsel][(row / G::PR) * G::CSTR + (row % G::PR) * G::PW];
+        float* r = &Ps[bsel][(row / PR) * CSTR + (row % PR) * PW];
         r[0] = 0.f;
-        r[W + 1] = 0.f;
+        r[WI + 1] = 0.f;
     }
 
     const int img0 = (t * G::TR) / G::H, y0 = (t * G::TR) % G::H;
@@ -141,12 +153,12 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
             const int q = prt + i * RPI;
-            const int cl = q / G::PR, pr = q % G::PR;
-            const int seg = pr / (G::SEGR + 2), rr = pr % (G::SEGR + 2);
-            const int img = img0 + seg, y = y0 + rr - 1;
-            const bool ok = q < NPR && img < cnt && (unsigned)y < (unsigned)G::H && c0 + cl < cend;
+            const int cl = q / PR, pr = q % PR;
+            const int seg = pr / PRS, rr = pr % PRS;
+            const int img = img0 + seg, y = S * y0 + rr - 1;
+            const bool ok = q < NPR && img < cnt && (unsigned)y < (unsigned)HI && c0 + cl < cend;
             rp[i] = ok ? *reinterpret_cast<const float4*>(
-                             inz + ((int64_t)(img * a.Cr + c0 + cl) * G::H + y) * W + px)
+                             inz + ((int64_t)(img * a.Cr + c0 + cl) * HI + y) * WI + px)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
             if (OP == OP_FWD && a.in_scale != nullptr) {  // applied in store(): the loads
                 bsc[i] = ok ? a.in_scale[z * a.aff_cs + c0 + cl] : 1.f;  // stay in flight over
@@ -201,7 +213,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
             const int q = prt + i * RPI;
             if (q < NPR) {
                 if (OP == OP_FWD && a.in_scale != nullptr) rp[i] = bn_relu4(rp[i], bsc[i], bsh[i]);
-                float* d = &Ps[buf][(q / G::PR) * G::CSTR + (q % G::PR) * G::PW + 1 + px];
+                float* d = &Ps[buf][(q / PR) * CSTR + (q % PR) * PW + 1 + px];
                 d[0] = rp[i].x;
                 d[1] = rp[i].y;
                 d[2] = rp[i].z;
@@ -261,7 +273,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
         const int n = wn * WN + j * 32 + col;  // local pixel
         const int ir = n / W, c = n % W;
         const int seg = ir / G::SEGR, lr = ir % G::SEGR;
-        b_lane[j] = h * G::CSTR + (seg * (G::SEGR + 2) + lr) * G::PW + c;
+        b_lane[j] = h * CSTR + (seg * PRS + S * lr) * PW + S * c;
     }
 
     if (cbeg < cend) {
@@ -280,7 +292,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 #pragma unroll 1
             for (int kh = 0; kh < 3; ++kh) {
                 const float* Ab = &As[buf][a_lane + kh * 3 * CK * BMP];
-                const float* Pb = &Ps[buf][kh * G::PW];
+                const float* Pb = &Ps[buf][kh * PW];
                 float av[2][FM], bv[2][FN];
                 auto fetch = [&](int j, int slot) {
                     const int kw = j / (CK / 2), cp = j % (CK / 2);
@@ -289,7 +301,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
                         av[slot][i] = Ab[(kw * CK + 2 * cp) * BMP + i * 32];
 #pragma unroll
                     for (int jj = 0; jj < FN; ++jj)
-                        bv[slot][jj] = Pb[b_lane[jj] + 2 * cp * G::CSTR + kw];
+                        bv[slot][jj] = Pb[b_lane[jj] + 2 * cp * CSTR + kw];
                 };
                 fetch(0, 0);
 #pragma unroll

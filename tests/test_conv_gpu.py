@@ -177,6 +177,12 @@ EXACT = [  # nclients, batch, cin, h, cout, k, stride, pad (square maps)
     (1, 32, 128, 16, 256, 3, 2, 1),
     (1, 32, 128, 16, 256, 1, 2, 0),
     (3, 19, 32, 8, 48, 3, 2, 1),
+    # stride-2 FWD on the direct kernel (S=2: 32->16, 16->8): split-K at one client,
+    # ragged counts, Cout off the tile (48), scalar weight staging (Cin % 4 != 0)
+    (3, 32, 64, 32, 96, 3, 2, 1),
+    (2, 17, 32, 16, 48, 3, 2, 1),
+    (2, 8, 6, 16, 40, 3, 2, 1),
+    (1, 5, 6, 32, 32, 3, 2, 1),
 ]
 
 
@@ -216,3 +222,18 @@ def test_conv_exact_integer(case):
         assert torch.equal(dx[z, :n].cpu().double(), xr.grad), f"dgrad z={z}"
         assert torch.equal(dw[z].cpu().double(), wr.grad), f"wgrad z={z}"
         assert torch.equal(db[z].cpu().double(), br.grad), f"bgrad z={z}"
+
+
+@pytest.mark.parametrize("h", [32, 16])
+def test_conv_s2_relu_epilogue(h):
+    """Stride-2 forward (direct kernel) with the fused ReLU epilogue == relu(plain)."""
+    C, B, cin, cout = 2, 12, 64, 128
+    g = torch.Generator().manual_seed(h)
+    x = torch.randn(C, B, cin, h, h, generator=g).to(DEV)
+    wt = (torch.randn(C, cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)).to(DEV)
+    bias = torch.randn(C, cout, generator=g).to(DEV)
+    y = torch.zeros(C, B, cout, h // 2, h // 2, device=DEV)
+    y2 = torch.zeros_like(y)
+    ops.conv2d_fwd(x, wt, bias, y, C, B, cin, h, h, cout, 3, 2, 1)
+    ops.conv2d_fwd(x, wt, bias, y2, C, B, cin, h, h, cout, 3, 2, 1, relu=True)
+    assert torch.equal(y2, torch.relu(y))
