@@ -35,7 +35,8 @@ struct BNArgs {
     float* save_invstd;
     float* dgamma;
     float* dbeta;
-    double* part;  // [z][C][S][2]
+    double* part;  // [z][C][SP][2]
+    int SP;        // partial pairs per (client, channel) merge() adds (S, or conv tiles)
     int64_t x_cs, y_cs, res_cs, dy_cs, yo_cs, dx_cs, dres_cs, p_cs, r_cs, g_cs;
     const int32_t* counts;
     int batch, C, HW, S, chunk;  // chunk: elements per slice (multiple of 4)
@@ -86,10 +87,10 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 // lane.  Every lane of the calling wave must call it with the same (z, c).  (A sequential
 // merge by one thread was S/8 dependent L2 round trips: the finalize on the critical path.)
 __device__ __forceinline__ void merge(const BNArgs& a, int z, int c, double& s0, double& s1) {
-    const double2* p = reinterpret_cast<const double2*>(a.part + (((int64_t)z * a.C + c) * a.S) * 2);
+    const double2* p = reinterpret_cast<const double2*>(a.part + (((int64_t)z * a.C + c) * a.SP) * 2);
     s0 = 0.0;
     s1 = 0.0;
-    for (int i = threadIdx.x & 63; i < a.S; i += 64) {
+    for (int i = threadIdx.x & 63; i < a.SP; i += 64) {
         const double2 v = p[i];
         s0 += v.x;
         s1 += v.y;
@@ -474,6 +475,7 @@ static BNArgs bn_args(int nclients, int batch, int C, int HW, const int32_t* cou
     a.C = C;
     a.HW = HW;
     bn_geometry(nclients, batch, C, HW, a.S, a.chunk);
+    a.SP = a.S;
     a.fd_hw = FastDiv(HW);
     a.vec = (HW & 3) == 0;
     return a;
@@ -565,7 +567,7 @@ extern "C" int fh_bn_finalize_tiles(const double* part, const float* gamma, cons
     FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr),
                "bn_finalize_tiles: running stats");
     BNArgs a = bn_args(nclients, batch, C, HW, counts);
-    a.S = (int)ceil_div((int64_t)batch * HW, 256);
+    a.S = a.SP = (int)ceil_div((int64_t)batch * HW, 256);
     a.part = (double*)part;
     a.gamma = gamma; a.beta = beta;
     a.rmean = running_mean; a.rvar = running_var; a.save_mean = save_mean;
@@ -598,7 +600,7 @@ extern "C" int fh_maxpool2_fwd_bnfinalize(
     FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr),
                "maxpool2_fwd_bnfinalize: running stats");
     BNArgs a = bn_args(nclients, batch, C, H * W, counts);
-    a.S = (int)ceil_div((int64_t)batch * H * W, 256);
+    a.S = a.SP = (int)ceil_div((int64_t)batch * H * W, 256);
     a.part = (double*)part;
     a.gamma = gamma; a.beta = beta;
     a.rmean = running_mean; a.rvar = running_var; a.save_mean = save_mean;
@@ -702,5 +704,31 @@ extern "C" int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* 
     FH_LAUNCH_CHECK("bn_bwd_pool reduce");
     FH_LAUNCH(bn_bwd_apply_kernel, grid, dim3(256), 0, st, a);
     FH_LAUNCH_CHECK("bn_bwd_pool apply");
+    return FH_OK;
+}
+
+// BN backward from statistics a convolution's DGRAD epilogue already took
+// (fh_conv2d_dgrad_bnstats: g is the ReLU-masked gradient, bn_part holds one fp64
+// (sum g, sum (x - mean) g) pair per (client, channel, 256-pixel tile)): the apply pass of
+// fh_bn_bwd only — dgamma / dbeta and dx = ((g - mean g) - (x - mean) k) invstd w.
+extern "C" int fh_bn_bwd_tiles(const double* part, const float* g, int64_t g_cs_, const float* x,
+                               int64_t x_cs, const float* gamma, int64_t p_cs,
+                               const float* save_mean, const float* save_invstd, float* dx,
+                               int64_t dx_cs, float* dgamma, float* dbeta, int64_t dg_cs,
+                               const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
+                               int32_t HW, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_bwd_tiles: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(part && g && x && gamma && save_mean && save_invstd, "bn_bwd_tiles: null pointer");
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.SP = (int)ceil_div((int64_t)batch * HW, 256);
+    a.part = (double*)part;
+    a.dy = g; a.x = x; a.gamma = gamma;
+    a.save_mean = (float*)save_mean; a.save_invstd = (float*)save_invstd;
+    a.dx = dx; a.dgamma = dgamma; a.dbeta = dbeta;
+    a.dy_cs = g_cs_; a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs; a.g_cs = dg_cs;
+    a.relu = 0;  // g is already masked
+    FH_LAUNCH(bn_bwd_apply_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
+    FH_LAUNCH_CHECK("bn_bwd_tiles");
     return FH_OK;
 }

@@ -492,22 +492,33 @@ splitk_sum_kernel(const float* __restrict__ part, float* __restrict__ dw, int64_
     }
 }
 
+// DGRAD split-K epilogue with BatchNorm backward statistics (DConvArgs::bnx and friends)
+struct BnBwdEpi {
+    const float* x;  // nullptr: off
+    int64_t x_cs;
+    const float* scale;
+    const float* shift;
+    int64_t s_cs;
+    const float* mean;
+};
+
 // FWD/DGRAD split-K epilogue: out[z][img][m][p] (=|+=) sum_s part[z][s][m][n] (+bias, relu).
-// bn_part (FWD, nullable): the BatchNorm statistics of the stored values of this block's
-// 256 pixels of channel m, one fp64 (sum, sum of squares) pair per (client, channel, tile)
-// as the unsplit dconv epilogue writes them (dconv_kernels.h DConvArgs::bn_part).
+// bn_part (nullable): one fp64 pair per (client, channel, 256-pixel tile) as the unsplit
+// dconv epilogue writes it (dconv_kernels.h DConvArgs::bn_part): FWD the BatchNorm
+// statistics (sum, sum of squares) of the stored values; DGRAD with bb.x the BN backward
+// statistics (sum g, sum (x - mean) g) of the ReLU-masked gradient g it stores.
 __global__ void __launch_bounds__(256)
 splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nfull,
                        float* __restrict__ out, int64_t out_cs, const float* __restrict__ bias,
                        int64_t b_cs, int relu, int accumulate, const int32_t* __restrict__ counts,
                        int batch, int sp, double* __restrict__ bn_part, int bn_tiles,
-                       DropArgs drop) {
+                       DropArgs drop, BnBwdEpi bb) {
     const int z = blockIdx.z, m = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int n = blockIdx.x * 256 + threadIdx.x;
     const bool valid = n < cnt * sp;
     if (!valid && bn_part == nullptr) return;
-    float s = 0.f;
+    float s = 0.f, d1f = 0.f;
     if (valid) {
         const float* p = part + ((int64_t)z * splits * M + m) * Nfull + n;
         const int64_t ss = (int64_t)M * Nfull;
@@ -525,12 +536,17 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
         if (drop.mode) s = apply_dropout(drop, z, ((int64_t)img * M + m) * sp + pix, s);
         float* o = out + z * out_cs + ((int64_t)img * M + m) * sp + pix;
         if (accumulate) s = *o + s;
+        if (bb.x) {  // ReLU mask of the BN in front; (x - mean) * g for its statistics
+            const float xv = bb.x[z * bb.x_cs + ((int64_t)img * M + m) * sp + pix];
+            if (!(xv * bb.scale[z * bb.s_cs + m] + bb.shift[z * bb.s_cs + m] > 0.f)) s = 0.f;
+            d1f = (xv - bb.mean[z * M + m]) * s;
+        }
         *o = s;
     }
     if (bn_part != nullptr) {  // block-uniform
         __shared__ double red[2][4];
         double d0 = valid ? (double)s : 0.0;
-        double d1 = d0 * d0;
+        double d1 = bb.x ? (double)d1f : d0 * d0;
         d0 = wave_sum(d0);
         d1 = wave_sum(d1);
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -757,7 +773,7 @@ static int run_mn(ConvArgs a, int kh, int kw, int stride, int nclients, void* ws
         dim3 eg((unsigned)ceil_div(a.N, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.N, out, out_cs, bias, b_cs, relu, accum, a.counts, a.batch, sp,
-                           (double*)nullptr, 0, a.drop);
+                           (double*)nullptr, 0, a.drop, BnBwdEpi{});
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -922,7 +938,9 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
                            OP == OP_FWD ? a.relu : 0, OP == OP_FWD ? 0 : a.accumulate, a.counts,
-                           a.batch, sp, OP == OP_FWD ? a.bn_part : nullptr, a.bn_tiles, DropArgs{});
+                           a.batch, sp, a.bn_part, a.bn_tiles, DropArgs{},
+                           BnBwdEpi{OP == OP_FWD ? nullptr : a.bnx, a.bnx_cs, a.bn_scale,
+                                    a.bn_shift, a.bns_cs, a.bn_mean});
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -1176,6 +1194,39 @@ extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, i
     a.M = cin; a.N = batch * h * w_; a.K = cout * kh * kw;
     return run_mn<OP_DGRAD>(a, kh, kw, stride, nclients, workspace, ws_bytes, dx, dx_cs, nullptr, 0,
                             0, accumulate, h * w_, as_stream(stream), "conv2d_dgrad");
+}
+
+// fh_conv2d_dgrad (3x3/s1/p1 direct path) whose input was relu(BN(bn_x)) — CIFAR10CNN
+// bn1/bn3/bn5 (models_pytorch.py:133-150): stores the ReLU-masked gradient
+// g = (bn_x*scale + shift > 0) ? dX : 0 (scale / shift: that BN's affine, fh_bn_fwd_stats /
+// fh_bn_finalize_tiles) and leaves the BN backward statistics (sum g, sum (bn_x - mean) g) in
+// bn_part (fh_conv_bnstats_bytes layout), so fh_bn_bwd_tiles replaces fh_bn_bwd's reduce
+// pass over g and bn_x.
+extern "C" int fh_conv2d_dgrad_bnstats(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
+                                       float* dx, int64_t dx_cs, const float* bn_x,
+                                       int64_t bnx_cs, const float* bn_scale,
+                                       const float* bn_shift, int64_t bns_cs,
+                                       const float* bn_mean, double* bn_part,
+                                       const int32_t* counts, int32_t nclients, int32_t batch,
+                                       int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                                       void* workspace, size_t ws_bytes, void* stream) {
+    int oh, ow;
+    int rc = conv_common_check(nclients, batch, cin, h, w_, cout, 3, 3, 1, 1, oh, ow);
+    if (rc) return rc;
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dy && w && dx && bn_x && bn_scale && bn_shift && bn_mean && bn_part,
+               "conv2d_dgrad_bnstats: null pointer");
+    FH_REQUIRE(dconv_supported(h, w_, 3, 3, 1, 1), "conv2d_dgrad_bnstats: needs the direct 3x3 "
+               "path (square 8/16/32 map, got %dx%d)", h, w_);
+    DConvArgs d{};
+    d.in = dy; d.wt = w; d.out = dx;
+    d.in_cs = dy_cs; d.w_cs = w_cs; d.out_cs = dx_cs;
+    d.counts = counts; d.batch = batch; d.Cr = cout; d.M = cin;
+    d.bn_part = bn_part; d.bn_tiles = (int)ceil_div((int64_t)batch * h * w_, 256);
+    d.bnx = bn_x; d.bnx_cs = bnx_cs; d.bn_scale = bn_scale; d.bn_shift = bn_shift;
+    d.bns_cs = bns_cs; d.bn_mean = bn_mean;
+    return run_dconv<OP_DGRAD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
+                               "conv2d_dgrad_bnstats");
 }
 
 extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,

@@ -48,6 +48,16 @@ struct DConvArgs {
     // epilogue kernel takes the statistics (conv.hip splitk_epilogue_kernel).
     double* bn_part;
     int bn_tiles;
+    // DGRAD with bn_part: BatchNorm BACKWARD statistics of the stored gradient.  The conv's
+    // input was relu(BN(bnx)); the kernel stores g = (bnx*bn_scale + bn_shift > 0) ? v : 0
+    // (the ReLU mask, bn.hip ReluMask) and writes per (client, channel, tile) the fp64 pair
+    // (sum g, sum (bnx - bn_mean) g) that bn_bwd_reduce_kernel would take from a second pass.
+    const float* bnx;
+    int64_t bnx_cs;
+    const float* bn_scale;
+    const float* bn_shift;
+    int64_t bns_cs;
+    const float* bn_mean;  // [client][M]
 };
 
 // Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
@@ -105,10 +115,10 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     static_assert(FM >= 1 && FN >= 1 && (CK % 2) == 0, "dconv tile");
 
     // one LDS block: the double-buffered weight / patch stages, reused after the K loop as
-    // the statistics image (FWD with bn_part)
+    // the statistics image (with bn_part)
     constexpr int LDS_MAIN = 2 * KS * BMP + 2 * PE;
-    constexpr int LDS_N = (OP == OP_FWD && S == 1 && BM * kStatPitch > LDS_MAIN) ? BM * kStatPitch
-                                                                      : LDS_MAIN;
+    constexpr int LDS_STAT = BM * kStatPitch + (OP == OP_DGRAD ? 3 * BM : 0);
+    constexpr int LDS_N = (S == 1 && LDS_STAT > LDS_MAIN) ? LDS_STAT : LDS_MAIN;
     __shared__ float smem[LDS_N];
     float (*As)[KS * BMP] = reinterpret_cast<float (*)[KS * BMP]>(smem);
     float (*Ps)[PE] = reinterpret_cast<float (*)[PE]>(smem + 2 * KS * BMP);
@@ -121,7 +131,9 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int t = blockIdx.x, m0 = blockIdx.y * BM;
     const int n0 = t * 256;
-    const bool stats = OP == OP_FWD && S == 1 && a.bn_part != nullptr && a.splits == 1;  // block-uniform
+    // block-uniform: BN statistics of the stored values (FWD) / BN backward statistics of
+    // the stored gradient (DGRAD)
+    const bool stats = S == 1 && a.bn_part != nullptr && a.splits == 1;
     if (n0 >= cnt * G::HW) {  // a tile past this client's images: zero statistics
         if (stats && tid < BM && m0 + tid < a.M) {
             double* q = a.bn_part + (((int64_t)z * a.M + m0 + tid) * a.bn_tiles + t) * 2;
@@ -323,6 +335,83 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 
     // ---- epilogue: lanes = 32 consecutive pixels -> coalesced stores ----
     const int rbase = 4 * h;
+    if constexpr (OP == OP_DGRAD) {
+        if (stats) {  // BN backward statistics (host: no accumulate)
+            float* red = smem;                         // [BM][kStatPitch] image
+            float* cst = smem + BM * kStatPitch;       // [3][BM] scale, shift, mean
+            if (tid < BM) {
+                const int m = m0 + tid;
+                const bool ok = m < M;
+                cst[tid] = ok ? a.bn_scale[z * a.bns_cs + m] : 0.f;
+                cst[BM + tid] = ok ? a.bn_shift[z * a.bns_cs + m] : 0.f;
+                cst[2 * BM + tid] = ok ? a.bn_mean[z * M + m] : 0.f;
+            }
+            __syncthreads();
+            // pass 1: g = ReLU-masked dX, stored and imaged; acc keeps (x - mean) * g, the
+            // fp32 product bn_bwd_reduce_kernel promotes
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int n = n0 + wn * WN + j * 32 + col;
+                const int img = n / G::HW, p = n % G::HW;
+                const bool live = img < cnt;
+                const float* xz = a.bnx + z * a.bnx_cs + (int64_t)img * M * G::HW + p;
+                float* op = a.out + z * a.out_cs + (int64_t)img * M * G::HW + p;
+                float xv[FM][16];  // all loads of the column first: `out` may alias `bnx`
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                        xv[i][r] = (live && m < M) ? xz[(int64_t)m * G::HW] : 0.f;
+                    }
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int ml = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                        const int m = m0 + ml;
+                        float g = 0.f, pv = 0.f;
+                        if (live && m < M) {
+                            g = (xv[i][r] * cst[ml] + cst[BM + ml] > 0.f) ? acc[i][j][r] : 0.f;
+                            pv = (xv[i][r] - cst[2 * BM + ml]) * g;
+                            op[(int64_t)m * G::HW] = g;
+                        }
+                        red[ml * kStatPitch + n - n0] = g;
+                        acc[i][j][r] = pv;
+                    }
+            }
+            constexpr int TPC = 256 / BM;
+            const int c = tid / TPC, q = tid % TPC;
+            auto image_sum = [&]() {  // per channel: TPC threads, fixed order, fp64
+                double s0 = 0.0;
+#pragma unroll 8
+                for (int k = 0; k < 256 / TPC; ++k) s0 += (double)red[c * kStatPitch + q + TPC * k];
+#pragma unroll
+                for (int o = 1; o < TPC; o <<= 1) s0 += __shfl_xor(s0, o, 64);
+                return s0;
+            };
+            __syncthreads();
+            const double sg = image_sum();
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        red[(wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase) * kStatPitch +
+                            wn * WN + j * 32 + col] = acc[i][j][r];
+            __syncthreads();
+            const double dot = image_sum();
+            const int m = m0 + c;
+            if (q == 0 && m < M) {
+                double* d = a.bn_part + (((int64_t)z * M + m) * a.bn_tiles + t) * 2;
+                d[0] = sg;
+                d[1] = dot;
+            }
+            return;
+        }
+    }
     // the bias of this lane's 16*FM output channels, read once into registers (inside the
     // store loop the compiler must re-read it after every store: `out` may alias `bias`)
     float bv_r[FM][16];
@@ -344,7 +433,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
         const int n = n0 + wn * WN + j * 32 + col;
         const int img = n / G::HW, p = n % G::HW;
         if (img >= cnt) {
-            if (OP == OP_FWD && stats) {  // past the client's images: contributes zero
+            if (stats) {  // past the client's images: contributes zero
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll

@@ -152,6 +152,10 @@ class PackedNet:
         # own launch); the pre-dropout ReLU output is then never written — every backward
         # decides the ReLU on the dropped output (equal wherever the keep-mask is 1)
         self.fused_dropout = os.environ.get("FH_FUSED_DROPOUT", "1") != "0"
+        # CIFAR10CNN backward: the ReLU mask and the BN backward statistics of bn1/bn3/bn5
+        # taken in the epilogue of the next conv's dgrad (fh_conv2d_dgrad_bnstats), so the BN
+        # backward is its apply pass only (FH_BN_BWD_EPILOGUE=0: reduce + apply)
+        self.bn_bwd_epilogue = os.environ.get("FH_BN_BWD_EPILOGUE", "1") != "0"
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -525,6 +529,7 @@ class PackedNet:
                              counts=cnt)
             ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dq, n, B, 2048, 512, counts=cnt)
         convs = self._CIFAR_CONVS
+        bn_tiles = None
         for i in range(len(convs) - 1, -1, -1):
             cv, ci, co, hw, bn = convs[i]
             dc = A(f"dc_{cv}", co, hw, hw)
@@ -537,11 +542,16 @@ class PackedNet:
                                 relu=True,
                                 pmask=A(f"m_{cv}", co, h2, h2, dtype=torch.uint8) if dm else None,
                                 p_drop=p, counts=cnt, beta=W(P_, f"{bn}.bias"))
+            elif bn_tiles is not None:  # g and its statistics from the next conv's dgrad
+                ops.bn_bwd_tiles(bn_tiles, A(f"dr_{cv}", co, hw, hw), A(f"c_{cv}", co, hw, hw),
+                                 W(P_, f"{bn}.weight"), sm, si, dc, W(G, f"{bn}.weight"),
+                                 W(G, f"{bn}.bias"), n, B, co, hw * hw, counts=cnt)
             else:           # dr was written by the next conv's dgrad
                 ops.bn_bwd(A(f"dr_{cv}", co, hw, hw), None, A(f"c_{cv}", co, hw, hw),
                            W(P_, f"{bn}.weight"), sm, si, dc, W(G, f"{bn}.weight"),
                            W(G, f"{bn}.bias"), n, B, co, hw * hw, relu=True, counts=cnt,
                            beta=W(P_, f"{bn}.bias"))
+            bn_tiles = None
             aff = None
             if i == 0:
                 xin = self.x
@@ -563,8 +573,14 @@ class PackedNet:
                 ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), dq, n, B, ci, hw, hw, co, 3, 1, 1,
                                  counts=cnt)
             else:
+                bb = None
+                if self._fused and self.bn_bwd_epilogue:
+                    pbn = convs[i - 1][4]
+                    bn_tiles = self._bn_part(pbn, ci, hw)
+                    bb = (A(f"c_{pcv}", ci, hw, hw), *self._bn_affine(pbn, ci),
+                          self._bn_save(pbn, ci)[0], bn_tiles)
                 ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), A(f"dr_{pcv}", ci, hw, hw), n, B, ci,
-                                 hw, hw, co, 3, 1, 1, counts=cnt)
+                                 hw, hw, co, 3, 1, 1, counts=cnt, bn_bwd=bb)
 
     # ---------------- FederatedResNet (models_pytorch.py:230-246, block :189-194)
     def _fwd_resnet(self, P_, bufs, n, cnt, train):

@@ -255,13 +255,24 @@ def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad,
 
 
 def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
-                 accumulate=False):
+                 accumulate=False, bn_bwd=None):
+    """bn_bwd = (bn_x, scale, shift, save_mean, part): the input was relu(BN(bn_x)) with that
+    BN's affine (scale, shift); dx receives the ReLU-masked gradient g and part the BN
+    backward statistics for bn_bwd_tiles (fh_conv2d_dgrad_bnstats, 3x3/s1/p1 only)."""
     ws, nb = _ws_for("fh_conv2d_dgrad_workspace", dy.device, nclients, batch, cin, h, wd, cout, k,
                      k, stride, pad)
     ev = PROBE.begin(_conv_tag("dgrad", cin, h, wd, cout, k, stride))
-    call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
-         nclients, batch, cin, h, wd, cout, k, k, stride, pad, int(accumulate), ptr(ws), nb,
-         stream_handle())
+    if bn_bwd is not None:
+        if accumulate or (k, stride, pad) != (3, 1, 1):
+            raise FedHipError("conv2d_dgrad(bn_bwd=...): 3x3/s1/p1 without accumulate only")
+        bx, sc, sh, mean, part = bn_bwd
+        call("fh_conv2d_dgrad_bnstats", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx),
+             ptr(bx), _cs(bx), ptr(sc), ptr(sh), _cs(sc), ptr(mean), ptr(part), _counts(counts),
+             nclients, batch, cin, h, wd, cout, ptr(ws), nb, stream_handle())
+    else:
+        call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx),
+             _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
+             int(accumulate), ptr(ws), nb, stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return dx
 
@@ -507,6 +518,14 @@ def bn_finalize_tiles(part, gamma, beta, rmean, rvar, save_mean, save_invstd, sc
          ptr(rvar), _cs(rmean), ptr(save_mean), ptr(save_invstd), ptr(scale), ptr(shift),
          _cs(scale), _counts(counts), nclients, batch, C, HW, float(eps), float(momentum),
          stream_handle())
+
+
+def bn_bwd_tiles(part, g, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclients, batch,
+                 C, HW, counts=None):
+    """bn_bwd's apply pass from the statistics conv2d_dgrad(bn_bwd=...) left (g masked)."""
+    call("fh_bn_bwd_tiles", ptr(part), ptr(g), _cs(g), ptr(x), _cs(x), ptr(gamma), _cs(gamma),
+         ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dgamma), ptr(dbeta),
+         _cs(dgamma), _counts(counts), nclients, batch, C, HW, stream_handle())
 
 
 def maxpool2_fwd_bnfinalize(part, gamma, beta, rmean, rvar, save_mean, save_invstd, scale,

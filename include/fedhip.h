@@ -128,6 +128,18 @@ int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs
                     int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
                     int32_t stride, int32_t pad, int32_t accumulate, void* workspace,
                     size_t ws_bytes, void* stream);
+/* fh_conv2d_dgrad of a 3x3/s1/p1 conv (direct path: square 8/16/32 maps) whose input was
+ * relu(BN(bn_x)): stores g = (bn_x*bn_scale + bn_shift > 0) ? dX : 0 and writes the BN
+ * backward partials (sum g, sum (bn_x - bn_mean) g) per (client, channel, 256-pixel tile)
+ * to bn_part (fh_conv_bnstats_bytes(nclients, batch, cin, h, w_) bytes) for
+ * fh_bn_bwd_tiles.  Replaces the reduce pass of fh_bn_bwd (bn.hip bn_bwd_reduce_kernel);
+ * reference: CIFAR10CNN conv -> bn -> relu -> conv, models_pytorch.py:133-150. */
+int fh_conv2d_dgrad_bnstats(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
+                            float* dx, int64_t dx_cs, const float* bn_x, int64_t bnx_cs,
+                            const float* bn_scale, const float* bn_shift, int64_t bns_cs,
+                            const float* bn_mean, double* bn_part, const int32_t* counts,
+                            int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
+                            int32_t cout, void* workspace, size_t ws_bytes, void* stream);
 /* dw (and db if non-NULL) are overwritten; the conv-bias gradient is folded into the
  * weight-gradient kernel.  workspace >= fh_conv2d_wgrad_workspace(...) bytes. */
 size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
@@ -207,6 +219,14 @@ int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int64_t yo_cs, 
               float* dgamma, float* dbeta, int64_t g_cs, const int32_t* counts, int32_t nclients,
               int32_t batch, int32_t C, int32_t HW, int32_t relu, void* workspace,
               size_t ws_bytes, void* stream);
+
+/* BN backward apply from the partials fh_conv2d_dgrad_bnstats left (g already masked):
+ * dgamma / dbeta (stride dg_cs) and dx, as fh_bn_bwd's second pass. */
+int fh_bn_bwd_tiles(const double* part, const float* g, int64_t g_cs, const float* x,
+                    int64_t x_cs, const float* gamma, int64_t p_cs, const float* save_mean,
+                    const float* save_invstd, float* dx, int64_t dx_cs, float* dgamma,
+                    float* dbeta, int64_t dg_cs, const int32_t* counts, int32_t nclients,
+                    int32_t batch, int32_t C, int32_t HW, void* stream);
 
 /* BN backward whose upstream gradient comes through MaxPool2d(2,2) (+ the Dropout
  * fused after it, p_drop / pmask as in fh_maxpool2_fwd; pmask NULL = no dropout):

@@ -14,13 +14,14 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _round(fuse, opt, sizes, rounds=2, bn_epilogue=False):
+def _round(fuse, opt, sizes, rounds=2, bn_epilogue=False, bn_bwd_epilogue=False):
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.3).to(DEV)
     S = len(sizes)
     eng = PackedTrainer(model, capacity=S, batch=32, device=DEV)
     eng.net.fuse_bn = fuse
     eng.net.bn_epilogue = bn_epilogue
+    eng.net.bn_bwd_epilogue = bn_bwd_epilogue
     for k in range(S):
         eng.load_module_state(k, model)
     eng.init_params = eng.params.clone()
@@ -260,3 +261,83 @@ def test_pool_finalize_matches_separate_launches(nc, C, hw, dm):
         assert torch.equal(q2[z, :k], q3[z, :k]) and torch.equal(i2[z, :k], i3[z, :k])
         if dm:
             assert torch.equal(m2[z, :k], m3[z, :k]) and torch.equal(m2[z, :k], outs[0][8][z, :k])
+
+
+# unsplit (many clients) and split-K (one client) DGRAD epilogues, every map width, ragged
+@pytest.mark.parametrize("nc,ci,co,hw", [(1, 32, 32, 32), (32, 32, 32, 32), (3, 64, 64, 16),
+                                         (1, 64, 64, 16), (24, 128, 128, 8), (1, 128, 128, 8),
+                                         (5, 32, 64, 16)])
+def test_dgrad_bn_bwd_stats_match_separate_pass(nc, ci, co, hw):
+    """fh_conv2d_dgrad_bnstats + fh_bn_bwd_tiles vs fh_conv2d_dgrad + fh_bn_bwd (relu, mask
+    recomputed from x): the stored g is dX with the ReLU mask applied, bit for bit; the
+    per-tile fp64 partials equal fp64 sums of g and of the fp32 (x - mean) * g; dgamma /
+    dbeta within 1 ulp and dx within 1e-5 of its scale (the same fp64 terms added in another
+    order can move the fp32 mean-of-g / k by an ulp)."""
+    B = 32
+    torch.manual_seed(nc * 13 + ci + hw)
+    cnt = torch.tensor([B] + [int(v) for v in torch.randint(1, B + 1, (nc - 1,))],
+                       dtype=torch.int32, device=DEV)
+    bx = torch.randn(nc, B, ci, hw, hw, device=DEV) * 1.3 + 0.1  # the BN input (conv output)
+    gamma = torch.rand(nc, ci, device=DEV) + 0.5
+    gamma[:, ::6] *= -1
+    beta = torch.randn(nc, ci, device=DEV) * 0.3
+    rm, rv = torch.zeros(nc, ci, device=DEV), torch.ones(nc, ci, device=DEV)
+    sm, si = torch.zeros(nc, ci, device=DEV), torch.zeros(nc, ci, device=DEV)
+    sc, sh = torch.zeros(nc, ci, device=DEV), torch.zeros(nc, ci, device=DEV)
+    ops.bn_fwd_stats(bx, gamma, beta, rm, rv, sm, si, sc, sh, nc, B, ci, hw * hw, counts=cnt)
+    dy = torch.randn(nc, B, co, hw, hw, device=DEV)
+    w = torch.randn(nc, co, ci, 3, 3, device=DEV) * 0.1
+    # separate: dgrad, then reduce + apply
+    dr = torch.zeros(nc, B, ci, hw, hw, device=DEV)
+    ops.conv2d_dgrad(dy, w, dr, nc, B, ci, hw, hw, co, 3, 1, 1, counts=cnt)
+    dx1 = torch.zeros_like(dr)
+    dg1, db1 = torch.zeros(nc, ci, device=DEV), torch.zeros(nc, ci, device=DEV)
+    ops.bn_bwd(dr, None, bx, gamma, sm, si, dx1, dg1, db1, nc, B, ci, hw * hw, relu=True,
+               counts=cnt, beta=beta)
+    # fused: dgrad with the mask + statistics, then the apply pass
+    g = torch.zeros_like(dr)
+    part = torch.full((nc, ci, ops.bnstats_tiles(B, hw, hw), 2), float("nan"),
+                      dtype=torch.float64, device=DEV)
+    ops.conv2d_dgrad(dy, w, g, nc, B, ci, hw, hw, co, 3, 1, 1, counts=cnt,
+                     bn_bwd=(bx, sc, sh, sm, part))
+    dx2 = torch.zeros_like(dr)
+    dg2, db2 = torch.zeros_like(dg1), torch.zeros_like(db1)
+    ops.bn_bwd_tiles(part, g, bx, gamma, sm, si, dx2, dg2, db2, nc, B, ci, hw * hw, counts=cnt)
+    torch.cuda.synchronize()
+    keep = bx * sc[:, None, :, None, None] + sh[:, None, :, None, None] > 0
+    gref = torch.where(keep, dr, torch.zeros_like(dr))
+    for z in range(nc):
+        k = int(cnt[z])
+        assert torch.equal(g[z, :k], gref[z, :k])
+    assert not torch.isnan(part).any()
+    T = part.shape[2]
+    prod = (bx - sm[:, None, :, None, None]) * gref  # fp32, as bn_bwd_reduce_kernel
+    terms = []
+    for t in (gref, prod):
+        tz = t.double().permute(0, 2, 1, 3, 4).reshape(nc, ci, B * hw * hw)
+        for z in range(nc):
+            tz[z, :, int(cnt[z]) * hw * hw:] = 0.0
+        terms.append(torch.nn.functional.pad(tz, (0, T * 256 - B * hw * hw)).reshape(nc, ci, T, 256))
+    torch.testing.assert_close(part[..., 0], terms[0].sum(-1), rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(part[..., 1], terms[1].sum(-1), rtol=1e-12, atol=1e-9)
+    assert _ulps(dg1, dg2) <= 1 and _ulps(db1, db2) <= 1
+    for z in range(nc):
+        k = int(cnt[z])
+        scale = dx1[z, :k].abs().max().item()
+        assert (dx1[z, :k] - dx2[z, :k]).abs().max().item() <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_dgrad_bn_bwd_epilogue_rounds_match(opt):
+    """Whole CIFAR10CNN rounds with the BN backward statistics from the dgrad epilogues vs
+    the reduce pass: the same training up to the fp64 summation order."""
+    sizes = [130, 70, 33, 9]
+    a, ma = _round(True, opt, sizes, bn_epilogue=True, bn_bwd_epilogue=True)
+    b, mb = _round(True, opt, sizes, bn_epilogue=True, bn_bwd_epilogue=False)
+    P = a.layout.P
+    d = (a.params[:, :P] - b.params[:, :P]).norm(dim=1)
+    upd = (b.params[:, :P] - b.init_params[:, :P]).norm(dim=1)
+    assert bool((d <= 1e-3 * upd).all()), (d, upd)
+    for ra, rb in zip(ma, mb):
+        for x, y in zip(ra, rb):
+            assert abs(x.loss - y.loss) <= 1e-4 * max(1.0, abs(y.loss))
