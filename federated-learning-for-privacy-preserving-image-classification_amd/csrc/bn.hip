@@ -233,6 +233,22 @@ maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __re
     const int z = blockIdx.y, c = blockIdx.x / bpc, sb = blockIdx.x - c * bpc;
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int64_t n = (int64_t)cnt * a.HW;
+    // this thread's window (one pooled element per thread: host bpc = ceil(batch*ohw/256)),
+    // loaded before the merge so the loads are in flight across it
+    const int OH = H / 2, OW = W / 2, ohw = OH * OW;
+    const int64_t per_ch = (int64_t)cnt * ohw;
+    const int64_t q = (int64_t)sb * 256 + threadIdx.x;
+    const bool live = q < per_ch;
+    int64_t e = 0;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
+    if (live) {
+        const int img = (int)(q / ohw), r = (int)(q - (int64_t)img * ohw);
+        const int oh = r / OW, ow = r - oh * OW;
+        const int64_t plane = (int64_t)img * a.C + c;
+        e = plane * ohw + r;  // maxpool2_fwd_kernel's element index
+        const float* pp = x + z * x_cs + plane * H * W + (2 * oh) * W + 2 * ow;
+        x0 = pp[0]; x1 = pp[1]; x2 = pp[W]; x3 = pp[W + 1];
+    }
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         double s0, s1;
@@ -263,38 +279,29 @@ maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __re
         }
     }
     __syncthreads();
+    if (!live) return;
     const float s = s_aff[0], t = s_aff[1];
-    const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
-    const int OH = H / 2, OW = W / 2, ohw = OH * OW;
-    const float* xb = x + z * x_cs;
-    const int64_t per_ch = (int64_t)cnt * ohw;
-    for (int64_t q = (int64_t)sb * 256 + threadIdx.x; q < per_ch; q += (int64_t)bpc * 256) {
-        const int img = (int)(q / ohw), r = (int)(q - (int64_t)img * ohw);
-        const int oh = r / OW, ow = r - oh * OW;
-        const int64_t plane = (int64_t)img * a.C + c;
-        const int64_t e = plane * ohw + r;  // maxpool2_fwd_kernel's element index
-        const float* pp = xb + plane * H * W + (2 * oh) * W + 2 * ow;
-        const float v0 = fmaxf(pp[0] * s + t, 0.f), v1 = fmaxf(pp[1] * s + t, 0.f);
-        const float v2 = fmaxf(pp[W] * s + t, 0.f), v3 = fmaxf(pp[W + 1] * s + t, 0.f);
-        float m = v0;
-        int am = 0;
-        if (v1 > m) { m = v1; am = 1; }
-        if (v2 > m) { m = v2; am = 2; }
-        if (v3 > m) { m = v3; am = 3; }
-        idx[z * i_cs + e] = (uint8_t)am;
-        if (drop_mode) {
-            uint8_t keep;
-            if (drop_mode == 1) {
-                const uint4 rr = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
-                keep = u01(rr.x) <= keep_prob ? 1 : 0;
-                mask[z * m_cs + e] = keep;
-            } else {
-                keep = mask[z * m_cs + e];
-            }
-            m = keep ? m * dscale : 0.f;
+    const float v0 = fmaxf(x0 * s + t, 0.f), v1 = fmaxf(x1 * s + t, 0.f);
+    const float v2 = fmaxf(x2 * s + t, 0.f), v3 = fmaxf(x3 * s + t, 0.f);
+    float m = v0;
+    int am = 0;
+    if (v1 > m) { m = v1; am = 1; }
+    if (v2 > m) { m = v2; am = 2; }
+    if (v3 > m) { m = v3; am = 3; }
+    idx[z * i_cs + e] = (uint8_t)am;
+    if (drop_mode) {
+        uint8_t keep;
+        if (drop_mode == 1) {
+            const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
+            const uint4 rr = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
+            keep = u01(rr.x) <= keep_prob ? 1 : 0;
+            mask[z * m_cs + e] = keep;
+        } else {
+            keep = mask[z * m_cs + e];
         }
-        y[z * y_cs + e] = m;
+        m = keep ? m * dscale : 0.f;
     }
+    y[z * y_cs + e] = m;
 }
 
 // eval mode: running statistics (LocalTrainer._validate_epoch / evaluate_model)
@@ -730,5 +737,40 @@ extern "C" int fh_bn_bwd_tiles(const double* part, const float* g, int64_t g_cs_
     a.relu = 0;  // g is already masked
     FH_LAUNCH(bn_bwd_apply_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
     FH_LAUNCH_CHECK("bn_bwd_tiles");
+    return FH_OK;
+}
+
+// fh_bn_bwd_pool's apply pass from the partials fh_conv2d_dgrad_bnstats took with pidx (the
+// statistics over the pooled grid's tiles, routed to the window argmax): dgamma / dbeta and
+// dx, the gradient routed from dpool / pidx / pmask and the ReLU mask recomputed from x.
+extern "C" int fh_bn_bwd_pool_tiles(const double* part, const float* dpool, int64_t dp_cs,
+                                    const uint8_t* pidx, int64_t pi_cs, const uint8_t* pmask,
+                                    int64_t pm_cs, float p_drop, const float* x, int64_t x_cs,
+                                    const float* gamma, const float* beta, int64_t p_cs,
+                                    const float* save_mean, const float* save_invstd, float* dx,
+                                    int64_t dx_cs, float* dgamma, float* dbeta, int64_t g_cs,
+                                    const int32_t* counts, int32_t nclients, int32_t batch,
+                                    int32_t C, int32_t H, int32_t W, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2 && !(H & 1) && !(W & 1),
+               "bn_bwd_pool_tiles: bad shape");
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "bn_bwd_pool_tiles: p=%g", p_drop);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(part && dpool && pidx && x && gamma && beta && save_mean && save_invstd,
+               "bn_bwd_pool_tiles: null pointer");
+    const int HW = H * W;
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.SP = (int)ceil_div((int64_t)batch * (HW / 4), 256);
+    a.part = (double*)part;
+    a.dpool = dpool; a.pidx = pidx; a.pmask = pmask;
+    a.dp_cs = dp_cs; a.pi_cs = pi_cs; a.pm_cs = pm_cs;
+    a.pscale = 1.0f / (1.0f - p_drop);
+    a.W = W;
+    a.fd_w = FastDiv(W);
+    a.vec = (HW & 3) == 0 && (W & 3) == 0;
+    a.x = x; a.gamma = gamma; a.beta = beta; a.save_mean = (float*)save_mean;
+    a.save_invstd = (float*)save_invstd; a.dx = dx; a.dgamma = dgamma; a.dbeta = dbeta;
+    a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs; a.g_cs = g_cs; a.relu = 1;
+    FH_LAUNCH(bn_bwd_apply_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
+    FH_LAUNCH_CHECK("bn_bwd_pool_tiles");
     return FH_OK;
 }

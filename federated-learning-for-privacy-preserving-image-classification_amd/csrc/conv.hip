@@ -500,6 +500,11 @@ struct BnBwdEpi {
     const float* shift;
     int64_t s_cs;
     const float* mean;
+    const uint8_t* pidx;  // non-null: routed through a 2x2 max-pool (+ dropout)
+    const uint8_t* pmask;
+    int64_t pi_cs, pm_cs;
+    float pscale;
+    int pw;  // pooled map width (the epilogue's map), x is 2pw wide
 };
 
 // FWD/DGRAD split-K epilogue: out[z][img][m][p] (=|+=) sum_s part[z][s][m][n] (+bias, relu).
@@ -518,7 +523,7 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
     const int n = blockIdx.x * 256 + threadIdx.x;
     const bool valid = n < cnt * sp;
     if (!valid && bn_part == nullptr) return;
-    float s = 0.f, d1f = 0.f;
+    float s = 0.f, d0f = 0.f, d1f = 0.f;
     if (valid) {
         const float* p = part + ((int64_t)z * splits * M + m) * Nfull + n;
         const int64_t ss = (int64_t)M * Nfull;
@@ -537,15 +542,28 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
         float* o = out + z * out_cs + ((int64_t)img * M + m) * sp + pix;
         if (accumulate) s = *o + s;
         if (bb.x) {  // ReLU mask of the BN in front; (x - mean) * g for its statistics
-            const float xv = bb.x[z * bb.x_cs + ((int64_t)img * M + m) * sp + pix];
-            if (!(xv * bb.scale[z * bb.s_cs + m] + bb.shift[z * bb.s_cs + m] > 0.f)) s = 0.f;
-            d1f = (xv - bb.mean[z * M + m]) * s;
+            const int64_t e = ((int64_t)img * M + m) * sp + pix;
+            float xv, gu = s;
+            if (bb.pidx) {
+                const int code = bb.pidx[z * bb.pi_cs + e];
+                if (bb.pmask) gu = bb.pmask[z * bb.pm_cs + e] ? s * bb.pscale : 0.f;
+                const int py = pix / bb.pw, px = pix - py * bb.pw;
+                xv = bb.x[z * bb.x_cs + ((int64_t)img * M + m) * 4 * sp +
+                          (2 * py + (code >> 1)) * (2 * bb.pw) + 2 * px + (code & 1)];
+            } else {
+                xv = bb.x[z * bb.x_cs + e];
+            }
+            const float g =
+                (xv * bb.scale[z * bb.s_cs + m] + bb.shift[z * bb.s_cs + m] > 0.f) ? gu : 0.f;
+            d0f = g;
+            d1f = (xv - bb.mean[z * M + m]) * g;
+            if (!bb.pidx) s = g;
         }
         *o = s;
     }
     if (bn_part != nullptr) {  // block-uniform
         __shared__ double red[2][4];
-        double d0 = valid ? (double)s : 0.0;
+        double d0 = !valid ? 0.0 : bb.x ? (double)d0f : (double)s;
         double d1 = bb.x ? (double)d1f : d0 * d0;
         d0 = wave_sum(d0);
         d1 = wave_sum(d1);
@@ -940,7 +958,8 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
                            OP == OP_FWD ? a.relu : 0, OP == OP_FWD ? 0 : a.accumulate, a.counts,
                            a.batch, sp, a.bn_part, a.bn_tiles, DropArgs{},
                            BnBwdEpi{OP == OP_FWD ? nullptr : a.bnx, a.bnx_cs, a.bn_scale,
-                                    a.bn_shift, a.bns_cs, a.bn_mean});
+                                    a.bn_shift, a.bns_cs, a.bn_mean, a.pidx, a.pmask, a.pi_cs,
+                                    a.pm_cs, a.pscale, w});
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -1201,12 +1220,17 @@ extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, i
 // g = (bn_x*scale + shift > 0) ? dX : 0 (scale / shift: that BN's affine, fh_bn_fwd_stats /
 // fh_bn_finalize_tiles) and leaves the BN backward statistics (sum g, sum (bn_x - mean) g) in
 // bn_part (fh_conv_bnstats_bytes layout), so fh_bn_bwd_tiles replaces fh_bn_bwd's reduce
-// pass over g and bn_x.
+// pass over g and bn_x.  pidx non-null: relu(BN(bn_x)) went through MaxPool2d(2,2) (+ the
+// Dropout after it: pmask / p_drop, as fh_bn_bwd_pool) first — bn2/bn4 (:139-150); bn_x is
+// the 2h x 2w map, dX is stored unmasked and the statistics route it to the window argmax
+// (fh_bn_bwd_pool_tiles is then the apply pass).
 extern "C" int fh_conv2d_dgrad_bnstats(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
                                        float* dx, int64_t dx_cs, const float* bn_x,
                                        int64_t bnx_cs, const float* bn_scale,
                                        const float* bn_shift, int64_t bns_cs,
                                        const float* bn_mean, double* bn_part,
+                                       const uint8_t* pidx, int64_t pi_cs, const uint8_t* pmask,
+                                       int64_t pm_cs, float p_drop,
                                        const int32_t* counts, int32_t nclients, int32_t batch,
                                        int32_t cin, int32_t h, int32_t w_, int32_t cout,
                                        void* workspace, size_t ws_bytes, void* stream) {
@@ -1225,6 +1249,9 @@ extern "C" int fh_conv2d_dgrad_bnstats(const float* dy, int64_t dy_cs, const flo
     d.bn_part = bn_part; d.bn_tiles = (int)ceil_div((int64_t)batch * h * w_, 256);
     d.bnx = bn_x; d.bnx_cs = bnx_cs; d.bn_scale = bn_scale; d.bn_shift = bn_shift;
     d.bns_cs = bns_cs; d.bn_mean = bn_mean;
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "conv2d_dgrad_bnstats: p=%g", p_drop);
+    d.pidx = pidx; d.pmask = pidx ? pmask : nullptr; d.pi_cs = pi_cs; d.pm_cs = pm_cs;
+    d.pscale = 1.0f / (1.0f - p_drop);
     return run_dconv<OP_DGRAD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
                                "conv2d_dgrad_bnstats");
 }
@@ -1469,9 +1496,9 @@ template <int KT>
 __global__ void __launch_bounds__(256)
 linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const float* __restrict__ W,
                            int64_t w_cs, float* __restrict__ dX, int64_t dx_cs,
-                           const int32_t* __restrict__ counts, int batch, int K, int M) {
+                           const int32_t* __restrict__ counts, int batch, int K, int M,
+                           SkinnyBwdEpi ep) {
     __shared__ float red[3 * 16 * 64 * KT];
-    const SkinnyBwdEpi ep{nullptr, 0, 1.f, nullptr, 0};
     linear_dgrad_skinny_body<KT>(dY, dy_cs, W, w_cs, dX, dx_cs, counts, batch, K, M, blockIdx.y,
                                  blockIdx.x, red, ep);
 }
@@ -1613,11 +1640,11 @@ extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, i
             (int64_t)(in_f / 128) * nclients >= fill(256))
             FH_LAUNCH(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
                                dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs,
-                               counts, batch, in_f, out_f);
+                               counts, batch, in_f, out_f, SkinnyBwdEpi{nullptr, 0, 1.f, nullptr, 0});
         else
             FH_LAUNCH(linear_dgrad_skinny_kernel<1>, dim3((unsigned)(in_f / 32), nclients),
                                dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs,
-                               counts, batch, in_f, out_f);
+                               counts, batch, in_f, out_f, SkinnyBwdEpi{nullptr, 0, 1.f, nullptr, 0});
         FH_LAUNCH_CHECK("linear_dgrad skinny");
         return FH_OK;
     }
@@ -1648,11 +1675,19 @@ extern "C" int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy
     }
     const SkinnyBwdEpi ep{mask, m_cs, 1.0f / (1.0f - p_drop), relu_ref, r_cs};
     const int nw = (in_f / 128) * (int)ceil_div(out_f, 32);
-    if (kLinearSkinny != 2 && (int64_t)(in_f / 128) * nclients >= fill(256))
-        FH_LAUNCH(linear_bwd_fused_kernel<4>, dim3((unsigned)(nw + in_f / 128), nclients),
-                  dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, w, w_cs, dw, dw_cs, db,
-                  db_cs, dx, dx_cs, ep, counts, batch, in_f, out_f, nw);
-    else
+    if (kLinearSkinny != 2 && (int64_t)(in_f / 128) * nclients >= fill(256)) {
+        // wide launches: the two roles as two kernels — in one grid every WGRAD workgroup
+        // would carry the DGRAD role's 48 KB of LDS and stream dW at 3 workgroups per CU
+        // (fc1 at 32 clients: 190 us fused vs ~105 us as two launches)
+        FH_LAUNCH(linear_wgrad_skinny_kernel,
+                  dim3((unsigned)(in_f / 128), (unsigned)ceil_div(out_f, 32), nclients),
+                  dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
+                  counts, batch, in_f, out_f);
+        FH_LAUNCH_CHECK("linear_bwd_fused wgrad");
+        FH_LAUNCH(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
+                  dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs, counts, batch,
+                  in_f, out_f, ep);
+    } else
         FH_LAUNCH(linear_bwd_fused_kernel<1>, dim3((unsigned)(nw + in_f / 32), nclients),
                   dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, w, w_cs, dw, dw_cs, db,
                   db_cs, dx, dx_cs, ep, counts, batch, in_f, out_f, nw);

@@ -58,6 +58,14 @@ struct DConvArgs {
     const float* bn_shift;
     int64_t bns_cs;
     const float* bn_mean;  // [client][M]
+    // ... and pidx non-null: a 2x2 max-pool (+ dropout) sat between that ReLU and this conv
+    // (bnx is the full-resolution map, 2H x 2W).  dX is stored as is (the pool's output
+    // gradient); the statistics route it as maxpool2_bwd does: to the window argmax
+    // pidx (== (y&1)*2 + (x&1)), times the keep-mask pmask / (1 - p) when pmask is non-null.
+    const uint8_t* pidx;
+    const uint8_t* pmask;
+    int64_t pi_cs, pm_cs;
+    float pscale;
 };
 
 // Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
@@ -347,23 +355,57 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
                 cst[2 * BM + tid] = ok ? a.bn_mean[z * M + m] : 0.f;
             }
             __syncthreads();
-            // pass 1: g = ReLU-masked dX, stored and imaged; acc keeps (x - mean) * g, the
-            // fp32 product bn_bwd_reduce_kernel promotes
+            // pass 1: g = ReLU-masked dX (routed through the pool when pidx), imaged; acc
+            // keeps (x - mean) * g, the fp32 product bn_bwd_reduce_kernel promotes
+            const bool pooled = a.pidx != nullptr;
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 const int n = n0 + wn * WN + j * 32 + col;
                 const int img = n / G::HW, p = n % G::HW;
                 const bool live = img < cnt;
-                const float* xz = a.bnx + z * a.bnx_cs + (int64_t)img * M * G::HW + p;
                 float* op = a.out + z * a.out_cs + (int64_t)img * M * G::HW + p;
                 float xv[FM][16];  // all loads of the column first: `out` may alias `bnx`
+                int cd[FM][16];    // pooled: argmax (bits 0-1) | kept (bit 2)
+                if (pooled) {
+                    const int64_t e0 = (int64_t)img * M * G::HW + p;
 #pragma unroll
-                for (int i = 0; i < FM; ++i)
+                    for (int i = 0; i < FM; ++i)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
-                        xv[i][r] = (live && m < M) ? xz[(int64_t)m * G::HW] : 0.f;
-                    }
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                            int code = 0;
+                            if (live && m < M) {
+                                const int64_t e = e0 + (int64_t)m * G::HW;
+                                code = a.pidx[z * a.pi_cs + e];
+                                code |= (!a.pmask || a.pmask[z * a.pm_cs + e]) ? 4 : 0;
+                            }
+                            cd[i][r] = code;
+                        }
+                    const int py = p / G::H, px = p % G::H;
+                    const float* xz = a.bnx + z * a.bnx_cs + (int64_t)img * M * 4 * G::HW +
+                                      (2 * py) * (2 * G::H) + 2 * px;
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                            const int code = cd[i][r];
+                            xv[i][r] = (live && m < M)
+                                           ? xz[(int64_t)m * 4 * G::HW + (code >> 1 & 1) * 2 * G::H +
+                                                (code & 1)]
+                                           : 0.f;
+                        }
+                } else {
+                    const float* xz = a.bnx + z * a.bnx_cs + (int64_t)img * M * G::HW + p;
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                            xv[i][r] = (live && m < M) ? xz[(int64_t)m * G::HW] : 0.f;
+                            cd[i][r] = 4;
+                        }
+                }
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -372,9 +414,12 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
                         const int m = m0 + ml;
                         float g = 0.f, pv = 0.f;
                         if (live && m < M) {
-                            g = (xv[i][r] * cst[ml] + cst[BM + ml] > 0.f) ? acc[i][j][r] : 0.f;
+                            const float v = acc[i][j][r];
+                            float gu = v;  // the gradient reaching the BN-ReLU output element
+                            if (pooled) gu = !(cd[i][r] & 4) ? 0.f : a.pmask ? v * a.pscale : v;
+                            g = (xv[i][r] * cst[ml] + cst[BM + ml] > 0.f) ? gu : 0.f;
                             pv = (xv[i][r] - cst[2 * BM + ml]) * g;
-                            op[(int64_t)m * G::HW] = g;
+                            op[(int64_t)m * G::HW] = pooled ? v : g;
                         }
                         red[ml * kStatPitch + n - n0] = g;
                         acc[i][j][r] = pv;

@@ -46,8 +46,8 @@ SIGNATURES = {
                             I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_conv2d_dgrad": (I32, [P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, I32,
                               I32, I32, I32, I32, P, SZ, P]),
-    "fh_conv2d_dgrad_bnstats": (I32, [P, I64, P, I64, P, I64, P, I64, P, P, I64, P, P, P, I32,
-                                      I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_conv2d_dgrad_bnstats": (I32, [P, I64, P, I64, P, I64, P, I64, P, P, I64, P, P, P, I64,
+                                      P, I64, F32, P, I32, I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_conv2d_wgrad_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "fh_conv2d_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32,
                               I32, I32, I32, I32, I32, I32, P]),
@@ -93,6 +93,8 @@ SIGNATURES = {
                         I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_bn_bwd_tiles": (I32, [P, P, I64, P, I64, P, I64, P, P, P, I64, P, P, I64, P, I32, I32,
                               I32, I32, P]),
+    "fh_bn_bwd_pool_tiles": (I32, [P, P, I64, P, I64, P, I64, F32, P, I64, P, P, I64, P, P, P,
+                                   I64, P, P, I64, P, I32, I32, I32, I32, I32, P]),
     "fh_bn_bwd_pool": (I32, [P, I64, P, I64, P, I64, F32, P, I64, P, I64, P, P, I64, P, P, P, I64,
                              P, P, I64, P, I32, I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_conv2d_persample_sqnorm_workspace": (SZ, [I32] * 10),

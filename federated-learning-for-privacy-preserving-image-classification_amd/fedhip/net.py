@@ -534,7 +534,15 @@ class PackedNet:
             cv, ci, co, hw, bn = convs[i]
             dc = A(f"dc_{cv}", co, hw, hw)
             sm, si = self._bn_save(bn, co)
-            if i % 2 == 1:  # upstream gradient comes through pool(+dropout): fused routing
+            if i % 2 == 1 and bn_tiles is not None:  # statistics from the next conv's dgrad
+                h2 = hw // 2
+                ops.bn_bwd_pool_tiles(bn_tiles, dq, A(f"i_{cv}", co, h2, h2, dtype=torch.uint8),
+                                      A(f"c_{cv}", co, hw, hw), W(P_, f"{bn}.weight"),
+                                      W(P_, f"{bn}.bias"), sm, si, dc, W(G, f"{bn}.weight"),
+                                      W(G, f"{bn}.bias"), n, B, co, hw, hw,
+                                      pmask=A(f"m_{cv}", co, h2, h2, dtype=torch.uint8) if dm
+                                      else None, p_drop=p, counts=cnt)
+            elif i % 2 == 1:  # upstream gradient comes through pool(+dropout): fused routing
                 h2 = hw // 2
                 ops.bn_bwd_pool(dq, A(f"i_{cv}", co, h2, h2, dtype=torch.uint8), None,
                                 A(f"c_{cv}", co, hw, hw), W(P_, f"{bn}.weight"), sm, si, dc,
@@ -570,13 +578,21 @@ class PackedNet:
             pcv = convs[i - 1][0]
             if i % 2 == 0:  # input came from a pool: gradient goes to the pool output grad
                 dq = A(f"dq_{pcv}", ci, hw, hw)
+                bb = None
+                if self._fused and self.bn_bwd_epilogue:
+                    pbn = convs[i - 1][4]
+                    bn_tiles = self._bn_part(f"{pbn}.bwd", ci, hw)  # pooled-map tiles
+                    bb = (A(f"c_{pcv}", ci, 2 * hw, 2 * hw), *self._bn_affine(pbn, ci),
+                          self._bn_save(pbn, ci)[0], bn_tiles,
+                          A(f"i_{pcv}", ci, hw, hw, dtype=torch.uint8),
+                          A(f"m_{pcv}", ci, hw, hw, dtype=torch.uint8) if dm else None, p)
                 ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), dq, n, B, ci, hw, hw, co, 3, 1, 1,
-                                 counts=cnt)
+                                 counts=cnt, bn_bwd=bb)
             else:
                 bb = None
                 if self._fused and self.bn_bwd_epilogue:
                     pbn = convs[i - 1][4]
-                    bn_tiles = self._bn_part(pbn, ci, hw)
+                    bn_tiles = self._bn_part(f"{pbn}.bwd", ci, hw)
                     bb = (A(f"c_{pcv}", ci, hw, hw), *self._bn_affine(pbn, ci),
                           self._bn_save(pbn, ci)[0], bn_tiles)
                 ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), A(f"dr_{pcv}", ci, hw, hw), n, B, ci,

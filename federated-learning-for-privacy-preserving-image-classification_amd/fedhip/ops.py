@@ -256,19 +256,24 @@ def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad,
 
 def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
                  accumulate=False, bn_bwd=None):
-    """bn_bwd = (bn_x, scale, shift, save_mean, part): the input was relu(BN(bn_x)) with that
-    BN's affine (scale, shift); dx receives the ReLU-masked gradient g and part the BN
-    backward statistics for bn_bwd_tiles (fh_conv2d_dgrad_bnstats, 3x3/s1/p1 only)."""
+    """bn_bwd = (bn_x, scale, shift, save_mean, part[, pidx, pmask, p_drop]): the input was
+    relu(BN(bn_x)) with that BN's affine (scale, shift); dx receives the ReLU-masked gradient
+    g and part the BN backward statistics for bn_bwd_tiles (fh_conv2d_dgrad_bnstats,
+    3x3/s1/p1 only).  With pidx the ReLU output went through a 2x2 max-pool (+ dropout
+    pmask / p_drop) first: bn_x is the 2h x 2w map, dx is stored unmasked and the apply pass
+    is bn_bwd_pool_tiles."""
     ws, nb = _ws_for("fh_conv2d_dgrad_workspace", dy.device, nclients, batch, cin, h, wd, cout, k,
                      k, stride, pad)
     ev = PROBE.begin(_conv_tag("dgrad", cin, h, wd, cout, k, stride))
     if bn_bwd is not None:
         if accumulate or (k, stride, pad) != (3, 1, 1):
             raise FedHipError("conv2d_dgrad(bn_bwd=...): 3x3/s1/p1 without accumulate only")
-        bx, sc, sh, mean, part = bn_bwd
+        bx, sc, sh, mean, part = bn_bwd[:5]
+        pidx, pmask, p_drop = (tuple(bn_bwd[5:]) + (None, None, 0.0))[:3]
         call("fh_conv2d_dgrad_bnstats", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx),
-             ptr(bx), _cs(bx), ptr(sc), ptr(sh), _cs(sc), ptr(mean), ptr(part), _counts(counts),
-             nclients, batch, cin, h, wd, cout, ptr(ws), nb, stream_handle())
+             ptr(bx), _cs(bx), ptr(sc), ptr(sh), _cs(sc), ptr(mean), ptr(part), ptr(pidx),
+             _cs(pidx), ptr(pmask), _cs(pmask), float(p_drop), _counts(counts), nclients, batch,
+             cin, h, wd, cout, ptr(ws), nb, stream_handle())
     else:
         call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx),
              _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
@@ -526,6 +531,16 @@ def bn_bwd_tiles(part, g, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, n
     call("fh_bn_bwd_tiles", ptr(part), ptr(g), _cs(g), ptr(x), _cs(x), ptr(gamma), _cs(gamma),
          ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dgamma), ptr(dbeta),
          _cs(dgamma), _counts(counts), nclients, batch, C, HW, stream_handle())
+
+
+def bn_bwd_pool_tiles(part, dpool, pidx, x, gamma, beta, save_mean, save_invstd, dx, dgamma,
+                      dbeta, nclients, batch, C, H, W, pmask=None, p_drop=0.0, counts=None):
+    """bn_bwd_pool's apply pass from the statistics conv2d_dgrad(bn_bwd=(..., pidx, ...))
+    left."""
+    call("fh_bn_bwd_pool_tiles", ptr(part), ptr(dpool), _cs(dpool), ptr(pidx), _cs(pidx),
+         ptr(pmask), _cs(pmask), float(p_drop), ptr(x), _cs(x), ptr(gamma), ptr(beta),
+         _cs(gamma), ptr(save_mean), ptr(save_invstd), ptr(dx), _cs(dx), ptr(dgamma), ptr(dbeta),
+         _cs(dgamma), _counts(counts), nclients, batch, C, H, W, stream_handle())
 
 
 def maxpool2_fwd_bnfinalize(part, gamma, beta, rmean, rvar, save_mean, save_invstd, scale,

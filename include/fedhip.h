@@ -133,13 +133,19 @@ int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs
  * backward partials (sum g, sum (bn_x - bn_mean) g) per (client, channel, 256-pixel tile)
  * to bn_part (fh_conv_bnstats_bytes(nclients, batch, cin, h, w_) bytes) for
  * fh_bn_bwd_tiles.  Replaces the reduce pass of fh_bn_bwd (bn.hip bn_bwd_reduce_kernel);
- * reference: CIFAR10CNN conv -> bn -> relu -> conv, models_pytorch.py:133-150. */
+ * pidx non-NULL: a MaxPool2d(2,2) (+ Dropout: pmask / p_drop, pmask NULL = none) sat
+ * between the ReLU and this conv; bn_x is then the 2h x 2w map, dX is stored unmasked and
+ * the statistics route it to the window argmax (apply pass: fh_bn_bwd_pool_tiles).
+ * reference: CIFAR10CNN conv -> bn -> relu (-> pool -> dropout) -> conv,
+ * models_pytorch.py:133-150. */
 int fh_conv2d_dgrad_bnstats(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
                             float* dx, int64_t dx_cs, const float* bn_x, int64_t bnx_cs,
                             const float* bn_scale, const float* bn_shift, int64_t bns_cs,
-                            const float* bn_mean, double* bn_part, const int32_t* counts,
-                            int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
-                            int32_t cout, void* workspace, size_t ws_bytes, void* stream);
+                            const float* bn_mean, double* bn_part, const uint8_t* pidx,
+                            int64_t pi_cs, const uint8_t* pmask, int64_t pm_cs, float p_drop,
+                            const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
+                            int32_t h, int32_t w_, int32_t cout, void* workspace,
+                            size_t ws_bytes, void* stream);
 /* dw (and db if non-NULL) are overwritten; the conv-bias gradient is folded into the
  * weight-gradient kernel.  workspace >= fh_conv2d_wgrad_workspace(...) bytes. */
 size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
@@ -227,6 +233,16 @@ int fh_bn_bwd_tiles(const double* part, const float* g, int64_t g_cs, const floa
                     const float* save_invstd, float* dx, int64_t dx_cs, float* dgamma,
                     float* dbeta, int64_t dg_cs, const int32_t* counts, int32_t nclients,
                     int32_t batch, int32_t C, int32_t HW, void* stream);
+
+/* fh_bn_bwd_pool's apply pass from the partials fh_conv2d_dgrad_bnstats(pidx != NULL)
+ * left: dgamma / dbeta and dx (H x W: the BN's map), ReLU mask recomputed from x. */
+int fh_bn_bwd_pool_tiles(const double* part, const float* dpool, int64_t dp_cs,
+                         const uint8_t* pidx, int64_t pi_cs, const uint8_t* pmask, int64_t pm_cs,
+                         float p_drop, const float* x, int64_t x_cs, const float* gamma,
+                         const float* beta, int64_t p_cs, const float* save_mean,
+                         const float* save_invstd, float* dx, int64_t dx_cs, float* dgamma,
+                         float* dbeta, int64_t g_cs, const int32_t* counts, int32_t nclients,
+                         int32_t batch, int32_t C, int32_t H, int32_t W, void* stream);
 
 /* BN backward whose upstream gradient comes through MaxPool2d(2,2) (+ the Dropout
  * fused after it, p_drop / pmask as in fh_maxpool2_fwd; pmask NULL = no dropout):

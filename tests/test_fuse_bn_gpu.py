@@ -341,3 +341,77 @@ def test_dgrad_bn_bwd_epilogue_rounds_match(opt):
     for ra, rb in zip(ma, mb):
         for x, y in zip(ra, rb):
             assert abs(x.loss - y.loss) <= 1e-4 * max(1.0, abs(y.loss))
+
+
+@pytest.mark.parametrize("nc,ci,co,hw,dm", [(1, 32, 64, 16, True), (32, 32, 64, 16, True),
+                                            (3, 64, 128, 8, False), (1, 64, 128, 8, True),
+                                            (24, 64, 128, 8, True)])
+def test_dgrad_bn_bwd_stats_through_pool(nc, ci, co, hw, dm):
+    """fh_conv2d_dgrad_bnstats with pidx (the BN-ReLU output went through a 2x2 max-pool and
+    dropout) + fh_bn_bwd_pool_tiles vs fh_conv2d_dgrad + fh_bn_bwd_pool: dX bit-identical,
+    partials = fp64 sums of the routed, masked g and (x - mean) g over each pooled tile,
+    dgamma / dbeta within 1 ulp, dx within 1e-5 of its scale."""
+    B, p = 32, 0.3
+    H = 2 * hw
+    torch.manual_seed(nc * 17 + ci + hw)
+    cnt = torch.tensor([B] + [int(v) for v in torch.randint(1, B + 1, (nc - 1,))],
+                       dtype=torch.int32, device=DEV)
+    bx = torch.randn(nc, B, ci, H, H, device=DEV) * 1.3 + 0.1
+    gamma = torch.rand(nc, ci, device=DEV) + 0.5
+    gamma[:, ::6] *= -1
+    beta = torch.randn(nc, ci, device=DEV) * 0.3
+    rm, rv = torch.zeros(nc, ci, device=DEV), torch.ones(nc, ci, device=DEV)
+    sm, si = torch.zeros(nc, ci, device=DEV), torch.zeros(nc, ci, device=DEV)
+    sc, sh = torch.zeros(nc, ci, device=DEV), torch.zeros(nc, ci, device=DEV)
+    ops.bn_fwd_stats(bx, gamma, beta, rm, rv, sm, si, sc, sh, nc, B, ci, H * H, counts=cnt)
+    q = torch.zeros(nc, B, ci, hw, hw, device=DEV)
+    idx = torch.zeros(nc, B, ci, hw, hw, dtype=torch.uint8, device=DEV)
+    msk = torch.zeros_like(idx) if dm else None
+    ops.maxpool2_fwd(bx, q, idx, nc, B, ci, H, H, mask=msk, drop_mode=1 if dm else 0,
+                     p_drop=p, seed=3, counts=cnt, in_affine=(sc, sh))
+    pd = p if dm else 0.0
+    dy = torch.randn(nc, B, co, hw, hw, device=DEV)
+    w = torch.randn(nc, co, ci, 3, 3, device=DEV) * 0.1
+    dq1 = torch.zeros(nc, B, ci, hw, hw, device=DEV)
+    ops.conv2d_dgrad(dy, w, dq1, nc, B, ci, hw, hw, co, 3, 1, 1, counts=cnt)
+    dx1 = torch.zeros_like(bx)
+    dg1, db1 = torch.zeros(nc, ci, device=DEV), torch.zeros(nc, ci, device=DEV)
+    ops.bn_bwd_pool(dq1, idx, None, bx, gamma, sm, si, dx1, dg1, db1, nc, B, ci, H, H,
+                    relu=True, pmask=msk, p_drop=pd, counts=cnt, beta=beta)
+    dq2 = torch.zeros_like(dq1)
+    part = torch.full((nc, ci, ops.bnstats_tiles(B, hw, hw), 2), float("nan"),
+                      dtype=torch.float64, device=DEV)
+    ops.conv2d_dgrad(dy, w, dq2, nc, B, ci, hw, hw, co, 3, 1, 1, counts=cnt,
+                     bn_bwd=(bx, sc, sh, sm, part, idx, msk, pd))
+    dx2 = torch.zeros_like(bx)
+    dg2, db2 = torch.zeros_like(dg1), torch.zeros_like(db1)
+    ops.bn_bwd_pool_tiles(part, dq2, idx, bx, gamma, beta, sm, si, dx2, dg2, db2, nc, B, ci, H,
+                          H, pmask=msk, p_drop=pd, counts=cnt)
+    torch.cuda.synchronize()
+    for z in range(nc):
+        k = int(cnt[z])
+        assert torch.equal(dq1[z, :k], dq2[z, :k])
+    assert not torch.isnan(part).any()
+    # routed g on the pooled grid: the gradient at the argmax element, ReLU-masked there
+    gu = dq1 if msk is None else torch.where(msk.bool(), dq1 * (1.0 / (1.0 - pd)),
+                                              torch.zeros_like(dq1))
+    dyy, dxx = (idx.long() >> 1), (idx.long() & 1)
+    yy = 2 * torch.arange(hw, device=DEV).view(hw, 1) + dyy
+    xx = 2 * torch.arange(hw, device=DEV).view(1, hw) + dxx
+    xa = torch.gather(bx.reshape(nc, B, ci, H * H), 3, (yy * H + xx).reshape(nc, B, ci, -1))
+    xa = xa.reshape(nc, B, ci, hw, hw)
+    keep = xa * sc[:, None, :, None, None] + sh[:, None, :, None, None] > 0
+    g = torch.where(keep, gu, torch.zeros_like(gu))
+    prod = (xa - sm[:, None, :, None, None]) * g
+    T = part.shape[2]
+    for col, t in ((0, g), (1, prod)):
+        tz = t.double().permute(0, 2, 1, 3, 4).reshape(nc, ci, B * hw * hw)
+        for z in range(nc):
+            tz[z, :, int(cnt[z]) * hw * hw:] = 0.0
+        ref = torch.nn.functional.pad(tz, (0, T * 256 - B * hw * hw)).reshape(nc, ci, T, 256)
+        torch.testing.assert_close(part[..., col], ref.sum(-1), rtol=1e-12, atol=1e-9)
+    assert _ulps(dg1, dg2) <= 1 and _ulps(db1, db2) <= 1
+    for z in range(nc):
+        k = int(cnt[z])
+        scale = dx1[z, :k].abs().max().item()
+        assert (dx1[z, :k] - dx2[z, :k]).abs().max().item() <= 1e-5 * scale
