@@ -222,6 +222,8 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const BNArgs a, float*
 // maxpool2_fwd_kernel (window argmax, Philox keep-mask keyed by the pooled element index).
 // Block 0 of the channel writes save_mean / save_invstd, the running statistics and the
 // affine.
+constexpr int kPoolEpt = 4;  // pooled elements per thread in maxpool2_bnfin_kernel
+
 __global__ void __launch_bounds__(256)
 maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __restrict__ shift_out,
                       int64_t s_cs, const float* __restrict__ x, int64_t x_cs,
@@ -233,21 +235,26 @@ maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __re
     const int z = blockIdx.y, c = blockIdx.x / bpc, sb = blockIdx.x - c * bpc;
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int64_t n = (int64_t)cnt * a.HW;
-    // this thread's window (one pooled element per thread: host bpc = ceil(batch*ohw/256)),
-    // loaded before the merge so the loads are in flight across it
+    // this thread's windows (kPoolEpt pooled elements, 256 apart: host
+    // bpc = ceil(batch*ohw / (256*kPoolEpt))), loaded before the merge so the loads are in
+    // flight across it and one merge serves kPoolEpt*256 elements
     const int OH = H / 2, OW = W / 2, ohw = OH * OW;
     const int64_t per_ch = (int64_t)cnt * ohw;
-    const int64_t q = (int64_t)sb * 256 + threadIdx.x;
-    const bool live = q < per_ch;
-    int64_t e = 0;
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
-    if (live) {
-        const int img = (int)(q / ohw), r = (int)(q - (int64_t)img * ohw);
-        const int oh = r / OW, ow = r - oh * OW;
-        const int64_t plane = (int64_t)img * a.C + c;
-        e = plane * ohw + r;  // maxpool2_fwd_kernel's element index
-        const float* pp = x + z * x_cs + plane * H * W + (2 * oh) * W + 2 * ow;
-        x0 = pp[0]; x1 = pp[1]; x2 = pp[W]; x3 = pp[W + 1];
+    int64_t e[kPoolEpt];
+    float xv[kPoolEpt][4];
+#pragma unroll
+    for (int k = 0; k < kPoolEpt; ++k) {
+        const int64_t q = ((int64_t)sb * kPoolEpt + k) * 256 + threadIdx.x;
+        e[k] = -1;
+        xv[k][0] = xv[k][1] = xv[k][2] = xv[k][3] = 0.f;
+        if (q < per_ch) {
+            const int img = (int)(q / ohw), r = (int)(q - (int64_t)img * ohw);
+            const int oh = r / OW, ow = r - oh * OW;
+            const int64_t plane = (int64_t)img * a.C + c;
+            e[k] = plane * ohw + r;  // maxpool2_fwd_kernel's element index
+            const float* pp = x + z * x_cs + plane * H * W + (2 * oh) * W + 2 * ow;
+            xv[k][0] = pp[0]; xv[k][1] = pp[1]; xv[k][2] = pp[W]; xv[k][3] = pp[W + 1];
+        }
     }
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
@@ -279,29 +286,32 @@ maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __re
         }
     }
     __syncthreads();
-    if (!live) return;
     const float s = s_aff[0], t = s_aff[1];
-    const float v0 = fmaxf(x0 * s + t, 0.f), v1 = fmaxf(x1 * s + t, 0.f);
-    const float v2 = fmaxf(x2 * s + t, 0.f), v3 = fmaxf(x3 * s + t, 0.f);
-    float m = v0;
-    int am = 0;
-    if (v1 > m) { m = v1; am = 1; }
-    if (v2 > m) { m = v2; am = 2; }
-    if (v3 > m) { m = v3; am = 3; }
-    idx[z * i_cs + e] = (uint8_t)am;
-    if (drop_mode) {
-        uint8_t keep;
-        if (drop_mode == 1) {
-            const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
-            const uint4 rr = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
-            keep = u01(rr.x) <= keep_prob ? 1 : 0;
-            mask[z * m_cs + e] = keep;
-        } else {
-            keep = mask[z * m_cs + e];
+    const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
+#pragma unroll
+    for (int k = 0; k < kPoolEpt; ++k) {
+        if (e[k] < 0) continue;
+        const float v0 = fmaxf(xv[k][0] * s + t, 0.f), v1 = fmaxf(xv[k][1] * s + t, 0.f);
+        const float v2 = fmaxf(xv[k][2] * s + t, 0.f), v3 = fmaxf(xv[k][3] * s + t, 0.f);
+        float m = v0;
+        int am = 0;
+        if (v1 > m) { m = v1; am = 1; }
+        if (v2 > m) { m = v2; am = 2; }
+        if (v3 > m) { m = v3; am = 3; }
+        idx[z * i_cs + e[k]] = (uint8_t)am;
+        if (drop_mode) {
+            uint8_t keep;
+            if (drop_mode == 1) {
+                const uint4 rr = Philox::gen(seed, (uint64_t)z, (uint64_t)e[k]);
+                keep = u01(rr.x) <= keep_prob ? 1 : 0;
+                mask[z * m_cs + e[k]] = keep;
+            } else {
+                keep = mask[z * m_cs + e[k]];
+            }
+            m = keep ? m * dscale : 0.f;
         }
-        m = keep ? m * dscale : 0.f;
+        y[z * y_cs + e[k]] = m;
     }
-    y[z * y_cs + e] = m;
 }
 
 // eval mode: running statistics (LocalTrainer._validate_epoch / evaluate_model)
@@ -615,7 +625,7 @@ extern "C" int fh_maxpool2_fwd_bnfinalize(
     a.p_cs = p_cs; a.r_cs = r_cs;
     a.eps = eps; a.momentum = momentum;
     const int64_t per_ch = (int64_t)batch * (H / 2) * (W / 2);
-    const int bpc = (int)std::max<int64_t>(1, ceil_div(per_ch, 256));  // one element per thread
+    const int bpc = (int)std::max<int64_t>(1, ceil_div(per_ch, 256 * kPoolEpt));
     const float keep = 1.0f - p_drop;
     FH_LAUNCH(maxpool2_bnfin_kernel, dim3((unsigned)(C * bpc), nclients), dim3(256), 0,
               as_stream(stream), a, scale_out, shift_out, s_cs, x, x_cs, y, y_cs, idx, i_cs,
