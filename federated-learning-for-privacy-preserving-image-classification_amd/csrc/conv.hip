@@ -861,6 +861,11 @@ static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 2);  // tools/tail_
 static const int kDconvForceSplits = env_int("FH_DCONV_SPLITS", 0);  // sweeps: force splits
 static const int kDwgradForceSplits = env_int("FH_DWGRAD_SPLITS", 0);
 static const int kDconvCk32 = env_int("FH_DCONV_CK32", 8);  // sweeps: CK of the BM=32 tiles
+// XCD-aware workgroup order in the direct conv / wgrad kernels (dconv_kernels.h xcd_block):
+// off by default — measured neutral (CIFAR10CNN 32-client step: conv6 FWD 166.1 vs 166.3 us;
+// KT 265.6k vs 266.3k, profiles/r02_s3/xcd_ab.txt): those kernels are MFMA-bound and the
+// weight / activation re-reads it removes hide under the MMA loop.  FH_XCD_REMAP=1: on.
+static const int g_xcd_remap = env_int("FH_XCD_REMAP", 0);
 
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false,
                         bool ck4 = false) {
@@ -935,6 +940,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     a.splits = p.splits;
     a.cchunk = p.cchunk;
     a.Nfull = a.batch * sp;
+    a.xcd = g_xcd_remap;
     // float4 weight runs: 16-B aligned slices that never run past the tensor
     a.wvec = aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0);
     float* out = a.out;
@@ -1300,7 +1306,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         DWArgs d{};
         d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
         d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
-        d.splits = p.splits; d.stages_per_split = p.sps;
+        d.splits = p.splits; d.stages_per_split = p.sps; d.xcd = g_xcd_remap;
         d.part = (float*)workspace;
         const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
         d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
@@ -1326,7 +1332,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         DWArgs d{};
         d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
         d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
-        d.splits = p.splits; d.stages_per_split = p.sps;
+        d.splits = p.splits; d.stages_per_split = p.sps; d.xcd = g_xcd_remap;
         d.in_scale = in_scale; d.in_shift = in_shift; d.aff_cs = aff_cs;
         d.part = (float*)workspace;
         const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
@@ -1455,6 +1461,7 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
     for (int mb = mbeg; mb < mbeg + mw; mb += 8) {
         const float4 a = yok ? *reinterpret_cast<const float4*>(yrow + mb + 4 * h) : zero;
         float b[4][KT];
@@ -1468,13 +1475,25 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
             for (int t = 0; t < KT; ++t)
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a, q), b[q][t], acc[t], 0, 0, 0);
     }
-    if (wid > 0) {
+    // waves 1..3 hand their partials to wave 0 one at a time through one wave's worth of
+    // LDS (16 KB at KT = 4, so LDS does not cap the workgroups per CU); wave 0 adds them in
+    // wave order
+    for (int w = 1; w < 4; ++w) {
+        if (wid == w) {
 #pragma unroll
-        for (int t = 0; t < KT; ++t)
+            for (int t = 0; t < KT; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) red[(((wid - 1) * KT + t) * 16 + r) * 64 + lane] = acc[t][r];
+                for (int r = 0; r < 16; ++r) red[(t * 16 + r) * 64 + lane] = acc[t][r];
+        }
+        __syncthreads();
+        if (wid == 0) {
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] + red[(t * 16 + r) * 64 + lane];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (wid != 0) return;
 #pragma unroll
     for (int t = 0; t < KT; ++t)
@@ -1482,9 +1501,7 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
         for (int r = 0; r < 16; ++r) {
             const int img = (r & 3) + 8 * (r >> 2) + 4 * h;
             if (img >= cnt) continue;
-            float v = ((acc[t][r] + red[((0 * KT + t) * 16 + r) * 64 + lane]) +
-                       red[((1 * KT + t) * 16 + r) * 64 + lane]) +
-                      red[((2 * KT + t) * 16 + r) * 64 + lane];
+            float v = acc[t][r];
             const int64_t e = (int64_t)img * K + k0 + 32 * t + r32;
             if (ep.mask) v = ep.mask[z * ep.m_cs + e] ? v * ep.scale : 0.f;
             if (ep.relu_ref && !(ep.relu_ref[z * ep.r_cs + e] > 0.f)) v = 0.f;
@@ -1498,7 +1515,7 @@ linear_dgrad_skinny_kernel(const float* __restrict__ dY, int64_t dy_cs, const fl
                            int64_t w_cs, float* __restrict__ dX, int64_t dx_cs,
                            const int32_t* __restrict__ counts, int batch, int K, int M,
                            SkinnyBwdEpi ep) {
-    __shared__ float red[3 * 16 * 64 * KT];
+    __shared__ float red[16 * 64 * KT];
     linear_dgrad_skinny_body<KT>(dY, dy_cs, W, w_cs, dX, dx_cs, counts, batch, K, M, blockIdx.y,
                                  blockIdx.x, red, ep);
 }
@@ -1549,8 +1566,16 @@ linear_wgrad_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const floa
                            int64_t dy_cs, float* __restrict__ dW, int64_t dw_cs,
                            float* __restrict__ db, int64_t db_cs,
                            const int32_t* __restrict__ counts, int batch, int K, int M) {
+    // XCD-aware order: workgroups b and b + 8 share an XCD (round-robin dispatch), so the
+    // logical workgroup L = (b % 8) * (N / 8) + b / 8 puts each client's tiles — which all
+    // read that client's X and dY — on one XCD's L2 instead of all eight
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int N = gx * gy * gridDim.z;
+    int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    if ((N & 7) == 0) b = (b & 7) * (N >> 3) + (b >> 3);
+    const int kb = b % gx, rest = b / gx;
     linear_wgrad_skinny_body(X, x_cs, dY, dy_cs, dW, dw_cs, db, db_cs, counts, batch, K, M,
-                             blockIdx.z, blockIdx.x, blockIdx.y);
+                             rest / gy, kb, rest % gy);
 }
 
 // A whole linear backward in one launch: workgroups [0, nw) of each client are the skinny
@@ -1564,7 +1589,7 @@ linear_bwd_fused_kernel(const float* __restrict__ X, int64_t x_cs, const float* 
                         float* __restrict__ dW, int64_t dw_cs, float* __restrict__ db,
                         int64_t db_cs, float* __restrict__ dX, int64_t dx_cs, SkinnyBwdEpi ep,
                         const int32_t* __restrict__ counts, int batch, int K, int M, int nw) {
-    __shared__ float red[3 * 16 * 64 * KT];
+    __shared__ float red[16 * 64 * KT];
     const int z = blockIdx.y, bx = blockIdx.x;
     if (bx < nw) {
         const int kt = K / 128;

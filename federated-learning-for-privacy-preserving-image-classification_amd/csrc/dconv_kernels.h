@@ -66,6 +66,7 @@ struct DConvArgs {
     const uint8_t* pmask;
     int64_t pi_cs, pm_cs;
     float pscale;
+    int xcd;  // host: XCD-aware workgroup order (xcd_block)
 };
 
 // Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
@@ -81,6 +82,22 @@ __device__ __forceinline__ float4 bn_relu4(float4 v, float s, float t) {
     v.z = fmaxf(v.z * s + t, 0.f);
     v.w = fmaxf(v.w * s + t, 0.f);
     return v;
+}
+
+// XCD-aware workgroup order.  Workgroups b and b + 8 share an XCD (round-robin dispatch,
+// MI355X_MICROARCH.md "Workgroup dispatch"), so the logical workgroup
+// L = (b % 8) * (N / 8) + b / 8 gives each XCD a contiguous range of the x-fastest grid
+// order: one client's tiles — which all read that client's weights (conv) or X / dY
+// (wgrad) — share one XCD's L2 instead of being re-read into all eight.  Speed only: any
+// placement computes the same result.
+__device__ __forceinline__ void xcd_block(bool on, int& bx, int& by, int& bz) {
+    const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+    int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    if (on && (n & 7) == 0) b = (b & 7) * (n >> 3) + (b >> 3);
+    bx = b % gx;
+    const int r = b / gx;
+    by = r % gy;
+    bz = r / gy;
 }
 
 template <int W>
@@ -134,10 +151,12 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WAVES_N, wn = wid % WAVES_N;
-    const int z = blockIdx.z / a.splits;
-    const int split = blockIdx.z - z * a.splits;
+    int bx, by, bz;
+    xcd_block(a.xcd != 0, bx, by, bz);
+    const int z = bz / a.splits;
+    const int split = bz - z * a.splits;
     const int cnt = a.counts ? a.counts[z] : a.batch;
-    const int t = blockIdx.x, m0 = blockIdx.y * BM;
+    const int t = bx, m0 = by * BM;
     const int n0 = t * 256;
     // block-uniform: BN statistics of the stored values (FWD) / BN backward statistics of
     // the stored gradient (DGRAD)
@@ -489,7 +508,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
             continue;
         }
         if (a.splits > 1) {
-            float* op = a.out + ((int64_t)blockIdx.z * M) * a.Nfull + n;
+            float* op = a.out + ((int64_t)bz * M) * a.Nfull + n;
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -577,6 +596,7 @@ struct DWArgs {
     const float* in_scale;
     const float* in_shift;
     int64_t aff_cs;
+    int xcd;  // host: XCD-aware workgroup order (xcd_block)
 };
 
 // Two workgroups per CU when the double-buffered staging fits twice in the 160 KB LDS:
@@ -618,9 +638,11 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR>())) dc
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wpx = wid % WPX, wci = (wid / WPX) % WCI, wco = wid / (WPX * WCI);
-    const int split = blockIdx.x, z = blockIdx.z;
+    int bx, by, bz;
+    xcd_block(a.xcd != 0, bx, by, bz);
+    const int split = bx, z = bz;
     const int ntile_ci = a.cin / BN;
-    const int co0 = (blockIdx.y / ntile_ci) * BM, ci0 = (blockIdx.y % ntile_ci) * BN;
+    const int co0 = (by / ntile_ci) * BM, ci0 = (by % ntile_ci) * BN;
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int nst = (cnt * HW + SPX - 1) / SPX;
     const int sbeg = split * a.stages_per_split;
@@ -824,8 +846,10 @@ __global__ void __launch_bounds__(256) dconv_wgrad_small_kernel(const DWArgs a) 
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wpx = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int split = blockIdx.x, z = blockIdx.z;
-    const int co0 = blockIdx.y * 32;
+    int bx, by, bz;
+    xcd_block(a.xcd != 0, bx, by, bz);
+    const int split = bx, z = bz;
+    const int co0 = by * 32;
     const int cnt = a.counts ? a.counts[z] : a.batch;
     const int nst = (cnt * HW + SPX - 1) / SPX;
     const int sbeg = split * a.stages_per_split;
