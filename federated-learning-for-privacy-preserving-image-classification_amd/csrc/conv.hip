@@ -78,7 +78,17 @@ struct ConvArgs {
     int M, N, K;         // GEMM extents at full batch
     FastDiv fd_ohw, fd_ow, fd_hw, fd_w;
     DropArgs drop;       // FWD: dropout after bias / ReLU (unsplit launches; else the epilogue)
+    // OP_DGRAD_S2, nullable: the weights re-laid phase-major by pack_dgrad_s2_kernel —
+    // [client][phase][ci][co * taps + t] — so the A tile loads run along k (the gather from
+    // W[co][ci][kh][kw] touches one cache line per lane: address-bound)
+    const float* wp;
+    int64_t wp_cs;
 };
+
+// Taps of a stride-2 DGRAD phase before phase ph (3x3/p1: 1, 2, 2, 4; 1x1/p0: 1, 0, 0, 0)
+__host__ __device__ constexpr int s2_tap_prefix(int kh, int ph) {
+    return kh == 3 ? (ph == 0 ? 0 : ph == 1 ? 1 : ph == 2 ? 3 : 5) : (ph == 0 ? 0 : 1);
+}
 
 template <int OP, int KH, int KW, int S, int BM, int BN, int BK, int WAVES_M>
 __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
@@ -158,6 +168,9 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
     }
     const float* wz = nullptr;
     if constexpr (OP != OP_WGRAD) wz = a.wt + z * a.w_cs;
+    const float* wpz = nullptr;  // this (client, phase)'s packed weights [ci][co * taps]
+    if constexpr (DG2)
+        if (a.wp) wpz = a.wp + z * a.wp_cs + (int64_t)s2_tap_prefix(KH, 2 * py + px) * a.cin * a.cout;
 
     float ra[NA], rb[NB];
 
@@ -188,6 +201,10 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
             for (int i = 0; i < NA; ++i) {
                 const int e = tid + i * 256, mm = e / BK, kk = e % BK;
                 const int m = m0 + mm, k = k0 + kk;
+                if (a.wp) {
+                    ra[i] = (m < M && k < kend) ? wpz[(int64_t)m * (a.cout << lg_t) + k] : 0.f;
+                    continue;
+                }
                 const int co = k >> lg_t, t = k & ((1 << lg_t) - 1);
                 const int kh = KH == 3 ? (py ? 2 * (t >> lg_tw) : 1) : 0;
                 const int kw = KW == 3 ? (px ? 2 * (t & ((1 << lg_tw) - 1)) : 1) : 0;
@@ -803,6 +820,38 @@ static bool dgrad_s2_supported(int h, int w, int kh, int kw, int stride, int pad
            ((kh == 3 && kw == 3 && pad == 1) || (kh == 1 && kw == 1 && pad == 0));
 }
 
+// W[z][co][ci][kh][kw] -> wp[z][phase][ci][co * taps + t] (igemm OP_DGRAD_S2's k order:
+// t indexes the phase's taps, kh-major; 3x3/p1 phase (py, px) takes kh = 1 (py = 0) or
+// {0, 2} (py = 1), likewise kw)
+__global__ void __launch_bounds__(256)
+pack_dgrad_s2_kernel(const float* __restrict__ w, int64_t w_cs, float* __restrict__ wp,
+                     int64_t wp_cs, int cin, int cout, int KH) {
+    const int z = blockIdx.y;
+    const int KHW = KH * KH;
+    const int64_t total = (int64_t)cin * cout * KHW;
+    for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        // phase of e: the prefix table over ci*cout-sized blocks
+        const int blk = (int)(e / ((int64_t)cin * cout));
+        int ph = 0;
+        while (ph < 3 && s2_tap_prefix(KH, ph + 1) <= blk) ++ph;
+        const int py = ph >> 1, px = ph & 1;
+        const int nth = KH == 3 ? 1 + py : 1 - py, ntw = KH == 3 ? 1 + px : 1 - px;
+        const int taps = nth * ntw;
+        const int64_t r = e - (int64_t)s2_tap_prefix(KH, ph) * cin * cout;  // [ci][co*taps+t]
+        const int ci = (int)(r / ((int64_t)cout * taps));
+        const int k = (int)(r - (int64_t)ci * cout * taps);
+        const int co = k / taps, t = k - co * taps;
+        const int kh = KH == 3 ? (py ? 2 * (t / ntw) : 1) : 0;
+        const int kw = KH == 3 ? (px ? 2 * (t % ntw) : 1) : 0;
+        wp[z * wp_cs + e] = w[z * w_cs + ((int64_t)co * cin + ci) * KHW + kh * KH + kw];
+    }
+}
+
+static size_t dgrad_s2_pack_bytes(int cin, int cout, int kh, int nclients) {
+    return ((size_t)nclients * cin * cout * kh * kh * sizeof(float) + 255) / 256 * 256;
+}
+static const int g_dgrad_s2_pack = env_int("FH_DGRAD_S2_PACK", 1);  // A/B: 0 = gather W
+
 // GEMM per (client, phase): M = cin, N = batch * oh * ow, K <= cout * 4 (3x3) or cout (1x1)
 static Plan plan_dgrad_s2(int cin, int cout, int kh, int batch, int oh, int ow, int nclients) {
     return plan_mn(cin, batch * oh * ow, cout * (kh == 3 ? 4 : 1), nclients * 4);
@@ -811,6 +860,19 @@ static Plan plan_dgrad_s2(int cin, int cout, int kh, int batch, int oh, int ow, 
 static int run_dgrad_s2(ConvArgs a, int kh, int nclients, void* ws, size_t ws_bytes, float* out,
                         int64_t out_cs, int accum, hipStream_t st) {
     Plan p = plan_dgrad_s2(a.cin, a.cout, kh, a.batch, a.oh, a.ow, nclients);
+    // workspace: [packed weights][split-K slab]; the pack goes first so that it survives
+    // when the slab does not fit
+    const size_t pack = g_dgrad_s2_pack ? dgrad_s2_pack_bytes(a.cin, a.cout, kh, nclients) : 0;
+    if (pack && ws && ws_bytes >= pack) {
+        a.wp = (float*)ws;
+        a.wp_cs = (int64_t)a.cin * a.cout * kh * kh;
+        FH_LAUNCH(pack_dgrad_s2_kernel,
+                  dim3((unsigned)std::min<int64_t>(ceil_div(a.wp_cs, 256), 1024), nclients),
+                  dim3(256), 0, st, a.wt, a.w_cs, (float*)ws, a.wp_cs, a.cin, a.cout, kh);
+        FH_LAUNCH_CHECK("conv2d_dgrad s2 pack");
+        ws = (char*)ws + pack;
+        ws_bytes -= pack;
+    }
     if (p.splits > 1 && (!ws || ws_bytes < mn_ws_bytes(p, nclients * 4))) {
         p.splits = 1;
         p.kchunk = p.K;
@@ -900,14 +962,20 @@ static size_t dconv_ws_bytes(const DPlan& p, int nclients, int M, int batch, int
     return p.splits > 1 ? (size_t)nclients * p.splits * M * batch * hw * sizeof(float) : 0;
 }
 
-template <int OP, int W, int S = 1>
+template <int OP, int W, int S = 1, bool BNB = false>
 static int dconv_launch_w(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_t st) {
 #define FH_DC(BM, WMV, CK, VEC)                                                                 \
     if (p.bm == BM && p.ck == CK && (a.wvec != 0) == VEC) {                                     \
-        FH_LAUNCH((dconv_kernel<OP, W, BM, WMV, CK, VEC, S>), grid, dim3(256), 0, st, a);     \
+        FH_LAUNCH((dconv_kernel<OP, W, BM, WMV, CK, VEC, S, BNB>), grid, dim3(256), 0, st, a); \
         return FH_OK;                                                                           \
     }
-    if constexpr (S == 1) {
+    if constexpr (BNB && OP == OP_DGRAD) {  // BN-backward statistics epilogue (BM <= 64)
+        FH_DC(32, 1, 8, true)
+        FH_DC(32, 1, 4, true)
+        FH_DC(64, 2, 8, true)
+        FH_DC(32, 1, 8, false)
+        FH_DC(32, 1, 4, false)
+    } else if constexpr (S == 1) {
         FH_DC(32, 1, 8, true)
         FH_DC(32, 1, 4, true)
         FH_DC(64, 2, 8, true)
@@ -948,13 +1016,18 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     dim3 grid((unsigned)ceil_div(a.Nfull, 256), (unsigned)ceil_div(a.M, p.bm),
               (unsigned)(nclients * p.splits));
     int rc;
-    if constexpr (S == 1)
+    if constexpr (S == 2) {
+        rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
+                     : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
+    } else if (a.bn_part && p.splits == 1) {  // the statistics epilogue instances
+        rc = w == 32 ? dconv_launch_w<OP, 32, 1, true>(p, grid, a, st)
+           : w == 16 ? dconv_launch_w<OP, 16, 1, true>(p, grid, a, st)
+                     : dconv_launch_w<OP, 8, 1, true>(p, grid, a, st);
+    } else {
         rc = w == 32 ? dconv_launch_w<OP, 32>(p, grid, a, st)
            : w == 16 ? dconv_launch_w<OP, 16>(p, grid, a, st)
                      : dconv_launch_w<OP, 8>(p, grid, a, st);
-    else
-        rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
-                     : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
+    }
     if (rc) return rc;
     FH_LAUNCH_CHECK(name);
     if (p.splits > 1) {
@@ -1090,7 +1163,8 @@ extern "C" size_t fh_conv2d_dgrad_workspace(int32_t nclients, int32_t batch, int
         return dconv_ws_bytes(plan_dconv(cin, cout, batch, h * w_, nclients), nclients, cin, batch,
                               h * w_);
     if (dgrad_s2_supported(h, w_, kh, kw, stride, pad) && !g_dgrad_s2_off)
-        return mn_ws_bytes(plan_dgrad_s2(cin, cout, kh, batch, oh, ow, nclients), nclients * 4);
+        return (g_dgrad_s2_pack ? dgrad_s2_pack_bytes(cin, cout, kh, nclients) : 0) +
+               mn_ws_bytes(plan_dgrad_s2(cin, cout, kh, batch, oh, ow, nclients), nclients * 4);
     return mn_ws_bytes(plan_mn(cin, batch * h * w_, cout * kh * kw, nclients), nclients);
 }
 

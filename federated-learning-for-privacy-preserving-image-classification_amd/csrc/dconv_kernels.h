@@ -119,10 +119,14 @@ struct DGeom {
 // (2W + 2 columns with the halo), and a lane's operand address strides by 2 — the 3x3
 // shifts stay LDS immediates.  The channel stride of the patch is odd, so the two lane
 // halves (channel pair) fall on opposite bank parities.
-template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC, int S = 1>
+// BNB: the instance with the statistics epilogue — FWD the BatchNorm statistics, DGRAD the
+// BN-backward statistics (its registers would otherwise cost every instance an occupancy
+// step, e.g. DGRAD W=32 BM=32: 96 -> 114 VGPRs, 4 -> 3 waves per SIMD)
+template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC, int S = 1, bool BNB = false>
 __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     using G = DGeom<W>;
     static_assert(S == 1 || (S == 2 && OP == OP_FWD), "stride 2: forward only");
+    static_assert(!BNB || S == 1, "statistics epilogue: stride 1");
     constexpr int WI = S * W, HI = S * G::H;               // input map
     constexpr int PRS = S == 1 ? G::SEGR + 2 : 2 * G::SEGR + 1;  // input rows per segment
     constexpr int PW = WI + 2, PR = G::NI * PRS;
@@ -142,8 +146,8 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     // one LDS block: the double-buffered weight / patch stages, reused after the K loop as
     // the statistics image (with bn_part)
     constexpr int LDS_MAIN = 2 * KS * BMP + 2 * PE;
-    constexpr int LDS_STAT = BM * kStatPitch + (OP == OP_DGRAD ? 3 * BM : 0);
-    constexpr int LDS_N = (S == 1 && LDS_STAT > LDS_MAIN) ? LDS_STAT : LDS_MAIN;
+    constexpr int LDS_STAT = !BNB ? 0 : BM * kStatPitch + (OP == OP_DGRAD ? 3 * BM : 0);
+    constexpr int LDS_N = LDS_STAT > LDS_MAIN ? LDS_STAT : LDS_MAIN;
     __shared__ float smem[LDS_N];
     float (*As)[KS * BMP] = reinterpret_cast<float (*)[KS * BMP]>(smem);
     float (*Ps)[PE] = reinterpret_cast<float (*)[PE]>(smem + 2 * KS * BMP);
@@ -160,7 +164,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     const int n0 = t * 256;
     // block-uniform: BN statistics of the stored values (FWD) / BN backward statistics of
     // the stored gradient (DGRAD)
-    const bool stats = S == 1 && a.bn_part != nullptr && a.splits == 1;
+    const bool stats = BNB && a.bn_part != nullptr && a.splits == 1;
     if (n0 >= cnt * G::HW) {  // a tile past this client's images: zero statistics
         if (stats && tid < BM && m0 + tid < a.M) {
             double* q = a.bn_part + (((int64_t)z * a.M + m0 + tid) * a.bn_tiles + t) * 2;
@@ -362,7 +366,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 
     // ---- epilogue: lanes = 32 consecutive pixels -> coalesced stores ----
     const int rbase = 4 * h;
-    if constexpr (OP == OP_DGRAD) {
+    if constexpr (BNB && OP == OP_DGRAD) {
         if (stats) {  // BN backward statistics (host: no accumulate)
             float* red = smem;                         // [BM][kStatPitch] image
             float* cst = smem + BM * kStatPitch;       // [3][BM] scale, shift, mean
