@@ -597,6 +597,37 @@ extern "C" int fh_bn_finalize_tiles(const double* part, const float* gamma, cons
     return FH_OK;
 }
 
+// fh_bn_fwd_train's apply pass from the per-tile statistics a convolution epilogue wrote
+// (FederatedResNet's stem bn1 and block bn2, whose output is materialised because the next
+// block reads it twice, conv and residual): bn_apply_kernel merges the conv tiles instead of
+// bn_stats_kernel's slices -> y = [relu](x*alpha + beta' [+ res]), save_mean / save_invstd
+// and the running statistics.  y is never re-read for its statistics.
+extern "C" int fh_bn_apply_tiles(const double* part, const float* x, int64_t x_cs, float* y,
+                                 int64_t y_cs, const float* res, int64_t res_cs,
+                                 const float* gamma, const float* beta, int64_t p_cs,
+                                 float* running_mean, float* running_var, int64_t r_cs,
+                                 float* save_mean, float* save_invstd, const int32_t* counts,
+                                 int32_t nclients, int32_t batch, int32_t C, int32_t HW,
+                                 float eps, float momentum, int32_t relu, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_apply_tiles: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(part && x && y && gamma && beta && save_mean && save_invstd,
+               "bn_apply_tiles: null pointer");
+    FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr),
+               "bn_apply_tiles: running stats");
+    BNArgs a = bn_args(nclients, batch, C, HW, counts);
+    a.SP = (int)ceil_div((int64_t)batch * HW, 256);  // the conv epilogue's tiles
+    a.part = (double*)part;
+    a.x = x; a.y = y; a.res = res; a.gamma = gamma; a.beta = beta;
+    a.rmean = running_mean; a.rvar = running_var; a.save_mean = save_mean;
+    a.save_invstd = save_invstd;
+    a.x_cs = x_cs; a.y_cs = y_cs; a.res_cs = res_cs; a.p_cs = p_cs; a.r_cs = r_cs;
+    a.eps = eps; a.momentum = momentum; a.relu = relu;
+    FH_LAUNCH(bn_apply_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
+    FH_LAUNCH_CHECK("bn_apply_tiles");
+    return FH_OK;
+}
+
 // fh_bn_finalize_tiles + fh_maxpool2_fwd_bnrelu in one launch (maxpool2_bnfin_kernel).
 extern "C" int fh_maxpool2_fwd_bnfinalize(
         const double* part, const float* gamma, const float* beta, int64_t p_cs,

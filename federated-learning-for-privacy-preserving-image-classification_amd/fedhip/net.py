@@ -128,7 +128,7 @@ class PackedNet:
         self.seed = 0
         self.seed_dev = None  # device uint64 [1] = seed * 1000003 (graph replay)
         self.salt = 0  # per-lane key offset (a lane's slot 0 is not another lane's slot 0)
-        # CIFAR10CNN training: BN apply + ReLU folded into the consumers (FH_FUSE_BN=0: off)
+        # CIFAR10CNN and ResNet training: BN apply + ReLU folded into the consumers (FH_FUSE_BN=0: off)
         self.fuse_bn = os.environ.get("FH_FUSE_BN", "1") != "0"
         # ... and the BN statistics taken by the producing conv's epilogue instead of a
         # second pass over its output (FH_BN_EPILOGUE=0: the separate statistics pass)
@@ -600,22 +600,42 @@ class PackedNet:
 
     # ---------------- FederatedResNet (models_pytorch.py:230-246, block :189-194)
     def _fwd_resnet(self, P_, bufs, n, cnt, train):
+        """Training with fuse_bn: the statistics of every BN behind a direct 3x3/s1 conv come
+        from that conv's epilogue; each block's bn1 output is never written (bn1's affine is
+        applied on load by conv2's forward and weight gradient, as in CIFAR10CNN); the stem
+        bn1 and the block bn2 (+ residual) outputs are materialised by their apply pass only
+        (bn_apply_tiles) — the next block reads them twice (conv and residual)."""
         A, B, W = self.A, self.batch, self.W
         cin0 = self.in_shape[0]
+        fuse = train and self.fuse_bn
+        self._fused = fuse
+        epi = fuse and self.bn_epilogue
         c0, r0 = A("c_stem", 64, 32, 32), A("r_stem", 64, 32, 32)
+        part = self._bn_part("bn1", 64, 32) if epi else None
         ops.conv2d_fwd(self.x, W(P_, "conv1.weight"), None, c0, n, B, cin0, 32, 32, 64, 3, 1, 1,
-                       counts=cnt)
-        self._bn_train(P_, bufs, "bn1", c0, r0, n, 64, 1024, cnt, relu=True, train=train)
+                       counts=cnt, bn_stats=part)
+        if part is not None:
+            self._bn_apply_tiles(P_, bufs, "bn1", part, c0, r0, n, 64, 1024, cnt, relu=True)
+        else:
+            self._bn_train(P_, bufs, "bn1", c0, r0, n, 64, 1024, cnt, relu=True, train=train)
         xin = r0
         for b in self.blocks:
             pf, ci, co, s, hi, ho = b["pfx"], b["cin"], b["cout"], b["stride"], b["hin"], b["hout"]
-            a, ar = A(f"{pf}.a", co, ho, ho), A(f"{pf}.ar", co, ho, ho)
+            a = A(f"{pf}.a", co, ho, ho)
             bb, out = A(f"{pf}.b", co, ho, ho), A(f"{pf}.out", co, ho, ho)
+            p1 = self._bn_part(f"{pf}.bn1", co, ho) if epi and s == 1 else None
             ops.conv2d_fwd(xin, W(P_, f"{pf}.conv1.weight"), None, a, n, B, ci, hi, hi, co, 3, s, 1,
-                           counts=cnt)
-            self._bn_train(P_, bufs, f"{pf}.bn1", a, ar, n, co, ho * ho, cnt, relu=True, train=train)
-            ops.conv2d_fwd(ar, W(P_, f"{pf}.conv2.weight"), None, bb, n, B, co, ho, ho, co, 3, 1, 1,
-                           counts=cnt)
+                           counts=cnt, bn_stats=p1)
+            if fuse:
+                aff1 = self._bn_stats_only(P_, bufs, f"{pf}.bn1", a, p1, n, co, ho * ho, cnt)
+                c2_in = a
+            else:
+                aff1, c2_in = None, A(f"{pf}.ar", co, ho, ho)
+                self._bn_train(P_, bufs, f"{pf}.bn1", a, c2_in, n, co, ho * ho, cnt, relu=True,
+                               train=train)
+            p2 = self._bn_part(f"{pf}.bn2", co, ho) if epi else None
+            ops.conv2d_fwd(c2_in, W(P_, f"{pf}.conv2.weight"), None, bb, n, B, co, ho, ho, co, 3, 1,
+                           1, counts=cnt, in_affine=aff1, bn_stats=p2)
             if b["proj"]:
                 sc, scb = A(f"{pf}.sc", co, ho, ho), A(f"{pf}.scb", co, ho, ho)
                 ops.conv2d_fwd(xin, W(P_, f"{pf}.shortcut.0.weight"), None, sc, n, B, ci, hi, hi, co,
@@ -625,8 +645,12 @@ class PackedNet:
                 res = scb
             else:
                 res = xin
-            self._bn_train(P_, bufs, f"{pf}.bn2", bb, out, n, co, ho * ho, cnt, relu=True, res=res,
-                           train=train)
+            if p2 is not None:
+                self._bn_apply_tiles(P_, bufs, f"{pf}.bn2", p2, bb, out, n, co, ho * ho, cnt,
+                                     relu=True, res=res)
+            else:
+                self._bn_train(P_, bufs, f"{pf}.bn2", bb, out, n, co, ho * ho, cnt, relu=True,
+                               res=res, train=train)
             b["xin"] = xin
             xin = out
         f = A("feat", 256)
@@ -635,6 +659,30 @@ class PackedNet:
         if self._head:
             ops.linear_fwd(f, W(P_, "fc.weight"), W(P_, "fc.bias"), self.logits, n, B, 256,
                            self.num_classes, counts=cnt)
+
+    def _bn_apply_tiles(self, P_, bufs, name, part, x, y, n, C, HW, cnt, relu, res=None):
+        sm, si = self._bn_save(name, C)
+        ops.bn_apply_tiles(part, x, y, self.W(P_, f"{name}.weight"), self.W(P_, f"{name}.bias"),
+                           self.layout.bview(bufs, f"{name}.running_mean"),
+                           self.layout.bview(bufs, f"{name}.running_var"), sm, si, n, self.batch,
+                           C, HW, self.bn_eps, self.bn_momentum, relu=relu, res=res, counts=cnt)
+
+    def _bn_stats_only(self, P_, bufs, name, x, part, n, C, HW, cnt):
+        """Train-mode BN statistics (from the producing conv's tiles when part is given, else
+        a statistics pass over x) -> save_mean / save_invstd, running statistics and the
+        affine its consumers apply on load."""
+        sm, si = self._bn_save(name, C)
+        aff = self._bn_affine(name, C)
+        args = (self.W(P_, f"{name}.weight"), self.W(P_, f"{name}.bias"),
+                self.layout.bview(bufs, f"{name}.running_mean"),
+                self.layout.bview(bufs, f"{name}.running_var"), sm, si, aff[0], aff[1])
+        if part is not None:
+            ops.bn_finalize_tiles(part, *args, n, self.batch, C, HW, self.bn_eps,
+                                  self.bn_momentum, counts=cnt)
+        else:
+            ops.bn_fwd_stats(x, *args, n, self.batch, C, HW, self.bn_eps, self.bn_momentum,
+                             counts=cnt)
+        return aff
 
     def _bwd_resnet(self, P_, G, n, cnt):
         A, B, W = self.A, self.batch, self.W
@@ -667,17 +715,28 @@ class PackedNet:
             ops.bn_bwd(dout, A(f"{pf}.out", co, ho, ho), A(f"{pf}.b", co, ho, ho),
                        W(P_, f"{pf}.bn2.weight"), sm2, si2, db, W(G, f"{pf}.bn2.weight"),
                        W(G, f"{pf}.bn2.bias"), n, B, co, ho * ho, relu=True, dres=dres, counts=cnt)
-            ar = A(f"{pf}.ar", co, ho, ho)
+            a = A(f"{pf}.a", co, ho, ho)
+            aff1 = self._bn_affine(f"{pf}.bn1", co) if self._fused else None
+            ar = a if self._fused else A(f"{pf}.ar", co, ho, ho)
             ops.conv2d_wgrad(ar, db, W(G, f"{pf}.conv2.weight"), None, n, B, co, ho, ho, co, 3, 1, 1,
-                             counts=cnt)
+                             counts=cnt, in_affine=aff1)
             dar = A(f"{pf}.dar", co, ho, ho)
-            ops.conv2d_dgrad(db, W(P_, f"{pf}.conv2.weight"), dar, n, B, co, ho, ho, co, 3, 1, 1,
-                             counts=cnt)
             da = A(f"{pf}.da", co, ho, ho)
             sm1, si1 = self._bn_save(f"{pf}.bn1", co)
-            ops.bn_bwd(dar, None, A(f"{pf}.a", co, ho, ho), W(P_, f"{pf}.bn1.weight"), sm1, si1,
-                       da, W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co, ho * ho,
-                       relu=True, counts=cnt, beta=W(P_, f"{pf}.bn1.bias"))
+            if self._fused and self.bn_bwd_epilogue:
+                # conv2's dgrad masks by bn1's ReLU and leaves bn1's backward statistics
+                tiles = self._bn_part(f"{pf}.bn1.bwd", co, ho)
+                ops.conv2d_dgrad(db, W(P_, f"{pf}.conv2.weight"), dar, n, B, co, ho, ho, co, 3, 1,
+                                 1, counts=cnt, bn_bwd=(a, *aff1, sm1, tiles))
+                ops.bn_bwd_tiles(tiles, dar, a, W(P_, f"{pf}.bn1.weight"), sm1, si1, da,
+                                 W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co,
+                                 ho * ho, counts=cnt)
+            else:
+                ops.conv2d_dgrad(db, W(P_, f"{pf}.conv2.weight"), dar, n, B, co, ho, ho, co, 3, 1,
+                                 1, counts=cnt)
+                ops.bn_bwd(dar, None, a, W(P_, f"{pf}.bn1.weight"), sm1, si1, da,
+                           W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co, ho * ho,
+                           relu=True, counts=cnt, beta=W(P_, f"{pf}.bn1.bias"))
             xin = b["xin"]
             ops.conv2d_wgrad(xin, da, W(G, f"{pf}.conv1.weight"), None, n, B, ci, hi, hi, co, 3, s, 1,
                              counts=cnt)
@@ -735,7 +794,13 @@ class PackedNet:
         out = [A("r_stem", 64, 32, 32)]
         for b in self.blocks:
             pf, co, ho = b["pfx"], b["cout"], b["hout"]
-            out += [A(f"{pf}.ar", co, ho, ho), A(f"{pf}.out", co, ho, ho)]
+            if self._fused:  # bn1's output not materialised: the same fp32 ops here
+                sc, sh = self._bn_affine(f"{pf}.bn1", co)
+                ar = torch.clamp_min(A(f"{pf}.a", co, ho, ho) * sc[:, None, :, None, None]
+                                     + sh[:, None, :, None, None], 0.0)
+            else:
+                ar = A(f"{pf}.ar", co, ho, ho)
+            out += [ar, A(f"{pf}.out", co, ho, ho)]
         return out
 
     def mask_buffers(self):

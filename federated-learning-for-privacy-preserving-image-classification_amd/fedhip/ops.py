@@ -525,6 +525,16 @@ def bn_finalize_tiles(part, gamma, beta, rmean, rvar, save_mean, save_invstd, sc
          stream_handle())
 
 
+def bn_apply_tiles(part, x, y, gamma, beta, rmean, rvar, save_mean, save_invstd, nclients, batch,
+                   C, HW, eps=1e-5, momentum=0.1, relu=False, res=None, counts=None):
+    """bn_fwd_train with its statistics from the tiles a conv epilogue wrote (part, see
+    conv2d_fwd(bn_stats=...)): the apply pass only."""
+    call("fh_bn_apply_tiles", ptr(part), ptr(x), _cs(x), ptr(y), _cs(y), ptr(res), _cs(res),
+         ptr(gamma), ptr(beta), _cs(gamma), ptr(rmean), ptr(rvar), _cs(rmean), ptr(save_mean),
+         ptr(save_invstd), _counts(counts), nclients, batch, C, HW, float(eps), float(momentum),
+         int(relu), stream_handle())
+
+
 def bn_bwd_tiles(part, g, x, gamma, save_mean, save_invstd, dx, dgamma, dbeta, nclients, batch,
                  C, HW, counts=None):
     """bn_bwd's apply pass from the statistics conv2d_dgrad(bn_bwd=...) left (g masked)."""

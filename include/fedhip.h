@@ -428,6 +428,16 @@ int fh_bn_finalize_tiles(const double* part, const float* gamma, const float* be
                          float* shift_out, int64_t s_cs, const int32_t* counts,
                          int32_t nclients, int32_t batch, int32_t C, int32_t HW, float eps,
                          float momentum, void* stream);
+/* fh_bn_fwd_train (its apply pass: y = [relu](bn(x) [+ res]), save_mean / save_invstd,
+ * running statistics) from the tiles fh_conv2d_fwd_bnstats left — FederatedResNet's stem
+ * bn1 and block bn2 + residual + ReLU (models_pytorch.py:189-194, :241-242), whose output the
+ * next block reads twice and is therefore materialised. */
+int fh_bn_apply_tiles(const double* part, const float* x, int64_t x_cs, float* y, int64_t y_cs,
+                      const float* res, int64_t res_cs, const float* gamma, const float* beta,
+                      int64_t p_cs, float* running_mean, float* running_var, int64_t r_cs,
+                      float* save_mean, float* save_invstd, const int32_t* counts,
+                      int32_t nclients, int32_t batch, int32_t C, int32_t HW, float eps,
+                      float momentum, int32_t relu, void* stream);
 
 /* ---------------- launch planning ---------------------------------------------
  * Share of the chip (0, 1] that the split-K planners of the conv / linear entry points

@@ -14,9 +14,13 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _round(fuse, opt, sizes, rounds=2, bn_epilogue=False, bn_bwd_epilogue=False):
+def _round(fuse, opt, sizes, rounds=2, bn_epilogue=False, bn_bwd_epilogue=False,
+           resnet=False):
     torch.manual_seed(0)
-    model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.3).to(DEV)
+    if resnet:  # ResNet-8 (K3): stride-1 and stride-2 blocks, projection shortcuts
+        model = hm.ModelFactory.create_model("federated_resnet", num_blocks=[1, 1, 1]).to(DEV)
+    else:
+        model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.3).to(DEV)
     S = len(sizes)
     eng = PackedTrainer(model, capacity=S, batch=32, device=DEV)
     eng.net.fuse_bn = fuse
@@ -415,3 +419,81 @@ def test_dgrad_bn_bwd_stats_through_pool(nc, ci, co, hw, dm):
         k = int(cnt[z])
         scale = dx1[z, :k].abs().max().item()
         assert (dx1[z, :k] - dx2[z, :k]).abs().max().item() <= 1e-5 * scale
+
+
+# ---------------------------------------------------------------- FederatedResNet (r02)
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_resnet_fused_bn_rounds_bit_identical(opt):
+    """ResNet-8 with bn1 applied on load by conv2 (fwd + wgrad) and its statistics from a
+    separate statistics pass (fh_bn_fwd_stats): bit-identical to the materialised path."""
+    sizes = [70, 33, 9]
+    a, ma = _round(True, opt, sizes, resnet=True)
+    b, mb = _round(False, opt, sizes, resnet=True)
+    assert a.net._fused and not b.net._fused
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.bufs, b.bufs)
+    assert torch.equal(a.state1, b.state1)
+    for ra, rb in zip(ma, mb):
+        for x, y in zip(ra, rb):
+            assert (x.loss, x.accuracy) == (y.loss, y.accuracy)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_resnet_epilogue_bn_stats_rounds_match(opt):
+    """ResNet-8 rounds with the forward BN statistics from the conv epilogues (stem bn1,
+    stride-1 bn1, every bn2 via fh_bn_apply_tiles) and bn1's backward statistics from conv2's
+    dgrad epilogue vs the separate passes: the same training up to the fp64 summation order
+    of the statistics."""
+    sizes = [70, 33, 9]
+    a, ma = _round(True, opt, sizes, bn_epilogue=True, bn_bwd_epilogue=True, resnet=True)
+    b, mb = _round(True, opt, sizes, resnet=True)
+    P = a.layout.P
+    d = (a.params[:, :P] - b.params[:, :P]).norm(dim=1)
+    upd = (b.params[:, :P] - b.init_params[:, :P]).norm(dim=1)
+    assert bool((d <= 1e-3 * upd).all()), (d, upd)
+    torch.testing.assert_close(a.bufs, b.bufs, rtol=1e-4, atol=1e-5)
+    for ra, rb in zip(ma, mb):
+        for x, y in zip(ra, rb):
+            assert abs(x.loss - y.loss) <= 1e-4 * max(1.0, abs(y.loss))
+
+
+@pytest.mark.parametrize("nc,C,hw,res", [(1, 64, 32, False), (3, 64, 32, True),
+                                         (5, 128, 16, True), (8, 256, 8, True)])
+def test_bn_apply_tiles_matches_fwd_train(nc, C, hw, res):
+    """fh_conv2d_fwd_bnstats + fh_bn_apply_tiles vs fh_bn_fwd_train on the same conv output
+    (ReLU, with and without the residual, ragged counts): the saved / running statistics
+    within 1 ulp (the same fp64 terms added in a different order), y within 1e-5 (a 1-ulp
+    scale difference moves x*alpha + beta' by an ulp of x*alpha, not of y); y past a
+    client's count untouched."""
+    B = 32
+    torch.manual_seed(nc * 11 + C)
+    cnt = torch.tensor([B] + [int(v) for v in torch.randint(1, B + 1, (nc - 1,))],
+                       dtype=torch.int32, device=DEV)
+    x = torch.randn(nc, B, C, hw, hw, device=DEV)
+    w = torch.randn(nc, C, C, 3, 3, device=DEV) * 0.05
+    c = torch.zeros(nc, B, C, hw, hw, device=DEV)
+    part = torch.full((nc, C, ops.bnstats_tiles(B, hw, hw), 2), float("nan"),
+                      dtype=torch.float64, device=DEV)
+    ops.conv2d_fwd(x, w, None, c, nc, B, C, hw, hw, C, 3, 1, 1, counts=cnt, bn_stats=part)
+    r = torch.randn(nc, B, C, hw, hw, device=DEV) if res else None
+    gamma = torch.rand(nc, C, device=DEV) + 0.5
+    beta = torch.randn(nc, C, device=DEV) * 0.3
+    outs = []
+    for tiles in (False, True):
+        y = torch.full_like(c, 7.0)
+        rm, rv = torch.zeros(nc, C, device=DEV), torch.ones(nc, C, device=DEV)
+        sm, si = torch.zeros(nc, C, device=DEV), torch.zeros(nc, C, device=DEV)
+        if tiles:
+            ops.bn_apply_tiles(part, c, y, gamma, beta, rm, rv, sm, si, nc, B, C, hw * hw,
+                               relu=True, res=r, counts=cnt)
+        else:
+            ops.bn_fwd_train(c, y, gamma, beta, rm, rv, sm, si, nc, B, C, hw * hw, relu=True,
+                             res=r, counts=cnt)
+        outs.append((y, rm, rv, sm, si))
+    torch.cuda.synchronize()
+    for u, v in list(zip(*outs))[1:]:
+        assert _ulps(u, v) <= 1
+    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=1e-5, atol=1e-5)
+    y = outs[1][0]
+    for z in range(nc):
+        assert bool((y[z, int(cnt[z]):] == 7.0).all())
