@@ -1052,6 +1052,69 @@ static bool dconv_s2_supported(int h, int w, int kh, int kw, int stride, int pad
            (w == 16 || w == 32);
 }
 
+// 3x3 / stride 2 / pad 1 DGRAD on square 32->16 and 16->8 maps (ResNet down-sampling blocks):
+// dconv_dgrad_s2_kernel<grid width, CK = 8>, 32 dX channels per workgroup, split over the
+// reduction channels (cout) on small grids; FH_DCONV_DGRAD_S2=0 sends it back to the
+// implicit-GEMM phases (A/B).
+static const int g_dconv_dgrad_s2_off = env_int("FH_DCONV_DGRAD_S2", 1) == 0;
+static bool dconv_dgrad_s2_supported(int h, int w, int kh, int kw, int stride, int pad, int cin,
+                                     int cout) {
+    return !g_dconv_dgrad_s2_off && kh == 3 && kw == 3 && stride == 2 && pad == 1 && h == w &&
+           (w == 16 || w == 32) && cin % 32 == 0 && cout % 8 == 0;
+}
+// split planning (sweeps): target workgroups (two fit a CU) and the fewest reduction channels a
+// split keeps (every split writes a slab the size of dX: few long splits beat many short ones)
+static const int kDs2Fill = env_int("FH_DS2_FILL", 256);
+static const int kDs2MinCh = env_int("FH_DS2_MINCH", 32);
+static DPlan plan_dconv_dgrad_s2(int cin, int cout, int batch, int oh, int nclients) {
+    DPlan p{32, 8, 1, cout};
+    const int64_t blocks = ceil_div((int64_t)batch * oh * oh, 256) * ceil_div(cin, 32) * nclients;
+    const int chunks = (int)ceil_div(cout, 8);
+    const int maxs = std::max(1, (int)(cout / std::max(8, kDs2MinCh)));
+    if (blocks < fill(kDs2Fill) && chunks > 1) {
+        const int want = (int)std::min<int64_t>(ceil_div(fill(kDs2Fill), blocks), maxs);
+        const int per = (int)ceil_div(chunks, std::max(1, want));
+        p.cchunk = per * 8;
+        p.splits = (int)ceil_div(cout, p.cchunk);
+    }
+    if (p.splits <= 1) {
+        p.splits = 1;
+        p.cchunk = cout;
+    }
+    return p;
+}
+static int run_dconv_dgrad_s2(DConvArgs a, int oh, int nclients, void* ws, size_t ws_bytes,
+                              hipStream_t st) {
+    const int sp = 4 * oh * oh;  // dX pixels per image
+    DPlan p = plan_dconv_dgrad_s2(a.M, a.Cr, a.batch, oh, nclients);
+    if (p.splits > 1 && (!ws || ws_bytes < dconv_ws_bytes(p, nclients, a.M, a.batch, sp))) {
+        p.splits = 1;
+        p.cchunk = a.Cr;
+    }
+    a.splits = p.splits;
+    a.cchunk = p.cchunk;
+    a.Nfull = a.batch * sp;
+    a.xcd = g_xcd_remap;
+    float* out = a.out;
+    if (p.splits > 1) a.out = (float*)ws;
+    dim3 grid((unsigned)ceil_div((int64_t)a.batch * oh * oh, 256), (unsigned)ceil_div(a.M, 32),
+              (unsigned)(nclients * p.splits));
+    if (oh == 16) {
+        FH_LAUNCH((dconv_dgrad_s2_kernel<16, 8>), grid, dim3(256), 0, st, a);
+    } else {
+        FH_LAUNCH((dconv_dgrad_s2_kernel<8, 8>), grid, dim3(256), 0, st, a);
+    }
+    FH_LAUNCH_CHECK("conv2d_dgrad direct s2");
+    if (p.splits > 1) {
+        dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
+        FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits, a.M,
+                  a.Nfull, out, a.out_cs, nullptr, (int64_t)0, 0, a.accumulate, a.counts, a.batch,
+                  sp, nullptr, 0, DropArgs{}, BnBwdEpi{});
+        FH_LAUNCH_CHECK("conv2d_dgrad direct s2 epilogue");
+    }
+    return FH_OK;
+}
+
 // ---- direct 3x3 wgrad planning -------------------------------------------
 struct DWPlan {
     int wco, wci, wpx, sr, splits, sps;
@@ -1162,10 +1225,17 @@ extern "C" size_t fh_conv2d_dgrad_workspace(int32_t nclients, int32_t batch, int
     if (dconv_supported(h, w_, kh, kw, stride, pad))
         return dconv_ws_bytes(plan_dconv(cin, cout, batch, h * w_, nclients), nclients, cin, batch,
                               h * w_);
+    size_t direct_s2 = 0;
+    if (dconv_dgrad_s2_supported(h, w_, kh, kw, stride, pad, cin, cout))
+        direct_s2 = dconv_ws_bytes(plan_dconv_dgrad_s2(cin, cout, batch, oh, nclients), nclients,
+                                   cin, batch, h * w_);
     if (dgrad_s2_supported(h, w_, kh, kw, stride, pad) && !g_dgrad_s2_off)
-        return (g_dgrad_s2_pack ? dgrad_s2_pack_bytes(cin, cout, kh, nclients) : 0) +
-               mn_ws_bytes(plan_dgrad_s2(cin, cout, kh, batch, oh, ow, nclients), nclients * 4);
-    return mn_ws_bytes(plan_mn(cin, batch * h * w_, cout * kh * kw, nclients), nclients);
+        return std::max(direct_s2,
+                        (g_dgrad_s2_pack ? dgrad_s2_pack_bytes(cin, cout, kh, nclients) : 0) +
+                            mn_ws_bytes(plan_dgrad_s2(cin, cout, kh, batch, oh, ow, nclients),
+                                        nclients * 4));
+    return std::max(direct_s2,
+                    mn_ws_bytes(plan_mn(cin, batch * h * w_, cout * kh * kw, nclients), nclients));
 }
 
 static int conv2d_fwd_impl(const float* x, int64_t x_cs, const float* in_scale,
@@ -1282,6 +1352,14 @@ extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, i
         d.counts = counts; d.batch = batch; d.Cr = cout; d.M = cin; d.accumulate = accumulate;
         return run_dconv<OP_DGRAD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
                                    "conv2d_dgrad");
+    }
+    if (dconv_dgrad_s2_supported(h, w_, kh, kw, stride, pad, cin, cout) &&
+        (uintptr_t)w % 16 == 0 && w_cs % 4 == 0 && (uintptr_t)dx % 8 == 0 && dx_cs % 2 == 0) {
+        DConvArgs d{};
+        d.in = dy; d.wt = w; d.out = dx;
+        d.in_cs = dy_cs; d.w_cs = w_cs; d.out_cs = dx_cs;
+        d.counts = counts; d.batch = batch; d.Cr = cout; d.M = cin; d.accumulate = accumulate;
+        return run_dconv_dgrad_s2(d, oh, nclients, workspace, ws_bytes, as_stream(stream));
     }
     ConvArgs a = make_args(batch, cin, h, w_, cout, oh, ow, pad, counts);
     a.dy = dy; a.wt = w; a.out = dx;

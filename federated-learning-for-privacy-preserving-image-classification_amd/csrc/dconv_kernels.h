@@ -575,6 +575,211 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// DGRAD of the 3x3 / stride-2 / pad-1 convolution (ResNet down-sampling blocks,
+// models_pytorch.py:176-181) as a direct kernel.  dX pixel (2r+py, 2c+px) receives only
+// the taps with 2r + py + 1 - kh even: kh = 1 for py = 0 (dY row r), kh in {0, 2} for
+// py = 1 (rows r+1 and r), likewise kw / columns.  All four output parity phases therefore
+// read ONE dY patch at the four shifts (dy, dx) in {0,1}^2:
+//   dX[m][2r+py][2c+px] = sum_{ch, (kh,kw) of phase} W[ch][m][kh][kw] dY[ch][r+dy][c+dx]
+// with py = (kh != 1), dy = (kh == 0) and the same for columns.  A workgroup owns 256
+// dY-grid pixels (whole images: WG = 16 one image, WG = 8 four) x 32 dX channels, i.e.
+// 1024 dX pixels; each wave keeps one 32x32 accumulator per (phase, 32-pixel tile) and
+// issues, per channel pair, 18 MFMAs from 9 weight operands and 8 patch operands (all
+// ds_read immediates).  The patch is staged per reduction channel as whole dY images plus
+// a zero bottom row and right column (the +1 shifts past the map read zeros, written once).
+// dX leaves as float2 (phases px = 0, 1 are adjacent).  Split over the reduction channels
+// as dconv_kernel: the slab is laid out as the dX map itself (splitk_epilogue_kernel).
+// (The implicit-GEMM phase path, igemm_kernel<OP_DGRAD_S2>, stays for 1x1 shortcuts and
+// shapes this kernel does not take.)
+template <int WG, int CK>
+__global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs a) {
+    constexpr int HG = WG, HWG = WG * WG;         // dY grid (= the conv's output map)
+    constexpr int WX = 2 * WG, HWX = 4 * HWG;     // dX map
+    constexpr int TR = 256 / WG, NI = TR / HG;    // grid rows / whole images per tile
+    static_assert(TR % HG == 0 && NI >= 1 && WG % 4 == 0, "whole images per tile");
+    constexpr int PRS = HG + 1, PW = WG + 1;      // patch rows per image (+ zero row), pitch
+    constexpr int PR = NI * PRS;
+    constexpr int CSTR = (PR * PW) | 1;           // odd: the two lane halves' channels
+    constexpr int BM = 32, BMP = BM + 1;
+    constexpr int KS = 9 * CK;
+    constexpr int PE = CK * CSTR;
+    constexpr int PQ = WG / 4, RPI = 256 / PQ, NPR = CK * NI * HG;
+    constexpr int NPT = (NPR + RPI - 1) / RPI;
+    constexpr int NAV = (BM * KS / 4 + 255) / 256;
+    constexpr int FN = 2;                         // 64 grid pixels per wave
+    static_assert((CK % 2) == 0, "channel pairs");
+
+    __shared__ float smem[2 * KS * BMP + 2 * PE];
+    float (*As)[KS * BMP] = reinterpret_cast<float (*)[KS * BMP]>(smem);
+    float (*Ps)[PE] = reinterpret_cast<float (*)[PE]>(smem + 2 * KS * BMP);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int bx, by, bz;
+    xcd_block(a.xcd != 0, bx, by, bz);
+    const int z = bz / a.splits;
+    const int split = bz - z * a.splits;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int t = bx, m0 = by * BM;
+    const int n0 = t * 256;
+    if (n0 >= cnt * HWG) return;
+    const int cbeg = split * a.cchunk;
+    const int cend = min(a.Cr, cbeg + a.cchunk);
+    const int M = a.M;
+
+    // zero halo of both buffers: each image's bottom row and every row's right column
+    for (int q = tid; q < 2 * CK * PR; q += 256) {
+        const int bsel = q / (CK * PR), row = q % (CK * PR);
+        float* r = &Ps[bsel][(row / PR) * CSTR + (row % PR) * PW];
+        if ((row % PR) % PRS == HG) {
+#pragma unroll
+            for (int x = 0; x < PW; ++x) r[x] = 0.f;
+        } else {
+            r[WG] = 0.f;
+        }
+    }
+
+    const int img0 = t * NI;
+    const int prt = tid / PQ, px4 = (tid % PQ) * 4;
+    const float* inz = a.in + z * a.in_cs;
+    const float* wz = a.wt + z * a.w_cs;
+    float4 rp[NPT], ra[NAV];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int q = prt + i * RPI;
+            const int cl = q / (NI * HG), rem = q % (NI * HG);
+            const int img = img0 + rem / HG, y = rem % HG;
+            const bool ok = q < NPR && img < cnt && c0 + cl < cend;
+            rp[i] = ok ? *reinterpret_cast<const float4*>(
+                             inz + ((int64_t)(img * a.Cr + c0 + cl) * HG + y) * WG + px4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < NAV; ++i) {  // run of 9*BM floats per ch: W[c0+cl][m0 .. m0+BM)[9]
+            const int f = tid + i * 256;
+            const int cl = f / (BM * 9 / 4), j4 = f % (BM * 9 / 4);
+            ra[i] = (f < BM * KS / 4 && c0 + cl < cend)
+                        ? *reinterpret_cast<const float4*>(wz + ((int64_t)(c0 + cl) * M + m0) * 9 +
+                                                           4 * j4)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int q = prt + i * RPI;
+            if (q < NPR) {
+                const int cl = q / (NI * HG), rem = q % (NI * HG);
+                float* d = &Ps[buf][cl * CSTR + ((rem / HG) * PRS + rem % HG) * PW + px4];
+                d[0] = rp[i].x;
+                d[1] = rp[i].y;
+                d[2] = rp[i].z;
+                d[3] = rp[i].w;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NAV; ++i) {
+            const int f = tid + i * 256;
+            if (f < BM * KS / 4) {
+                const int cl = f / (BM * 9 / 4);
+                const float vv[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = 4 * (f % (BM * 9 / 4)) + u, m = k / 9, r9 = k % 9;
+                    As[buf][(r9 * CK + cl) * BMP + m] = (m0 + m < M) ? vv[u] : 0.f;
+                }
+            }
+        }
+    };
+
+    f32x16 acc[4][FN];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[ph][j][r] = 0.f;
+
+    const int h = lane >> 5, col = lane & 31;
+    const int a_lane = h * BMP + col;
+    int b_lane[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int n = wid * 64 + j * 32 + col;  // local grid pixel
+        const int il = n / HWG, p = n % HWG;
+        b_lane[j] = h * CSTR + (il * PRS + p / WG) * PW + p % WG;
+    }
+
+    if (cbeg < cend) {
+        load(cbeg);
+        store(0);
+        __syncthreads();
+        int buf = 0;
+        for (int c0 = cbeg; c0 < cend; c0 += CK) {
+            const bool more = c0 + CK < cend;
+            if (more) load(c0 + CK);
+            const float* Ab = &As[buf][a_lane];
+            const float* Pb = &Ps[buf][0];
+#pragma unroll
+            for (int cp = 0; cp < CK / 2; ++cp) {
+                float bv[4][FN], av[9];
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        bv[s][j] = Pb[b_lane[j] + 2 * cp * CSTR + (s >> 1) * PW + (s & 1)];
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) av[tap] = Ab[(tap * CK + 2 * cp) * BMP];
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) {
+                    const int kh = tap / 3, kw = tap % 3;
+                    const int ph = (kh != 1) * 2 + (kw != 1), sh = (kh == 0) * 2 + (kw == 0);
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[ph][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tap], bv[sh][j],
+                                                                          acc[ph][j], 0, 0, 0);
+                }
+            }
+            if (more) store(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
+    }
+
+    // ---- epilogue: per lane one grid pixel -> two float2 (px = 0, 1) per channel ----
+    const int rbase = 4 * h;
+    const bool split_out = a.splits > 1;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wid * 64 + j * 32 + col;
+        const int img = n / HWG, p = n % HWG, r = p / WG, c = p % WG;
+        if (img >= cnt) continue;
+#pragma unroll
+        for (int py = 0; py < 2; ++py) {
+            const int po = (2 * r + py) * WX + 2 * c;
+            float* op = split_out ? a.out + ((int64_t)bz * M) * a.Nfull + (int64_t)img * HWX + po
+                                  : a.out + z * a.out_cs + (int64_t)img * M * HWX + po;
+            const int64_t ms = split_out ? (int64_t)a.Nfull : (int64_t)HWX;
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                const int m = m0 + (rr & 3) + 8 * (rr >> 2) + rbase;
+                if (m < M) {
+                    float2 v = make_float2(acc[2 * py][j][rr], acc[2 * py + 1][j][rr]);
+                    float2* q = reinterpret_cast<float2*>(op + (int64_t)m * ms);
+                    if (!split_out && a.accumulate) {
+                        const float2 o = *q;
+                        v.x = o.x + v.x;
+                        v.y = o.y + v.y;
+                    }
+                    *q = v;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // WGRAD: dW[co][ci][kh][kw] = sum_pix dY[co][pix] * X[ci][pix + (kh-1, kw-1)]
 //
 // The reduction runs over pixels, so MFMA lanes must span co (A) and ci (B).

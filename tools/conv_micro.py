@@ -1,0 +1,70 @@
+"""Per-launch conv timing (HIP events, uncontended, eager): python tools/conv_micro.py
+[op:cin:hw:cout:k:s ...] [--clients 32,8,1] [--reps 20].  Prints us / TFLOP/s / frac of the fp32
+MFMA peak per (shape, client count).  Default shapes: the KT and ResNet conv layers."""
+import argparse
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "federated-learning-for-privacy-preserving-image-classification_amd"))
+from fedhip import ops  # noqa: E402
+
+PEAK = 157.3
+DEFAULT = ["wgrad:32:32:32:3:1", "wgrad:64:16:64:3:1", "wgrad:128:8:128:3:1",
+           "fwd:32:32:32:3:1", "dgrad:32:32:32:3:1", "fwd:128:8:128:3:1", "dgrad:128:8:128:3:1",
+           "dgrad:64:32:128:3:2", "dgrad:128:16:256:3:2", "wgrad:64:32:64:3:1",
+           "fwd:64:32:128:1:2", "dgrad:64:32:128:1:2", "wgrad:64:32:128:1:2"]
+
+
+def run(op, cin, hw, cout, k, s, nc, reps, B=32):
+    dev = torch.device("cuda")
+    pad = k // 2
+    oh = (hw + 2 * pad - k) // s + 1
+    x = torch.randn(nc, B, cin, hw, hw, device=dev)
+    w = torch.randn(nc, cout, cin, k, k, device=dev) * 0.05
+    dy = torch.randn(nc, B, cout, oh, oh, device=dev)
+    y = torch.empty(nc, B, cout, oh, oh, device=dev)
+    dx = torch.empty_like(x)
+    dw = torch.empty_like(w)
+    cnt = torch.full((nc,), B, dtype=torch.int32, device=dev)
+
+    def once():
+        if op == "fwd":
+            ops.conv2d_fwd(x, w, None, y, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt)
+        elif op == "dgrad":
+            ops.conv2d_dgrad(dy, w, dx, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt)
+        else:
+            ops.conv2d_wgrad(x, dy, dw, None, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt)
+    for _ in range(3):
+        once()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        once()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000 / reps
+    flops = 2.0 * nc * B * oh * oh * cout * cin * k * k
+    tf = flops / us / 1e6
+    return us, tf
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("shapes", nargs="*")
+    ap.add_argument("--clients", default="32,8,1")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    for sh in a.shapes or DEFAULT:
+        op, cin, hw, cout, k, s = sh.split(":")
+        for nc in [int(v) for v in a.clients.split(",")]:
+            us, tf = run(op, int(cin), int(hw), int(cout), int(k), int(s), nc, a.reps)
+            print(f"{sh:24s} clients {nc:3d}  {us:9.1f} us  {tf:6.1f} TF  frac {tf / PEAK:.3f}",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
