@@ -1085,6 +1085,7 @@ static DPlan plan_dconv_dgrad_s2(int cin, int cout, int batch, int oh, int nclie
 }
 static int run_dconv_dgrad_s2(DConvArgs a, int oh, int nclients, void* ws, size_t ws_bytes,
                               hipStream_t st) {
+    const bool sc = a.in2 != nullptr;
     const int sp = 4 * oh * oh;  // dX pixels per image
     DPlan p = plan_dconv_dgrad_s2(a.M, a.Cr, a.batch, oh, nclients);
     if (p.splits > 1 && (!ws || ws_bytes < dconv_ws_bytes(p, nclients, a.M, a.batch, sp))) {
@@ -1099,10 +1100,14 @@ static int run_dconv_dgrad_s2(DConvArgs a, int oh, int nclients, void* ws, size_
     if (p.splits > 1) a.out = (float*)ws;
     dim3 grid((unsigned)ceil_div((int64_t)a.batch * oh * oh, 256), (unsigned)ceil_div(a.M, 32),
               (unsigned)(nclients * p.splits));
-    if (oh == 16) {
-        FH_LAUNCH((dconv_dgrad_s2_kernel<16, 8>), grid, dim3(256), 0, st, a);
+    if (oh == 16 && sc) {
+        FH_LAUNCH((dconv_dgrad_s2_kernel<16, 8, true>), grid, dim3(256), 0, st, a);
+    } else if (oh == 16) {
+        FH_LAUNCH((dconv_dgrad_s2_kernel<16, 8, false>), grid, dim3(256), 0, st, a);
+    } else if (sc) {
+        FH_LAUNCH((dconv_dgrad_s2_kernel<8, 8, true>), grid, dim3(256), 0, st, a);
     } else {
-        FH_LAUNCH((dconv_dgrad_s2_kernel<8, 8>), grid, dim3(256), 0, st, a);
+        FH_LAUNCH((dconv_dgrad_s2_kernel<8, 8, false>), grid, dim3(256), 0, st, a);
     }
     FH_LAUNCH_CHECK("conv2d_dgrad direct s2");
     if (p.splits > 1) {
@@ -1412,6 +1417,40 @@ extern "C" int fh_conv2d_dgrad_bnstats(const float* dy, int64_t dy_cs, const flo
     d.pscale = 1.0f / (1.0f - p_drop);
     return run_dconv<OP_DGRAD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
                                "conv2d_dgrad_bnstats");
+}
+
+// The DGRAD of a ResNet down-sampling block's input in one launch (models_pytorch.py:176-194:
+// conv1 3x3 / stride 2 / pad 1 and the 1x1 / stride-2 projection shortcut read the same
+// input): dx (=|+=) dgrad3x3(dy, w) + dgrad1x1s2(dy_sc, w_sc).  dy_sc has dy's shape, w_sc is
+// [cout][cin] per client.  Direct stride-2 kernel only (square 32 / 16 maps, cin % 32 == 0,
+// cout % 8 == 0, 16-B aligned weights, 8-B aligned dx rows): FH_E_UNSUPPORTED otherwise.
+// Workspace: fh_conv2d_dgrad_workspace of the 3x3 conv.
+extern "C" int fh_conv2d_dgrad_s2_shortcut(const float* dy, int64_t dy_cs, const float* w,
+                                           int64_t w_cs, const float* dy_sc, int64_t dysc_cs,
+                                           const float* w_sc, int64_t wsc_cs, float* dx,
+                                           int64_t dx_cs, const int32_t* counts,
+                                           int32_t nclients, int32_t batch, int32_t cin,
+                                           int32_t h, int32_t w_, int32_t cout,
+                                           int32_t accumulate, void* workspace, size_t ws_bytes,
+                                           void* stream) {
+    int oh, ow;
+    int rc = conv_common_check(nclients, batch, cin, h, w_, cout, 3, 3, 2, 1, oh, ow);
+    if (rc) return rc;
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(dy && w && dy_sc && w_sc && dx, "conv2d_dgrad_s2_shortcut: null pointer");
+    if (!(dconv_dgrad_s2_supported(h, w_, 3, 3, 2, 1, cin, cout) && (uintptr_t)w % 16 == 0 &&
+          w_cs % 4 == 0 && (uintptr_t)dx % 8 == 0 && dx_cs % 2 == 0 &&
+          (uintptr_t)dy_sc % 16 == 0 && dysc_cs % 4 == 0)) {
+        set_error("conv2d_dgrad_s2_shortcut: outside the direct stride-2 kernel (%dx%d, cin %d, "
+                  "cout %d)", h, w_, cin, cout);
+        return FH_E_UNSUPPORTED;
+    }
+    DConvArgs d{};
+    d.in = dy; d.wt = w; d.out = dx;
+    d.in_cs = dy_cs; d.w_cs = w_cs; d.out_cs = dx_cs;
+    d.in2 = dy_sc; d.wt2 = w_sc; d.in2_cs = dysc_cs; d.w2_cs = wsc_cs;
+    d.counts = counts; d.batch = batch; d.Cr = cout; d.M = cin; d.accumulate = accumulate;
+    return run_dconv_dgrad_s2(d, oh, nclients, workspace, ws_bytes, as_stream(stream));
 }
 
 extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,

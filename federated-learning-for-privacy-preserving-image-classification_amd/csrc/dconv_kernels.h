@@ -67,6 +67,11 @@ struct DConvArgs {
     int64_t pi_cs, pm_cs;
     float pscale;
     int xcd;  // host: XCD-aware workgroup order (xcd_block)
+    // dconv_dgrad_s2_kernel<SC>: the ResNet projection shortcut's 1x1 / stride-2 DGRAD folded
+    // in — dX[m][2r][2c] += sum_ch wt2[ch][m] in2[ch][r][c] (in2 = its output gradient)
+    const float* in2;
+    const float* wt2;
+    int64_t in2_cs, w2_cs;
 };
 
 // Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
@@ -591,7 +596,12 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
 // as dconv_kernel: the slab is laid out as the dX map itself (splitk_epilogue_kernel).
 // (The implicit-GEMM phase path, igemm_kernel<OP_DGRAD_S2>, stays for 1x1 shortcuts and
 // shapes this kernel does not take.)
-template <int WG, int CK>
+// SC: the block's 1x1 / stride-2 projection shortcut (models_pytorch.py:183-187) reads the
+// same input pixels (2r, 2c) = phase (0, 0), so its DGRAD joins that phase's accumulators: one
+// more MFMA per channel pair from the shortcut's output gradient (staged per chunk as the
+// tile's 256 grid pixels) and its 1x1 weights.  The separate launch, its mostly-zero dX write
+// and this kernel's read-modify-write of dX disappear.
+template <int WG, int CK, bool SC>
 __global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs a) {
     constexpr int HG = WG, HWG = WG * WG;         // dY grid (= the conv's output map)
     constexpr int WX = 2 * WG, HWX = 4 * HWG;     // dX map
@@ -608,10 +618,17 @@ __global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs 
     constexpr int NAV = (BM * KS / 4 + 255) / 256;
     constexpr int FN = 2;                         // 64 grid pixels per wave
     static_assert((CK % 2) == 0, "channel pairs");
+    // SC staging: the shortcut gradient [CK][256 (+1 pitch)], its weights [CK][BMP]
+    constexpr int P2STR = 257, P2E = SC ? CK * P2STR : 0, A2E = SC ? CK * BMP : 0;
+    constexpr int NQ2 = SC ? (CK * 64 + 255) / 256 : 0;    // float4 quads per thread
+    constexpr int NA2 = SC ? (CK * BM + 255) / 256 : 0;    // weights per thread
+    static_assert(!SC || (CK * 64) % 256 == 0, "shortcut staging");
 
-    __shared__ float smem[2 * KS * BMP + 2 * PE];
+    __shared__ float smem[2 * KS * BMP + 2 * PE + 2 * P2E + 2 * A2E];
     float (*As)[KS * BMP] = reinterpret_cast<float (*)[KS * BMP]>(smem);
     float (*Ps)[PE] = reinterpret_cast<float (*)[PE]>(smem + 2 * KS * BMP);
+    float* P2s = smem + 2 * KS * BMP + 2 * PE;          // [2][P2E]
+    float* A2s = P2s + 2 * P2E;                         // [2][A2E]
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -644,7 +661,28 @@ __global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs 
     const float* inz = a.in + z * a.in_cs;
     const float* wz = a.wt + z * a.w_cs;
     float4 rp[NPT], ra[NAV];
+    float4 rq[NQ2 > 0 ? NQ2 : 1];
+    float rw[NA2 > 0 ? NA2 : 1];
     auto load = [&](int c0) {
+        if constexpr (SC) {
+            const float* in2z = a.in2 + z * a.in2_cs;
+#pragma unroll
+            for (int i = 0; i < NQ2; ++i) {  // quad f: channel f / 64, tile pixels 4 (f % 64) ..
+                const int f = tid + i * 256, cl = f / 64, n = 4 * (f % 64);
+                const int img = img0 + n / HWG;
+                const bool ok = img < cnt && c0 + cl < cend;
+                rq[i] = ok ? *reinterpret_cast<const float4*>(
+                                 in2z + ((int64_t)img * a.Cr + c0 + cl) * HWG + n % HWG)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            const float* w2z = a.wt2 + z * a.w2_cs;
+#pragma unroll
+            for (int i = 0; i < NA2; ++i) {  // W_sc[c0 + cl][m0 + m] (layout [cout][cin])
+                const int e = tid + i * 256, cl = e / BM, m = e % BM;
+                rw[i] = (e < CK * BM && c0 + cl < cend && m0 + m < M)
+                            ? w2z[(int64_t)(c0 + cl) * M + m0 + m] : 0.f;
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
             const int q = prt + i * RPI;
@@ -666,6 +704,22 @@ __global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs 
         }
     };
     auto store = [&](int buf) {
+        if constexpr (SC) {
+#pragma unroll
+            for (int i = 0; i < NQ2; ++i) {
+                const int f = tid + i * 256;
+                float* d = P2s + buf * P2E + (f / 64) * P2STR + 4 * (f % 64);
+                d[0] = rq[i].x;
+                d[1] = rq[i].y;
+                d[2] = rq[i].z;
+                d[3] = rq[i].w;
+            }
+#pragma unroll
+            for (int i = 0; i < NA2; ++i) {
+                const int e = tid + i * 256;
+                if (e < CK * BM) A2s[buf * A2E + (e / BM) * BMP + e % BM] = rw[i];
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
             const int q = prt + i * RPI;
@@ -721,6 +775,8 @@ __global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs 
             if (more) load(c0 + CK);
             const float* Ab = &As[buf][a_lane];
             const float* Pb = &Ps[buf][0];
+            const float* A2b = A2s + buf * A2E + a_lane;
+            const float* P2b = P2s + buf * P2E + h * P2STR + wid * 64 + col;
 #pragma unroll
             for (int cp = 0; cp < CK / 2; ++cp) {
                 float bv[4][FN], av[9];
@@ -739,6 +795,13 @@ __global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs 
                     for (int j = 0; j < FN; ++j)
                         acc[ph][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tap], bv[sh][j],
                                                                           acc[ph][j], 0, 0, 0);
+                }
+                if constexpr (SC) {  // the shortcut's 1x1: phase (0, 0), shift (0, 0)
+                    const float a2 = A2b[2 * cp * BMP];
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                            a2, P2b[2 * cp * P2STR + j * 32], acc[0][j], 0, 0, 0);
                 }
             }
             if (more) store(buf ^ 1);

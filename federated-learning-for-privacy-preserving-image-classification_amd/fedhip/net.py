@@ -156,6 +156,9 @@ class PackedNet:
         # taken in the epilogue of the next conv's dgrad (fh_conv2d_dgrad_bnstats), so the BN
         # backward is its apply pass only (FH_BN_BWD_EPILOGUE=0: reduce + apply)
         self.bn_bwd_epilogue = os.environ.get("FH_BN_BWD_EPILOGUE", "1") != "0"
+        # ResNet down-sampling blocks: conv1's and the projection shortcut's input gradients
+        # in one direct stride-2 launch (fh_conv2d_dgrad_s2_shortcut; FH_FUSED_SHORTCUT=0: two)
+        self.fused_shortcut = os.environ.get("FH_FUSED_SHORTCUT", "1") != "0"
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -748,6 +751,12 @@ class PackedNet:
                            W(G, f"{pf}.shortcut.1.bias"), n, B, co, ho * ho, relu=False, counts=cnt)
                 ops.conv2d_wgrad(xin, dsc, W(G, f"{pf}.shortcut.0.weight"), None, n, B, ci, hi, hi,
                                  co, 1, s, 0, counts=cnt)
+                # conv1's and the shortcut's input gradients in one launch (direct stride-2
+                # kernel), else the shortcut's dgrad and conv1's accumulated onto it
+                if s == 2 and self.fused_shortcut and ops.conv2d_dgrad_s2_shortcut(
+                        da, W(P_, f"{pf}.conv1.weight"), dsc, W(P_, f"{pf}.shortcut.0.weight"),
+                        din, n, B, ci, hi, hi, co, counts=cnt):
+                    continue
                 ops.conv2d_dgrad(dsc, W(P_, f"{pf}.shortcut.0.weight"), din, n, B, ci, hi, hi, co,
                                  1, s, 0, counts=cnt)
             ops.conv2d_dgrad(da, W(P_, f"{pf}.conv1.weight"), din, n, B, ci, hi, hi, co, 3, s, 1,

@@ -10,6 +10,7 @@ the arithmetic is the kernels'.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -280,6 +281,31 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
              int(accumulate), ptr(ws), nb, stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
     return dx
+
+
+_DCONV_DGRAD_S2 = os.environ.get("FH_DCONV_DGRAD_S2", "1") != "0"
+
+
+def conv2d_dgrad_s2_shortcut(dy, w, dy_sc, w_sc, dx, nclients, batch, cin, h, wd, cout,
+                             counts=None, accumulate=False):
+    """A ResNet down-sampling block's input gradient in one launch: conv2d_dgrad(dy, w)
+    (3x3/s2/p1) + conv2d_dgrad(dy_sc, w_sc) (the 1x1/s2 projection shortcut)
+    (fh_conv2d_dgrad_s2_shortcut).  Returns False (nothing issued) outside the direct
+    stride-2 kernel; the caller then issues the two dgrads."""
+    if not (_DCONV_DGRAD_S2 and h == wd and h in (16, 32) and cin % 32 == 0 and cout % 8 == 0
+            and w.data_ptr() % 16 == 0 and w.stride(0) % 4 == 0 and dx.data_ptr() % 8 == 0
+            and dx.stride(0) % 2 == 0 and dy_sc.data_ptr() % 16 == 0
+            and dy_sc.stride(0) % 4 == 0):
+        return False
+    ws, nb = _ws_for("fh_conv2d_dgrad_workspace", dy.device, nclients, batch, cin, h, wd, cout, 3,
+                     3, 2, 1)
+    ev = PROBE.begin(_conv_tag("dgrad", cin, h, wd, cout, 3, 2) + "+sc")
+    call("fh_conv2d_dgrad_s2_shortcut", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dy_sc), _cs(dy_sc),
+         ptr(w_sc), _cs(w_sc), ptr(dx), _cs(dx), _counts(counts), nclients, batch, cin, h, wd,
+         cout, int(accumulate), ptr(ws), nb, stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, 3, 2, 1) +
+              _conv_flops(nclients, batch, cin, h, wd, cout, 1, 2, 0))
+    return True
 
 
 def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,

@@ -428,6 +428,18 @@ int fh_bn_finalize_tiles(const double* part, const float* gamma, const float* be
                          float* shift_out, int64_t s_cs, const int32_t* counts,
                          int32_t nclients, int32_t batch, int32_t C, int32_t HW, float eps,
                          float momentum, void* stream);
+/* The input gradient of a ResNet down-sampling block in one launch (models_pytorch.py:176-194:
+ * conv1 3x3/s2/p1 and the 1x1/s2 projection shortcut read the same input):
+ * dx (=|+=) dgrad_3x3s2(dy, w) + dgrad_1x1s2(dy_sc, w_sc); dy_sc has dy's shape, w_sc is
+ * [cout][cin] per client.  Replaces the two fh_conv2d_dgrad calls (the second accumulating).
+ * Direct stride-2 kernel only (square 32/16 maps, cin % 32 == 0, cout % 8 == 0, aligned
+ * rows): FH_E_UNSUPPORTED otherwise.  Workspace: fh_conv2d_dgrad_workspace of the 3x3. */
+int fh_conv2d_dgrad_s2_shortcut(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,
+                                const float* dy_sc, int64_t dysc_cs, const float* w_sc,
+                                int64_t wsc_cs, float* dx, int64_t dx_cs, const int32_t* counts,
+                                int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
+                                int32_t cout, int32_t accumulate, void* workspace, size_t ws_bytes,
+                                void* stream);
 /* fh_bn_fwd_train (its apply pass: y = [relu](bn(x) [+ res]), save_mean / save_invstd,
  * running statistics) from the tiles fh_conv2d_fwd_bnstats left — FederatedResNet's stem
  * bn1 and block bn2 + residual + ReLU (models_pytorch.py:189-194, :241-242), whose output the

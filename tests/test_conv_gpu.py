@@ -237,3 +237,46 @@ def test_conv_s2_relu_epilogue(h):
     ops.conv2d_fwd(x, wt, bias, y, C, B, cin, h, h, cout, 3, 2, 1)
     ops.conv2d_fwd(x, wt, bias, y2, C, B, cin, h, h, cout, 3, 2, 1, relu=True)
     assert torch.equal(y2, torch.relu(y))
+
+
+@pytest.mark.parametrize("C,B,cin,h,cout,acc", [(8, 32, 64, 32, 128, False),
+                                                (1, 32, 128, 16, 256, False),
+                                                (3, 19, 32, 16, 48, True),
+                                                (2, 32, 64, 32, 128, True)])
+def test_dgrad_s2_shortcut_exact_integer(C, B, cin, h, cout, acc):
+    """fh_conv2d_dgrad_s2_shortcut (conv1 3x3/s2 and the 1x1/s2 projection shortcut of a
+    ResNet down-sampling block in one launch): small-integer operands, so the result must
+    equal the fp64 sum of both input gradients bit for bit — unsplit grids, the split-K
+    grid (one client), ragged counts, accumulate onto a residual gradient; images past a
+    client's count untouched."""
+    g = torch.Generator().manual_seed(C * 100 + cin)
+    oh = h // 2
+    wt = torch.randint(-2, 3, (C, cout, cin, 3, 3), generator=g).float()
+    wsc = torch.randint(-2, 3, (C, cout, cin, 1, 1), generator=g).float()
+    dy = torch.randint(-2, 3, (C, B, cout, oh, oh), generator=g).float()
+    dsc = torch.randint(-2, 3, (C, B, cout, oh, oh), generator=g).float()
+    base = torch.randint(-3, 4, (C, B, cin, h, h), generator=g).float()
+    counts = torch.tensor([B - (i * 3) % min(B, 7) for i in range(C)], dtype=torch.int32)
+    dx = base.to(DEV) if acc else torch.full((C, B, cin, h, h), 9.0, device=DEV)
+    assert ops.conv2d_dgrad_s2_shortcut(dy.to(DEV), wt.to(DEV), dsc.to(DEV), wsc.to(DEV), dx, C, B,
+                                        cin, h, h, cout, counts=counts.to(DEV), accumulate=acc)
+    torch.cuda.synchronize()
+    for z in range(C):
+        n = int(counts[z])
+        xr = torch.zeros(n, cin, h, h, dtype=torch.float64, requires_grad=True)
+        y = F.conv2d(xr, wt[z].double(), stride=2, padding=1)
+        ysc = F.conv2d(xr, wsc[z].double(), stride=2)
+        (y * dy[z, :n].double()).sum().add((ysc * dsc[z, :n].double()).sum()).backward()
+        ref = xr.grad + (base[z, :n].double() if acc else 0.0)
+        assert torch.equal(dx[z, :n].cpu().double(), ref), f"z={z}"
+        tail = base[z, n:] if acc else torch.full_like(base[z, n:], 9.0)
+        assert torch.equal(dx[z, n:].cpu(), tail)
+
+
+def test_dgrad_s2_shortcut_declines_unsupported():
+    """Outside the direct stride-2 kernel (8x8 map, cin % 32 != 0) the fused entry point
+    issues nothing and returns False (the caller runs the two dgrads)."""
+    z = torch.zeros
+    assert not ops.conv2d_dgrad_s2_shortcut(z(1, 2, 16, 4, 4, device=DEV), z(1, 16, 8, 3, 3, device=DEV),
+                                            z(1, 2, 16, 4, 4, device=DEV), z(1, 16, 8, 1, 1, device=DEV),
+                                            z(1, 2, 8, 8, 8, device=DEV), 1, 2, 8, 8, 8, 16)
