@@ -1120,6 +1120,14 @@ static int run_dconv_dgrad_s2(DConvArgs a, int oh, int nclients, void* ws, size_
     return FH_OK;
 }
 
+// 1x1 / stride 2 / pad 0 forward on square 32->16 and 16->8 maps (the ResNet projection
+// shortcut): pw_s2_fwd_kernel<output width, CK = 16>; FH_PW_S2=0: back to the implicit GEMM
+static const int g_pw_s2_off = env_int("FH_PW_S2", 1) == 0;
+static bool pw_s2_supported(int h, int w, int kh, int kw, int stride, int pad, int cin) {
+    return !g_pw_s2_off && kh == 1 && kw == 1 && stride == 2 && pad == 0 && h == w &&
+           (w == 16 || w == 32) && cin % 16 == 0;
+}
+
 // ---- direct 3x3 wgrad planning -------------------------------------------
 struct DWPlan {
     int wco, wci, wpx, sr, splits, sps;
@@ -1273,6 +1281,20 @@ static int conv2d_fwd_impl(const float* x, int64_t x_cs, const float* in_scale,
         d.counts = counts; d.batch = batch; d.Cr = cin; d.M = cout; d.relu = relu;
         return run_dconv<OP_FWD, 2>(d, ow, nclients, workspace, ws_bytes, oh * ow,
                                     as_stream(stream), "conv2d_fwd_s2");
+    }
+    if (!in_scale && !bn_part && pw_s2_supported(h, w_, kh, kw, stride, pad, cin) &&
+        (uintptr_t)x % 16 == 0 && x_cs % 4 == 0 && (uintptr_t)w % 16 == 0 && w_cs % 4 == 0) {
+        DConvArgs d{};
+        d.in = x; d.wt = w; d.bias = bias; d.out = y;
+        d.in_cs = x_cs; d.w_cs = w_cs; d.b_cs = b_cs; d.out_cs = y_cs;
+        d.counts = counts; d.batch = batch; d.Cr = cin; d.M = cout; d.relu = relu;
+        dim3 grid((unsigned)ceil_div((int64_t)batch * oh * ow, 256), (unsigned)ceil_div(cout, 64),
+                  (unsigned)nclients);
+        hipStream_t st = as_stream(stream);
+        if (ow == 16) FH_LAUNCH((pw_s2_fwd_kernel<16, 16>), grid, dim3(256), 0, st, d);
+        else FH_LAUNCH((pw_s2_fwd_kernel<8, 16>), grid, dim3(256), 0, st, d);
+        FH_LAUNCH_CHECK("conv2d_fwd 1x1 s2");
+        return FH_OK;
     }
     if (in_scale || bn_part) {
         set_error("conv2d_fwd_bnrelu / _bnstats: need the direct 3x3 path (3x3/s1/p1, square "

@@ -843,6 +843,126 @@ __global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs 
 }
 
 // ---------------------------------------------------------------------------
+// 1x1 / stride-2 / pad-0 FORWARD (the ResNet projection shortcut, models_pytorch.py:183-187):
+// Y[m][r][c] = sum_ch W[m][ch] X[ch][2r][2c].  A workgroup owns 256 output pixels (whole
+// images: WO = 16 one, WO = 8 four) x 64 output channels; per chunk of CK input channels it
+// stages the even input rows as float4 runs keeping the even columns (x, z) — Xs[ch][256 +1]
+// — and the weights as float4 runs of W[m][ch..] transposed into Ws[ch][64 +1]; 4 waves =
+// 2 (channels) x 2 (pixel halves), 1 x 4 32x32 accumulators each.  The implicit GEMM
+// gathered every operand with its own address arithmetic (2-4 % of peak); here the X read
+// bounds it.
+template <int WO, int CK>
+__global__ void __launch_bounds__(256) pw_s2_fwd_kernel(const DConvArgs a) {
+    constexpr int HWO = WO * WO, WI = 2 * WO, HI = 2 * WO;
+    constexpr int NI = 256 / HWO;                 // whole output images per tile
+    static_assert(256 % HWO == 0 && WO % 2 == 0, "tile geometry");
+    constexpr int BM = 64, BMP = BM + 1, XP = 257;
+    constexpr int QPC = 128;                      // float4 runs per channel (2 pixels each)
+    constexpr int NQ = CK * QPC / 256, NW = CK * BM / 4 / 256;
+    static_assert(NQ >= 1 && NW >= 1 && (CK * QPC) % 256 == 0 && (CK * BM / 4) % 256 == 0 &&
+                  CK % 4 == 0, "staging");
+    __shared__ float Xs[2][CK * XP];
+    __shared__ float Ws[2][CK * BMP];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int z = blockIdx.z, t = blockIdx.x, m0 = blockIdx.y * BM;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int n0 = t * 256;
+    if (n0 >= cnt * HWO) return;
+    const int M = a.M, Cr = a.Cr;
+    const int img0 = t * NI;
+    const float* xz = a.in + z * a.in_cs;
+    const float* wz = a.wt + z * a.w_cs;
+
+    float4 rx[NQ], rw[NW];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            const int f = tid + i * 256, cl = f / QPC, n = 2 * (f % QPC);  // output pixels n, n+1
+            const int il = n / HWO, p = n % HWO, r = p / WO, c = p % WO;
+            const int img = img0 + il;
+            rx[i] = (img < cnt && c0 + cl < Cr)
+                        ? *reinterpret_cast<const float4*>(
+                              xz + ((int64_t)(img * Cr + c0 + cl) * HI + 2 * r) * WI + 2 * c)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const int f = tid + i * 256, m = f / (CK / 4), j4 = f % (CK / 4);
+            rw[i] = (m0 + m < M && c0 + 4 * j4 < Cr)
+                        ? *reinterpret_cast<const float4*>(wz + (int64_t)(m0 + m) * Cr + c0 + 4 * j4)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            const int f = tid + i * 256;
+            float* d = &Xs[buf][(f / QPC) * XP + 2 * (f % QPC)];
+            d[0] = rx[i].x;
+            d[1] = rx[i].z;
+        }
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const int f = tid + i * 256, m = f / (CK / 4), j4 = f % (CK / 4);
+            Ws[buf][(4 * j4 + 0) * BMP + m] = rw[i].x;
+            Ws[buf][(4 * j4 + 1) * BMP + m] = rw[i].y;
+            Ws[buf][(4 * j4 + 2) * BMP + m] = rw[i].z;
+            Ws[buf][(4 * j4 + 3) * BMP + m] = rw[i].w;
+        }
+    };
+
+    f32x16 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const int h = lane >> 5, col = lane & 31;
+    load(0);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int c0 = 0; c0 < Cr; c0 += CK) {
+        const bool more = c0 + CK < Cr;
+        if (more) load(c0 + CK);
+        const float* Ab = &Ws[buf][h * BMP + wm * 32 + col];
+        const float* Bb = &Xs[buf][h * XP + wn * 128 + col];
+#pragma unroll
+        for (int cp = 0; cp < CK / 2; ++cp) {
+            const float av = Ab[2 * cp * BMP];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, Bb[2 * cp * XP + j * 32], acc[j],
+                                                              0, 0, 0);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+
+    const float* bz = a.bias ? a.bias + z * a.b_cs : nullptr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 128 + j * 32 + col;
+        const int img = n / HWO, p = n % HWO;
+        if (img >= cnt) continue;
+        float* op = a.out + z * a.out_cs + (int64_t)img * M * HWO + p;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (m < M) {
+                float v = acc[j][r];
+                if (bz) v = v + bz[m];
+                if (a.relu) v = fmaxf(v, 0.f);
+                op[(int64_t)m * HWO] = v;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // WGRAD: dW[co][ci][kh][kw] = sum_pix dY[co][pix] * X[ci][pix + (kh-1, kw-1)]
 //
 // The reduction runs over pixels, so MFMA lanes must span co (A) and ci (B).
