@@ -1178,6 +1178,29 @@ static DWPlan plan_dwgrad_small(int cout, int batch, int w, int nclients) {
     return p;
 }
 
+// 3x3 / stride 2 / pad 1 WGRAD on square 32->16 / 16->8 maps (ResNet down-sampling blocks):
+// dconv_wgrad_kernel<output width, WCO = 2, WCI = 1, WPX = 2, 64-pixel stages, S = 2> — 64 x 32
+// (co, ci) tiles, so each staged input patch (2*SEGR+1 rows) feeds twice the MFMAs;
+// FH_DWGRAD_S2=0: back to the implicit GEMM
+static const int g_dwgrad_s2_off = env_int("FH_DWGRAD_S2", 1) == 0;
+static bool dwgrad_s2_supported(int cin, int cout, int h, int w, int kh, int kw, int stride,
+                                int pad) {
+    return !g_dwgrad_s2_off && kh == 3 && kw == 3 && stride == 2 && pad == 1 && h == w &&
+           (w == 16 || w == 32) && cin % 32 == 0 && cout % 64 == 0;
+}
+static DWPlan plan_dwgrad_s2(int cout, int cin, int batch, int wo, int nclients) {
+    DWPlan p{2, 1, 2, 64 / wo, 1, 1};
+    const int64_t tiles = (int64_t)(cout / 64) * (cin / 32) * nclients;
+    const int nst = (int)ceil_div((int64_t)batch * wo * wo, (int64_t)p.sr * wo);
+    const int occ = dwgrad_occ(wo, 2, 1, p.sr, 2);
+    const int want = (int)std::min<int64_t>(
+        std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks * occ), tiles)),
+        std::max(1, nst / kDwgradMinSps));
+    p.sps = (int)ceil_div(nst, want);
+    p.splits = (int)ceil_div(nst, p.sps);
+    return p;
+}
+
 static size_t dwgrad_ws_bytes(const DWPlan& p, int nclients, int M, int N) {
     const size_t wb = (size_t)nclients * p.splits * M * N * sizeof(float);
     return ((wb + 255) / 256) * 256 + (size_t)nclients * p.splits * M * sizeof(float);
@@ -1485,6 +1508,9 @@ extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int
         direct = dwgrad_ws_bytes(plan_dwgrad(cout, cin, batch, w_, nclients), nclients, cout, cin * 9);
     if (dwgrad_small_supported(cin, cout, h, w_, kh, kw, stride, pad))
         direct = dwgrad_ws_bytes(plan_dwgrad_small(cout, batch, w_, nclients), nclients, cout, cin * 9);
+    if (dwgrad_s2_supported(cin, cout, h, w_, kh, kw, stride, pad))
+        direct = dwgrad_ws_bytes(plan_dwgrad_s2(cout, cin, batch, ow, nclients), nclients, cout,
+                                 cin * 9);
     return std::max(direct, wgrad_ws_bytes(plan_wgrad(cout, cin * kh * kw, batch * oh * ow, nclients),
                                            nclients));
 }
@@ -1565,6 +1591,31 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
                            (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
                            (const float*)d.bias_part, db, db_cs, a.M);
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
+        return FH_OK;
+    }
+    if (aligned && !in_scale && dwgrad_s2_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
+        const DWPlan p = plan_dwgrad_s2(cout, cin, batch, ow, nclients);
+        const size_t need = dwgrad_ws_bytes(p, nclients, a.M, a.N);
+        FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
+        DWArgs d{};
+        d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
+        d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
+        d.splits = p.splits; d.stages_per_split = p.sps; d.xcd = g_xcd_remap;
+        d.part = (float*)workspace;
+        const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
+        d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
+        hipStream_t st = as_stream(stream);
+        dim3 grid((unsigned)p.splits, (unsigned)((cout / 64) * (cin / 32)), (unsigned)nclients);
+        if (ow == 16) FH_LAUNCH((dconv_wgrad_kernel<16, 2, 1, 2, 4, 2>), grid, dim3(256), 0, st, d);
+        else FH_LAUNCH((dconv_wgrad_kernel<8, 2, 1, 2, 8, 2>), grid, dim3(256), 0, st, d);
+        FH_LAUNCH_CHECK("conv2d_wgrad direct s2");
+        const int MN = a.M * a.N;
+        const int wblocks = (int)ceil_div(MN, 64);
+        const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
+        FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+                  (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
+                  (const float*)d.bias_part, db, db_cs, a.M);
+        FH_LAUNCH_CHECK("conv2d_wgrad s2 reduce");
         return FH_OK;
     }
     Plan p = plan_wgrad(a.M, a.N, a.K, nclients);

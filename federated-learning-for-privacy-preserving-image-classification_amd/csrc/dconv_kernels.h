@@ -995,34 +995,40 @@ struct DWArgs {
 // then ask the allocator for two waves per SIMD (144 accumulator AGPRs + <= 112 VGPRs),
 // so one workgroup's staging + barrier overlaps the other's MFMAs.
 // (host planner: the same formula picks the workgroup target, conv.hip plan_dwgrad)
-constexpr int dwgrad_occ(int W, int WCO, int WCI, int SR) {
+// S = 2: the 3x3 / stride-2 / pad-1 convolution of the ResNet down-sampling blocks (W = the
+// OUTPUT width): a stage's patch is the 2*SEGR+1 input rows its output rows read, 2W+2 wide
+// with the halo, and a lane's operand address strides by 2 (pixel pair -> columns 2c, 2c+2).
+constexpr int dwgrad_occ(int W, int WCO, int WCI, int SR, int S = 1) {
     const int SEGR = SR < W ? SR : W, NI = SR / SEGR;
-    const int PR = NI * (SEGR + 2), CSTR = (PR * (W + 2)) | 1;
+    const int PR = NI * (S == 1 ? SEGR + 2 : 2 * SEGR + 1), CSTR = (PR * (S * W + 2)) | 1;
     const int bytes = 4 * 2 * (SR * W * (32 * WCO + 1) + 32 * WCI * CSTR);
     return 2 * bytes <= 160 * 1024 ? 2 : 1;
 }
-template <int W, int WCO, int WCI, int SR>
+template <int W, int WCO, int WCI, int SR, int S>
 constexpr int dwgrad_occupancy() {
-    constexpr int occ = dwgrad_occ(W, WCO, WCI, SR);
+    constexpr int occ = dwgrad_occ(W, WCO, WCI, SR, S);
     return occ;
 }
 
-template <int W, int WCO, int WCI, int WPX, int SR>
-__global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR>())) dconv_wgrad_kernel(const DWArgs a) {
-    constexpr int H = W, HW = H * W;
+template <int W, int WCO, int WCI, int WPX, int SR, int S = 1>
+__global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>())) dconv_wgrad_kernel(const DWArgs a) {
+    constexpr int H = W, HW = H * W;                // output map
+    constexpr int WI = S * W, HI = S * H;           // input map
     constexpr int SPX = SR * W;                     // pixels per stage
     constexpr int SEGR = SR < H ? SR : H;
     constexpr int NI = SR / SEGR;
-    constexpr int PW = W + 2, PR = NI * (SEGR + 2);
+    constexpr int PRS = S == 1 ? SEGR + 2 : 2 * SEGR + 1;  // patch rows per image segment
+    constexpr int PW = WI + 2, PR = NI * PRS;
     constexpr int CSTR = (PR * PW) | 1;
     constexpr int BM = 32 * WCO, BN = 32 * WCI;
     constexpr int BMP = BM + 1;
     constexpr int RPW = SR / WPX;                   // rows per wave per stage
     // staging with float4 global loads: dY rows of SPX pixels, patch rows of W pixels
     constexpr int DQ = SPX / 4, COI = 256 / DQ, NDY = BM / COI;
-    constexpr int PQ = W / 4, RPI = 256 / PQ, NPR = BN * PR, NPT = (NPR + RPI - 1) / RPI;
+    constexpr int PQ = WI / 4, RPI = 256 / PQ, NPR = BN * PR, NPT = (NPR + RPI - 1) / RPI;
     constexpr int DSZ = SPX * BMP, PSZ = BN * CSTR, BUF = DSZ + PSZ;
     static_assert(WCO * WCI * WPX == 4 && RPW >= 1 && SR % WPX == 0, "wave grid");
+    static_assert(S == 1 || S == 2, "stride");
     static_assert(BM % COI == 0 && (SR % H == 0 || H % SR == 0), "stage geometry");
 
     __shared__ float smem[2 * BUF];   // double-buffered [Dys | Ps]
@@ -1048,7 +1054,7 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR>())) dc
         const int bsel = q / NPR, row = q % NPR, cl = row / PR, pr = row % PR;
         float* r = smem + bsel * BUF + DSZ + cl * CSTR + pr * PW;
         r[0] = 0.f;
-        r[W + 1] = 0.f;
+        r[WI + 1] = 0.f;
     }
 
     const int dco = tid / DQ, dp = (tid % DQ) * 4;      // dY: channel row, pixel quad
@@ -1071,11 +1077,11 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR>())) dc
         for (int i = 0; i < NPT; ++i) {
             const int q = prt + i * RPI;
             const int cl = q / PR, pr = q % PR;
-            const int seg = pr / (SEGR + 2), rr = pr % (SEGR + 2);
-            const int img = img0 + seg, y = y0 + rr - 1;
-            const bool ok = q < NPR && img < cnt && (unsigned)y < (unsigned)H;
+            const int seg = pr / PRS, rr = pr % PRS;
+            const int img = img0 + seg, y = S * y0 + rr - 1;
+            const bool ok = q < NPR && img < cnt && (unsigned)y < (unsigned)HI;
             rp[i] = ok ? *reinterpret_cast<const float4*>(
-                             xz + ((int64_t)(img * a.cin + ci0 + cl) * H + y) * W + px)
+                             xz + ((int64_t)(img * a.cin + ci0 + cl) * HI + y) * WI + px)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
             if (a.in_scale != nullptr) {  // applied in store() (loads stay in flight)
                 bsc[i] = ok ? a.in_scale[z * a.aff_cs + ci0 + cl] : 1.f;
@@ -1117,7 +1123,7 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR>())) dc
 
     const int h = lane >> 5, col = lane & 31;
     const int a_off = h * BMP + wco * 32 + col;
-    const int b_off = DSZ + (wci * 32 + col) * CSTR + h;
+    const int b_off = DSZ + (wci * 32 + col) * CSTR + S * h;
     if (sbeg < send) {
         load(sbeg);
         store(0);
@@ -1131,7 +1137,7 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR>())) dc
 #pragma unroll 1
             for (int rr = 0; rr < RPW; ++rr) {
                 const int r = wpx * RPW + rr;                  // stage row
-                const int prow = (r / SEGR) * (SEGR + 2) + r % SEGR;
+                const int prow = (r / SEGR) * PRS + S * (r % SEGR);
                 const float* Ar = Al + r * W * BMP;
                 const float* Br = Bl + prow * PW;
 #pragma unroll 4
@@ -1140,7 +1146,7 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR>())) dc
                     bsum += av;
                     float bv[9];
 #pragma unroll
-                    for (int s = 0; s < 9; ++s) bv[s] = Br[(s / 3) * PW + 2 * cp + (s % 3)];
+                    for (int s = 0; s < 9; ++s) bv[s] = Br[(s / 3) * PW + S * 2 * cp + (s % 3)];
 #pragma unroll
                     for (int s = 0; s < 9; ++s)
                         acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[s], acc[s], 0, 0, 0);
