@@ -1796,6 +1796,7 @@ __device__ __forceinline__ void linear_wgrad_skinny_body(
     const int m0 = mblock * 32;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int k0 = kblock * 128 + wid * 32;
+    if (k0 >= K) return;  // K % 128 != 0 (K % 32 == 0): the last block's spare waves
     const int cnt = counts ? counts[z] : batch;
     const int r32 = lane & 31, h = lane >> 5;
     const bool mok = m0 + r32 < M;
@@ -1856,7 +1857,7 @@ linear_bwd_fused_kernel(const float* __restrict__ X, int64_t x_cs, const float* 
     __shared__ float red[16 * 64 * KT];
     const int z = blockIdx.y, bx = blockIdx.x;
     if (bx < nw) {
-        const int kt = K / 128;
+        const int kt = (K + 127) / 128;
         linear_wgrad_skinny_body(X, x_cs, dY, dy_cs, dW, dw_cs, db, db_cs, counts, batch, K, M,
                                  z, bx % kt, bx / kt);
     } else {
@@ -1956,26 +1957,32 @@ extern "C" int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_bwd_fused: p=%g", p_drop);
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && dy && w && dw && dx, "linear_bwd_fused: null pointer");
-    if (!(batch <= 32 && in_f % 128 == 0 && out_f % 32 == 0 && skinny_aligned(dy, dy_cs) &&
+    if (!(batch <= 32 && in_f % 32 == 0 && out_f % 32 == 0 && skinny_aligned(dy, dy_cs) &&
           w_cs % 4 == 0)) {
-        set_error("linear_bwd_fused: needs batch <= 32, in_f %% 128 == 0, out_f %% 32 == 0 and "
+        set_error("linear_bwd_fused: needs batch <= 32, in_f %% 32 == 0, out_f %% 32 == 0 and "
                   "aligned dY (got %d, %d, %d)", batch, in_f, out_f);
         return FH_E_UNSUPPORTED;
     }
     const SkinnyBwdEpi ep{mask, m_cs, 1.0f / (1.0f - p_drop), relu_ref, r_cs};
-    const int nw = (in_f / 128) * (int)ceil_div(out_f, 32);
-    if (kLinearSkinny != 2 && (int64_t)(in_f / 128) * nclients >= fill(256)) {
+    const int kb = (int)ceil_div(in_f, 128);  // WGRAD k-blocks (spare waves return)
+    const int nw = kb * (int)ceil_div(out_f, 32);
+    if (kLinearSkinny != 2 && (int64_t)kb * nclients >= fill(256)) {
         // wide launches: the two roles as two kernels — in one grid every WGRAD workgroup
         // would carry the DGRAD role's 48 KB of LDS and stream dW at 3 workgroups per CU
         // (fc1 at 32 clients: 190 us fused vs ~105 us as two launches)
         FH_LAUNCH(linear_wgrad_skinny_kernel,
-                  dim3((unsigned)(in_f / 128), (unsigned)ceil_div(out_f, 32), nclients),
+                  dim3((unsigned)kb, (unsigned)ceil_div(out_f, 32), nclients),
                   dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
                   counts, batch, in_f, out_f);
         FH_LAUNCH_CHECK("linear_bwd_fused wgrad");
-        FH_LAUNCH(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
-                  dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs, counts, batch,
-                  in_f, out_f, ep);
+        if (in_f % 128 == 0)
+            FH_LAUNCH(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
+                      dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs, counts,
+                      batch, in_f, out_f, ep);
+        else  // SimpleCNN fc1 (3136 = 98 x 32): one 32-feature tile per workgroup
+            FH_LAUNCH(linear_dgrad_skinny_kernel<1>, dim3((unsigned)(in_f / 32), nclients),
+                      dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs, counts,
+                      batch, in_f, out_f, ep);
     } else
         FH_LAUNCH(linear_bwd_fused_kernel<1>, dim3((unsigned)(nw + in_f / 32), nclients),
                   dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, w, w_cs, dw, dw_cs, db,
@@ -1993,10 +2000,10 @@ extern "C" int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, in
                                float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
                                size_t ws_bytes, const int32_t* counts, int32_t nclients,
                                int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
-    if (kLinearSkinny && nclients > 0 && batch <= 32 && in_f % 128 == 0 && out_f > 0 && x &&
+    if (kLinearSkinny && nclients > 0 && batch <= 32 && in_f % 32 == 0 && out_f > 0 && x &&
         dy && dw) {
         FH_LAUNCH(linear_wgrad_skinny_kernel,
-                           dim3((unsigned)(in_f / 128), (unsigned)ceil_div(out_f, 32), nclients),
+                           dim3((unsigned)ceil_div(in_f, 128), (unsigned)ceil_div(out_f, 32), nclients),
                            dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
                            counts, batch, in_f, out_f);
         FH_LAUNCH_CHECK("linear_wgrad skinny");

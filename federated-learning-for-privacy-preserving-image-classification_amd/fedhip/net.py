@@ -298,10 +298,13 @@ class PackedNet:
             mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
             ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
                             relu_out=self._fc_in, counts=cnt)
-        ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136,
-                         128, counts=cnt)
         dp2 = A("dp2", 64, 7, 7)
-        ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
+        if not (self.fused_linear_bwd and ops.linear_bwd_fused(
+                A("p2", 64, 7, 7), dh1, W(P_, "fc1.weight"), W(G, "fc1.weight"),
+                W(G, "fc1.bias"), dp2, n, B, 3136, 128, counts=cnt)):
+            ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B,
+                             3136, 128, counts=cnt)
+            ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
         p1, a2, da2, dp1, hp = self._simple_maps()
         ops.maxpool2_bwd(dp2, A("i2", 64, 7, 7, dtype=torch.uint8), da2, n, B, 64, 14, 14,
                          xin=a2, counts=cnt)

@@ -100,7 +100,12 @@ def test_head_matches_separate_ops(nc, F, K, p):
 @pytest.mark.parametrize("nc,in_f,out_f,p,relu", [(3, 512, 256, 0.3, True),
                                                   (32, 2048, 512, 0.0, False),
                                                   (1, 2048, 512, 0.0, False),
-                                                  (7, 512, 256, 0.5, True)])
+                                                  (7, 512, 256, 0.5, True),
+                                                  # SimpleCNN fc1 (3136 = 24.5 x 128): the
+                                                  # last WGRAD block's spare waves, one-tile
+                                                  # DGRAD; fused grid and the wide two-launch
+                                                  (3, 3136, 128, 0.0, False),
+                                                  (32, 3136, 128, 0.0, False)])
 def test_linear_bwd_fused_bit_identical(nc, in_f, out_f, p, relu):
     """One launch == linear_wgrad + linear_dgrad + dropout_bwd, bit for bit (same MFMA
     bodies; the ReLU decided on the dropped input e equals the one on h where kept)."""
@@ -132,11 +137,11 @@ def test_linear_bwd_fused_bit_identical(nc, in_f, out_f, p, relu):
 
 
 def test_linear_bwd_fused_declines_unsupported_shapes():
-    x = torch.zeros(1, 32, 3136, device=DEV)  # SimpleCNN fc1: in_f % 128 != 0
+    x = torch.zeros(1, 32, 100, device=DEV)  # in_f % 32 != 0
     dy = torch.zeros(1, 32, 128, device=DEV)
-    w = torch.zeros(1, 128, 3136, device=DEV)
-    assert not ops.linear_bwd_fused(x, dy, w, torch.zeros(1, 128, 3136, device=DEV), None,
-                                    torch.zeros_like(x), 1, 32, 3136, 128)
+    w = torch.zeros(1, 128, 100, device=DEV)
+    assert not ops.linear_bwd_fused(x, dy, w, torch.zeros(1, 128, 100, device=DEV), None,
+                                    torch.zeros_like(x), 1, 32, 100, 128)
 
 
 @pytest.mark.parametrize("nc,in_f,out_f", [(1, 2048, 512), (32, 2048, 512), (5, 512, 256),
