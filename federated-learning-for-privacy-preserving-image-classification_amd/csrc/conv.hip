@@ -917,6 +917,10 @@ static const int kDconvBlocks = env_int("FH_DCONV_BLOCKS", 512);
 static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 64);
 static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 256);
 static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 4);
+// ... or, from this many clients on the ResNet shapes, one wave per 32x32 of a 64x64 (co, ci)
+// tile: faster per launch at 16 clients, but neutral per round (K4 +0.5 %, K5 -0.3 %,
+// interleaved x3, profiles/r02_wide) — off unless FH_DWGRAD_WIDE_MIN is set (e.g. 8)
+static const int kDwgradWideMin = env_int("FH_DWGRAD_WIDE_MIN", 1 << 30);
 // RGB-layer wgrad target: 512 workgroups (42 -> 34 us at 32 clients, profiles/r01_v12)
 static const int kDwgradSmallBlocks = env_int("FH_DWGRAD_SMALL_BLOCKS", 512);
 static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 2);  // tools/tail_sweep.py
@@ -1140,7 +1144,13 @@ static bool dwgrad_supported(int cin, int cout, int h, int w, int kh, int kw, in
 static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     DWPlan p{1, 1, 4, 128 / w, 1, 1};
     const bool co64 = cout % 64 == 0, ci64 = cin % 64 == 0;
-    if (kDwgradWpx == 4) p = {1, 1, 4, 128 / w, 1, 1};
+    // many clients on the ResNet shapes (64 ch at 32x32, 256 ch at 8x8): 64x64 tiles, each
+    // staged byte feeding 2x the MFMAs (tools/wpx_sweep.sh at 16 clients: 256ch 8x8 420 -> 359
+    // us, 64ch 32x32 398 -> 371 us; 128ch 16x16 / 8x8 lose, and KT lost 0.6 % with them)
+    const bool wide_shape = w == 32 || (cin >= 256 && cout >= 256);
+    if (kDwgradWpx == 4 && co64 && ci64 && wide_shape && nclients >= kDwgradWideMin)
+        p = {2, 2, 1, 64 / w, 1, 1};
+    else if (kDwgradWpx == 4) p = {1, 1, 4, 128 / w, 1, 1};
     else if (kDwgradWpx == 2 && co64) p = {2, 1, 2, 128 / w, 1, 1};
     else if (kDwgradWpx == 2 && ci64) p = {1, 2, 2, 128 / w, 1, 1};
     else if (co64 && ci64) p = {2, 2, 1, 64 / w, 1, 1};
