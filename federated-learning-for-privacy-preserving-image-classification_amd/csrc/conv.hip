@@ -1697,6 +1697,9 @@ extern "C" int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float*
 // stays on the implicit GEMM.
 namespace fh {
 static const int kLinearSkinny = env_int("FH_LINEAR_SKINNY", 1);
+// A/B: FH_SKINNY32=0 keeps the skinny WGRAD / fused linear backward to in_f % 128 == 0 (the
+// SimpleCNN fc1 WGRAD then runs on the implicit GEMM)
+static const int kSkinny32 = env_int("FH_SKINNY32", 1);
 
 __device__ __forceinline__ float f4at(const float4& v, int q) {
     return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
@@ -1967,8 +1970,8 @@ extern "C" int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_bwd_fused: p=%g", p_drop);
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && dy && w && dw && dx, "linear_bwd_fused: null pointer");
-    if (!(batch <= 32 && in_f % 32 == 0 && out_f % 32 == 0 && skinny_aligned(dy, dy_cs) &&
-          w_cs % 4 == 0)) {
+    if (!(batch <= 32 && in_f % (kSkinny32 ? 32 : 128) == 0 && out_f % 32 == 0 &&
+          skinny_aligned(dy, dy_cs) && w_cs % 4 == 0)) {
         set_error("linear_bwd_fused: needs batch <= 32, in_f %% 32 == 0, out_f %% 32 == 0 and "
                   "aligned dY (got %d, %d, %d)", batch, in_f, out_f);
         return FH_E_UNSUPPORTED;
@@ -2010,8 +2013,8 @@ extern "C" int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, in
                                float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
                                size_t ws_bytes, const int32_t* counts, int32_t nclients,
                                int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
-    if (kLinearSkinny && nclients > 0 && batch <= 32 && in_f % 32 == 0 && out_f > 0 && x &&
-        dy && dw) {
+    if (kLinearSkinny && nclients > 0 && batch <= 32 && in_f % (kSkinny32 ? 32 : 128) == 0 &&
+        out_f > 0 && x && dy && dw) {
         FH_LAUNCH(linear_wgrad_skinny_kernel,
                            dim3((unsigned)ceil_div(in_f, 128), (unsigned)ceil_div(out_f, 32), nclients),
                            dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,

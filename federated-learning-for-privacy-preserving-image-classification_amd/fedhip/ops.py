@@ -379,12 +379,15 @@ def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
 
 
 # ------------------------------------------------------------------ DP-SGD (per-sample clip)
+_SKINNY_IN = 32 if os.environ.get("FH_SKINNY32", "1") != "0" else 128
+
+
 def linear_bwd_fused(x, dy, w, dw, db, dx, nclients, batch, in_f, out_f, mask=None, p_drop=0.0,
                      relu_ref=None, counts=None):
     """linear_wgrad + linear_dgrad + dropout_bwd(dx, mask, relu_out) in one launch
     (fh_linear_bwd_fused).  Returns False (nothing issued) when the shape is outside the
     fused kernel (the caller then issues the three ops)."""
-    if not (batch <= 32 and in_f % 32 == 0 and out_f % 32 == 0 and dy.data_ptr() % 16 == 0
+    if not (batch <= 32 and in_f % _SKINNY_IN == 0 and out_f % 32 == 0 and dy.data_ptr() % 16 == 0
             and dy.stride(0) % 4 == 0 and w.stride(0) % 4 == 0):
         return False
     if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
