@@ -626,6 +626,126 @@ splitk_epilogue_s2_kernel(const float* __restrict__ part, int splits, int M, int
 }
 
 // ---------------------------------------------------------------------------
+// Single-input-channel 3x3 / stride 1 / pad 1 convolution (SimpleCNN conv1 on 28x28 MNIST
+// maps, models_pytorch.py:66-70) — K = 9, so an implicit GEMM spends its time on operand
+// gathers and a 16-deep k tile that is mostly zeros.  FWD: one thread per output pixel, its
+// 9 input taps in registers, the COUT x 9 weights + bias in LDS; y stores coalesced per
+// channel (the layer is bound by writing y).  WGRAD: a block = 8 output channels x a chunk of
+// the client's pixels, each thread 8 x 9 tap products + 8 bias terms in registers, a fixed-
+// order wave / block reduction into a per-chunk slab reduced by splitk_sum_kernel.
+constexpr int kC1Chunk = 2048;  // WGRAD pixels per block (8 per thread, loads 4 pixels ahead)
+
+template <int COUT>
+__global__ void __launch_bounds__(256)
+conv_c1_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ w,
+                   int64_t w_cs, const float* __restrict__ bias, int64_t b_cs,
+                   float* __restrict__ y, int64_t y_cs, const int32_t* __restrict__ counts,
+                   int batch, int H, int W, int relu) {
+    __shared__ float ws[COUT * 9], bs[COUT];
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    for (int i = threadIdx.x; i < COUT * 9; i += 256) ws[i] = w[z * w_cs + i];
+    for (int i = threadIdx.x; i < COUT; i += 256) bs[i] = bias ? bias[z * b_cs + i] : 0.f;
+    __syncthreads();
+    const int HW = H * W;
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= cnt * HW) return;
+    const int img = n / HW, p = n - img * HW, r = p / W, c = p - r * W;
+    const float* xi = x + z * x_cs + (int64_t)img * HW;
+    float t[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            const int yy = r + kh - 1, xx = c + kw - 1;
+            t[kh * 3 + kw] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                                 ? xi[yy * W + xx] : 0.f;
+        }
+    float* yo = y + z * y_cs + (int64_t)img * COUT * HW + p;
+#pragma unroll 4
+    for (int co = 0; co < COUT; ++co) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) v = fmaf(ws[co * 9 + k], t[k], v);
+        v = v + bs[co];
+        if (relu) v = fmaxf(v, 0.f);
+        yo[(int64_t)co * HW] = v;
+    }
+}
+
+// part[z][chunk][co*9 + k], bpart[z][chunk][co]  (dwgrad_ws_bytes layout, splits = chunks)
+__global__ void __launch_bounds__(256)
+conv_c1_wgrad_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ dy,
+                     int64_t dy_cs, float* __restrict__ part, float* __restrict__ bpart,
+                     const int32_t* __restrict__ counts, int batch, int H, int W, int cout,
+                     int nchunks) {
+    __shared__ float red[4][8 * 10];
+    const int chunk = blockIdx.x, cg = blockIdx.y, z = blockIdx.z;
+    const int cnt = counts ? counts[z] : batch;
+    const int HW = H * W;
+    const int n0 = chunk * kC1Chunk, n1 = min(cnt * HW, n0 + kC1Chunk);
+    float acc[8][10];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 10; ++k) acc[j][k] = 0.f;
+    const float* xz = x + z * x_cs;
+    const float* dz = dy + z * dy_cs + (int64_t)cg * 8 * HW;
+    // four pixels per pass, all their loads issued before the FMAs (the loop is bound by load
+    // latency, not by the 80 FMAs a pixel costs); pixels past the chunk contribute zeros
+    constexpr int U = 4;
+    for (int nb = n0 + threadIdx.x; nb < n1; nb += U * 256) {
+        float t[U][9], g[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int n = nb + u * 256;
+            const bool ok = n < n1;
+            const int nn = ok ? n : n0;
+            const int img = nn / HW, p = nn - img * HW, r = p / W, c = p - r * W;
+            const float* xi = xz + (int64_t)img * HW;
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    const int yy = r + kh - 1, xx = c + kw - 1;
+                    t[u][kh * 3 + kw] =
+                        (ok && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                            ? xi[yy * W + xx] : 0.f;
+                }
+            const float* di = dz + (int64_t)img * cout * HW + p;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[u][j] = ok ? di[(int64_t)j * HW] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) acc[j][k] = fmaf(g[u][j], t[u][k], acc[j][k]);
+                acc[j][9] += g[u][j];
+            }
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            const float v = wave_sum(acc[j][k]);
+            if (lane == 0) red[wid][j * 10 + k] = v;
+        }
+    __syncthreads();
+    if (threadIdx.x < 80) {
+        const int j = threadIdx.x / 10, k = threadIdx.x % 10;
+        const float v = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                        (red[2][threadIdx.x] + red[3][threadIdx.x]);
+        const int co = cg * 8 + j;
+        const int64_t slab = (int64_t)z * nchunks + chunk;
+        if (k < 9) part[slab * cout * 9 + co * 9 + k] = v;
+        else if (bpart) bpart[slab * cout + co] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
 struct Tile {
@@ -1211,6 +1331,17 @@ static DWPlan plan_dwgrad_s2(int cout, int cin, int batch, int wo, int nclients)
     return p;
 }
 
+// single-input-channel 3x3 / s1 / p1 (SimpleCNN conv1): conv_c1_fwd_kernel / conv_c1_wgrad_kernel;
+// FH_CONV_C1=0: back to the implicit GEMM
+static const int g_conv_c1_off = env_int("FH_CONV_C1", 1) == 0;
+static bool conv_c1_supported(int cin, int cout, int kh, int kw, int stride, int pad) {
+    return !g_conv_c1_off && cin == 1 && kh == 3 && kw == 3 && stride == 1 && pad == 1 &&
+           (cout == 32 || cout == 64);
+}
+static int conv_c1_chunks(int batch, int h, int w) {
+    return (int)ceil_div((int64_t)batch * h * w, kC1Chunk);
+}
+
 static size_t dwgrad_ws_bytes(const DWPlan& p, int nclients, int M, int N) {
     const size_t wb = (size_t)nclients * p.splits * M * N * sizeof(float);
     return ((wb + 255) / 256) * 256 + (size_t)nclients * p.splits * M * sizeof(float);
@@ -1306,6 +1437,18 @@ static int conv2d_fwd_impl(const float* x, int64_t x_cs, const float* in_scale,
         d.bn_part = bn_part; d.bn_tiles = (int)ceil_div((int64_t)batch * h * w_, 256);
         return run_dconv<OP_FWD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
                                  "conv2d_fwd");
+    }
+    if (!in_scale && !bn_part && conv_c1_supported(cin, cout, kh, kw, stride, pad)) {
+        dim3 grid((unsigned)ceil_div((int64_t)batch * h * w_, 256), (unsigned)nclients);
+        hipStream_t st = as_stream(stream);
+        if (cout == 32)
+            FH_LAUNCH(conv_c1_fwd_kernel<32>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
+                      b_cs, y, y_cs, counts, batch, h, w_, relu);
+        else
+            FH_LAUNCH(conv_c1_fwd_kernel<64>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
+                      b_cs, y, y_cs, counts, batch, h, w_, relu);
+        FH_LAUNCH_CHECK("conv2d_fwd c1");
+        return FH_OK;
     }
     if (!in_scale && !bn_part && dconv_s2_supported(h, w_, kh, kw, stride, pad)) {
         DConvArgs d{};
@@ -1521,6 +1664,10 @@ extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int
     if (dwgrad_s2_supported(cin, cout, h, w_, kh, kw, stride, pad))
         direct = dwgrad_ws_bytes(plan_dwgrad_s2(cout, cin, batch, ow, nclients), nclients, cout,
                                  cin * 9);
+    if (conv_c1_supported(cin, cout, kh, kw, stride, pad)) {
+        DWPlan p{1, 1, 1, 1, conv_c1_chunks(batch, h, w_), 1};
+        direct = dwgrad_ws_bytes(p, nclients, cout, 9);
+    }
     return std::max(direct, wgrad_ws_bytes(plan_wgrad(cout, cin * kh * kw, batch * oh * ow, nclients),
                                            nclients));
 }
@@ -1547,6 +1694,28 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
     if (in_scale && !(aligned && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad))) {
         set_error("conv2d_wgrad_bnrelu: needs the direct 3x3 wgrad (16-B aligned, channels %% 32)");
         return FH_E_UNSUPPORTED;
+    }
+    if (!in_scale && conv_c1_supported(cin, cout, kh, kw, stride, pad)) {
+        DWPlan p{1, 1, 1, 1, conv_c1_chunks(batch, h, w_), 1};
+        const size_t need = dwgrad_ws_bytes(p, nclients, cout, 9);
+        FH_REQUIRE(workspace && ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes,
+                   need);
+        float* part = (float*)workspace;
+        const size_t wbytes = ((size_t)nclients * p.splits * cout * 9 * sizeof(float) + 255) / 256 * 256;
+        float* bpart = db ? (float*)((char*)workspace + wbytes) : nullptr;
+        hipStream_t st = as_stream(stream);
+        FH_LAUNCH(conv_c1_wgrad_kernel, dim3((unsigned)p.splits, (unsigned)(cout / 8), nclients),
+                  dim3(256), 0, st, x, x_cs, dy, dy_cs, part, bpart, counts, batch, h, w_, cout,
+                  p.splits);
+        FH_LAUNCH_CHECK("conv2d_wgrad c1");
+        const int MN = cout * 9;
+        const int wblocks = (int)ceil_div(MN, 64);
+        const int bblocks = db ? (int)ceil_div(cout, 64) : 0;
+        FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+                  (const float*)part, dw, dw_cs, p.splits, MN, wblocks, (const float*)bpart, db,
+                  db_cs, cout);
+        FH_LAUNCH_CHECK("conv2d_wgrad c1 reduce");
+        return FH_OK;
     }
     if (aligned && dwgrad_small_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
         const DWPlan p = plan_dwgrad_small(cout, batch, w_, nclients);

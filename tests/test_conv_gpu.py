@@ -183,6 +183,11 @@ EXACT = [  # nclients, batch, cin, h, cout, k, stride, pad (square maps)
     (2, 17, 32, 16, 48, 3, 2, 1),
     (2, 8, 6, 16, 40, 3, 2, 1),
     (1, 5, 6, 32, 32, 3, 2, 1),
+    # single input channel (SimpleCNN conv1 on 28x28 MNIST maps): direct c1 FWD / WGRAD,
+    # ragged counts, several pixel chunks, 64 output channels
+    (3, 17, 1, 28, 32, 3, 1, 1),
+    (1, 32, 1, 28, 32, 3, 1, 1),
+    (2, 9, 1, 16, 64, 3, 1, 1),
 ]
 
 
