@@ -673,12 +673,75 @@ conv_c1_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* __res
     }
 }
 
-// part[z][chunk][co*9 + k], bpart[z][chunk][co]  (dwgrad_ws_bytes layout, splits = chunks)
+// conv_c1_fwd_kernel (+ bias, ReLU) fused with the 2x2 max-pool after it (SimpleCNN conv1 ->
+// ReLU -> pool1, models_pytorch.py:80-82): one thread per POOLED pixel computes its 2x2 window
+// of conv outputs per channel with conv_c1_fwd_kernel's operations and pools them as
+// maxpool2_fwd_kernel does (strict >, window order) -> y (pooled planes yh x yw, the map in the
+// top-left corner) and the uint8 argmax idx; the full-resolution ReLU output is never written
+// (the backward's ReLU mask at the argmax is y > 0: conv_c1_wgrad_kernel<true>).
+template <int COUT>
+__global__ void __launch_bounds__(256)
+conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ w,
+                        int64_t w_cs, const float* __restrict__ bias, int64_t b_cs,
+                        float* __restrict__ y, int64_t y_cs, uint8_t* __restrict__ idx,
+                        int64_t i_cs, const int32_t* __restrict__ counts, int batch, int H,
+                        int W, int yh, int yw) {
+    __shared__ float ws[COUT * 9], bs[COUT];
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    for (int i = threadIdx.x; i < COUT * 9; i += 256) ws[i] = w[z * w_cs + i];
+    for (int i = threadIdx.x; i < COUT; i += 256) bs[i] = bias ? bias[z * b_cs + i] : 0.f;
+    __syncthreads();
+    const int OH = H / 2, OW = W / 2, OHW = OH * OW;
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= cnt * OHW) return;
+    const int img = n / OHW, q = n - img * OHW, oh = q / OW, ow = q - oh * OW;
+    const float* xi = x + z * x_cs + (int64_t)img * H * W;
+    float t[4][4];  // input rows 2oh-1 .. 2oh+2, columns 2ow-1 .. 2ow+2 (zero padding)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int yy = 2 * oh + i - 1, xx = 2 * ow + j - 1;
+            t[i][j] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) ? xi[yy * W + xx]
+                                                                               : 0.f;
+        }
+    float* yo = y + z * y_cs + (int64_t)img * COUT * yh * yw + oh * yw + ow;
+    uint8_t* io = idx + z * i_cs + (int64_t)img * COUT * OHW + q;
+#pragma unroll 2
+    for (int co = 0; co < COUT; ++co) {
+        float v[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {  // window slot s = (dy, dx) = (s >> 1, s & 1)
+            float a = 0.f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k)
+                a = fmaf(ws[co * 9 + k], t[(s >> 1) + k / 3][(s & 1) + k % 3], a);
+            a = a + bs[co];
+            v[s] = fmaxf(a, 0.f);
+        }
+        float m = v[0];
+        int am = 0;
+        if (v[1] > m) { m = v[1]; am = 1; }
+        if (v[2] > m) { m = v[2]; am = 2; }
+        if (v[3] > m) { m = v[3]; am = 3; }
+        yo[(int64_t)co * yh * yw] = m;
+        io[(int64_t)co * OHW] = (uint8_t)am;
+    }
+}
+
+// part[z][chunk][co*9 + k], bpart[z][chunk][co]  (dwgrad_ws_bytes layout, splits = chunks).
+// POOLED: dy is not materialised — the gradient of pixel (r, c) is the pooled gradient
+// gp[r/2][c/2] (planes gh x gw) if (r, c) is its window's argmax and the pooled ReLU output
+// yp there is > 0, else 0: maxpool2_bwd_kernel's routing and ReLU mask (xin at the argmax is
+// the pooled value), so the products are the same as on its output.
+template <bool POOLED>
 __global__ void __launch_bounds__(256)
 conv_c1_wgrad_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ dy,
                      int64_t dy_cs, float* __restrict__ part, float* __restrict__ bpart,
                      const int32_t* __restrict__ counts, int batch, int H, int W, int cout,
-                     int nchunks) {
+                     int nchunks, const uint8_t* __restrict__ pidx, int64_t pi_cs,
+                     const float* __restrict__ yp, int64_t yp_cs, int gh, int gw) {
     __shared__ float red[4][8 * 10];
     const int chunk = blockIdx.x, cg = blockIdx.y, z = blockIdx.z;
     const int cnt = counts ? counts[z] : batch;
@@ -712,9 +775,25 @@ conv_c1_wgrad_kernel(const float* __restrict__ x, int64_t x_cs, const float* __r
                         (ok && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
                             ? xi[yy * W + xx] : 0.f;
                 }
-            const float* di = dz + (int64_t)img * cout * HW + p;
+            if constexpr (POOLED) {
+                const int OH = H / 2, OW = W / 2;
+                const int oh = r >> 1, ow = c >> 1, code = (r & 1) * 2 + (c & 1);
+                const int64_t pl = (int64_t)img * cout + cg * 8;
+                const uint8_t* ii = pidx + z * pi_cs + pl * OH * OW + oh * OW + ow;
+                const int64_t gq = pl * gh * gw + oh * gw + ow;
+                const float* gi = dy + z * dy_cs + gq;
+                const float* yi = yp + z * yp_cs + gq;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) g[u][j] = ok ? di[(int64_t)j * HW] : 0.f;
+                for (int j = 0; j < 8; ++j) {
+                    const bool hit = ok && ii[(int64_t)j * OH * OW] == code &&
+                                     yi[(int64_t)j * gh * gw] > 0.f;
+                    g[u][j] = hit ? gi[(int64_t)j * gh * gw] : 0.f;
+                }
+            } else {
+                const float* di = dz + (int64_t)img * cout * HW + p;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) g[u][j] = ok ? di[(int64_t)j * HW] : 0.f;
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -1651,6 +1730,70 @@ extern "C" int fh_conv2d_dgrad_s2_shortcut(const float* dy, int64_t dy_cs, const
     return run_dconv_dgrad_s2(d, oh, nclients, workspace, ws_bytes, as_stream(stream));
 }
 
+// SimpleCNN conv1 -> ReLU -> 2x2 max-pool in one launch (conv_c1_pool_fwd_kernel): y = the
+// pooled output in planes yh x yw (the H/2 x W/2 map in the top-left corner; yh = H/2, yw = W/2
+// for dense planes), idx the dense uint8 argmax [img][cout][H/2][W/2].  cin = 1, 3x3 / s1 /
+// p1, cout 32 or 64; the same values as fh_conv2d_fwd(relu) + fh_maxpool2_fwd.
+extern "C" int fh_conv2d_c1_pool_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                                     const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                                     uint8_t* idx, int64_t i_cs, const int32_t* counts,
+                                     int32_t nclients, int32_t batch, int32_t h, int32_t w_,
+                                     int32_t cout, int32_t yh, int32_t yw, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && h >= 2 && w_ >= 2 && !(h & 1) && !(w_ & 1) &&
+               yh >= h / 2 && yw >= w_ / 2, "conv2d_c1_pool_fwd: bad shape");
+    FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_fwd: cout %d (32 or 64)", cout);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && w && y && idx, "conv2d_c1_pool_fwd: null pointer");
+    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256), (unsigned)nclients);
+    hipStream_t st = as_stream(stream);
+    if (cout == 32)
+        FH_LAUNCH(conv_c1_pool_fwd_kernel<32>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
+                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw);
+    else
+        FH_LAUNCH(conv_c1_pool_fwd_kernel<64>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
+                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw);
+    FH_LAUNCH_CHECK("conv2d_c1_pool_fwd");
+    return FH_OK;
+}
+
+// Its backward's weight gradient: fh_maxpool2_bwd(dpool, idx, xin = the ReLU output) +
+// fh_conv2d_wgrad in one pass — the full-resolution gradient is never written; dpool and y
+// (the pooled ReLU output, whose sign is the mask at the argmax) in planes gh x gw.
+// Workspace: fh_conv2d_wgrad_workspace(nclients, batch, 1, h, w, cout, 3, 3, 1, 1).
+extern "C" int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float* dpool,
+                                       int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
+                                       const float* y, int64_t y_cs, float* dw, int64_t dw_cs,
+                                       float* db, int64_t db_cs, void* workspace,
+                                       size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                                       int32_t batch, int32_t h, int32_t w_, int32_t cout,
+                                       int32_t gh, int32_t gw, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && h >= 2 && w_ >= 2 && !(h & 1) && !(w_ & 1) &&
+               gh >= h / 2 && gw >= w_ / 2, "conv2d_c1_pool_wgrad: bad shape");
+    FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_wgrad: cout %d (32 or 64)", cout);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && dpool && idx && y && dw, "conv2d_c1_pool_wgrad: null pointer");
+    DWPlan p{1, 1, 1, 1, conv_c1_chunks(batch, h, w_), 1};
+    const size_t need = dwgrad_ws_bytes(p, nclients, cout, 9);
+    FH_REQUIRE(workspace && ws_bytes >= need, "conv2d_c1_pool_wgrad: workspace %zu < %zu",
+               ws_bytes, need);
+    float* part = (float*)workspace;
+    const size_t wbytes = ((size_t)nclients * p.splits * cout * 9 * sizeof(float) + 255) / 256 * 256;
+    float* bpart = db ? (float*)((char*)workspace + wbytes) : nullptr;
+    hipStream_t st = as_stream(stream);
+    FH_LAUNCH(conv_c1_wgrad_kernel<true>, dim3((unsigned)p.splits, (unsigned)(cout / 8), nclients),
+              dim3(256), 0, st, x, x_cs, dpool, dp_cs, part, bpart, counts, batch, h, w_, cout,
+              p.splits, idx, i_cs, y, y_cs, gh, gw);
+    FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad");
+    const int MN = cout * 9;
+    const int wblocks = (int)ceil_div(MN, 64);
+    const int bblocks = db ? (int)ceil_div(cout, 64) : 0;
+    FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
+              (const float*)part, dw, dw_cs, p.splits, MN, wblocks, (const float*)bpart, db, db_cs,
+              cout);
+    FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad reduce");
+    return FH_OK;
+}
+
 extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
                                             int32_t w_, int32_t cout, int32_t kh, int32_t kw,
                                             int32_t stride, int32_t pad) {
@@ -1704,9 +1847,10 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         const size_t wbytes = ((size_t)nclients * p.splits * cout * 9 * sizeof(float) + 255) / 256 * 256;
         float* bpart = db ? (float*)((char*)workspace + wbytes) : nullptr;
         hipStream_t st = as_stream(stream);
-        FH_LAUNCH(conv_c1_wgrad_kernel, dim3((unsigned)p.splits, (unsigned)(cout / 8), nclients),
-                  dim3(256), 0, st, x, x_cs, dy, dy_cs, part, bpart, counts, batch, h, w_, cout,
-                  p.splits);
+        FH_LAUNCH(conv_c1_wgrad_kernel<false>,
+                  dim3((unsigned)p.splits, (unsigned)(cout / 8), nclients), dim3(256), 0, st, x,
+                  x_cs, dy, dy_cs, part, bpart, counts, batch, h, w_, cout, p.splits,
+                  (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0);
         FH_LAUNCH_CHECK("conv2d_wgrad c1");
         const int MN = cout * 9;
         const int wblocks = (int)ceil_div(MN, 64);

@@ -79,6 +79,10 @@ SIGNATURES = {
                                    I32, F32, F32, P]),
     "fh_conv2d_dgrad_s2_shortcut": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I32, I32,
                                           I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_conv2d_c1_pool_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
+                                    I32, I32, I32, I32, P]),
+    "fh_conv2d_c1_pool_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, SZ, P,
+                                      I32, I32, I32, I32, I32, I32, I32, P]),
     "fh_bn_apply_tiles": (I32, [P, P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, P, P, I32,
                                 I32, I32, I32, F32, F32, I32, P]),
     "fh_conv2d_fwd_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,

@@ -137,6 +137,7 @@ class PackedTrainer:
         if dpsgd is not None:  # the per-sample passes read the dense maps and fc1's ReLU output
             self.net.pad_maps = False
             self.net.fused_dropout = False
+            self.net.fuse_pool1 = False
         if dpsgd is not None:
             self._sq = torch.zeros(capacity, batch, dtype=torch.float64, device=dev)
             self._coef = torch.zeros(capacity, batch, device=dev)

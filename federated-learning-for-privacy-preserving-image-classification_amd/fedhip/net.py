@@ -159,6 +159,14 @@ class PackedNet:
         # ResNet down-sampling blocks: conv1's and the projection shortcut's input gradients
         # in one direct stride-2 launch (fh_conv2d_dgrad_s2_shortcut; FH_FUSED_SHORTCUT=0: two)
         self.fused_shortcut = os.environ.get("FH_FUSED_SHORTCUT", "1") != "0"
+        # SimpleCNN training: conv1 -> ReLU -> pool1 in one launch and its weight gradient
+        # straight from the pooled gradient (fh_conv2d_c1_pool_*; the full-resolution conv1
+        # output and its gradient are never written).  Bit-identical, but measured 2.5 %
+        # slower on K2 (a thread per pooled pixel: 4x the serial work per thread, a quarter of
+        # the workgroups; profiles/r02_c1/K2_fuse_pool1_rejected.txt): off unless
+        # FH_FUSE_POOL1=1.  (DP-SGD's per-sample passes read the full-resolution maps.)
+        self.fuse_pool1 = os.environ.get("FH_FUSE_POOL1", "0") == "1"
+        self._pool1_fused = False
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -261,9 +269,14 @@ class PackedNet:
         i1, i2 = A("i1", 32, 14, 14, dtype=torch.uint8), A("i2", 64, 7, 7, dtype=torch.uint8)
         h1, d1 = A("h1", 128), A("d1", 128)
         m1 = A("m1", 128, dtype=torch.uint8)
-        ops.conv2d_fwd(self.x, W(P_, "conv1.weight"), W(P_, "conv1.bias"), a1, n, B, 1, 28, 28,
-                       32, 3, 1, 1, relu=True, counts=cnt)
-        ops.maxpool2_fwd(a1, p1, i1, n, B, 32, 28, 28, counts=cnt)
+        self._pool1_fused = train and self.fuse_pool1
+        if self._pool1_fused:
+            ops.conv2d_c1_pool_fwd(self.x, W(P_, "conv1.weight"), W(P_, "conv1.bias"), p1, i1, n,
+                                   B, 28, 28, 32, counts=cnt)
+        else:
+            ops.conv2d_fwd(self.x, W(P_, "conv1.weight"), W(P_, "conv1.bias"), a1, n, B, 1, 28,
+                           28, 32, 3, 1, 1, relu=True, counts=cnt)
+            ops.maxpool2_fwd(a1, p1, i1, n, B, 32, 28, 28, counts=cnt)
         ops.conv2d_fwd(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, n, B, 32, hp, hp, 64,
                        3, 1, 1, relu=True, counts=cnt)
         ops.maxpool2_fwd(a2, p2, i2, n, B, 64, 14, 14, counts=cnt)
@@ -312,6 +325,11 @@ class PackedNet:
                          3, 1, 1, counts=cnt)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt)
+        if self._pool1_fused:
+            ops.conv2d_c1_pool_wgrad(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8), p1,
+                                     W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 28, 28, 32,
+                                     counts=cnt)
+            return
         da1 = A("da1", 32, 28, 28)
         ops.maxpool2_bwd(dp1, A("i1", 32, 14, 14, dtype=torch.uint8), da1, n, B, 32, 28, 28,
                          xin=A("a1", 32, 28, 28), counts=cnt)
@@ -790,8 +808,19 @@ class PackedNet:
         """Post-ReLU activations in forward order (their > 0 pattern is the ReLU mask)."""
         A = self.A
         if self.family == "SimpleCNN":
-            a2 = self._simple_maps()[1][..., :14, :14]
-            return [A("a1", 32, 28, 28), a2, self._fc_in]  # dropped fc1 output: see fused_dropout
+            p1, a2 = self._simple_maps()[:2]
+            a2 = a2[..., :14, :14]
+            a1 = A("a1", 32, 28, 28)
+            if self._pool1_fused:  # conv1's output not written: its value at each window's
+                # argmax is the pooled value (the backward uses no other element of it)
+                pooled = p1[..., :14, :14]
+                code = A("i1", 32, 14, 14, dtype=torch.uint8).long()
+                a1 = torch.zeros_like(a1)
+                for dy in (0, 1):
+                    for dx in (0, 1):
+                        a1[..., dy::2, dx::2] = torch.where(code == 2 * dy + dx, pooled,
+                                                            torch.zeros_like(pooled))
+            return [a1, a2, self._fc_in]  # dropped fc1 output: see fused_dropout
         if self.family == "CIFAR10CNN":
             if self._fused:  # BN outputs not materialised: the same fp32 ops on the host side
                 out = []

@@ -308,6 +308,35 @@ def conv2d_dgrad_s2_shortcut(dy, w, dy_sc, w_sc, dx, nclients, batch, cin, h, wd
     return True
 
 
+def conv2d_c1_pool_fwd(x, w, bias, y, idx, nclients, batch, h, wd, cout, counts=None):
+    """relu(conv3x3(x) + bias) (cin = 1) -> 2x2 max-pool in one launch
+    (fh_conv2d_c1_pool_fwd): y [clients, batch, cout, yh, yw] pooled planes (the map in the
+    top-left corner), idx the dense uint8 argmax [clients, batch, cout, h/2, w/2]."""
+    require_device(x, "x")
+    yh, yw = y.shape[-2], y.shape[-1]
+    ev = PROBE.begin(_conv_tag("fwd", 1, h, wd, cout, 3, 1) + "+pool")
+    call("fh_conv2d_c1_pool_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y),
+         _cs(y), ptr(idx), _cs(idx), _counts(counts), nclients, batch, h, wd, cout, yh, yw,
+         stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1))
+    return y
+
+
+def conv2d_c1_pool_wgrad(x, dpool, idx, y, dw, db, nclients, batch, h, wd, cout, counts=None):
+    """conv2d_c1_pool_fwd's weight gradient from the pooled gradient dpool (planes like y):
+    maxpool2_bwd(xin = the ReLU output) + conv2d_wgrad in one pass
+    (fh_conv2d_c1_pool_wgrad)."""
+    ws, nb = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, 1, h, wd, cout, 3, 3,
+                     1, 1)
+    gh, gw = dpool.shape[-2], dpool.shape[-1]
+    ev = PROBE.begin(_conv_tag("wgrad", 1, h, wd, cout, 3, 1) + "+pool")
+    call("fh_conv2d_c1_pool_wgrad", ptr(x), _cs(x), ptr(dpool), _cs(dpool), ptr(idx), _cs(idx),
+         ptr(y), _cs(y), ptr(dw), _cs(dw), ptr(db), _cs(db), ptr(ws), nb, _counts(counts),
+         nclients, batch, h, wd, cout, gh, gw, stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1))
+    return dw
+
+
 def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
                  in_affine=None):
     """in_affine as in conv2d_fwd (fh_conv2d_wgrad_bnrelu)."""

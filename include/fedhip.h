@@ -440,6 +440,24 @@ int fh_conv2d_dgrad_s2_shortcut(const float* dy, int64_t dy_cs, const float* w, 
                                 int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
                                 int32_t cout, int32_t accumulate, void* workspace, size_t ws_bytes,
                                 void* stream);
+/* SimpleCNN conv1 -> ReLU -> 2x2 max-pool (models_pytorch.py:80-82) in one launch: cin = 1,
+ * 3x3/s1/p1, cout 32 or 64; y = the pooled output in planes yh x yw (map in the top-left
+ * corner), idx the dense uint8 window argmax; the same values as fh_conv2d_fwd(relu=1) +
+ * fh_maxpool2_fwd, the full-resolution ReLU output never written. */
+int fh_conv2d_c1_pool_fwd(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                          const float* bias, int64_t b_cs, float* y, int64_t y_cs, uint8_t* idx,
+                          int64_t i_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                          int32_t h, int32_t w_, int32_t cout, int32_t yh, int32_t yw,
+                          void* stream);
+/* Its weight gradient: fh_maxpool2_bwd(dpool, idx, xin = ReLU output) + fh_conv2d_wgrad in
+ * one pass (the ReLU mask at the argmax is y > 0); dpool / y in planes gh x gw.  Workspace:
+ * fh_conv2d_wgrad_workspace(nclients, batch, 1, h, w, cout, 3, 3, 1, 1). */
+int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float* dpool, int64_t dp_cs,
+                            const uint8_t* idx, int64_t i_cs, const float* y, int64_t y_cs,
+                            float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
+                            size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                            int32_t batch, int32_t h, int32_t w_, int32_t cout, int32_t gh,
+                            int32_t gw, void* stream);
 /* fh_bn_fwd_train (its apply pass: y = [relu](bn(x) [+ res]), save_mean / save_invstd,
  * running statistics) from the tiles fh_conv2d_fwd_bnstats left — FederatedResNet's stem
  * bn1 and block bn2 + residual + ReLU (models_pytorch.py:189-194, :241-242), whose output the
