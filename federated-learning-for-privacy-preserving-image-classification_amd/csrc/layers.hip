@@ -82,7 +82,11 @@ maxpool2_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const uint8_t* 
                     int64_t i_cs, const uint8_t* __restrict__ mask, int64_t m_cs,
                     const float* __restrict__ xin, int64_t x_cs, float* __restrict__ dx,
                     int64_t dx_cs, const int32_t* __restrict__ counts, int batch, int C, int H,
-                    int W, float scale, int gh, int gw, int xh, int xw) {
+                    int W, float scale, int gh, int gw, int xh, int xw,
+                    const float* __restrict__ yin, int64_t yin_cs) {
+    // yin (nullable): the pooled ReLU output (planes gh x gw) — the ReLU mask at the argmax
+    // is yin > 0, the same decision as xin at the argmax (that IS the pooled value), for a
+    // forward that never wrote the full-resolution xin (fh_conv2d_c1_pool_fwd)
     // dy planes gh x gw, dx / xin planes xh x xw (maps in the top-left corner, see
     // maxpool2_fwd_kernel); idx / mask dense
     const int z = blockIdx.y;
@@ -101,6 +105,7 @@ maxpool2_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const uint8_t* 
         const int64_t base = plane * xh * xw + (2 * oh) * xw + 2 * ow;
         const int64_t off[4] = {0, 1, xw, xw + 1};
         if (xin && !(xin[z * x_cs + base + off[a]] > 0.f)) g = 0.f;
+        if (yin && !(yin[z * yin_cs + plane * gh * gw + oh * gw + ow] > 0.f)) g = 0.f;
         float* d = dx + z * dx_cs + base;
 #pragma unroll
         for (int q = 0; q < 4; ++q) d[off[q]] = (q == a) ? g : 0.f;
@@ -690,7 +695,8 @@ static int maxpool2_bwd_impl(const float* dy, int64_t dy_cs, const uint8_t* idx,
                              const uint8_t* mask, int64_t m_cs, float p_drop, const float* xin,
                              int64_t x_cs, float* dx, int64_t dx_cs, const int32_t* counts,
                              int32_t nclients, int32_t batch, int32_t C, int32_t H, int32_t W,
-                             void* stream, int32_t gh, int32_t gw, int32_t xh, int32_t xw) {
+                             void* stream, int32_t gh, int32_t gw, int32_t xh, int32_t xw,
+                             const float* yin = nullptr, int64_t yin_cs = 0) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && H >= 2 && W >= 2 && !(H & 1) && !(W & 1),
                "maxpool2_bwd: bad shape");
     FH_REQUIRE(gh >= H / 2 && gw >= W / 2 && xh >= H && xw >= W, "maxpool2_bwd: plane %dx%d / "
@@ -701,7 +707,7 @@ static int maxpool2_bwd_impl(const float* dy, int64_t dy_cs, const uint8_t* idx,
     const int64_t per = (int64_t)batch * C * (H / 2) * (W / 2);
     FH_LAUNCH(maxpool2_bwd_kernel, dim3(ew_grid(per), nclients), dim3(256), 0,
                        as_stream(stream), dy, dy_cs, idx, i_cs, mask, m_cs, xin, x_cs, dx, dx_cs,
-                       counts, batch, C, H, W, scale, gh, gw, xh, xw);
+                       counts, batch, C, H, W, scale, gh, gw, xh, xw, yin, yin_cs);
     FH_LAUNCH_CHECK("maxpool2_bwd");
     return FH_OK;
 }
@@ -740,6 +746,18 @@ extern "C" int fh_maxpool2_bwd_pitched(const float* dy, int64_t dy_cs, const uin
                                        int32_t gw, int32_t xh, int32_t xw, void* stream) {
     return maxpool2_bwd_impl(dy, dy_cs, idx, i_cs, mask, m_cs, p_drop, xin, x_cs, dx, dx_cs,
                              counts, nclients, batch, C, H, W, stream, gh, gw, xh, xw);
+}
+
+// fh_maxpool2_bwd_pitched with the ReLU mask taken from the pooled output y (planes gh x gw)
+// instead of the full-resolution ReLU output (after fh_conv2d_c1_pool_fwd, which never wrote it)
+extern "C" int fh_maxpool2_bwd_ymask(const float* dy, int64_t dy_cs, const uint8_t* idx,
+                                     int64_t i_cs, const float* y, int64_t y_cs, float* dx,
+                                     int64_t dx_cs, const int32_t* counts, int32_t nclients,
+                                     int32_t batch, int32_t C, int32_t H, int32_t W, int32_t gh,
+                                     int32_t gw, int32_t xh, int32_t xw, void* stream) {
+    FH_REQUIRE(y || nclients == 0, "maxpool2_bwd_ymask: null pooled output");
+    return maxpool2_bwd_impl(dy, dy_cs, idx, i_cs, nullptr, 0, 0.f, nullptr, 0, dx, dx_cs, counts,
+                             nclients, batch, C, H, W, stream, gh, gw, xh, xw, y, y_cs);
 }
 
 extern "C" int fh_dropout_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* mask,

@@ -79,6 +79,8 @@ SIGNATURES = {
                                    I32, F32, F32, P]),
     "fh_conv2d_dgrad_s2_shortcut": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I32, I32,
                                           I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_maxpool2_bwd_ymask": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32,
+                                    I32, I32, I32, I32, P]),
     "fh_conv2d_c1_pool_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
                                     I32, I32, I32, I32, P]),
     "fh_conv2d_c1_pool_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, SZ, P,

@@ -138,6 +138,7 @@ class PackedTrainer:
             self.net.pad_maps = False
             self.net.fused_dropout = False
             self.net.fuse_pool1 = False
+            self.net.fuse_pool1_bwd = False
         if dpsgd is not None:
             self._sq = torch.zeros(capacity, batch, dtype=torch.float64, device=dev)
             self._coef = torch.zeros(capacity, batch, device=dev)

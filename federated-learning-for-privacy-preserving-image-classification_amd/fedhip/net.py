@@ -159,13 +159,18 @@ class PackedNet:
         # ResNet down-sampling blocks: conv1's and the projection shortcut's input gradients
         # in one direct stride-2 launch (fh_conv2d_dgrad_s2_shortcut; FH_FUSED_SHORTCUT=0: two)
         self.fused_shortcut = os.environ.get("FH_FUSED_SHORTCUT", "1") != "0"
-        # SimpleCNN training: conv1 -> ReLU -> pool1 in one launch and its weight gradient
-        # straight from the pooled gradient (fh_conv2d_c1_pool_*; the full-resolution conv1
-        # output and its gradient are never written).  Bit-identical, but measured 2.5 %
-        # slower on K2 (a thread per pooled pixel: 4x the serial work per thread, a quarter of
-        # the workgroups; profiles/r02_c1/K2_fuse_pool1_rejected.txt): off unless
-        # FH_FUSE_POOL1=1.  (DP-SGD's per-sample passes read the full-resolution maps.)
-        self.fuse_pool1 = os.environ.get("FH_FUSE_POOL1", "0") == "1"
+        # SimpleCNN training: conv1 -> ReLU -> pool1 in one launch (fh_conv2d_c1_pool_fwd; the
+        # full-resolution conv1 output is never written) and pool1's backward masked by the
+        # pooled output (maxpool2_bwd_ymask): bit-identical, K2 +3.5 % (interleaved x3,
+        # profiles/r02_c1/K2_fuse_pool1_fwd_ab.txt).  FH_FUSE_POOL1=0: two launches.
+        # (DP-SGD's per-sample passes read the full-resolution maps: off there.)
+        self.fuse_pool1 = os.environ.get("FH_FUSE_POOL1", "1") != "0"
+        # ... its backward half alone (conv1's weight gradient from pool1's gradient, the
+        # full-resolution gradient never written) works after either forward
+        # (measured 7 % slower on K2: the per-pixel gathers of argmax / pooled value / pooled
+        # gradient cost more than the full-resolution gradient pass; off unless
+        # FH_FUSE_POOL1_BWD=1 — the fused forward's backward is maxpool2_bwd_ymask + wgrad)
+        self.fuse_pool1_bwd = os.environ.get("FH_FUSE_POOL1_BWD", "0") == "1"
         self._pool1_fused = False
 
     # -------------------------------------------------------------- helpers
@@ -325,14 +330,18 @@ class PackedNet:
                          3, 1, 1, counts=cnt)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt)
-        if self._pool1_fused:
+        if self.fuse_pool1_bwd:
             ops.conv2d_c1_pool_wgrad(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8), p1,
                                      W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 28, 28, 32,
                                      counts=cnt)
             return
         da1 = A("da1", 32, 28, 28)
-        ops.maxpool2_bwd(dp1, A("i1", 32, 14, 14, dtype=torch.uint8), da1, n, B, 32, 28, 28,
-                         xin=A("a1", 32, 28, 28), counts=cnt)
+        if self._pool1_fused:  # a1 not written: the ReLU mask at the argmax is p1 > 0
+            ops.maxpool2_bwd_ymask(dp1, A("i1", 32, 14, 14, dtype=torch.uint8), p1, da1, n, B,
+                                   32, 28, 28, counts=cnt)
+        else:
+            ops.maxpool2_bwd(dp1, A("i1", 32, 14, 14, dtype=torch.uint8), da1, n, B, 32, 28, 28,
+                             xin=A("a1", 32, 28, 28), counts=cnt)
         ops.conv2d_wgrad(self.x, da1, W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 1, 28, 28, 32,
                          3, 1, 1, counts=cnt)
 

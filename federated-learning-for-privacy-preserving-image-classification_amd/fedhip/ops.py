@@ -703,6 +703,14 @@ def maxpool2_bwd(dy, idx, dx, nclients, batch, C, H, W, mask=None, p_drop=0.0, x
          H, W, stream_handle())
 
 
+def maxpool2_bwd_ymask(dy, idx, y, dx, nclients, batch, C, H, W, counts=None):
+    """maxpool2_bwd with the ReLU mask from the pooled output y (planes like dy) instead of
+    the full-resolution xin (fh_maxpool2_bwd_ymask)."""
+    call("fh_maxpool2_bwd_ymask", ptr(dy), _cs(dy), ptr(idx), _cs(idx), ptr(y), _cs(y), ptr(dx),
+         _cs(dx), _counts(counts), nclients, batch, C, H, W, dy.shape[-2], dy.shape[-1],
+         dx.shape[-2], dx.shape[-1], stream_handle())
+
+
 def dropout_fwd(x, y, mask, nclients, batch, per_img, p_drop, drop_mode=1, seed=0, counts=None,
                 seed_dev=None):
     call("fh_dropout_fwd", ptr(x), _cs(x), ptr(y), _cs(y), ptr(mask), _cs(mask), _counts(counts),

@@ -449,6 +449,14 @@ int fh_conv2d_c1_pool_fwd(const float* x, int64_t x_cs, const float* w, int64_t 
                           int64_t i_cs, const int32_t* counts, int32_t nclients, int32_t batch,
                           int32_t h, int32_t w_, int32_t cout, int32_t yh, int32_t yw,
                           void* stream);
+/* fh_maxpool2_bwd (pitched planes: dy / y gh x gw, dx xh x xw) with the ReLU mask at the
+ * argmax taken from the pooled output y (> 0), for a forward that never wrote the
+ * full-resolution ReLU output (fh_conv2d_c1_pool_fwd); no dropout. */
+int fh_maxpool2_bwd_ymask(const float* dy, int64_t dy_cs, const uint8_t* idx, int64_t i_cs,
+                          const float* y, int64_t y_cs, float* dx, int64_t dx_cs,
+                          const int32_t* counts, int32_t nclients, int32_t batch, int32_t C,
+                          int32_t H, int32_t W, int32_t gh, int32_t gw, int32_t xh, int32_t xw,
+                          void* stream);
 /* Its weight gradient: fh_maxpool2_bwd(dpool, idx, xin = ReLU output) + fh_conv2d_wgrad in
  * one pass (the ReLU mask at the argmax is y > 0); dpool / y in planes gh x gw.  Workspace:
  * fh_conv2d_wgrad_workspace(nclients, batch, 1, h, w, cout, 3, 3, 1, 1). */

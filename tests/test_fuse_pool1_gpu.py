@@ -14,12 +14,13 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _round(fuse, opt, sizes, rounds=2):
+def _round(fuse, opt, sizes, rounds=2, fuse_bwd=None):
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model("simple_cnn", dropout_rate=0.25).to(DEV)
     S = len(sizes)
     eng = PackedTrainer(model, capacity=S, batch=32, device=DEV)
     eng.net.fuse_pool1 = fuse
+    eng.net.fuse_pool1_bwd = fuse if fuse_bwd is None else fuse_bwd
     for k in range(S):
         eng.load_module_state(k, model)
     g = torch.Generator().manual_seed(5)
@@ -36,12 +37,15 @@ def _round(fuse, opt, sizes, rounds=2):
     return eng, metrics
 
 
-@pytest.mark.parametrize("opt", ["sgd", "adam"])
-def test_fused_pool1_rounds_bit_identical(opt):
+@pytest.mark.parametrize("opt,fwd,bwd", [("sgd", True, False), ("adam", True, False),
+                                         ("sgd", True, True), ("sgd", False, True)])
+def test_fused_pool1_rounds_bit_identical(opt, fwd, bwd):
+    """fwd: conv1+ReLU+pool1 in one launch (the backward then masks by the pooled output,
+    maxpool2_bwd_ymask); bwd: conv1's weight gradient straight from pool1's gradient."""
     sizes = [130, 70, 33, 9]
-    a, ma = _round(True, opt, sizes)
-    b, mb = _round(False, opt, sizes)
-    assert a.net._pool1_fused and not b.net._pool1_fused
+    a, ma = _round(fwd, opt, sizes, fuse_bwd=bwd)
+    b, mb = _round(False, opt, sizes, fuse_bwd=False)
+    assert a.net._pool1_fused == fwd and not b.net._pool1_fused
     assert torch.equal(a.params, b.params)
     assert torch.equal(a.state1, b.state1)
     for ra, rb in zip(ma, mb):
