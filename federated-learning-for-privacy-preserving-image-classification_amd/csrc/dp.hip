@@ -12,13 +12,15 @@
 // between (clip decision and sigma are computed on the device).
 #include "fh_common.h"
 
+#include <cstdlib>
+
 namespace fh {
 
 // One block per (segment, client): fp64 sum of squares of the fp32 delta.  1024 threads and
 // float4 loads over the 16-B aligned body of the segment (scalar head / tail): one segment can
 // be the whole fc1 weight (SimpleCNN 401,408 elements), which a 256-thread scalar loop took
 // 0.67 ms per client row to walk.
-constexpr int kSqThreads = 1024;
+template <int kSqThreads>
 __global__ void __launch_bounds__(kSqThreads)
 dp_sqnorm_kernel(const float* __restrict__ local, int64_t ls, const float* __restrict__ global,
                  int64_t gs, const int64_t* __restrict__ seg_off, int nseg,
@@ -138,7 +140,13 @@ extern "C" int fh_dp_delta_sqnorm(const float* local, int64_t local_stride, cons
     FH_REQUIRE(num_clients >= 0 && nseg >= 0, "dp_delta_sqnorm: bad sizes");
     if (num_clients == 0 || nseg == 0) return FH_OK;
     FH_REQUIRE(local && seg_offsets && seg_sqnorm, "dp_delta_sqnorm: null pointer");
-    FH_LAUNCH(dp_sqnorm_kernel, dim3(nseg, num_clients), dim3(kSqThreads), 0, as_stream(stream),
+    // A/B: FH_DP_SQ_THREADS=256 (the round-1 block size)
+    static const int threads = getenv("FH_DP_SQ_THREADS") ? atoi(getenv("FH_DP_SQ_THREADS")) : 1024;
+    if (threads == 256)
+        FH_LAUNCH(dp_sqnorm_kernel<256>, dim3(nseg, num_clients), dim3(256), 0, as_stream(stream),
+                  local, local_stride, global, global_stride, seg_offsets, nseg, seg_sqnorm);
+    else
+    FH_LAUNCH(dp_sqnorm_kernel<1024>, dim3(nseg, num_clients), dim3(1024), 0, as_stream(stream),
                        local, local_stride, global, global_stride, seg_offsets, nseg, seg_sqnorm);
     FH_LAUNCH_CHECK("dp_delta_sqnorm");
     return FH_OK;
