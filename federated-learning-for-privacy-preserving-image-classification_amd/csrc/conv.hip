@@ -1120,6 +1120,11 @@ static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 4);
 // tile: faster per launch at 16 clients, but neutral per round (K4 +0.5 %, K5 -0.3 %,
 // interleaved x3, profiles/r02_wide) — off unless FH_DWGRAD_WIDE_MIN is set (e.g. 8)
 static const int kDwgradWideMin = env_int("FH_DWGRAD_WIDE_MIN", 1 << 30);
+// stage pixels of the 8x8-map WGRAD: 64 = one image per stage, 43 KB of LDS, two workgroups
+// (waves) per CU, which leaves room beside the other lanes' kernels: KT 265.8k -> 270.0k
+// (interleaved x3, profiles/r02_spx) although per launch it is even; FH_DWGRAD_SPX8=128: two
+// images per stage, 85 KB, one workgroup per CU (the round-1 choice)
+static const int kDwgradSpx8 = env_int("FH_DWGRAD_SPX8", 64) == 128 ? 128 : 64;
 // RGB-layer wgrad target: 512 workgroups (42 -> 34 us at 32 clients, profiles/r01_v12)
 static const int kDwgradSmallBlocks = env_int("FH_DWGRAD_SMALL_BLOCKS", 512);
 static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 2);  // tools/tail_sweep.py
@@ -1349,7 +1354,7 @@ static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     const bool wide_shape = w == 32 || (cin >= 256 && cout >= 256);
     if (kDwgradWpx == 4 && co64 && ci64 && wide_shape && nclients >= kDwgradWideMin)
         p = {2, 2, 1, 64 / w, 1, 1};
-    else if (kDwgradWpx == 4) p = {1, 1, 4, 128 / w, 1, 1};
+    else if (kDwgradWpx == 4) p = {1, 1, 4, (w == 8 ? kDwgradSpx8 : 128) / w, 1, 1};
     else if (kDwgradWpx == 2 && co64) p = {2, 1, 2, 128 / w, 1, 1};
     else if (kDwgradWpx == 2 && ci64) p = {1, 2, 2, 128 / w, 1, 1};
     else if (co64 && ci64) p = {2, 2, 1, 64 / w, 1, 1};
@@ -1435,6 +1440,9 @@ static int dwgrad_launch_w(const DWPlan& p, dim3 grid, const DWArgs& a, hipStrea
         return FH_OK;                                                                         \
     }
     FH_DW(1, 1, 4, 128)
+    if constexpr (W == 8) {  // 64-pixel stages: half the LDS, two workgroups per CU
+        FH_DW(1, 1, 4, 64)
+    }
     FH_DW(2, 1, 2, 128)
     FH_DW(1, 2, 2, 128)
     FH_DW(2, 2, 1, 64)

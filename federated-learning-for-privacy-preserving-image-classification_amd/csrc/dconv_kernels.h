@@ -1166,7 +1166,7 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
     if constexpr (WPX > 1) {
         // every wave parks 3 shifts of its accumulators in LDS; then all 256 threads sum
         // the WPX pixel partials (fixed order) and write the slab
-        constexpr int SG = 3;
+        constexpr int SG = (WPX * WT * 3 * 16 * 64 <= 2 * BUF) ? 3 : 1;  // shifts per round
         static_assert(WPX * WT * SG * 16 * 64 <= 2 * BUF, "reduction scratch");
         const int wt_me = wco * WCI + wci;
         float* op = a.part + slab * a.N;
