@@ -1124,6 +1124,9 @@ static const int kDwgradWideMin = env_int("FH_DWGRAD_WIDE_MIN", 1 << 30);
 // (waves) per CU, which leaves room beside the other lanes' kernels: KT 265.8k -> 270.0k
 // (interleaved x3, profiles/r02_spx) although per launch it is even; FH_DWGRAD_SPX8=128: two
 // images per stage, 85 KB, one workgroup per CU (the round-1 choice)
+// 32x32-map WGRAD with one dY stage buffer (FH_DWGRAD_SDY32=1): 69 KB of LDS, two workgroups
+// per CU, one more barrier per stage
+static const int kDwgradSdy32 = env_int("FH_DWGRAD_SDY32", 0);
 static const int kDwgradSpx8 = env_int("FH_DWGRAD_SPX8", 64) == 128 ? 128 : 64;
 // RGB-layer wgrad target: 512 workgroups (42 -> 34 us at 32 clients, profiles/r01_v12)
 static const int kDwgradSmallBlocks = env_int("FH_DWGRAD_SMALL_BLOCKS", 512);
@@ -1364,7 +1367,8 @@ static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
     // one workgroup per CU per resident wave (the 16x16 instance holds two: +3-5 % on those
     // layers at 512 workgroups; the one-wave instances lose with two rounds of workgroups)
-    const int occ = dwgrad_occ(w, p.wco, p.wci, p.sr);
+    const int occ = dwgrad_occ(w, p.wco, p.wci, p.sr, 1,
+                               kDwgradSdy32 && w == 32 && p.wco == 1 && p.wci == 1 && p.wpx == 4);
     // >= 4 stages per split: fewer, longer splits beat a wide slab in the few-client tail
     const int want = (int)std::min<int64_t>(
         std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks * occ), tiles)),
@@ -1438,6 +1442,12 @@ static int dwgrad_launch_w(const DWPlan& p, dim3 grid, const DWArgs& a, hipStrea
         FH_LAUNCH((dconv_wgrad_kernel<W, WCO, WCI, WPX, SPXV / W>), grid, dim3(256), 0, \
                            st, a);                                                            \
         return FH_OK;                                                                         \
+    }
+    if constexpr (W == 32) {  // one dY stage buffer: 69 KB, two workgroups per CU
+        if (kDwgradSdy32 && p.wco == 1 && p.wci == 1 && p.wpx == 4 && p.sr == 4) {
+            FH_LAUNCH((dconv_wgrad_kernel<32, 1, 1, 4, 4, 1, true>), grid, dim3(256), 0, st, a);
+            return FH_OK;
+        }
     }
     FH_DW(1, 1, 4, 128)
     if constexpr (W == 8) {  // 64-pixel stages: half the LDS, two workgroups per CU

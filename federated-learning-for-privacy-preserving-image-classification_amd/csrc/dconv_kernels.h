@@ -998,20 +998,23 @@ struct DWArgs {
 // S = 2: the 3x3 / stride-2 / pad-1 convolution of the ResNet down-sampling blocks (W = the
 // OUTPUT width): a stage's patch is the 2*SEGR+1 input rows its output rows read, 2W+2 wide
 // with the halo, and a lane's operand address strides by 2 (pixel pair -> columns 2c, 2c+2).
-constexpr int dwgrad_occ(int W, int WCO, int WCI, int SR, int S = 1) {
+// SDY: one dY stage buffer (the patch stays double-buffered) — the next stage's dY is stored
+// after a barrier that retires the current one; on 32x32 maps this brings the workgroup from
+// 86 to 69 KB of LDS, i.e. two per CU.
+constexpr int dwgrad_occ(int W, int WCO, int WCI, int SR, int S = 1, bool SDY = false) {
     const int SEGR = SR < W ? SR : W, NI = SR / SEGR;
     const int PR = NI * (S == 1 ? SEGR + 2 : 2 * SEGR + 1), CSTR = (PR * (S * W + 2)) | 1;
-    const int bytes = 4 * 2 * (SR * W * (32 * WCO + 1) + 32 * WCI * CSTR);
+    const int bytes = 4 * ((SDY ? 1 : 2) * SR * W * (32 * WCO + 1) + 2 * 32 * WCI * CSTR);
     return 2 * bytes <= 160 * 1024 ? 2 : 1;
 }
-template <int W, int WCO, int WCI, int SR, int S>
+template <int W, int WCO, int WCI, int SR, int S, bool SDY>
 constexpr int dwgrad_occupancy() {
-    constexpr int occ = dwgrad_occ(W, WCO, WCI, SR, S);
+    constexpr int occ = dwgrad_occ(W, WCO, WCI, SR, S, SDY);
     return occ;
 }
 
-template <int W, int WCO, int WCI, int WPX, int SR, int S = 1>
-__global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>())) dconv_wgrad_kernel(const DWArgs a) {
+template <int W, int WCO, int WCI, int WPX, int SR, int S = 1, bool SDY = false>
+__global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S, SDY>())) dconv_wgrad_kernel(const DWArgs a) {
     constexpr int H = W, HW = H * W;                // output map
     constexpr int WI = S * W, HI = S * H;           // input map
     constexpr int SPX = SR * W;                     // pixels per stage
@@ -1031,7 +1034,10 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
     static_assert(S == 1 || S == 2, "stride");
     static_assert(BM % COI == 0 && (SR % H == 0 || H % SR == 0), "stage geometry");
 
-    __shared__ float smem[2 * BUF];   // double-buffered [Dys | Ps]
+    constexpr int SMEM = SDY ? DSZ + 2 * PSZ : 2 * BUF;
+    __shared__ float smem[SMEM];   // double-buffered [Dys | Ps] (SDY: [Dys | Ps0 | Ps1])
+    auto dbase = [](int bsel) { return SDY ? 0 : bsel * BUF; };
+    auto pbase = [](int bsel) { return SDY ? DSZ + bsel * PSZ : bsel * BUF + DSZ; };
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1052,7 +1058,7 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
     // halo columns of the patch are always zero (pad = 1): write them once
     for (int q = tid; q < 2 * NPR; q += 256) {
         const int bsel = q / NPR, row = q % NPR, cl = row / PR, pr = row % PR;
-        float* r = smem + bsel * BUF + DSZ + cl * CSTR + pr * PW;
+        float* r = smem + pbase(bsel) + cl * CSTR + pr * PW;
         r[0] = 0.f;
         r[WI + 1] = 0.f;
     }
@@ -1089,8 +1095,8 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
             }
         }
     };
-    auto store = [&](int bsel) {
-        float* D = smem + bsel * BUF;
+    auto store_d = [&](int bsel) {
+        float* D = smem + dbase(bsel);
 #pragma unroll
         for (int i = 0; i < NDY; ++i) {
             float* d = D + dp * BMP + dco + i * COI;
@@ -1099,7 +1105,9 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
             d[2 * BMP] = rd[i].z;
             d[3 * BMP] = rd[i].w;
         }
-        float* P = D + DSZ;
+    };
+    auto store_p = [&](int bsel) {
+        float* P = smem + pbase(bsel);
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
             const int q = prt + i * RPI;
@@ -1113,6 +1121,10 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
             }
         }
     };
+    auto store = [&](int bsel) {
+        store_d(bsel);
+        store_p(bsel);
+    };
 
     f32x16 acc[9];
 #pragma unroll
@@ -1123,7 +1135,7 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
 
     const int h = lane >> 5, col = lane & 31;
     const int a_off = h * BMP + wco * 32 + col;
-    const int b_off = DSZ + (wci * 32 + col) * CSTR + S * h;
+    const int b_off = (wci * 32 + col) * CSTR + S * h;
     if (sbeg < send) {
         load(sbeg);
         store(0);
@@ -1132,8 +1144,8 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
         for (int st = sbeg; st < send; ++st) {
             const bool more = st + 1 < send;
             if (more) load(st + 1);
-            const float* Al = smem + bsel * BUF + a_off;
-            const float* Bl = smem + bsel * BUF + b_off;
+            const float* Al = smem + dbase(bsel) + a_off;
+            const float* Bl = smem + pbase(bsel) + b_off;
 #pragma unroll 1
             for (int rr = 0; rr < RPW; ++rr) {
                 const int r = wpx * RPW + rr;                  // stage row
@@ -1152,7 +1164,15 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
                         acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[s], acc[s], 0, 0, 0);
                 }
             }
-            if (more) store(bsel ^ 1);
+            if (more) {
+                if constexpr (SDY) {  // the one dY buffer: every wave has finished reading it
+                    store_p(bsel ^ 1);
+                    __syncthreads();
+                    store_d(bsel ^ 1);
+                } else {
+                    store(bsel ^ 1);
+                }
+            }
             __syncthreads();
             bsel ^= 1;
         }
@@ -1166,8 +1186,8 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S>()))
     if constexpr (WPX > 1) {
         // every wave parks 3 shifts of its accumulators in LDS; then all 256 threads sum
         // the WPX pixel partials (fixed order) and write the slab
-        constexpr int SG = (WPX * WT * 3 * 16 * 64 <= 2 * BUF) ? 3 : 1;  // shifts per round
-        static_assert(WPX * WT * SG * 16 * 64 <= 2 * BUF, "reduction scratch");
+        constexpr int SG = (WPX * WT * 3 * 16 * 64 <= SMEM) ? 3 : 1;  // shifts per round
+        static_assert(WPX * WT * SG * 16 * 64 <= SMEM, "reduction scratch");
         const int wt_me = wco * WCI + wci;
         float* op = a.part + slab * a.N;
 #pragma unroll
