@@ -278,3 +278,34 @@ def create_adaptive_config(client_capabilities: Dict[str, Any]) -> FederatedTrai
     return FederatedTrainingConfig(local_epochs=epochs, batch_size=bs, learning_rate=lr,
                                    optimizer_type="adam", early_stopping_patience=None,
                                    save_checkpoints=True, validation_split=0.1)
+
+
+def validate_training_data(train_loader) -> Dict[str, Any]:
+    """Pre-flight check of a (data, targets) loader (reference :504-560).
+
+    Host-side only: it looks at the loader's length and its first batch (NCHW float data,
+    integer targets) and never raises — problems come back as {'valid': False, 'error': …},
+    the same keys and messages as the reference."""
+    try:
+        n = len(train_loader)
+        if n == 0:
+            raise ValueError("Training data loader is empty")
+        batch = next(iter(train_loader))
+        if len(batch) != 2:
+            raise ValueError("Expected (data, targets) tuple from data loader")
+        data, targets = batch
+        if not isinstance(data, torch.Tensor):
+            raise ValueError("Data must be a torch.Tensor")
+        if not isinstance(targets, torch.Tensor):
+            raise ValueError("Targets must be a torch.Tensor")
+        if data.dim() != 4:
+            raise ValueError(f"Expected 4D data tensor, got shape {data.shape}")
+        b, c, h, w = data.shape
+        out = {"valid": True, "num_batches": n, "batch_size": b, "data_shape": (c, h, w),
+               "num_classes": int(torch.unique(targets).numel()),
+               "data_type": str(data.dtype), "targets_type": str(targets.dtype)}
+        logger.info("Training data validation passed: %s", out)
+        return out
+    except Exception as e:  # the reference reports, it does not raise
+        logger.error("Training data validation failed: %s", e)
+        return {"valid": False, "error": str(e)}
