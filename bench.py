@@ -117,8 +117,6 @@ def make_rank_data(cfg, train_sizes, my_slots, device, seed, raw=True):
         c, h, w = cfg["shape"]
         shp = (total, h, w) if c == 1 else (total, h, w, c)
         data = torch.randint(0, 256, shp, generator=g, device=device, dtype=torch.uint8)
-        if os.environ.get("FH_BENCH_CONST_DATA"):  # diagnostics: power / clock sensitivity
-            data.fill_(int(os.environ["FH_BENCH_CONST_DATA"]))
     else:
         data = torch.randn(total, *cfg["shape"], generator=g, device=device)
     labels = torch.randint(0, cfg["classes"], (total,), generator=g, device=device)
@@ -133,6 +131,40 @@ def flops_key(cfg):
     return cfg["model"]
 
 
+def host_cpu_info():
+    """The host the CPU baseline ran on: model name, physical cores (unique (package, core)
+    pairs of /proc/cpuinfo), logical CPUs this process may run on (affinity) and the
+    cgroup CPU quota, if any (the GPU box gives a job a share of a larger machine)."""
+    model, cores = None, set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+        if phys is not None:
+            cores.add((phys, core))
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    return {"model": model, "physical_cores": len(cores) or None, "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(cfg, train_sizes, opt="sgd", lr=0.01, seconds=12.0):
     """The reference's client round on the host cores — oracle/ (the CPU restatement pinned
     bit-exact to the reference LocalTrainer / privacy / compression / FedAvg): clients of
@@ -145,7 +177,14 @@ def cpu_baseline(cfg, train_sizes, opt="sgd", lr=0.01, seconds=12.0):
     sample) until ~`seconds` of this work; the sample's client-images / its wall time is
     the baseline.  Data generation is not timed."""
     from oracle import compress_ref, data_ref, fedavg_ref, privacy_ref, train_ref
-    threads = torch.get_num_threads()
+    host = host_cpu_info()
+    # one thread per physical core this job may use: min(physical cores, affinity, cgroup
+    # quota) — the box's share of its host, not the whole machine's core count
+    lim = [v for v in (host["physical_cores"], host["affinity_cpus"], host["cgroup_cpu_quota"])
+           if v]
+    threads = max(1, int(min(lim))) if lim else torch.get_num_threads()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
     c, h, w = cfg["shape"]
     tf = ops.DataTransform.mnist() if c == 1 else ops.DataTransform.cifar10()
@@ -195,9 +234,11 @@ def cpu_baseline(cfg, train_sizes, opt="sgd", lr=0.01, seconds=12.0):
     t0 = time.perf_counter()
     fedavg_ref.weighted_average(rows, fedavg_ref.calculate_sample_weights(ns))
     busy += time.perf_counter() - t0
+    torch.set_num_threads(prev_threads)
     extras = ", update DP" if cfg["dp"] else ""
     extras += ", top-k compression" if cfg.get("compression") else ""
     return {"value": imgs / busy, "unit": "client-images/s", "cores": threads, "kind": "port",
+            "host": host,
             "sample": f"{nclients} clients of this workload ({imgs} client-images: whole "
                       f"shards, {cfg['epochs']} local epoch(s), per-sample host transforms, "
                       f"batch 32, {opt} lr {lr}{extras}, FedAvg of the sample) in "
@@ -347,43 +388,93 @@ def measured_traffic(tag, flops_per_launch=None):
     return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="KT", choices=sorted(CONFIGS))
-    ap.add_argument("--opt", default="sgd")
-    ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--probe", default=None, help="conv launch tag to time (default: auto)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-instances", action="store_true",
-                    help="skip the instrumented per-launch-shape round")
-    ap.add_argument("--rounds-target", type=float, default=0.91,
-                    help="rounds-to-accuracy half of the metric (K1 MNIST proxy); 0 disables")
-    ap.add_argument("--rounds-max", type=int, default=30)
-    ap.add_argument("--fp32-data", action="store_true",
-                    help="pre-normalised fp32 shards instead of uint8 images + on-device transform")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
-    ap.add_argument("--one-device", action="store_true",
-                    help="rehearsal: every rank on cuda:0 (multi-rank path on a 1-GPU box)")
-    ap.add_argument("--lanes", type=int, default=None,
-                    help="concurrent client lanes per GPU (default: planner / FH_LANES)")
-    args = ap.parse_args()
-    cfg = CONFIGS[args.config]
-    world, rank, dev = setup(args)
+def summarize_instances(inst, buckets, peak):
+    """Instrumented-round launch records -> the bench line's roofline fields.
 
+    inst:    {tag: (launches, ms, flops)};  buckets: {(tag, bucket): (launches, ms, flops,
+    bytes)}.  A launch shape is MFMA-bound when its algorithmic intensity (flops / bytes)
+    is above the ridge FP32_MFMA_PEAK / HBM_PEAK (19.7 FLOP/B), HBM-bound below it."""
+    ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    tot = {}
+    for (tag, _), (n, t, f, b) in buckets.items():
+        a = tot.setdefault(tag, [0, 0.0, 0.0, 0.0])
+        a[0] += n; a[1] += t; a[2] += f; a[3] += b
+    rows = sorted(tot.items(), key=lambda kv: -kv[1][1])
+
+    def row(tag, n, t, f, b):
+        bound = "mfma" if f > ridge * b else "hbm"
+        return {"launch": tag, "launches": n, "total_ms": round(t, 3),
+                "avg_us": round(1e3 * t / n, 2), "bound": bound,
+                "tflops": round(f / (t * 1e-3) / 1e12, 2),
+                "frac": round(f / (t * 1e-3) / 1e12 / peak, 4),
+                "gbs": round(b / (t * 1e-3) / 1e9, 1),
+                "hbm_frac": round(b / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    instances = [row(tag, *v) for tag, v in rows]
+    by_bucket = [dict(row(tag, *v), clients=bk) for (tag, bk), v in
+                 sorted(buckets.items(), key=lambda kv: (-tot[kv[0][0]][1], kv[0][1]))]
+    T = sum(v[1] for v in tot.values())
+    F = sum(v[2] for v in tot.values())
+    conv_all = {"tflops": round(F / (T * 1e-3) / 1e12, 2),
+                "frac": round(F / (T * 1e-3) / 1e12 / peak, 4), "total_ms": round(T, 2),
+                "launches": sum(v[0] for v in tot.values())}
+    return rows, instances, by_bucket, conv_all
+
+
+def roofline_of(tag, n, t, f, b, peak, hbm=False):
+    """The roofline object of one launch shape averaged over all its launches."""
+    common = {"kernel": tag, "launches_timed": n, "avg_launch_ms": round(t / n, 4),
+              "flops_per_launch": round(f / n), "bytes_per_launch": round(b / n),
+              "measured": "HIP events on the launch stream around every launch of one "
+                          "instrumented round of this workload (eager, lanes serialised); "
+                          "small tail launches include host issue gaps (conservative)"}
+    if hbm:
+        ach = b / (t * 1e-3) / 1e9
+        return dict(common, bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=None)
+    ach = f / (t * 1e-3) / 1e12
+    return dict(common, bound="mfma", achieved=round(ach, 2), peak=peak, unit="TFLOP/s",
+                frac=round(ach / peak, 4), traffic=measured_traffic(tag, f / n))
+
+
+_MAPS_THREAD = None
+
+
+def dump_maps_periodically(path, period=0.1):
+    """Diagnostics (rocprofv3 --pmc crash): copy /proc/self/maps to `path`
+    every `period` s from a daemon thread, so the last snapshot before a crash shows what
+    was mapped near the faulting address.  Reads only; the workload is unchanged."""
+    global _MAPS_THREAD
+    if _MAPS_THREAD is not None:
+        return
+    import threading
+
+    def loop():
+        n = 0
+        while True:
+            try:
+                data = open("/proc/self/maps").read()
+                with open(path + ".tmp", "w") as fh:
+                    fh.write(f"# snapshot {n} t={time.time():.3f}\n" + data)
+                os.replace(path + ".tmp", path)
+            except OSError:
+                pass
+            n += 1
+            time.sleep(period)
+    _MAPS_THREAD = threading.Thread(target=loop, daemon=True)
+    _MAPS_THREAD.start()
+
+
+def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
+    """Measure one BASELINE config: warmup rounds, `steps` timed rounds (barrier +
+    synchronize on both sides, max over ranks), then one instrumented round.  Returns the
+    rank-0 result dict (None on other ranks)."""
+    cfg = CONFIGS[key]
     labels, train = build_clients(cfg, world)
     C = len(train)
     assign = lpt_assign(train, world)
     mine = assign[rank]
     torch.manual_seed(0)
     template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
-    if os.environ.get("FH_BENCH_ZERO_WEIGHTS"):  # diagnostics: power / clock sensitivity
-        with torch.no_grad():
-            for prm in template.parameters():
-                prm.zero_()
     dp = DPConfig(epsilon=cfg["dp"]) if cfg["dp"] else None
     raw = not args.fp32_data
     tf = None
@@ -397,7 +488,6 @@ def main():
     rr = RankRound(template, train, mine, epochs=cfg["epochs"], device=dev, dp=dp,
                    lanes=args.lanes, transform=tf, compression=comp)
     data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, rank, raw=raw)
-    my_images = cfg["epochs"] * sum(train[k] for k in mine)
     total_images = cfg["epochs"] * sum(train)
 
     # launch probe: dominant conv kernel (the largest-FLOP 3x3 fwd launch of the model)
@@ -405,16 +495,16 @@ def main():
         "cifar10_cnn": "conv_dgrad:c32x32x32->32k3s1",
         "simple_cnn": "conv_dgrad:c32x14x14->64k3s1",
         "federated_resnet": "conv_dgrad:c64x32x32->64k3s1"}[cfg["model"]]
-    ops.PROBE.tag = probe_tag
+    ops.PROBE.reset()
+    ops.PROBE.tag, ops.PROBE.enabled = probe_tag, False
     # timed rounds: full-width full-batch steps run eagerly with the probe armed (the
     # engine replays every other step from its captured graph)
     rr.trainer.probe_full = False
 
     gen = torch.Generator().manual_seed(7)
-    if os.environ.get("FH_DUMP_MAPS"):  # diagnostics: where libraries live (profiler crashes)
-        with open("/proc/self/maps") as src, open(os.environ["FH_DUMP_MAPS"], "w") as dst:
-            dst.write(src.read())
-    for w in range(args.warmup):
+    if os.environ.get("FH_DUMP_MAPS"):
+        dump_maps_periodically(os.environ["FH_DUMP_MAPS"])
+    for w in range(warmup):
         rr.run(data, lab, offs, args.opt, args.lr, seed=w, generator=gen)
     torch.cuda.synchronize()
     if world > 1:
@@ -422,7 +512,7 @@ def main():
     torch.cuda.synchronize()
     rr.trainer.probe_full = True
     t0 = time.perf_counter()
-    for s in range(args.steps):
+    for s in range(steps):
         rr.run(data, lab, offs, args.opt, args.lr, seed=100 + s, generator=gen)
     torch.cuda.synchronize()
     if world > 1:
@@ -439,85 +529,193 @@ def main():
     # one instrumented round (untimed, every step eager, the lanes one after another so a
     # launch never shares the chip with another lane's): HIP events around EVERY conv /
     # linear launch — every client count, ragged and tail steps included
-    inst = None
+    inst = buckets = None
     if not args.no_instances:
         ops.PROBE.reset()
         ops.PROBE.tag, ops.PROBE.enabled = "*", True
         rr.run(data, lab, offs, args.opt, args.lr, seed=999, generator=gen, serialize_lanes=True)
         ops.PROBE.enabled = False
         inst = ops.PROBE.by_tag()
+        buckets = ops.PROBE.by_tag_bucket()
+    if rank != 0:
+        return None
+    value = total_images * steps / elapsed
+    fl = TRAIN_FLOPS[flops_key(cfg)]
+    peak = FP32_MFMA_PEAK_TFLOPS
+    full = None
+    if probe:
+        ach = probe["flops_per_launch"] / (probe["avg_ms"] * 1e-3) / 1e12
+        full = {"kernel": probe_tag, "achieved": round(ach, 2), "frac": round(ach / peak, 4),
+                "launches_timed": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4),
+                "note": "full-width full-batch launches of the timed rounds only"}
+    roof = roof_hbm = instances = by_bucket = conv_all = None
+    if inst:
+        rows, instances, by_bucket, conv_all = summarize_instances(inst, buckets, peak)
+        # the roofline kernel: the launch shape with the largest share of the round's
+        # conv/linear time, averaged over ALL its launches (every client count, ragged
+        # batches, tail steps); roofline_hbm: the same for the largest HBM-bound shape
+        tag, v = rows[0]
+        ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+        roof = roofline_of(tag, *v, peak, hbm=v[2] <= ridge * v[3])
+        hb = [(tg, vv) for tg, vv in rows if vv[2] <= ridge * vv[3]]
+        if hb:
+            roof_hbm = roofline_of(hb[0][0], *hb[0][1], peak, hbm=True)
+    out = {
+        "metric": "client-images/sec/node", "value": round(value, 1),
+        "unit": "client-images/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(1000 * elapsed / steps, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": ("synthetic uint8 CIFAR/MNIST-shaped images resident in HBM, the "
+                 "reference loaders' transforms (crop/flip/normalise) applied on the chip "
+                 "each step" if raw else "synthetic N(0,1) CIFAR/MNIST-shaped fp32 tensors "
+                 "resident in HBM") + "; Dirichlet shard sizes from the reference "
+                "partitioner restatement",
+        "config": {"workload": f"{key}: {cfg['model']} {C} clients "
+                               f"({cfg['clients']}/GPU), {cfg['strategy']}"
+                               f"{'(a=' + str(cfg['alpha']) + ')' if cfg['strategy'] == 'non_iid' else ''}, "
+                               f"{cfg['epochs']} local epoch(s), batch 32, {args.opt} lr {args.lr}, "
+                               f"DP eps={cfg['dp']}, "
+                               f"{'compression ' + str(cfg['compression']) + ', ' if cfg.get('compression') else ''}"
+                               f"FedAvg{' RCCL all-reduce' if world > 1 else ''}"
+                               + (f" [{world}/{cfg['config_gpus']} GPU slice of the "
+                                  f"{cfg['clients'] * cfg['config_gpus']}-client config]"
+                                  if cfg.get('config_gpus') else ""),
+                   "clients": C, "images_per_round": total_images, "batch": 32,
+                   "parallelism": f"client-packed x{world} GPU",
+                   "lanes": rr.trainer.cut},
+        "achieved_tflops_step": round(value * fl / 1e12, 2),
+        "round_frac": round(value * fl / 1e12 / peak, 4),
+        "roofline": roof,
+        "roofline_hbm": roof_hbm,
+        "roofline_full_width_probe": full,
+        "conv_linear_all_launches": conv_all,
+        "instances": instances,
+        "instances_by_clients": by_bucket,
+    }
+    if world == 1 and rtt and args.rounds_target > 0:
+        out["rounds_to_target"] = rounds_to_target(dev, args.rounds_target, args.rounds_max,
+                                                   args.opt, args.lr)
+    if world == 1 and cpu and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, [train[k] for k in rr.slots], args.opt, args.lr)
+    del rr, data, lab
+    torch.cuda.empty_cache()
+    return out
 
-    if rank == 0:
-        value = total_images * args.steps / elapsed
-        fl = TRAIN_FLOPS[flops_key(cfg)]
-        peak = FP32_MFMA_PEAK_TFLOPS
-        roof, full = None, None
-        if probe:
-            ach = probe["flops_per_launch"] / (probe["avg_ms"] * 1e-3) / 1e12
-            full = {"kernel": probe_tag, "achieved": round(ach, 2), "frac": round(ach / peak, 4),
-                    "launches_timed": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4),
-                    "note": "full-width full-batch launches of the timed rounds only"}
-        instances, conv_all = None, None
-        if inst:
-            rows = sorted(inst.items(), key=lambda kv: -kv[1][1])
-            instances = [{"launch": tag, "launches": n, "total_ms": round(t, 3),
-                          "avg_us": round(1e3 * t / n, 2),
-                          "tflops": round(f / (t * 1e-3) / 1e12, 2),
-                          "frac": round(f / (t * 1e-3) / 1e12 / peak, 4)} for tag, (n, t, f) in rows]
-            T = sum(t for _, t, _ in inst.values())
-            F = sum(f for _, _, f in inst.values())
-            conv_all = {"tflops": round(F / (T * 1e-3) / 1e12, 2),
-                        "frac": round(F / (T * 1e-3) / 1e12 / peak, 4), "total_ms": round(T, 2),
-                        "launches": sum(n for n, _, _ in inst.values())}
-            # the roofline kernel: the launch shape with the largest share of the round's
-            # conv/linear time, averaged over ALL its launches (every client count, ragged
-            # batches, tail steps)
-            tag, (n, t, f) = rows[0]
-            ach = f / (t * 1e-3) / 1e12
-            roof = {"bound": "mfma", "kernel": tag, "achieved": round(ach, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                    "traffic": measured_traffic(tag, f / n),
-                    "launches_timed": n, "avg_launch_ms": round(t / n, 4),
-                    "flops_per_launch": round(f / n),
-                    "measured": "HIP events on the launch stream around every launch of one "
-                                "instrumented round of this workload (eager, lanes serialised); "
-                                "small tail launches include host issue gaps (conservative)"}
-        out = {
-            "metric": "client-images/sec/node", "value": round(value, 1),
-            "unit": "client-images/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": ("synthetic uint8 CIFAR/MNIST-shaped images resident in HBM, the "
-                     "reference loaders' transforms (crop/flip/normalise) applied on the chip "
-                     "each step" if raw else "synthetic N(0,1) CIFAR/MNIST-shaped fp32 tensors "
-                     "resident in HBM") + "; Dirichlet shard sizes from the reference "
-                    "partitioner restatement",
-            "config": {"workload": f"{args.config}: {cfg['model']} {C} clients "
-                                   f"({cfg['clients']}/GPU), {cfg['strategy']}"
-                                   f"{'(a=' + str(cfg['alpha']) + ')' if cfg['strategy'] == 'non_iid' else ''}, "
-                                   f"{cfg['epochs']} local epoch(s), batch 32, {args.opt} lr {args.lr}, "
-                                   f"DP eps={cfg['dp']}, "
-                                   f"{'compression ' + str(cfg['compression']) + ', ' if cfg.get('compression') else ''}"
-                                   f"FedAvg{' RCCL all-reduce' if world > 1 else ''}"
-                                   + (f" [{world}/{cfg['config_gpus']} GPU slice of the "
-                                      f"{cfg['clients'] * cfg['config_gpus']}-client config]"
-                                      if cfg.get('config_gpus') else ""),
-                       "clients": C, "images_per_round": total_images, "batch": 32,
-                       "parallelism": f"client-packed x{world} GPU",
-                       "lanes": rr.trainer.cut},
+
+def run_dpsgd(args, dev, steps, warmup):
+    """`--config K2-dpsgd`: the K2 workload (SimpleCNN, 32 Dirichlet(0.5) clients, one
+    local epoch) trained with per-sample DP-SGD (north_star extension, not in the
+    reference): every step clips each image's gradient to C = 1 by the per-image norm
+    passes (conv / linear per-sample square-norm tiles, fh_dpsgd_clip_coef, rows scaled
+    before the WGRADs) and adds N(0, (sigma C)^2) with the reference's Gaussian-mechanism
+    sigma (privacy.py:209, eps = 1, delta = 1e-5).  One lane (PackedTrainer), fp32 N(0,1)
+    data.  Algorithmic work per image: SimpleCNN's train FLOPs + 2 * MACs for the norms."""
+    from fedhip.engine import DPSGDConfig, PackedTrainer
+    cfg = CONFIGS["K2"]
+    labels, train = build_clients(cfg, 1)
+    order = sorted(range(len(train)), key=lambda k: (-train[k], k))
+    sizes = [train[k] for k in order]
+    torch.manual_seed(0)
+    model = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
+    eng = PackedTrainer(model, capacity=len(sizes), batch=32, device=dev,
+                        dpsgd=DPSGDConfig(max_grad_norm=1.0, epsilon=1.0, delta=1e-5))
+    for k in range(len(sizes)):
+        eng.load_module_state(k, model)
+    g = torch.Generator(device=dev).manual_seed(1000)
+    data = torch.randn(sum(sizes), *cfg["shape"], generator=g, device=dev)
+    lab = torch.randint(0, cfg["classes"], (sum(sizes),), generator=g, device=dev)
+    offs = np.cumsum([0] + sizes[:-1]).tolist()
+    gen = torch.Generator().manual_seed(7)
+    for _ in range(warmup):
+        eng.run_round(data, lab, offs, eng.make_plan(sizes, 1, generator=gen), args.opt, args.lr)
+    plans = [eng.make_plan(sizes, 1, generator=gen) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for pl in plans:
+        eng.run_round(data, lab, offs, pl, args.opt, args.lr)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ops.PROBE.reset()
+    ops.PROBE.tag, ops.PROBE.enabled = "*", True
+    eng.run_round(data, lab, offs, eng.make_plan(sizes, 1, generator=gen), args.opt, args.lr)
+    ops.PROBE.enabled = False
+    peak = FP32_MFMA_PEAK_TFLOPS
+    rows, instances, by_bucket, conv_all = summarize_instances(ops.PROBE.by_tag(),
+                                                               ops.PROBE.by_tag_bucket(), peak)
+    ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    ps = [(t, v) for t, v in rows if "psnorm" in t]
+    value = sum(sizes) * steps / elapsed
+    macs = (TRAIN_FLOPS["simple_cnn"] + 2 * 225_792) / 6  # MACs/img (first layer counted 4x)
+    fl = TRAIN_FLOPS["simple_cnn"] + 2 * macs
+    return {"metric": "client-images/sec/node", "value": round(value, 1),
+            "unit": "client-images/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
+            "ms_per_step": round(1000 * elapsed / steps, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic N(0,1) MNIST-shaped fp32 tensors resident in HBM; Dirichlet "
+                    "shard sizes from the reference partitioner restatement",
+            "config": {"workload": f"K2-dpsgd: simple_cnn {len(sizes)} clients non_iid(a=0.5), 1 "
+                                   f"local epoch, batch 32, per-sample DP-SGD C=1 eps=1 "
+                                   f"delta=1e-5, {args.opt} lr {args.lr} (one lane)",
+                       "clients": len(sizes), "images_per_round": sum(sizes)},
             "achieved_tflops_step": round(value * fl / 1e12, 2),
             "round_frac": round(value * fl / 1e12 / peak, 4),
-            "roofline": roof,
-            "roofline_full_width_probe": full,
-            "conv_linear_all_launches": conv_all,
-            "instances": instances,
-        }
-        if world == 1 and args.rounds_target > 0:
-            out["rounds_to_target"] = rounds_to_target(dev, args.rounds_target, args.rounds_max,
-                                                       args.opt, args.lr)
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cfg, [train[k] for k in rr.slots], args.opt,
-                                               args.lr)
+            "roofline": roofline_of(rows[0][0], *rows[0][1], peak,
+                                    hbm=rows[0][1][2] <= ridge * rows[0][1][3]),
+            "roofline_psnorm": [roofline_of(t, *v, peak, hbm=v[2] <= ridge * v[3])
+                                for t, v in ps],
+            "conv_linear_all_launches": conv_all, "instances": instances,
+            "instances_by_clients": by_bucket}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="KT", choices=sorted(CONFIGS) + ["K2-dpsgd"])
+    ap.add_argument("--opt", default="sgd")
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--probe", default=None, help="conv launch tag to time (default: auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-instances", action="store_true",
+                    help="skip the instrumented per-launch-shape round")
+    ap.add_argument("--no-k2", action="store_true",
+                    help="N=1 KT run: skip the K2 block (BASELINE.json's 1-GPU config)")
+    ap.add_argument("--rounds-target", type=float, default=0.91,
+                    help="rounds-to-accuracy half of the metric (K1 MNIST proxy); 0 disables")
+    ap.add_argument("--rounds-max", type=int, default=30)
+    ap.add_argument("--fp32-data", action="store_true",
+                    help="pre-normalised fp32 shards instead of uint8 images + on-device transform")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (multi-rank path on a 1-GPU box)")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="concurrent client lanes per GPU (default: planner / FH_LANES)")
+    args = ap.parse_args()
+    world, rank, dev = setup(args)
+    if args.config == "K2-dpsgd":
+        if world != 1:
+            raise SystemExit("K2-dpsgd: one GPU only")
+        out = run_dpsgd(args, dev, args.steps, args.warmup)
+        out["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("FH_")}
+        print(json.dumps(out), flush=True)
+        return
+    out = run_config(args.config, args, world, rank, dev, args.steps, args.warmup, rtt=True)
+    # BASELINE.json's only 1-GPU config (K2: SimpleCNN, 32 Dirichlet(0.5) clients, update DP
+    # eps=1.0 timed) rides along the default N=1 line, measured the same way
+    if world == 1 and args.config == "KT" and not args.no_k2:
+        k2 = run_config("K2", args, world, rank, dev, max(args.steps, 3), args.warmup)
+        if k2 is not None:
+            out["k2"] = {k: k2[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
+                                           "warmup", "config", "achieved_tflops_step",
+                                           "round_frac", "roofline", "roofline_hbm",
+                                           "conv_linear_all_launches", "instances",
+                                           "instances_by_clients", "cpu_baseline") if k in k2}
+    if rank == 0:
+        # every FH_* knob in the environment (diagnostics / A-B switches): none is set in a
+        # driver run; a line measured with one set says so here
+        out["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("FH_")}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

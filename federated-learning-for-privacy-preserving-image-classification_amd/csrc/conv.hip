@@ -26,6 +26,7 @@
 namespace fh {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // OP_DGRAD_S2: DGRAD of a stride-2 convolution (3x3/p1 or 1x1/p0) split into the four
 // output-pixel parity phases (ih % 2, iw % 2).  A phase's pixels receive only the taps whose
@@ -471,42 +472,101 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
 
 namespace fh {
 
-// Split-K sums, deterministic: 64 outputs per block, 4 wave-groups each summing an
-// interleaved quarter of the splits, combined in a fixed order.  Blocks past the
-// weight part reduce the conv-bias partials the WGRAD kernel folded in.
+// Split-K sums of the WGRAD slabs, deterministic (r03).  A thread owns four consecutive
+// outputs (one float4 of every split's slab) and one of G contiguous ranges of the splits,
+// summed in split order with eight loads in flight; the G range sums are added in range
+// order through LDS.  A block covers 256 / G float4s; G grows with the split count (about
+// eight splits per thread), so a one-client layer with 128 splits still spreads over
+// thousands of threads.  The r02 kernel ran 64 scalar outputs per block (73,728 blocks for
+// one 128x8x8 layer of 32 clients: 35 us for 56 MB).
+// Blocks past the weight part reduce the conv-bias partials the WGRAD kernel folded in.
+template <int G>
 __global__ void __launch_bounds__(256)
 splitk_sum_kernel(const float* __restrict__ part, float* __restrict__ dw, int64_t dw_cs, int splits,
                   int MN, int wblocks, const float* __restrict__ bpart, float* __restrict__ db,
                   int64_t db_cs, int Mb) {
-    __shared__ float red[4][64];
-    const int z = blockIdx.y, l = threadIdx.x & 63, q = threadIdx.x >> 6;
+    constexpr int C = 256 / G;  // float4 columns per block
+    __shared__ float4 red[G > 1 ? 256 : 1];
+    const int z = blockIdx.y, t = threadIdx.x;
     const bool is_w = (int)blockIdx.x < wblocks;
-    const int e = (is_w ? blockIdx.x : blockIdx.x - wblocks) * 64 + l;
+    const int blk = is_w ? blockIdx.x : blockIdx.x - wblocks;
     const int lim = is_w ? MN : Mb;
     const float* src = is_w ? part + (int64_t)z * splits * MN : bpart + (int64_t)z * splits * Mb;
-    float s = 0.f;
-    if (e < lim) {
-        // loads of 8 splits issued together, then added in split order (same sum, bit for
-        // bit, as the one-at-a-time loop; without this every split is a dependent HBM trip)
-        for (int i0 = q; i0 < splits; i0 += 4 * 8) {
-            float v[8];
+    const int e0 = (blk * C + t % C) * 4;
+    const int piece = t / C;
+    const int s0 = (int)((int64_t)splits * piece / G), s1 = (int)((int64_t)splits * (piece + 1) / G);
+    const bool vec = (lim & 3) == 0;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e0 < lim) {
+        for (int i0 = s0; i0 < s1; i0 += 8) {
+            float4 v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int i = i0 + 4 * j;
-                v[j] = i < splits ? src[(int64_t)i * lim + e] : 0.f;
+                const int i = i0 + j;
+                const float* p = src + (int64_t)i * lim + e0;
+                if (i >= s1) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                else if (vec) v[j] = *reinterpret_cast<const float4*>(p);
+                else v[j] = make_float4(p[0], e0 + 1 < lim ? p[1] : 0.f, e0 + 2 < lim ? p[2] : 0.f,
+                                        e0 + 3 < lim ? p[3] : 0.f);
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                if (i0 + 4 * j < splits) s += v[j];
+                if (i0 + j < s1) {
+                    acc.x += v[j].x;
+                    acc.y += v[j].y;
+                    acc.z += v[j].z;
+                    acc.w += v[j].w;
+                }
         }
     }
-    red[q][l] = s;
-    __syncthreads();
-    if (q == 0 && e < lim) {
-        const float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
-        if (is_w) dw[z * dw_cs + e] = v;
-        else db[z * db_cs + e] = v;
+    if constexpr (G > 1) {
+        red[t] = acc;
+        __syncthreads();
+        if (piece != 0) return;
+#pragma unroll
+        for (int g = 1; g < G; ++g) {
+            const float4 o = red[t + C * g];
+            acc.x += o.x;
+            acc.y += o.y;
+            acc.z += o.z;
+            acc.w += o.w;
+        }
     }
+    if (e0 >= lim) return;
+    float* o = is_w ? dw + z * dw_cs + e0 : db + z * db_cs + e0;
+    if (vec && ((uintptr_t)o & 15) == 0) {
+        *reinterpret_cast<float4*>(o) = acc;
+    } else {
+        o[0] = acc.x;
+        if (e0 + 1 < lim) o[1] = acc.y;
+        if (e0 + 2 < lim) o[2] = acc.z;
+        if (e0 + 3 < lim) o[3] = acc.w;
+    }
+}
+
+// the WGRAD reduction launch: dW[z] = sum over splits of part[z][split] (and db from bpart)
+static int splitk_sum(const float* part, float* dw, int64_t dw_cs, int splits, int MN,
+                      const float* bpart, float* db, int64_t db_cs, int M, int nclients,
+                      hipStream_t st) {
+    int G = 1;
+    while (G < 16 && splits >= 16 * G) G *= 2;  // ~8-15 splits per thread
+    const int per = 1024 / G;                   // outputs per block
+    const int wblocks = (int)ceil_div(MN, per);
+    const int bblocks = db ? (int)ceil_div(M, per) : 0;
+    const dim3 grid(wblocks + bblocks, nclients);
+#define FH_SKS(GV)                                                                              \
+    if (G == GV) {                                                                              \
+        FH_LAUNCH(splitk_sum_kernel<GV>, grid, dim3(256), 0, st, part, dw, dw_cs, splits, MN,  \
+                  wblocks, bpart, db, db_cs, M);                                                \
+        return FH_OK;                                                                           \
+    }
+    FH_SKS(1)
+    FH_SKS(2)
+    FH_SKS(4)
+    FH_SKS(8)
+    FH_SKS(16)
+#undef FH_SKS
+    return FH_E_UNSUPPORTED;
 }
 
 // DGRAD split-K epilogue with BatchNorm backward statistics (DConvArgs::bnx and friends)
@@ -1378,6 +1438,26 @@ static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
     return p;
 }
 
+// r03 quadrant-wave WGRAD (dconv_kernels.h dwgrad_q_kernel): 32x32 (co, ci) tiles, 128-pixel
+// stages, three 45 KB workgroups per CU; splits of the stage run fill ~kDwqBlocks workgroups.
+// FH_DWGRAD_Q=0 runs the r02 kernel instead (A/B on the box only).
+static const int g_dwq = env_int("FH_DWGRAD_Q", 1);
+static const int kDwqBlocks = env_int("FH_DWQ_BLOCKS", 512);
+// stage pixels: 128 = one buffer, stored between two barriers (default: the best of the
+// r03 sweep, profiles/r03_dwq/); 64 = two 64-pixel buffers, the next stage stored half-way
+// through this one's MFMAs, one barrier per stage (FH_DWQ_SPX=64)
+static const int kDwqSpx = env_int("FH_DWQ_SPX", 128) == 64 ? 64 : 128;
+static DWPlan plan_dwq(int cout, int cin, int batch, int w, int nclients) {
+    DWPlan p{1, 1, 4, kDwqSpx / w, 1, 1};
+    const int64_t tiles = (int64_t)(cout / 32) * (cin / 32) * nclients;
+    const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)kDwqSpx);
+    const int want = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(fill(kDwqBlocks), tiles)),
+                                            std::max(1, nst / kDwgradMinSps));
+    p.sps = (int)ceil_div(nst, kDwgradForceSplits > 0 ? std::min(kDwgradForceSplits, nst) : want);
+    p.splits = (int)ceil_div(nst, p.sps);
+    return p;
+}
+
 // RGB first layer (cin == 3): (ci,kh,kw) = 27 on the MFMA lanes, pixels split 4 ways
 static bool dwgrad_small_supported(int cin, int cout, int h, int w, int kh, int kw, int stride,
                                    int pad) {
@@ -1803,11 +1883,7 @@ extern "C" int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float
               p.splits, idx, i_cs, y, y_cs, gh, gw);
     FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad");
     const int MN = cout * 9;
-    const int wblocks = (int)ceil_div(MN, 64);
-    const int bblocks = db ? (int)ceil_div(cout, 64) : 0;
-    FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
-              (const float*)part, dw, dw_cs, p.splits, MN, wblocks, (const float*)bpart, db, db_cs,
-              cout);
+    if (const int _r = splitk_sum((const float*)part, dw, dw_cs, p.splits, MN, (const float*)bpart, db, db_cs, cout, nclients, st)) return _r;
     FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad reduce");
     return FH_OK;
 }
@@ -1819,7 +1895,9 @@ extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int
     if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
     size_t direct = 0;
     if (dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad))  // (misaligned data: igemm)
-        direct = dwgrad_ws_bytes(plan_dwgrad(cout, cin, batch, w_, nclients), nclients, cout, cin * 9);
+        direct = dwgrad_ws_bytes(g_dwq ? plan_dwq(cout, cin, batch, w_, nclients)
+                                       : plan_dwgrad(cout, cin, batch, w_, nclients),
+                                 nclients, cout, cin * 9);
     if (dwgrad_small_supported(cin, cout, h, w_, kh, kw, stride, pad))
         direct = dwgrad_ws_bytes(plan_dwgrad_small(cout, batch, w_, nclients), nclients, cout, cin * 9);
     if (dwgrad_s2_supported(cin, cout, h, w_, kh, kw, stride, pad))
@@ -1871,11 +1949,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
                   (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0);
         FH_LAUNCH_CHECK("conv2d_wgrad c1");
         const int MN = cout * 9;
-        const int wblocks = (int)ceil_div(MN, 64);
-        const int bblocks = db ? (int)ceil_div(cout, 64) : 0;
-        FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
-                  (const float*)part, dw, dw_cs, p.splits, MN, wblocks, (const float*)bpart, db,
-                  db_cs, cout);
+        if (const int _r = splitk_sum((const float*)part, dw, dw_cs, p.splits, MN, (const float*)bpart, db, db_cs, cout, nclients, st)) return _r;
         FH_LAUNCH_CHECK("conv2d_wgrad c1 reduce");
         return FH_OK;
     }
@@ -1897,11 +1971,41 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         else FH_LAUNCH((dconv_wgrad_small_kernel<8, 3>), grid, dim3(256), 0, st, d);
         FH_LAUNCH_CHECK("conv2d_wgrad small-cin");
         const int MN = a.M * a.N;
-        const int wblocks = (int)ceil_div(MN, 64);
-        const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
-        FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
-                           (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
-                           (const float*)d.bias_part, db, db_cs, a.M);
+        if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)d.bias_part, db, db_cs, a.M, nclients, st)) return _r;
+        FH_LAUNCH_CHECK("conv2d_wgrad reduce");
+        return FH_OK;
+    }
+    if (aligned && g_dwq && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
+        const DWPlan p = plan_dwq(cout, cin, batch, w_, nclients);
+        DWArgs d{};
+        d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
+        d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
+        d.splits = p.splits; d.stages_per_split = p.sps; d.xcd = g_xcd_remap;
+        d.in_scale = in_scale; d.in_shift = in_shift; d.aff_cs = aff_cs;
+        hipStream_t st = as_stream(stream);
+        dim3 grid((unsigned)p.splits, (unsigned)((cout / 32) * (cin / 32)), (unsigned)nclients);
+        if (p.splits == 1) {  // one split per tile: dW / db straight from the kernel
+            d.dw = dw; d.dw_cs = dw_cs; d.db = db; d.db_cs = db_cs;
+        } else {
+            const size_t need = dwgrad_ws_bytes(p, nclients, a.M, a.N);
+            FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
+            d.part = (float*)workspace;
+            const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
+            d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
+        }
+        if (p.sr * w_ == 64) {
+            if (w_ == 32) FH_LAUNCH((dwgrad_q_kernel<32, 64, true>), grid, dim3(256), 0, st, d);
+            else if (w_ == 16) FH_LAUNCH((dwgrad_q_kernel<16, 64, true>), grid, dim3(256), 0, st, d);
+            else FH_LAUNCH((dwgrad_q_kernel<8, 64, true>), grid, dim3(256), 0, st, d);
+        } else {
+            if (w_ == 32) FH_LAUNCH((dwgrad_q_kernel<32, 128, false>), grid, dim3(256), 0, st, d);
+            else if (w_ == 16) FH_LAUNCH((dwgrad_q_kernel<16, 128, false>), grid, dim3(256), 0, st, d);
+            else FH_LAUNCH((dwgrad_q_kernel<8, 128, false>), grid, dim3(256), 0, st, d);
+        }
+        FH_LAUNCH_CHECK("conv2d_wgrad direct (quadrant waves)");
+        if (p.splits == 1) return FH_OK;
+        const int MN = a.M * a.N;
+        if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)d.bias_part, db, db_cs, a.M, nclients, st)) return _r;
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
         return FH_OK;
     }
@@ -1926,11 +2030,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         if (rc) return rc;
         FH_LAUNCH_CHECK("conv2d_wgrad direct");
         const int MN = a.M * a.N;
-        const int wblocks = (int)ceil_div(MN, 64);
-        const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
-        FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
-                           (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
-                           (const float*)d.bias_part, db, db_cs, a.M);
+        if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)d.bias_part, db, db_cs, a.M, nclients, st)) return _r;
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
         return FH_OK;
     }
@@ -1951,11 +2051,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         else FH_LAUNCH((dconv_wgrad_kernel<8, 2, 1, 2, 8, 2>), grid, dim3(256), 0, st, d);
         FH_LAUNCH_CHECK("conv2d_wgrad direct s2");
         const int MN = a.M * a.N;
-        const int wblocks = (int)ceil_div(MN, 64);
-        const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
-        FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
-                  (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
-                  (const float*)d.bias_part, db, db_cs, a.M);
+        if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)d.bias_part, db, db_cs, a.M, nclients, st)) return _r;
         FH_LAUNCH_CHECK("conv2d_wgrad s2 reduce");
         return FH_OK;
     }
@@ -1986,11 +2082,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
     if (rc) return rc;
     FH_LAUNCH_CHECK("conv2d_wgrad");
     const int MN = a.M * a.N;
-    const int wblocks = (int)ceil_div(MN, 64);
-    const int bblocks = db ? (int)ceil_div(a.M, 64) : 0;
-    FH_LAUNCH(splitk_sum_kernel, dim3(wblocks + bblocks, nclients), dim3(256), 0, st,
-                       (const float*)workspace, dw, dw_cs, p.splits, MN, wblocks,
-                       (const float*)a.bias_part, db, db_cs, a.M);
+    if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)a.bias_part, db, db_cs, a.M, nclients, st)) return _r;
     FH_LAUNCH_CHECK("conv2d_wgrad reduce");
     return FH_OK;
 }

@@ -989,6 +989,11 @@ struct DWArgs {
     const float* in_shift;
     int64_t aff_cs;
     int xcd;  // host: XCD-aware workgroup order (xcd_block)
+    // dwgrad_q_kernel with splits == 1: dW (and db when non-null) written directly
+    float* dw;
+    int64_t dw_cs;
+    float* db;
+    int64_t db_cs;
 };
 
 // Two workgroups per CU when the double-buffered staging fits twice in the 160 KB LDS:
@@ -1235,6 +1240,214 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S, SDY
             const int m = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
 #pragma unroll
             for (int s = 0; s < 9; ++s) op[(int64_t)m * a.N + ci * 9 + s] = acc[s][r];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// WGRAD, 3x3 / stride 1 / pad 1 (r03): dW[co][ci][kh][kw] = sum_pix dY[co][pix] X[ci][pix+s].
+//
+// A workgroup owns a 32x32 (co, ci) tile of one client and a run of SPX-pixel stages; each
+// of its four waves owns one 16x16 quadrant of the tile for all nine shifts (nine
+// v_mfma_f32_16x16x4_f32 accumulators, 36 registers) and walks EVERY pixel of the stage, four
+// pixels (the MFMA's k) at a time: one dY operand and nine shifted patch operands (the shift
+// is an LDS immediate) per nine MFMAs.  Against the r01/r02 kernel (32x32x2 MFMAs, 144
+// accumulator registers per wave, pixels split over the four waves) this
+//   * drops the cross-wave LDS combine of the epilogue — a wave's sums are final for its
+//     split, the tile goes out through one LDS transpose as coalesced rows;
+//   * fits three workgroups in a CU (<= 53 KB of LDS, <= 168 registers): dY [32 co][SPX+2]
+//     and the patch [32 ci][rows][W+4], both pitches = 2 (mod 4) so a 16-lane x 2-k operand
+//     read touches 32 distinct banks;
+//   * keeps the summation order a pure function of the plan (per split: stages in order,
+//     pixels in order inside a stage; splits summed in order by splitk_sum_kernel).
+// DB = false: one 128-pixel staging buffer; the next stage's global loads go to registers
+// while this stage is multiplied and are written to LDS between two barriers.
+// DB = true: two 64-pixel buffers; the next stage is written to the other buffer half-way
+// through this stage's MFMAs, one barrier per stage (the workgroups on a CU start together,
+// so with one buffer their store phases coincide and nothing hides them).
+// splits == 1 (many tiles): dW / db written directly, no reduction launch.
+constexpr int dwq_buf_floats(int W, int SPX) {
+    const int SR = SPX / W, SEGR = SR < W ? SR : W, NI = SR / SEGR;
+    return 32 * (SPX + 2) + 32 * (NI * (SEGR + 2) * (W + 4) + 2);
+}
+constexpr int dwq_lds_floats(int W, int SPX, bool DB) {
+    const int st = (DB ? 2 : 1) * dwq_buf_floats(W, SPX);
+    return st > 32 * 289 + 128 ? st : 32 * 289 + 128;
+}
+
+template <int W, int SPX, bool DB>
+__global__ void __launch_bounds__(256, 3) dwgrad_q_kernel(const DWArgs a) {
+    constexpr int H = W, HW = H * W;
+    constexpr int SR = SPX / W;
+    constexpr int SEGR = SR < H ? SR : H, NI = SR / SEGR;
+    constexpr int PRS = SEGR + 2, PW = W + 4, PR = NI * PRS;
+    constexpr int CSTR = PR * PW + 2;  // = 2 (mod 4): lanes (m, k) -> banks 2m*odd + k, distinct
+    constexpr int DP = SPX + 2;        // dY pitch, = 2 (mod 4) likewise
+    constexpr int DSZ = 32 * DP, BUF = dwq_buf_floats(W, SPX);
+    constexpr int DQ = SPX / 4, CPP = 256 / DQ, NDY = 32 / CPP;  // dY float4s per thread
+    constexpr int PQ = W / 4, NPQ = 32 * PR * PQ;               // patch float4s
+    constexpr int NPT = (NPQ + 255) / 256;                       // ... per thread
+    constexpr int RP = 289;                                      // epilogue row pitch
+    static_assert(256 % DQ == 0 && 32 % CPP == 0, "staging");
+    static_assert(SR % SEGR == 0 && (SR <= H || SR % H == 0), "stage geometry");
+    static_assert(!DB || SR % 2 == 0 || SR == 1, "half-stage store point");
+    static_assert(dwq_lds_floats(W, SPX, DB) * 4 <= 160 * 1024 / 3, "three workgroups per CU");
+    __shared__ float smem[dwq_lds_floats(W, SPX, DB)];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cq = wid & 1, nq = wid >> 1;  // this wave's 16x16 quadrant (co half, ci half)
+    int bx, by, bz;
+    xcd_block(a.xcd != 0, bx, by, bz);
+    const int split = bx, z = bz;
+    const int ntile_ci = a.cin / 32;
+    const int co0 = (by / ntile_ci) * 32, ci0 = (by % ntile_ci) * 32;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int nst = (cnt * HW + SPX - 1) / SPX;
+    const int sbeg = split * a.stages_per_split;
+    const int send = min(nst, sbeg + a.stages_per_split);
+    const float* xz = a.x + z * a.x_cs;
+    const float* dyz = a.dy + z * a.dy_cs;
+    const bool do_bias = (a.bias_part != nullptr || a.db != nullptr) && ci0 == 0;
+
+    // zero halo columns (image columns -1 and W): written once, never overwritten
+    for (int q = tid; q < (DB ? 2 : 1) * 32 * PR; q += 256) {
+        const int b = q / (32 * PR), r0 = q % (32 * PR);
+        float* r = smem + b * BUF + DSZ + (r0 / PR) * CSTR + (r0 % PR) * PW;
+        r[1] = 0.f;
+        r[W + 2] = 0.f;
+    }
+
+    const int dq = tid % DQ, dco = tid / DQ;  // dY: pixel quad, first channel row
+    float4 rd[NDY], rp[NPT];
+    float bsc[NPT], bsh[NPT];
+    auto load = [&](int st) {
+        const int gp = st * SPX + 4 * dq;
+        const int img = gp / HW, pix = gp % HW;
+        const bool ok = img < cnt;
+        const float* src = dyz + ((int64_t)(img * a.M + co0 + dco) * HW + pix);
+#pragma unroll
+        for (int i = 0; i < NDY; ++i)
+            rd[i] = ok ? *reinterpret_cast<const float4*>(src + (int64_t)i * CPP * HW)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int img0 = (st * SPX) / HW, y0 = ((st * SPX) % HW) / W;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int q = tid + 256 * i;
+            const int quad = q % PQ, row = q / PQ, ci = row / PR, pr = row % PR;
+            const int im = img0 + pr / PRS, y = y0 + pr % PRS - 1;
+            const bool okp = (NPQ % 256 == 0 || q < NPQ) && im < cnt && (unsigned)y < (unsigned)H;
+            rp[i] = okp ? *reinterpret_cast<const float4*>(
+                              xz + ((int64_t)(im * a.cin + ci0 + ci) * HW + y * W + 4 * quad))
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.in_scale != nullptr) {  // applied in store(): the loads stay in flight
+                bsc[i] = okp ? a.in_scale[z * a.aff_cs + ci0 + ci] : 1.f;
+                bsh[i] = okp ? a.in_shift[z * a.aff_cs + ci0 + ci] : 0.f;
+            }
+        }
+    };
+    auto store = [&](int b) {
+        float* D = smem + b * BUF;
+        float* P = D + DSZ;
+#pragma unroll
+        for (int i = 0; i < NDY; ++i) {
+            float2* d = reinterpret_cast<float2*>(D + (dco + i * CPP) * DP + 4 * dq);
+            d[0] = make_float2(rd[i].x, rd[i].y);
+            d[1] = make_float2(rd[i].z, rd[i].w);
+        }
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int q = tid + 256 * i;
+            if (NPQ % 256 != 0 && q >= NPQ) continue;
+            const int quad = q % PQ, row = q / PQ, ci = row / PR, pr = row % PR;
+            if (a.in_scale != nullptr) rp[i] = bn_relu4(rp[i], bsc[i], bsh[i]);
+            float2* d = reinterpret_cast<float2*>(P + ci * CSTR + pr * PW + 2 + 4 * quad);
+            d[0] = make_float2(rp[i].x, rp[i].y);
+            d[1] = make_float2(rp[i].z, rp[i].w);
+        }
+    };
+
+    f32x4 acc[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    const int m = lane & 15, kk = lane >> 4;
+    const int a_off = (cq * 16 + m) * DP + kk;
+    const int b_off = DSZ + (nq * 16 + m) * CSTR + kk + 1;
+    const bool bias_wave = do_bias && nq == 0;
+    auto rows = [&](int b, int r0, int r1) {
+        const float* Ab = smem + b * BUF + a_off;
+        const float* Bb = smem + b * BUF + b_off;
+#pragma unroll 1
+        for (int r = r0; r < r1; ++r) {
+            const float* Ar = Ab + r * W;
+            const float* Br = Bb + ((r / SEGR) * PRS + r % SEGR) * PW;
+#pragma unroll
+            for (int g = 0; g < W / 4; ++g) {
+                const float av = Ar[4 * g];
+                float bv[9];
+#pragma unroll
+                for (int s = 0; s < 9; ++s) bv[s] = Br[(s / 3) * PW + 4 * g + (s % 3)];
+                if (bias_wave) bsum += av;
+#pragma unroll
+                for (int s = 0; s < 9; ++s)
+                    acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[s], acc[s], 0, 0, 0);
+            }
+        }
+    };
+
+    if (sbeg < send) {
+        load(sbeg);
+        store(0);
+        __syncthreads();
+        int b = 0;
+        for (int st = sbeg; st < send; ++st) {
+            const bool more = st + 1 < send;
+            if (more) load(st + 1);
+            if constexpr (DB) {
+                constexpr int HALF = SR / 2 > 0 ? SR / 2 : 1;
+                rows(b, 0, HALF);
+                if (more) store(b ^ 1);  // the other buffer: last read before the barrier
+                rows(b, HALF, SR);
+                __syncthreads();
+                b ^= 1;
+            } else {
+                rows(0, 0, SR);
+                if (more) {
+                    __syncthreads();  // every wave is done reading this stage
+                    store(0);
+                    __syncthreads();
+                }
+            }
+        }
+    }
+
+    // ---- epilogue: the tile through LDS as [co][ci*9 + s] rows, then coalesced stores ----
+    __syncthreads();
+    float* red = smem;
+#pragma unroll
+    for (int s = 0; s < 9; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            red[(cq * 16 + 4 * kk + j) * RP + (nq * 16 + m) * 9 + s] = acc[s][j];
+    float* bred = smem + 32 * RP;
+    if (bias_wave) bred[cq * 64 + lane] = bsum;
+    __syncthreads();
+    const bool direct = a.splits == 1 && a.dw != nullptr;
+    const int64_t slab = ((int64_t)z * a.splits + split) * a.M;
+    float* out = direct ? a.dw + z * a.dw_cs : a.part + slab * a.N;
+#pragma unroll 4
+    for (int e = tid; e < 32 * 288; e += 256) {
+        const int co = e / 288, n = e - co * 288;
+        out[(int64_t)(co0 + co) * a.N + ci0 * 9 + n] = red[co * RP + n];
+    }
+    if (do_bias && tid < 32) {  // lanes l, l+16, l+32, l+48 of a wave: the same co
+        const float* bb = bred + (tid >> 4) * 64 + (tid & 15);
+        const float v = ((bb[0] + bb[16]) + bb[32]) + bb[48];
+        if (direct) {
+            if (a.db != nullptr) a.db[z * a.db_cs + co0 + tid] = v;
+        } else {
+            a.bias_part[slab + co0 + tid] = v;
         }
     }
 }

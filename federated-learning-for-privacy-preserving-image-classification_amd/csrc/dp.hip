@@ -140,14 +140,10 @@ extern "C" int fh_dp_delta_sqnorm(const float* local, int64_t local_stride, cons
     FH_REQUIRE(num_clients >= 0 && nseg >= 0, "dp_delta_sqnorm: bad sizes");
     if (num_clients == 0 || nseg == 0) return FH_OK;
     FH_REQUIRE(local && seg_offsets && seg_sqnorm, "dp_delta_sqnorm: null pointer");
-    // A/B: FH_DP_SQ_THREADS=256 (the round-1 block size)
-    static const int threads = getenv("FH_DP_SQ_THREADS") ? atoi(getenv("FH_DP_SQ_THREADS")) : 1024;
-    if (threads == 256)
-        FH_LAUNCH(dp_sqnorm_kernel<256>, dim3(nseg, num_clients), dim3(256), 0, as_stream(stream),
-                  local, local_stride, global, global_stride, seg_offsets, nseg, seg_sqnorm);
-    else
+    // 1024 threads per (segment, client): r02 s3 measured the 256-thread block at 0.67 ms per
+    // K2 round on SimpleCNN's fc1.weight segment alone
     FH_LAUNCH(dp_sqnorm_kernel<1024>, dim3(nseg, num_clients), dim3(1024), 0, as_stream(stream),
-                       local, local_stride, global, global_stride, seg_offsets, nseg, seg_sqnorm);
+              local, local_stride, global, global_stride, seg_offsets, nseg, seg_sqnorm);
     FH_LAUNCH_CHECK("dp_delta_sqnorm");
     return FH_OK;
 }

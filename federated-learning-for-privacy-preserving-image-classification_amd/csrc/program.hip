@@ -17,6 +17,7 @@
 // while the same step is captured into a HIP graph and compares the two: a step that
 // contains anything the recorder cannot see (a memset, a copy, a kernel launched outside
 // libfedhip) makes the recording invalid and the caller replays the graph instead.
+#include <algorithm>
 #include <memory>
 #include <vector>
 
@@ -102,6 +103,41 @@ extern "C" int fh_graph_node_counts(void* graph, int32_t* kernels_out, int32_t* 
     }
     *kernels_out = k;
     *others_out = o;
+    return FH_OK;
+}
+
+// The recording is a faithful copy of the captured graph: the graph holds no work node
+// other than kernels (no memset / copy / foreign node types) and its kernels are the
+// recorded ones — the same function for every launch, compared as multisets of kernel
+// functions (node order in a graph is not launch order).  A libfedhip launch recorded on a
+// stream that was not being captured, or a foreign kernel captured beside the library's,
+// fails the comparison even when the counts agree.
+extern "C" int fh_program_matches_graph(void* program, void* graph, int32_t* match_out) {
+    auto* r = (Recorder*)program;
+    if (!r || !graph || !match_out) {
+        fh::set_error("fh_program_matches_graph: null argument");
+        return FH_E_INVALID;
+    }
+    *match_out = 0;
+    hipGraph_t g = (hipGraph_t)graph;
+    size_t n = 0;
+    FH_HIPCHK(hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
+    std::vector<hipGraphNode_t> nodes(n);
+    if (n) FH_HIPCHK(hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
+    std::vector<const void*> got, want;
+    for (size_t i = 0; i < n; ++i) {
+        hipGraphNodeType t;
+        FH_HIPCHK(hipGraphNodeGetType(nodes[i], &t), "hipGraphNodeGetType");
+        if (t == hipGraphNodeTypeEmpty) continue;
+        if (t != hipGraphNodeTypeKernel) return FH_OK;  // a memset / copy / other node
+        hipKernelNodeParams kp{};
+        FH_HIPCHK(hipGraphKernelNodeGetParams(nodes[i], &kp), "hipGraphKernelNodeGetParams");
+        got.push_back(kp.func);
+    }
+    for (const auto& k : r->kernels) want.push_back(k.func);
+    std::sort(got.begin(), got.end());
+    std::sort(want.begin(), want.end());
+    *match_out = got == want ? 1 : 0;
     return FH_OK;
 }
 

@@ -128,6 +128,7 @@ SIGNATURES = {
     "fh_record_begin": (I32, [P]),
     "fh_record_end": (I32, [P, P]),
     "fh_graph_node_counts": (I32, [P, P, P]),
+    "fh_program_matches_graph": (I32, [P, P, P]),
     "fh_program_launch": (I32, [P, P]),
     "fh_program_destroy": (I32, [P]),
     "fh_copy_bytes": (I32, [P, P, I64, P]),
@@ -177,16 +178,8 @@ def stream_handle(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-# Diagnostics only (timing ablations, tools/r02_ablate.sh): entry points named in
-# FH_ABLATE are not called at all, so a benchmark measures what the round would cost
-# without them.  The results are wrong by construction; never set it outside a timing probe.
-_ABLATE = frozenset(v for v in os.environ.get("FH_ABLATE", "").split(",") if v)
-
-
 def call(name: str, *args):
     """Invoke a status-returning entry point; raise FedHipError on failure."""
-    if name in _ABLATE:
-        return 0
     lib = load()
     rc = getattr(lib, name)(*args)
     if rc != 0:

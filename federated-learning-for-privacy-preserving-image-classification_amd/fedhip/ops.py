@@ -90,12 +90,14 @@ class LaunchProbe:
         ev.record()
         return (tag, ev)
 
-    def end(self, h, flops):
+    def end(self, h, flops, nbytes=0.0, clients=0):
+        """flops / nbytes: the launch's algorithmic work — every operand read
+        and every result written once; clients: its active-client count (bench.py buckets)."""
         if h is None:
             return
         e2 = torch.cuda.Event(enable_timing=True)
         e2.record()
-        self.records.append((h[0], h[1], e2, flops))
+        self.records.append((h[0], h[1], e2, flops, nbytes, clients))
 
     def reset(self):
         self.records, self.seen = [], {}
@@ -104,17 +106,31 @@ class LaunchProbe:
         torch.cuda.synchronize()
         if not self.records:
             return None
-        ms = [a.elapsed_time(b) for _, a, b, _ in self.records]
-        fl = [f for _, _, _, f in self.records]
+        ms = [r[1].elapsed_time(r[2]) for r in self.records]
+        fl = [r[3] for r in self.records]
         return {"launches": len(ms), "avg_ms": sum(ms) / len(ms), "flops_per_launch": sum(fl) / len(fl)}
 
     def by_tag(self):
         """{tag: (launches, total ms, total flops)} over every recorded launch."""
         torch.cuda.synchronize()
         out = {}
-        for tag, a, b, f in self.records:
+        for tag, a, b, f, _, _ in self.records:
             n, t, fl = out.get(tag, (0, 0.0, 0.0))
             out[tag] = (n + 1, t + a.elapsed_time(b), fl + f)
+        return out
+
+    BUCKETS = ((1, 1), (2, 8), (9, 32), (33, 1 << 30))
+
+    def by_tag_bucket(self):
+        """{(tag, "lo-hi"): (launches, total ms, total flops, total bytes)}: the same records
+        split by the launch's active-client count (1, 2-8, 9-32, >32)."""
+        torch.cuda.synchronize()
+        out = {}
+        for tag, a, b, f, nb, c in self.records:
+            lo, hi = next(bk for bk in self.BUCKETS if bk[0] <= max(c, 1) <= bk[1])
+            key = (tag, f"{lo}" if lo == hi else f"{lo}-{hi if hi < (1 << 30) else ''}")
+            n, t, fl, by = out.get(key, (0, 0, 0.0, 0.0))
+            out[key] = (n + 1, t + a.elapsed_time(b), fl + f, by + nb)
         return out
 
 
@@ -123,6 +139,18 @@ PROBE = LaunchProbe()
 
 def _conv_tag(kind, cin, h, w, cout, k, s):
     return f"conv_{kind}:c{cin}x{h}x{w}->{cout}k{k}s{s}"
+
+
+def _conv_bytes(nclients, batch, cin, h, wd, cout, k, stride, pad):
+    """Algorithmic HBM bytes of one conv launch (FWD, DGRAD or WGRAD alike): both activation
+    tensors and the weights, each once."""
+    oh = (h + 2 * pad - k) // stride + 1
+    ow = (wd + 2 * pad - k) // stride + 1
+    return 4.0 * nclients * (batch * (cin * h * wd + cout * oh * ow) + cout * cin * k * k)
+
+
+def _linear_bytes(nclients, batch, in_f, out_f, acts=2, weights=1):
+    return 4.0 * nclients * (batch * (acts - 1) * in_f + batch * out_f + weights * in_f * out_f)
 
 
 def _ws(device) -> Workspace:
@@ -168,11 +196,13 @@ class Program:
         return cls(handle, nk.value)
 
     def complete_for(self, graph) -> bool:
-        """True when the recording saw every work node of `graph` (captured in the same
-        pass): the same number of kernels and no memset / copy / foreign node."""
-        k, o = ctypes.c_int32(), ctypes.c_int32()
-        call("fh_graph_node_counts", graph.raw_cuda_graph(), ctypes.byref(k), ctypes.byref(o))
-        return o.value == 0 and k.value == self.kernels
+        """True when the recording is a faithful copy of `graph` (captured in the same pass):
+        no memset / copy / other node, and the graph's kernels are the recorded kernels
+        (multisets of kernel functions: a foreign kernel in the capture or a recorded
+        launch on another stream fails it even with equal counts)."""
+        m = ctypes.c_int32()
+        call("fh_program_matches_graph", self.handle, graph.raw_cuda_graph(), ctypes.byref(m))
+        return m.value == 1
 
     def launch(self, stream):
         call("fh_program_launch", self.handle, stream.cuda_stream)
@@ -213,11 +243,6 @@ def _ws_for(fn_name, device, *args):
 
 
 # ------------------------------------------------------------------ conv / linear
-# diagnostics only (timing ablations): linear layers with these input widths are skipped
-_ABLATE_LINEAR = frozenset(int(v) for v in __import__("os").environ.get("FH_ABLATE_LINEAR", "")
-                           .split(",") if v)
-
-
 def _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad):
     oh = (h + 2 * pad - k) // stride + 1
     ow = (wd + 2 * pad - k) // stride + 1
@@ -251,7 +276,8 @@ def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad,
         call("fh_conv2d_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y),
              _cs(y), _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
              int(relu), ptr(ws), nb, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad),
+              _conv_bytes(nclients, batch, cin, h, wd, cout, k, stride, pad), nclients)
     return y
 
 
@@ -279,7 +305,8 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
         call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx),
              _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
              int(accumulate), ptr(ws), nb, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad),
+              _conv_bytes(nclients, batch, cin, h, wd, cout, k, stride, pad), nclients)
     return dx
 
 
@@ -304,7 +331,10 @@ def conv2d_dgrad_s2_shortcut(dy, w, dy_sc, w_sc, dx, nclients, batch, cin, h, wd
          ptr(w_sc), _cs(w_sc), ptr(dx), _cs(dx), _counts(counts), nclients, batch, cin, h, wd,
          cout, int(accumulate), ptr(ws), nb, stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, 3, 2, 1) +
-              _conv_flops(nclients, batch, cin, h, wd, cout, 1, 2, 0))
+              _conv_flops(nclients, batch, cin, h, wd, cout, 1, 2, 0),
+              _conv_bytes(nclients, batch, cin, h, wd, cout, 3, 2, 1) +
+              _conv_bytes(nclients, batch, 0, h, wd, cout, 1, 2, 0) + 4.0 * nclients * cout * cin,
+              nclients)
     return True
 
 
@@ -318,7 +348,9 @@ def conv2d_c1_pool_fwd(x, w, bias, y, idx, nclients, batch, h, wd, cout, counts=
     call("fh_conv2d_c1_pool_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y),
          _cs(y), ptr(idx), _cs(idx), _counts(counts), nclients, batch, h, wd, cout, yh, yw,
          stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1))
+    pooled = nclients * batch * cout * (h // 2) * (wd // 2)  # fp32 y + uint8 argmax
+    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1),
+              4.0 * nclients * (batch * h * wd + cout * 9) + 5.0 * pooled, nclients)
     return y
 
 
@@ -333,7 +365,9 @@ def conv2d_c1_pool_wgrad(x, dpool, idx, y, dw, db, nclients, batch, h, wd, cout,
     call("fh_conv2d_c1_pool_wgrad", ptr(x), _cs(x), ptr(dpool), _cs(dpool), ptr(idx), _cs(idx),
          ptr(y), _cs(y), ptr(dw), _cs(dw), ptr(db), _cs(db), ptr(ws), nb, _counts(counts),
          nclients, batch, h, wd, cout, gh, gw, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1))
+    pooled = nclients * batch * cout * (h // 2) * (wd // 2)  # dpool + y fp32, argmax uint8
+    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1),
+              4.0 * nclients * (batch * h * wd + cout * 9) + 9.0 * pooled, nclients)
     return dw
 
 
@@ -352,19 +386,19 @@ def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pa
         call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db),
              _cs(db), ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k,
              stride, pad, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad))
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad),
+              _conv_bytes(nclients, batch, cin, h, wd, cout, k, stride, pad), nclients)
     return dw
 
 
 def linear_fwd(x, w, bias, y, nclients, batch, in_f, out_f, relu=False, counts=None):
-    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
-        return None
     require_device(x, "x")
     ws, nb = _ws_for("fh_linear_fwd_workspace", x.device, nclients, batch, in_f, out_f)
     ev = PROBE.begin(f"linear_fwd:{in_f}->{out_f}")
     call("fh_linear_fwd", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y),
          _counts(counts), nclients, batch, in_f, out_f, int(relu), ptr(ws), nb, stream_handle())
-    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f)
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f,
+              _linear_bytes(nclients, batch, in_f, out_f), nclients)
     return y
 
 
@@ -372,8 +406,6 @@ def linear_fwd_dropout(x, w, bias, y, mask, nclients, batch, in_f, out_f, p_drop
                        relu=True, seed=0, counts=None, seed_dev=None):
     """linear_fwd + dropout_fwd in one product (fh_linear_fwd_dropout): y is the dropped
     output, mask the keep-mask (drop_mode 1 generates it, 2 reads it)."""
-    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
-        return None
     require_device(x, "x")
     ws, nb = _ws_for("fh_linear_fwd_workspace", x.device, nclients, batch, in_f, out_f)
     ev = PROBE.begin(f"linear_fwd:{in_f}->{out_f}")
@@ -381,29 +413,28 @@ def linear_fwd_dropout(x, w, bias, y, mask, nclients, batch, in_f, out_f, p_drop
          _cs(y), ptr(mask), _cs(mask), _counts(counts), nclients, batch, in_f, out_f, int(relu),
          int(drop_mode), float(p_drop), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), ptr(ws), nb,
          stream_handle())
-    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f)
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f,
+              _linear_bytes(nclients, batch, in_f, out_f), nclients)
     return y
 
 
 def linear_dgrad(dy, w, dx, nclients, batch, in_f, out_f, counts=None):
-    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
-        return None
     ws, nb = _ws_for("fh_linear_dgrad_workspace", dy.device, nclients, batch, in_f, out_f)
     ev = PROBE.begin(f"linear_dgrad:{in_f}->{out_f}")
     call("fh_linear_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx), _counts(counts),
          nclients, batch, in_f, out_f, ptr(ws), nb, stream_handle())
-    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f)
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f,
+              _linear_bytes(nclients, batch, in_f, out_f), nclients)
     return dx
 
 
 def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
-    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
-        return None
     ws, nb = _ws_for("fh_linear_wgrad_workspace", x.device, nclients, batch, in_f, out_f)
     ev = PROBE.begin(f"linear_wgrad:{in_f}->{out_f}")
     call("fh_linear_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
          ptr(ws), nb, _counts(counts), nclients, batch, in_f, out_f, stream_handle())
-    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f)
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f,
+              _linear_bytes(nclients, batch, in_f, out_f), nclients)
     return dw
 
 
@@ -419,14 +450,13 @@ def linear_bwd_fused(x, dy, w, dw, db, dx, nclients, batch, in_f, out_f, mask=No
     if not (batch <= 32 and in_f % _SKINNY_IN == 0 and out_f % 32 == 0 and dy.data_ptr() % 16 == 0
             and dy.stride(0) % 4 == 0 and w.stride(0) % 4 == 0):
         return False
-    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
-        return True
     ev = PROBE.begin(f"linear_bwd:{in_f}->{out_f}")
     call("fh_linear_bwd_fused", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dw),
          _cs(dw), ptr(db), _cs(db), ptr(dx), _cs(dx), ptr(mask), _cs(mask), float(p_drop),
          ptr(relu_ref), _cs(relu_ref), _counts(counts), nclients, batch, in_f, out_f,
          stream_handle())
-    PROBE.end(ev, 4.0 * nclients * batch * in_f * out_f)
+    PROBE.end(ev, 4.0 * nclients * batch * in_f * out_f,
+              _linear_bytes(nclients, batch, in_f, out_f, acts=3, weights=2), nclients)
     return True
 
 
@@ -436,30 +466,37 @@ def linear_head_ce(x, w, bias, targets, logits, dlogits, dw, db, dx, nclients, b
     """Last linear layer forward + cross-entropy (ce_fwd_bwd's outputs) + that layer's
     backward + the dropout/ReLU backward of its input, one launch per client
     (fh_linear_head_ce)."""
-    if in_f in _ABLATE_LINEAR:  # diagnostics only (_lib._ABLATE)
-        return
     ev = PROBE.begin(f"linear_head:{in_f}->{num_classes}")
     call("fh_linear_head_ce", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(targets),
          _cs(targets), ptr(logits), _cs(logits), ptr(dlogits), _cs(dlogits), ptr(loss_out),
          ptr(acc_loss), ptr(acc_correct), ptr(acc_seen), ptr(reset), ptr(dw), _cs(dw), ptr(db),
          _cs(db), ptr(dx), _cs(dx), ptr(mask), _cs(mask), float(p_drop), int(bool(relu_in)),
          _counts(counts), nclients, batch, in_f, num_classes, stream_handle())
-    PROBE.end(ev, 6.0 * nclients * batch * in_f * num_classes)
+    PROBE.end(ev, 6.0 * nclients * batch * in_f * num_classes,
+              _linear_bytes(nclients, batch, in_f, num_classes, acts=3, weights=2), nclients)
 
 
 def conv2d_persample_sqnorm(x, dy, sqnorm, nclients, batch, cin, h, wd, cout, k, stride, pad,
                             with_bias=True, counts=None):
     ws, nb = _ws_for("fh_conv2d_persample_sqnorm_workspace", x.device, nclients, batch, cin, h,
                      wd, cout, k, k, stride, pad)
+    # per-image weight-gradient norms: the WGRAD product per image (2 * MACs per image)
+    ev = PROBE.begin(_conv_tag("psnorm", cin, h, wd, cout, k, stride))
     call("fh_conv2d_persample_sqnorm", ptr(x), _cs(x), ptr(dy), _cs(dy), int(with_bias),
          ptr(sqnorm), ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k,
          stride, pad, stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad),
+              _conv_bytes(nclients, batch, cin, h, wd, cout, k, stride, pad) -
+              4.0 * nclients * cout * cin * k * k, nclients)
 
 
 def linear_persample_sqnorm(x, dy, sqnorm, nclients, batch, in_f, out_f, with_bias=True,
                             counts=None):
+    ev = PROBE.begin(f"linear_psnorm:{in_f}->{out_f}")
     call("fh_linear_persample_sqnorm", ptr(x), _cs(x), ptr(dy), _cs(dy), int(with_bias),
          ptr(sqnorm), _counts(counts), nclients, batch, in_f, out_f, stream_handle())
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f,
+              _linear_bytes(nclients, batch, in_f, out_f, weights=0), nclients)
 
 
 def dpsgd_clip_coef(sqnorm, coef, nclients, batch, max_norm, counts=None):

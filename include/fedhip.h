@@ -503,6 +503,14 @@ int fh_stream_destroy(void* stream);
 int fh_record_begin(void** program_out);
 int fh_record_end(void* program, int32_t* kernels_out);
 int fh_graph_node_counts(void* graph, int32_t* kernels_out, int32_t* others_out);
+
+/*
+ * fh_program_matches_graph: *match_out = 1 when `program` (fh_record_begin/end) is a faithful
+ * copy of the captured hipGraph_t `graph`: no non-kernel work node in the graph, and the
+ * graph's kernel functions equal the recorded ones as multisets.  0 otherwise (the caller
+ * replays the graph).  Stronger than comparing fh_graph_node_counts with the recorded count.
+ */
+int fh_program_matches_graph(void* program, void* graph, int32_t* match_out);
 int fh_program_launch(void* program, void* stream);
 int fh_program_destroy(void* program);
 /* dst[0:nbytes) = src[0:nbytes) by a kernel (16-B aligned, nbytes % 16 == 0): the per-step

@@ -1,6 +1,10 @@
-"""BASELINE.json's multi-GPU configs, one GPU's slice each, as whole rounds through the
-product path (fedhip.round.RankRound) against the CPU oracle.
+"""BASELINE.json's configs as whole rounds through the product path
+(fedhip.round.RankRound) against the CPU oracle — K2 (its only 1-GPU config) and one GPU's
+slice of each multi-GPU config.
 
+  K2  MNIST SimpleCNN (dropout 0.25 on, as the reference model), Dirichlet(0.5) shards
+      from the reference partitioner, update-level DP eps=1.0 — the HIP run's dropout
+      masks are replayed in the oracle
   K3  CIFAR-10 ResNet-8 [1,1,1], non-IID clients, update-level DP eps=4.0
   K4  CIFAR-10 "ResNet-18" = FederatedResNet [2,2,2], 5 local epochs,
       update compression on (top-k 0.9, the reference TopKSparsificationCompressor's
@@ -41,6 +45,16 @@ DEV = torch.device("cuda")
 B = 32
 
 
+def k2_sizes():
+    """Dirichlet(0.5) shards of 240 MNIST labels over 5 clients, reference partitioner
+    (data_loader.py:139-177) + 90 % train split."""
+    labels = np.random.default_rng(3).integers(0, 10, size=240)
+    random.seed(0)
+    np.random.seed(0)
+    parts = partition(labels, 5, "non_iid", 0.5)
+    return train_split_sizes([len(parts.get(c, [])) for c in range(5)], 0.1)
+
+
 def k5_sizes():
     """Dirichlet(0.1) shards of 120 CIFAR-100 labels over 6 clients, reference partitioner
     (data_loader.py:139-177) + 90 % train split: [0, 4, 1, 0, 1, 103]."""
@@ -52,13 +66,15 @@ def k5_sizes():
 
 
 CASES = {
+    "K2": dict(model="simple_cnn", kw={}, classes=10, sizes=k2_sizes, epochs=1, dp=1.0,
+               comp=None, shape=(1, 28, 28)),
     "K3": dict(model="federated_resnet", kw={"num_blocks": [1, 1, 1]}, classes=10,
                sizes=[70, 41, 33, 9], epochs=1, dp=4.0, comp=None),
     "K4-topk": dict(model="federated_resnet", kw={}, classes=10, sizes=[36, 12, 5], epochs=5,
                     dp=None, comp=CompressionConfig("topk", sparsity_ratio=0.9)),
     "K4-quant8": dict(model="federated_resnet", kw={}, classes=10, sizes=[33, 7], epochs=2,
                       dp=None, comp=CompressionConfig("quantization", bits=8, symmetric=True)),
-    "K5": dict(model="federated_resnet", kw={"num_classes": 100}, classes=100, sizes=None,
+    "K5": dict(model="federated_resnet", kw={"num_classes": 100}, classes=100, sizes=k5_sizes,
                epochs=1, dp=2.0, comp=None),
 }
 
@@ -70,7 +86,8 @@ def _split(row, layout):
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_config_round_matches_oracle(case):
     c = CASES[case]
-    sizes = c["sizes"] or k5_sizes()
+    sizes = c["sizes"]() if callable(c["sizes"]) else c["sizes"]
+    shape = c.get("shape", (3, 32, 32))
     C, lr = len(sizes), 0.01
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model(c["model"], **c["kw"])
@@ -81,13 +98,18 @@ def test_config_round_matches_oracle(case):
                    dp=DPConfig(epsilon=c["dp"]) if c["dp"] else None, compression=c["comp"])
     L, S, P = rr.trainer.layout, len(rr.slots), rr.P
     g = torch.Generator().manual_seed(77)
-    datas = {k: (torch.randn(n, 3, 32, 32, generator=g),
+    datas = {k: (torch.randn(n, *shape, generator=g),
                  torch.randint(0, c["classes"], (n,), generator=g)) for k, n in enumerate(sizes)}
     data = torch.cat([datas[k][0] for k in rr.slots]).to(DEV)
     labels = torch.cat([datas[k][1] for k in rr.slots]).to(DEV)
     offs = np.cumsum([0] + [sizes[k] for k in rr.slots][:-1]).tolist()
-    snaps, trained = [], {}
-    rr.trainer.lanes[0].on_step = lambda e, n: snaps.append(pool_snapshot(e, n))
+    snaps, drops, trained = [], [], {}
+
+    def on_step(e, n):
+        snaps.append(pool_snapshot(e, n))
+        drops.append([b[:n].cpu().clone() for b in e.net.mask_buffers()])  # keep-masks drawn
+    rr.trainer.lanes[0].on_step = on_step
+    dropout = getattr(model, "dropout_rate", 0.0) > 0
     rr.on_trained = lambda params, s: trained.setdefault("rows", params[:s, :P].clone())
     noise = None
     if c["dp"]:
@@ -119,8 +141,11 @@ def test_config_round_matches_oracle(case):
                 gs = e * st + j
                 idx = plan["index"][gs, i, :plan["counts"][gs, i]]
                 xb, yb = datas[k][0][idx], datas[k][1][idx]
-                li, cc, _, _ = train_ref.train_step(ref, optr, xb, yb)
-                l64, _, _, _ = train_ref.train_step(ref64, opt64, xb.double(), yb,
+                mk = None
+                if dropout:  # the HIP run's keep-masks, replayed by both oracle twins
+                    mk = [b[i, :idx.numel()].reshape(idx.numel(), -1) for b in drops[gs]]
+                li, cc, _, _ = train_ref.train_step(ref, optr, xb, yb, masks=mk)
+                l64, _, _, _ = train_ref.train_step(ref64, opt64, xb.double(), yb, masks=mk,
                                                     pools=sliced(snaps[gs][i], idx.numel()),
                                                     relus=rsliced(snaps[gs][i], idx.numel()))
                 running, r64, correct, seen = running + li, r64 + l64, correct + cc, \

@@ -166,6 +166,9 @@ EXACT = [  # nclients, batch, cin, h, cout, k, stride, pad (square maps)
     (1, 32, 64, 16, 128, 3, 1, 1),
     (5, 32, 128, 8, 128, 3, 1, 1),
     (2, 13, 64, 8, 64, 3, 1, 1),
+    # r03 quadrant-wave WGRAD: one split per tile (>= 512 tiles: dW / db written directly,
+    # no reduction launch), ragged counts
+    (32, 8, 128, 8, 128, 3, 1, 1),
     (2, 9, 3, 32, 32, 3, 1, 1),
     (2, 8, 64, 16, 128, 3, 2, 1),
     (2, 8, 64, 16, 128, 1, 2, 0),

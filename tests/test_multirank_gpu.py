@@ -22,6 +22,10 @@ Checks (per round):
     difference can flip a max-pool near-tie, which re-routes a gradient:
     measured 2 % of the update for the largest client, so the bound is 5 % — batches
     drawn from another client's stream, or another client's noise, miss it by 100x.
+    The model runs with dropout off: dropout and augmentation Philox streams are keyed by
+    (rank salt, lane, slot row), not by the global client id, so with dropout on a client's
+    masks DO change with its placement (statistically equivalent, not identical; DESIGN.md
+    §7) — layout invariance is claimed for shuffling and DP noise only.
 """
 import os
 
