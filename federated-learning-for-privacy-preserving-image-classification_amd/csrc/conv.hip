@@ -884,6 +884,158 @@ conv_c1_wgrad_kernel(const float* __restrict__ x, int64_t x_cs, const float* __r
     }
 }
 
+// SimpleCNN conv1 WGRAD on the matrix cores (r03).  dW[co][tap] = sum_px dY[co][px] T[px][tap]
+// is a GEMM with a long pixel reduction: M = COUT, N = 16 taps (the 9 shifts, tap 9 = 1.0 gives
+// the bias gradient, taps 10-15 zero), K = pixels, one v_mfma_f32_16x16x4_f32 per 16 output
+// channels and 4 pixels.  A workgroup takes a run of 4-row stages of one client (dY [COUT][4
+// rows] and the 6 input rows with a zero halo staged in LDS, pitches = 2 (mod 4)); wave w
+// multiplies stage row w, so per stage a wave issues W/4 x COUT/16 MFMAs from one patch read
+// (per-lane tap offset) and COUT/16 dY reads per 4 pixels.  The four waves' sums are added
+// in wave order at the end; splits of the stage run land in the same slab as
+// conv_c1_wgrad_kernel (splitk_sum).  The VALU kernel it replaces (80 fmaf per pixel per
+// 8 channels, runtime divisions per pixel) moved 1.3 TB/s at 32 clients (79.7 us).
+// H % 4 == 0, W % 4 == 0, W <= 32.
+// POOLED: dY is not materialised — it is routed from the pooled gradient as
+// maxpool2_bwd_ymask does (conv_c1_wgrad_kernel<true> above): pixel (y, x) takes dpool[y/2][x/2]
+// (planes gh x gw) when it is its window's argmax (idx, dense) and the pooled ReLU output yp
+// there is > 0, else 0 — per staged quad two pooled values, two argmax bytes, two yp values.
+// The same fp32 values reach the same MFMA chain, so the result equals the unfused pair
+// (maxpool2_bwd_ymask + this kernel on its output) bit for bit.
+template <int COUT, bool POOLED>
+__global__ void __launch_bounds__(256)
+conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ dy,
+                          int64_t dy_cs, float* __restrict__ part, float* __restrict__ bpart,
+                          const int32_t* __restrict__ counts, int batch, int H, int W,
+                          int nsplits, int sps, const uint8_t* __restrict__ pidx, int64_t pi_cs,
+                          const float* __restrict__ yp, int64_t yp_cs, int gh, int gw) {
+    constexpr int NQ = COUT / 16;     // 16-channel groups
+    constexpr int MAXW = 32;
+    constexpr int DP = 4 * MAXW + 2;  // dY pitch per channel (4 rows), = 2 (mod 4)
+    constexpr int PW = MAXW + 4;      // patch row pitch: image column c at 2 + c
+    constexpr int NDQ = COUT * MAXW / 256;  // dY float4s per thread (upper bound)
+    __shared__ float Ds[COUT * DP];
+    __shared__ float Ps[6 * PW];
+    __shared__ float red[4][COUT * 10];
+    const int split = blockIdx.x, z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int HW = H * W, Q = W / 4;
+    const int nst = cnt * (H / 4);
+    const int sbeg = split * sps, send = min(nst, sbeg + sps);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const float* xz = x + z * x_cs;
+    const float* dyz = dy + z * dy_cs;
+    if (tid < 6) {  // zero halo columns -1 and W (never overwritten)
+        Ps[tid * PW + 1] = 0.f;
+        Ps[tid * PW + W + 2] = 0.f;
+    }
+    const int nd4 = COUT * 4 * Q;
+    float4 rd[NDQ], rx = make_float4(0.f, 0.f, 0.f, 0.f);
+    float2 pg[POOLED ? NDQ : 1], py[POOLED ? NDQ : 1];  // POOLED: raw loads, routed in store()
+    int pc[POOLED ? NDQ : 1];                            // argmax bytes | code row << 16
+    auto load = [&](int st) {
+        const int img = (4 * st) / H, y0 = (4 * st) % H;
+#pragma unroll
+        for (int i = 0; i < NDQ; ++i) {
+            const int q = tid + 256 * i;
+            const int co = q / (4 * Q), rem = q % (4 * Q), rr = rem / Q, qq = rem % Q;
+            if constexpr (POOLED) {
+                const int yy = y0 + rr, OHW = (H / 2) * (W / 2);
+                const int64_t pl = (int64_t)img * COUT + co;
+                const int64_t go = pl * gh * gw + (yy >> 1) * gw + 2 * qq;
+                const int64_t io = pl * OHW + (yy >> 1) * (W / 2) + 2 * qq;
+                const bool ok = q < nd4;
+                pg[i] = ok ? make_float2(dyz[go], dyz[go + 1]) : make_float2(0.f, 0.f);
+                py[i] = ok ? make_float2(yp[z * yp_cs + go], yp[z * yp_cs + go + 1])
+                           : make_float2(0.f, 0.f);
+                pc[i] = ok ? (pidx[z * pi_cs + io] | (pidx[z * pi_cs + io + 1] << 8) |
+                              ((yy & 1) << 17))
+                           : 0;
+            } else {
+                rd[i] = q < nd4 ? *reinterpret_cast<const float4*>(
+                                      dyz + ((int64_t)(img * COUT + co) * HW + (y0 + rr) * W + 4 * qq))
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        if (tid < 6 * Q) {
+            const int pr = tid / Q, qq = tid % Q, y = y0 + pr - 1;
+            rx = (unsigned)y < (unsigned)H
+                     ? *reinterpret_cast<const float4*>(xz + (int64_t)img * HW + y * W + 4 * qq)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int i = 0; i < NDQ; ++i) {
+            const int q = tid + 256 * i;
+            if constexpr (POOLED) {  // maxpool2_bwd_kernel's routing: (code == a) ? g : 0
+                const int r = pc[i] >> 16, i0 = pc[i] & 0xff, i1 = (pc[i] >> 8) & 0xff;
+                const float g0 = py[i].x > 0.f ? pg[i].x : 0.f, g1 = py[i].y > 0.f ? pg[i].y : 0.f;
+                rd[i] = make_float4(i0 == r ? g0 : 0.f, i0 == (r | 1) ? g0 : 0.f,
+                                    i1 == r ? g1 : 0.f, i1 == (r | 1) ? g1 : 0.f);
+            }
+            if (q < nd4) {
+                const int co = q / (4 * Q), rem = q % (4 * Q), rr = rem / Q, qq = rem % Q;
+                float2* d = reinterpret_cast<float2*>(Ds + co * DP + rr * W + 4 * qq);
+                d[0] = make_float2(rd[i].x, rd[i].y);
+                d[1] = make_float2(rd[i].z, rd[i].w);
+            }
+        }
+        if (tid < 6 * Q) {
+            const int pr = tid / Q, qq = tid % Q;
+            float2* d = reinterpret_cast<float2*>(Ps + pr * PW + 2 + 4 * qq);
+            d[0] = make_float2(rx.x, rx.y);
+            d[1] = make_float2(rx.z, rx.w);
+        }
+    };
+    // lane roles: m / n = lane & 15 (channel of the A operand / tap of the B operand),
+    // k = lane >> 4 (pixel of the 4-pixel group)
+    const int mn = lane & 15, kk = lane >> 4;
+    const int toff = mn < 9 ? (mn / 3) * PW + mn % 3 + 1 : 0;
+    const float tconst = mn == 9 ? 1.f : 0.f;
+    f32x4 acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (sbeg < send) {
+        load(sbeg);
+        store();
+        __syncthreads();
+        for (int st = sbeg; st < send; ++st) {
+            const bool more = st + 1 < send;
+            if (more) load(st + 1);
+            const float* Pr = Ps + wid * PW + kk + toff;
+            const float* Dr = Ds + mn * DP + wid * W + kk;
+            for (int g = 0; g < Q; ++g) {
+                const float b = mn < 9 ? Pr[4 * g] : tconst;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+                    acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(Dr[q * 16 * DP + 4 * g], b, acc[q],
+                                                                  0, 0, 0);
+            }
+            if (more) {
+                __syncthreads();
+                store();
+                __syncthreads();
+            }
+        }
+    }
+    // D[co][tap]: lane holds taps mn, channels q*16 + 4*kk + r
+    if (mn < 10) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[wid][(q * 16 + 4 * kk + r) * 10 + mn] = acc[q][r];
+    }
+    __syncthreads();
+    const int64_t slab = (int64_t)z * nsplits + split;
+    for (int e = tid; e < COUT * 10; e += 256) {
+        const float v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+        const int co = e / 10, k = e % 10;
+        if (k < 9) part[slab * COUT * 9 + co * 9 + k] = v;
+        else if (bpart) bpart[slab * COUT + co] = v;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
@@ -1174,31 +1326,14 @@ static bool dconv_supported(int h, int w, int kh, int kw, int stride, int pad) {
 // (co, ci) tile and ~256 workgroups (one per CU at its 86 KB of LDS)
 static const int kDconvBlocks = env_int("FH_DCONV_BLOCKS", 512);
 static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 64);
+// stride-2 WGRAD (dconv_wgrad_kernel<W, 2, 1, 2, .., S=2>): workgroup target per resident wave
 static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 256);
-static const int kDwgradWpx = env_int("FH_DWGRAD_WPX", 4);
-// ... or, from this many clients on the ResNet shapes, one wave per 32x32 of a 64x64 (co, ci)
-// tile: faster per launch at 16 clients, but neutral per round (K4 +0.5 %, K5 -0.3 %,
-// interleaved x3, profiles/r02_wide) — off unless FH_DWGRAD_WIDE_MIN is set (e.g. 8)
-static const int kDwgradWideMin = env_int("FH_DWGRAD_WIDE_MIN", 1 << 30);
-// stage pixels of the 8x8-map WGRAD: 64 = one image per stage, 43 KB of LDS, two workgroups
-// (waves) per CU, which leaves room beside the other lanes' kernels: KT 265.8k -> 270.0k
-// (interleaved x3, profiles/r02_spx) although per launch it is even; FH_DWGRAD_SPX8=128: two
-// images per stage, 85 KB, one workgroup per CU (the round-1 choice)
-// 32x32-map WGRAD with one dY stage buffer (FH_DWGRAD_SDY32=1): 69 KB of LDS, two workgroups
-// per CU, one more barrier per stage
-static const int kDwgradSdy32 = env_int("FH_DWGRAD_SDY32", 0);
-static const int kDwgradSpx8 = env_int("FH_DWGRAD_SPX8", 64) == 128 ? 128 : 64;
 // RGB-layer wgrad target: 512 workgroups (42 -> 34 us at 32 clients, profiles/r01_v12)
 static const int kDwgradSmallBlocks = env_int("FH_DWGRAD_SMALL_BLOCKS", 512);
 static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 2);  // tools/tail_sweep.py
 static const int kDconvForceSplits = env_int("FH_DCONV_SPLITS", 0);  // sweeps: force splits
 static const int kDwgradForceSplits = env_int("FH_DWGRAD_SPLITS", 0);
 static const int kDconvCk32 = env_int("FH_DCONV_CK32", 8);  // sweeps: CK of the BM=32 tiles
-// XCD-aware workgroup order in the direct conv / wgrad kernels (dconv_kernels.h xcd_block):
-// off by default — measured neutral (CIFAR10CNN 32-client step: conv6 FWD 166.1 vs 166.3 us;
-// KT 265.6k vs 266.3k, profiles/r02_s3/xcd_ab.txt): those kernels are MFMA-bound and the
-// weight / activation re-reads it removes hide under the MMA loop.  FH_XCD_REMAP=1: on.
-static const int g_xcd_remap = env_int("FH_XCD_REMAP", 0);
 
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false,
                         bool ck4 = false) {
@@ -1279,7 +1414,6 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     a.splits = p.splits;
     a.cchunk = p.cchunk;
     a.Nfull = a.batch * sp;
-    a.xcd = g_xcd_remap;
     // float4 weight runs: 16-B aligned slices that never run past the tensor
     a.wvec = aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0);
     float* out = a.out;
@@ -1366,7 +1500,6 @@ static int run_dconv_dgrad_s2(DConvArgs a, int oh, int nclients, void* ws, size_
     a.splits = p.splits;
     a.cchunk = p.cchunk;
     a.Nfull = a.batch * sp;
-    a.xcd = g_xcd_remap;
     float* out = a.out;
     if (p.splits > 1) a.out = (float*)ws;
     dim3 grid((unsigned)ceil_div((int64_t)a.batch * oh * oh, 256), (unsigned)ceil_div(a.M, 32),
@@ -1408,44 +1541,15 @@ static bool dwgrad_supported(int cin, int cout, int h, int w, int kh, int kw, in
     return dconv_supported(h, w, kh, kw, stride, pad) && cin % 32 == 0 && cout % 32 == 0;
 }
 
-static DWPlan plan_dwgrad(int cout, int cin, int batch, int w, int nclients) {
-    DWPlan p{1, 1, 4, 128 / w, 1, 1};
-    const bool co64 = cout % 64 == 0, ci64 = cin % 64 == 0;
-    // many clients on the ResNet shapes (64 ch at 32x32, 256 ch at 8x8): 64x64 tiles, each
-    // staged byte feeding 2x the MFMAs (tools/wpx_sweep.sh at 16 clients: 256ch 8x8 420 -> 359
-    // us, 64ch 32x32 398 -> 371 us; 128ch 16x16 / 8x8 lose, and KT lost 0.6 % with them)
-    const bool wide_shape = w == 32 || (cin >= 256 && cout >= 256);
-    if (kDwgradWpx == 4 && co64 && ci64 && wide_shape && nclients >= kDwgradWideMin)
-        p = {2, 2, 1, 64 / w, 1, 1};
-    else if (kDwgradWpx == 4) p = {1, 1, 4, (w == 8 ? kDwgradSpx8 : 128) / w, 1, 1};
-    else if (kDwgradWpx == 2 && co64) p = {2, 1, 2, 128 / w, 1, 1};
-    else if (kDwgradWpx == 2 && ci64) p = {1, 2, 2, 128 / w, 1, 1};
-    else if (co64 && ci64) p = {2, 2, 1, 64 / w, 1, 1};
-    else if (co64) p = {2, 1, 2, 128 / w, 1, 1};
-    else if (ci64) p = {1, 2, 2, 128 / w, 1, 1};
-    const int64_t tiles = (int64_t)(cout / (32 * p.wco)) * (cin / (32 * p.wci)) * nclients;
-    const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)p.sr * w);
-    // one workgroup per CU per resident wave (the 16x16 instance holds two: +3-5 % on those
-    // layers at 512 workgroups; the one-wave instances lose with two rounds of workgroups)
-    const int occ = dwgrad_occ(w, p.wco, p.wci, p.sr, 1,
-                               kDwgradSdy32 && w == 32 && p.wco == 1 && p.wci == 1 && p.wpx == 4);
-    // >= 4 stages per split: fewer, longer splits beat a wide slab in the few-client tail
-    const int want = (int)std::min<int64_t>(
-        std::max<int64_t>(1, ceil_div(fill(kDwgradBlocks * occ), tiles)),
-        std::max(1, nst / kDwgradMinSps));
-    p.sps = (int)ceil_div(nst, kDwgradForceSplits > 0 ? std::min(kDwgradForceSplits, nst) : want);
-    p.splits = (int)ceil_div(nst, p.sps);
-    return p;
-}
-
 // r03 quadrant-wave WGRAD (dconv_kernels.h dwgrad_q_kernel): 32x32 (co, ci) tiles, 128-pixel
-// stages, three 45 KB workgroups per CU; splits of the stage run fill ~kDwqBlocks workgroups.
-// FH_DWGRAD_Q=0 runs the r02 kernel instead (A/B on the box only).
-static const int g_dwq = env_int("FH_DWGRAD_Q", 1);
+// stages, three 45 KB workgroups per CU; splits of the stage run fill ~kDwqBlocks workgroups
+// (512: tools/r03_wgrad_ab.sh sweep, profiles/r03_dwq/).  KT against the r02 kernel (32x32x2
+// MFMAs, four pixel-waves, one 86 KB workgroup per CU): 270.3k / 272.1k vs 269.3k / 269.2k
+// client-images/s, interleaved.
 static const int kDwqBlocks = env_int("FH_DWQ_BLOCKS", 512);
-// stage pixels: 128 = one buffer, stored between two barriers (default: the best of the
-// r03 sweep, profiles/r03_dwq/); 64 = two 64-pixel buffers, the next stage stored half-way
-// through this one's MFMAs, one barrier per stage (FH_DWQ_SPX=64)
+// stage pixels: 128 = one buffer, stored between two barriers (default); 64 = two 64-pixel
+// buffers, the next stage stored half-way through this one's MFMAs, one barrier per stage
+// (FH_DWQ_SPX=64; measured within noise of 128, profiles/r03_dwq/)
 static const int kDwqSpx = env_int("FH_DWQ_SPX", 128) == 64 ? 64 : 128;
 static DWPlan plan_dwq(int cout, int cin, int batch, int w, int nclients) {
     DWPlan p{1, 1, 4, kDwqSpx / w, 1, 1};
@@ -1509,36 +1613,23 @@ static bool conv_c1_supported(int cin, int cout, int kh, int kw, int stride, int
 static int conv_c1_chunks(int batch, int h, int w) {
     return (int)ceil_div((int64_t)batch * h * w, kC1Chunk);
 }
+// conv1 WGRAD on the matrix cores (conv_c1_wgrad_mfma_kernel): 4-row stages, ~kC1MfmaBlocks
+// workgroups (the kernel is HBM-bound: many small workgroups keep loads in flight)
+static const int kC1MfmaBlocks = env_int("FH_C1_MFMA_BLOCKS", 1024);
+static bool conv_c1_mfma_ok(int h, int w) { return h % 4 == 0 && w % 4 == 0 && w <= 32; }
+static DWPlan plan_c1_mfma(int batch, int h, int nclients) {
+    const int nst = batch * (h / 4);
+    int want = (int)std::max<int64_t>(1, ceil_div(fill(kC1MfmaBlocks), std::max(nclients, 1)));
+    want = std::min(want, std::max(1, nst / 2));
+    DWPlan p{1, 1, 1, 4, 1, 1};
+    p.sps = (int)ceil_div(nst, want);
+    p.splits = (int)ceil_div(nst, p.sps);
+    return p;
+}
 
 static size_t dwgrad_ws_bytes(const DWPlan& p, int nclients, int M, int N) {
     const size_t wb = (size_t)nclients * p.splits * M * N * sizeof(float);
     return ((wb + 255) / 256) * 256 + (size_t)nclients * p.splits * M * sizeof(float);
-}
-
-template <int W>
-static int dwgrad_launch_w(const DWPlan& p, dim3 grid, const DWArgs& a, hipStream_t st) {
-#define FH_DW(WCO, WCI, WPX, SPXV)                                                             \
-    if (p.wco == WCO && p.wci == WCI && p.wpx == WPX && p.sr * W == SPXV) {                   \
-        FH_LAUNCH((dconv_wgrad_kernel<W, WCO, WCI, WPX, SPXV / W>), grid, dim3(256), 0, \
-                           st, a);                                                            \
-        return FH_OK;                                                                         \
-    }
-    if constexpr (W == 32) {  // one dY stage buffer: 69 KB, two workgroups per CU
-        if (kDwgradSdy32 && p.wco == 1 && p.wci == 1 && p.wpx == 4 && p.sr == 4) {
-            FH_LAUNCH((dconv_wgrad_kernel<32, 1, 1, 4, 4, 1, true>), grid, dim3(256), 0, st, a);
-            return FH_OK;
-        }
-    }
-    FH_DW(1, 1, 4, 128)
-    if constexpr (W == 8) {  // 64-pixel stages: half the LDS, two workgroups per CU
-        FH_DW(1, 1, 4, 64)
-    }
-    FH_DW(2, 1, 2, 128)
-    FH_DW(1, 2, 2, 128)
-    FH_DW(2, 2, 1, 64)
-#undef FH_DW
-    set_error("dconv_wgrad: no instantiation");
-    return FH_E_UNSUPPORTED;
 }
 
 }  // namespace fh
@@ -1870,7 +1961,9 @@ extern "C" int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float
     FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_wgrad: cout %d (32 or 64)", cout);
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && dpool && idx && y && dw, "conv2d_c1_pool_wgrad: null pointer");
+    const bool mfma = conv_c1_mfma_ok(h, w_) && (uintptr_t)x % 16 == 0 && x_cs % 4 == 0;
     DWPlan p{1, 1, 1, 1, conv_c1_chunks(batch, h, w_), 1};
+    if (mfma) p = plan_c1_mfma(batch, h, nclients);
     const size_t need = dwgrad_ws_bytes(p, nclients, cout, 9);
     FH_REQUIRE(workspace && ws_bytes >= need, "conv2d_c1_pool_wgrad: workspace %zu < %zu",
                ws_bytes, need);
@@ -1878,6 +1971,23 @@ extern "C" int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float
     const size_t wbytes = ((size_t)nclients * p.splits * cout * 9 * sizeof(float) + 255) / 256 * 256;
     float* bpart = db ? (float*)((char*)workspace + wbytes) : nullptr;
     hipStream_t st = as_stream(stream);
+    if (mfma) {  // conv_c1_wgrad_mfma_kernel<POOLED>: the routed gradient on the matrix cores
+        const dim3 grid((unsigned)p.splits, (unsigned)nclients);
+        if (cout == 32)
+            FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
+                      dp_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps, idx, i_cs, y,
+                      y_cs, gh, gw);
+        else
+            FH_LAUNCH((conv_c1_wgrad_mfma_kernel<64, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
+                      dp_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps, idx, i_cs, y,
+                      y_cs, gh, gw);
+        FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad mfma");
+        if (const int _r = splitk_sum((const float*)part, dw, dw_cs, p.splits, cout * 9,
+                                      (const float*)bpart, db, db_cs, cout, nclients, st))
+            return _r;
+        FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad reduce");
+        return FH_OK;
+    }
     FH_LAUNCH(conv_c1_wgrad_kernel<true>, dim3((unsigned)p.splits, (unsigned)(cout / 8), nclients),
               dim3(256), 0, st, x, x_cs, dpool, dp_cs, part, bpart, counts, batch, h, w_, cout,
               p.splits, idx, i_cs, y, y_cs, gh, gw);
@@ -1895,17 +2005,19 @@ extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int
     if (oh <= 0 || ow <= 0 || nclients <= 0) return 0;
     size_t direct = 0;
     if (dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad))  // (misaligned data: igemm)
-        direct = dwgrad_ws_bytes(g_dwq ? plan_dwq(cout, cin, batch, w_, nclients)
-                                       : plan_dwgrad(cout, cin, batch, w_, nclients),
-                                 nclients, cout, cin * 9);
+        direct = dwgrad_ws_bytes(plan_dwq(cout, cin, batch, w_, nclients), nclients, cout,
+                                 cin * 9);
     if (dwgrad_small_supported(cin, cout, h, w_, kh, kw, stride, pad))
         direct = dwgrad_ws_bytes(plan_dwgrad_small(cout, batch, w_, nclients), nclients, cout, cin * 9);
     if (dwgrad_s2_supported(cin, cout, h, w_, kh, kw, stride, pad))
         direct = dwgrad_ws_bytes(plan_dwgrad_s2(cout, cin, batch, ow, nclients), nclients, cout,
                                  cin * 9);
     if (conv_c1_supported(cin, cout, kh, kw, stride, pad)) {
-        DWPlan p{1, 1, 1, 1, conv_c1_chunks(batch, h, w_), 1};
+        DWPlan p{1, 1, 1, 1, conv_c1_chunks(batch, h, w_), 1};  // (also the fused-pool form)
         direct = dwgrad_ws_bytes(p, nclients, cout, 9);
+        if (conv_c1_mfma_ok(h, w_))
+            direct = std::max(direct, dwgrad_ws_bytes(plan_c1_mfma(batch, h, nclients), nclients,
+                                                      cout, 9));
     }
     return std::max(direct, wgrad_ws_bytes(plan_wgrad(cout, cin * kh * kw, batch * oh * ow, nclients),
                                            nclients));
@@ -1934,6 +2046,32 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         set_error("conv2d_wgrad_bnrelu: needs the direct 3x3 wgrad (16-B aligned, channels %% 32)");
         return FH_E_UNSUPPORTED;
     }
+    if (!in_scale && conv_c1_supported(cin, cout, kh, kw, stride, pad) && conv_c1_mfma_ok(h, w_) &&
+        ((uintptr_t)x % 16 == 0) && ((uintptr_t)dy % 16 == 0) && x_cs % 4 == 0 && dy_cs % 4 == 0) {
+        const DWPlan p = plan_c1_mfma(batch, h, nclients);
+        const size_t need = dwgrad_ws_bytes(p, nclients, cout, 9);
+        FH_REQUIRE(workspace && ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes,
+                   need);
+        float* part = (float*)workspace;
+        const size_t wbytes = ((size_t)nclients * p.splits * cout * 9 * sizeof(float) + 255) / 256 * 256;
+        float* bpart = db ? (float*)((char*)workspace + wbytes) : nullptr;
+        hipStream_t st = as_stream(stream);
+        const dim3 grid((unsigned)p.splits, (unsigned)nclients);
+        if (cout == 32)
+            FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, false>), grid, dim3(256), 0, st, x, x_cs, dy,
+                      dy_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps,
+                      (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0);
+        else
+            FH_LAUNCH((conv_c1_wgrad_mfma_kernel<64, false>), grid, dim3(256), 0, st, x, x_cs, dy,
+                      dy_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps,
+                      (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0);
+        FH_LAUNCH_CHECK("conv2d_wgrad c1 mfma");
+        if (const int _r = splitk_sum((const float*)part, dw, dw_cs, p.splits, cout * 9,
+                                      (const float*)bpart, db, db_cs, cout, nclients, st))
+            return _r;
+        FH_LAUNCH_CHECK("conv2d_wgrad c1 reduce");
+        return FH_OK;
+    }
     if (!in_scale && conv_c1_supported(cin, cout, kh, kw, stride, pad)) {
         DWPlan p{1, 1, 1, 1, conv_c1_chunks(batch, h, w_), 1};
         const size_t need = dwgrad_ws_bytes(p, nclients, cout, 9);
@@ -1960,7 +2098,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         DWArgs d{};
         d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
         d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
-        d.splits = p.splits; d.stages_per_split = p.sps; d.xcd = g_xcd_remap;
+        d.splits = p.splits; d.stages_per_split = p.sps;
         d.part = (float*)workspace;
         const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
         d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
@@ -1975,12 +2113,12 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
         return FH_OK;
     }
-    if (aligned && g_dwq && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
+    if (aligned && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
         const DWPlan p = plan_dwq(cout, cin, batch, w_, nclients);
         DWArgs d{};
         d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
         d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
-        d.splits = p.splits; d.stages_per_split = p.sps; d.xcd = g_xcd_remap;
+        d.splits = p.splits; d.stages_per_split = p.sps;
         d.in_scale = in_scale; d.in_shift = in_shift; d.aff_cs = aff_cs;
         hipStream_t st = as_stream(stream);
         dim3 grid((unsigned)p.splits, (unsigned)((cout / 32) * (cin / 32)), (unsigned)nclients);
@@ -2009,31 +2147,6 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
         return FH_OK;
     }
-    if (aligned && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
-        const DWPlan p = plan_dwgrad(cout, cin, batch, w_, nclients);
-        const size_t need = dwgrad_ws_bytes(p, nclients, a.M, a.N);
-        FH_REQUIRE(ws_bytes >= need, "conv2d_wgrad: workspace %zu < %zu", ws_bytes, need);
-        DWArgs d{};
-        d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
-        d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
-        d.splits = p.splits; d.stages_per_split = p.sps; d.xcd = g_xcd_remap;
-        d.in_scale = in_scale; d.in_shift = in_shift; d.aff_cs = aff_cs;
-        d.part = (float*)workspace;
-        const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
-        d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
-        hipStream_t st = as_stream(stream);
-        dim3 grid((unsigned)p.splits, (unsigned)((cout / (32 * p.wco)) * (cin / (32 * p.wci))),
-                  (unsigned)nclients);
-        rc = w_ == 32 ? dwgrad_launch_w<32>(p, grid, d, st)
-           : w_ == 16 ? dwgrad_launch_w<16>(p, grid, d, st)
-                      : dwgrad_launch_w<8>(p, grid, d, st);
-        if (rc) return rc;
-        FH_LAUNCH_CHECK("conv2d_wgrad direct");
-        const int MN = a.M * a.N;
-        if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)d.bias_part, db, db_cs, a.M, nclients, st)) return _r;
-        FH_LAUNCH_CHECK("conv2d_wgrad reduce");
-        return FH_OK;
-    }
     if (aligned && !in_scale && dwgrad_s2_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
         const DWPlan p = plan_dwgrad_s2(cout, cin, batch, ow, nclients);
         const size_t need = dwgrad_ws_bytes(p, nclients, a.M, a.N);
@@ -2041,7 +2154,7 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         DWArgs d{};
         d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
         d.batch = batch; d.cin = cin; d.M = cout; d.N = a.N;
-        d.splits = p.splits; d.stages_per_split = p.sps; d.xcd = g_xcd_remap;
+        d.splits = p.splits; d.stages_per_split = p.sps;
         d.part = (float*)workspace;
         const size_t wbytes = ((size_t)nclients * p.splits * a.M * a.N * sizeof(float) + 255) / 256 * 256;
         d.bias_part = db ? (float*)((char*)workspace + wbytes) : nullptr;
@@ -2140,6 +2253,14 @@ struct SkinnyBwdEpi {
     float scale;           // 1 / (1 - p)
     const float* relu_ref; // the layer input [z][b][K]: zero where it is not > 0 (nullable)
     int64_t r_cs;
+    // nullable: the layer input is a flattened 2x2 max-pool output [C][OH][OW] (SimpleCNN
+    // fc1 after pool2).  dX is then written as the pool INPUT's gradient — planes xh x xw,
+    // the 2OH x 2OW map in the top-left — routed to the window argmax pidx (dense
+    // [C][OH][OW]) and zero elsewhere, maxpool2_bwd_kernel's values exactly (relu_ref = the
+    // pooled ReLU output: the mask at the argmax)
+    const uint8_t* pidx;
+    int64_t pi_cs;
+    int pow_, pohw, xh, xw;
 };
 
 template <int KT>
@@ -2205,7 +2326,19 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
             const int64_t e = (int64_t)img * K + k0 + 32 * t + r32;
             if (ep.mask) v = ep.mask[z * ep.m_cs + e] ? v * ep.scale : 0.f;
             if (ep.relu_ref && !(ep.relu_ref[z * ep.r_cs + e] > 0.f)) v = 0.f;
-            dX[z * dx_cs + e] = v;
+            if (ep.pidx) {
+                const int f = k0 + 32 * t + r32, c = f / ep.pohw, rem = f - c * ep.pohw;
+                const int oh = rem / ep.pow_, ow = rem - oh * ep.pow_;
+                const int a = ep.pidx[z * ep.pi_cs + e];
+                float* d = dX + z * dx_cs +
+                           ((int64_t)(img * (K / ep.pohw) + c) * ep.xh + 2 * oh) * ep.xw + 2 * ow;
+                d[0] = a == 0 ? v : 0.f;
+                d[1] = a == 1 ? v : 0.f;
+                d[ep.xw] = a == 2 ? v : 0.f;
+                d[ep.xw + 1] = a == 3 ? v : 0.f;
+            } else {
+                dX[z * dx_cs + e] = v;
+            }
         }
 }
 
@@ -2366,11 +2499,11 @@ extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, i
             (int64_t)(in_f / 128) * nclients >= fill(256))
             FH_LAUNCH(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
                                dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs,
-                               counts, batch, in_f, out_f, SkinnyBwdEpi{nullptr, 0, 1.f, nullptr, 0});
+                               counts, batch, in_f, out_f, SkinnyBwdEpi{nullptr, 0, 1.f, nullptr, 0, nullptr, 0, 1, 1, 0, 0});
         else
             FH_LAUNCH(linear_dgrad_skinny_kernel<1>, dim3((unsigned)(in_f / 32), nclients),
                                dim3(256), 0, as_stream(stream), dy, dy_cs, w, w_cs, dx, dx_cs,
-                               counts, batch, in_f, out_f, SkinnyBwdEpi{nullptr, 0, 1.f, nullptr, 0});
+                               counts, batch, in_f, out_f, SkinnyBwdEpi{nullptr, 0, 1.f, nullptr, 0, nullptr, 0, 1, 1, 0, 0});
         FH_LAUNCH_CHECK("linear_dgrad skinny");
         return FH_OK;
     }
@@ -2382,15 +2515,11 @@ extern "C" int fh_linear_dgrad(const float* dy, int64_t dy_cs, const float* w, i
 // the layer input, fh_dropout_bwd) in one launch: batch <= 32, in_f % 128 == 0,
 // out_f % 32 == 0, 16-B aligned dY rows; FH_E_UNSUPPORTED otherwise (the caller then issues
 // the three entry points).  mask / relu_ref nullable; db nullable.
-extern "C" int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
-                                   const float* w, int64_t w_cs, float* dw, int64_t dw_cs,
-                                   float* db, int64_t db_cs, float* dx, int64_t dx_cs,
-                                   const uint8_t* mask, int64_t m_cs, float p_drop,
-                                   const float* relu_ref, int64_t r_cs, const int32_t* counts,
-                                   int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f,
-                                   void* stream) {
-    FH_REQUIRE(nclients >= 0 && batch > 0 && in_f > 0 && out_f > 0, "linear_bwd_fused: bad shape");
-    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_bwd_fused: p=%g", p_drop);
+static int linear_bwd_fused_impl(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                                 const float* w, int64_t w_cs, float* dw, int64_t dw_cs,
+                                 float* db, int64_t db_cs, float* dx, int64_t dx_cs,
+                                 const SkinnyBwdEpi& ep, const int32_t* counts, int32_t nclients,
+                                 int32_t batch, int32_t in_f, int32_t out_f, void* stream) {
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && dy && w && dw && dx, "linear_bwd_fused: null pointer");
     if (!(batch <= 32 && in_f % (kSkinny32 ? 32 : 128) == 0 && out_f % 32 == 0 &&
@@ -2399,7 +2528,6 @@ extern "C" int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy
                   "aligned dY (got %d, %d, %d)", batch, in_f, out_f);
         return FH_E_UNSUPPORTED;
     }
-    const SkinnyBwdEpi ep{mask, m_cs, 1.0f / (1.0f - p_drop), relu_ref, r_cs};
     const int kb = (int)ceil_div(in_f, 128);  // WGRAD k-blocks (spare waves return)
     const int nw = kb * (int)ceil_div(out_f, 32);
     if (kLinearSkinny != 2 && (int64_t)kb * nclients >= fill(256)) {
@@ -2425,6 +2553,41 @@ extern "C" int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy
                   db_cs, dx, dx_cs, ep, counts, batch, in_f, out_f, nw);
     FH_LAUNCH_CHECK("linear_bwd_fused");
     return FH_OK;
+}
+
+extern "C" int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                                   const float* w, int64_t w_cs, float* dw, int64_t dw_cs,
+                                   float* db, int64_t db_cs, float* dx, int64_t dx_cs,
+                                   const uint8_t* mask, int64_t m_cs, float p_drop,
+                                   const float* relu_ref, int64_t r_cs, const int32_t* counts,
+                                   int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f,
+                                   void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && in_f > 0 && out_f > 0, "linear_bwd_fused: bad shape");
+    FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_bwd_fused: p=%g", p_drop);
+    const SkinnyBwdEpi ep{mask, m_cs, 1.0f / (1.0f - p_drop), relu_ref, r_cs, nullptr, 0, 1, 1, 0, 0};
+    return linear_bwd_fused_impl(x, x_cs, dy, dy_cs, w, w_cs, dw, dw_cs, db, db_cs, dx, dx_cs, ep,
+                                 counts, nclients, batch, in_f, out_f, stream);
+}
+
+// fh_linear_bwd_fused for a layer whose input x is a flattened 2x2 max-pool output of
+// ReLU'd maps [C][OH][OW] (SimpleCNN fc1 after pool2, models_pytorch.py:91-95): dX is written
+// as the gradient of the POOL INPUT (fh_maxpool2_bwd's output, planes xh x xw with the
+// 2OH x 2OW map in the top-left corner, other elements untouched), routed to the window
+// argmax pidx (dense [C][OH][OW]) with the ReLU mask x > 0 at it — the separate
+// fh_maxpool2_bwd launch and the pooled gradient tensor disappear.  Same values bit for bit.
+extern "C" int fh_linear_bwd_fused_pool(const float* x, int64_t x_cs, const float* dy,
+                                        int64_t dy_cs, const float* w, int64_t w_cs, float* dw,
+                                        int64_t dw_cs, float* db, int64_t db_cs, float* dx,
+                                        int64_t dx_cs, const uint8_t* pidx, int64_t pi_cs,
+                                        const int32_t* counts, int32_t nclients, int32_t batch,
+                                        int32_t C, int32_t OH, int32_t OW, int32_t xh, int32_t xw,
+                                        int32_t out_f, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && OH > 0 && OW > 0 && xh >= 2 * OH &&
+               xw >= 2 * OW && out_f > 0, "linear_bwd_fused_pool: bad shape");
+    FH_REQUIRE(pidx || nclients == 0, "linear_bwd_fused_pool: null argmax");
+    const SkinnyBwdEpi ep{nullptr, 0, 1.f, x, x_cs, pidx, pi_cs, OW, OH * OW, xh, xw};
+    return linear_bwd_fused_impl(x, x_cs, dy, dy_cs, w, w_cs, dw, dw_cs, db, db_cs, dx, dx_cs, ep,
+                                 counts, nclients, batch, C * OH * OW, out_f, stream);
 }
 
 extern "C" size_t fh_linear_wgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f,

@@ -66,7 +66,6 @@ struct DConvArgs {
     const uint8_t* pmask;
     int64_t pi_cs, pm_cs;
     float pscale;
-    int xcd;  // host: XCD-aware workgroup order (xcd_block)
     // dconv_dgrad_s2_kernel<SC>: the ResNet projection shortcut's 1x1 / stride-2 DGRAD folded
     // in — dX[m][2r][2c] += sum_ch wt2[ch][m] in2[ch][r][c] (in2 = its output gradient)
     const float* in2;
@@ -89,20 +88,13 @@ __device__ __forceinline__ float4 bn_relu4(float4 v, float s, float t) {
     return v;
 }
 
-// XCD-aware workgroup order.  Workgroups b and b + 8 share an XCD (round-robin dispatch,
-// MI355X_MICROARCH.md "Workgroup dispatch"), so the logical workgroup
-// L = (b % 8) * (N / 8) + b / 8 gives each XCD a contiguous range of the x-fastest grid
-// order: one client's tiles — which all read that client's weights (conv) or X / dY
-// (wgrad) — share one XCD's L2 instead of being re-read into all eight.  Speed only: any
-// placement computes the same result.
-__device__ __forceinline__ void xcd_block(bool on, int& bx, int& by, int& bz) {
-    const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
-    int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    if (on && (n & 7) == 0) b = (b & 7) * (n >> 3) + (b >> 3);
-    bx = b % gx;
-    const int r = b / gx;
-    by = r % gy;
-    bz = r / gy;
+// Workgroup coordinates.  (r02 measured an XCD-aware remap of this order — each XCD a
+// contiguous range so one client's tiles share an L2 — neutral on these MFMA-bound kernels,
+// KT 265.6k vs 266.3k, profiles/r02_s3/xcd_ab.txt; removed in r03.)
+__device__ __forceinline__ void block_xyz(int& bx, int& by, int& bz) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    bz = blockIdx.z;
 }
 
 template <int W>
@@ -161,7 +153,7 @@ __global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WAVES_N, wn = wid % WAVES_N;
     int bx, by, bz;
-    xcd_block(a.xcd != 0, bx, by, bz);
+    block_xyz(bx, by, bz);
     const int z = bz / a.splits;
     const int split = bz - z * a.splits;
     const int cnt = a.counts ? a.counts[z] : a.batch;
@@ -633,7 +625,7 @@ __global__ void __launch_bounds__(256, 2) dconv_dgrad_s2_kernel(const DConvArgs 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     int bx, by, bz;
-    xcd_block(a.xcd != 0, bx, by, bz);
+    block_xyz(bx, by, bz);
     const int z = bz / a.splits;
     const int split = bz - z * a.splits;
     const int cnt = a.counts ? a.counts[z] : a.batch;
@@ -963,18 +955,19 @@ __global__ void __launch_bounds__(256) pw_s2_fwd_kernel(const DConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// WGRAD: dW[co][ci][kh][kw] = sum_pix dY[co][pix] * X[ci][pix + (kh-1, kw-1)]
+// WGRAD of the ResNet 3x3 / stride-2 / pad-1 down-sampling convolutions (r02; the stride-1
+// layers moved to dwgrad_q_kernel below in r03):
+// dW[co][ci][kh][kw] = sum_pix dY[co][pix] * X[ci][2 pix + (kh-1, kw-1)]
 //
-// The reduction runs over pixels, so MFMA lanes must span co (A) and ci (B).
-// Each wave keeps nine 32x32 accumulators, one per (kh,kw) shift: per pixel
-// pair it reads one dY operand and nine shifted patch operands (the shift is
-// again an LDS immediate) for nine MFMAs.  A stage is SR rows (64 or 128
-// pixels) of dY (staged [pix][co]) and the matching X rows with zero halo
-// (staged [ci][row][W+2], channel stride odd so 32 channels on 32 lanes hit 32
-// banks).  The four waves tile (co, ci, pixel-rows); waves that split pixels
-// are summed through LDS in a fixed order.  Every workgroup writes its
-// partial for one pixel split into the slab [z][split][co][ci*9+s] (the conv
-// bias gradient = sum of dY rows rides along), reduced by splitk_sum_kernel.
+// The reduction runs over pixels, so MFMA lanes span co (A) and ci (B).  Each wave keeps
+// nine 32x32 accumulators, one per (kh,kw) shift: per pixel pair it reads one dY operand
+// and nine shifted patch operands (the shift is an LDS immediate) for nine MFMAs.  A stage
+// is SR output rows of dY (staged [pix][co]) and the 2*SR+1 input rows they read with a zero
+// halo (staged [ci][row][2W+2], channel stride odd so 32 channels on 32 lanes hit 32 banks).
+// The four waves tile (co, ci, pixel-rows); waves that split pixels are summed through LDS
+// in a fixed order.  Every workgroup writes its partial for one pixel split into the slab
+// [z][split][co][ci*9+s] (the conv bias gradient = sum of dY rows rides along), reduced by
+// splitk_sum_kernel.
 struct DWArgs {
     const float* x;
     const float* dy;
@@ -988,7 +981,6 @@ struct DWArgs {
     const float* in_scale;
     const float* in_shift;
     int64_t aff_cs;
-    int xcd;  // host: XCD-aware workgroup order (xcd_block)
     // dwgrad_q_kernel with splits == 1: dW (and db when non-null) written directly
     float* dw;
     int64_t dw_cs;
@@ -997,29 +989,18 @@ struct DWArgs {
 };
 
 // Two workgroups per CU when the double-buffered staging fits twice in the 160 KB LDS:
-// then ask the allocator for two waves per SIMD (144 accumulator AGPRs + <= 112 VGPRs),
-// so one workgroup's staging + barrier overlaps the other's MFMAs.
-// (host planner: the same formula picks the workgroup target, conv.hip plan_dwgrad)
-// S = 2: the 3x3 / stride-2 / pad-1 convolution of the ResNet down-sampling blocks (W = the
-// OUTPUT width): a stage's patch is the 2*SEGR+1 input rows its output rows read, 2W+2 wide
-// with the halo, and a lane's operand address strides by 2 (pixel pair -> columns 2c, 2c+2).
-// SDY: one dY stage buffer (the patch stays double-buffered) — the next stage's dY is stored
-// after a barrier that retires the current one; on 32x32 maps this brings the workgroup from
-// 86 to 69 KB of LDS, i.e. two per CU.
-constexpr int dwgrad_occ(int W, int WCO, int WCI, int SR, int S = 1, bool SDY = false) {
+// then ask the allocator for two waves per SIMD (host planner: the same formula, conv.hip
+// plan_dwgrad_s2).  W = the OUTPUT width: a stage's patch is the 2*SEGR+1 input rows its
+// output rows read, 2W+2 wide with the halo, and a lane's operand address strides by 2.
+constexpr int dwgrad_occ(int W, int WCO, int WCI, int SR, int S = 1) {
     const int SEGR = SR < W ? SR : W, NI = SR / SEGR;
     const int PR = NI * (S == 1 ? SEGR + 2 : 2 * SEGR + 1), CSTR = (PR * (S * W + 2)) | 1;
-    const int bytes = 4 * ((SDY ? 1 : 2) * SR * W * (32 * WCO + 1) + 2 * 32 * WCI * CSTR);
+    const int bytes = 4 * (2 * SR * W * (32 * WCO + 1) + 2 * 32 * WCI * CSTR);
     return 2 * bytes <= 160 * 1024 ? 2 : 1;
 }
-template <int W, int WCO, int WCI, int SR, int S, bool SDY>
-constexpr int dwgrad_occupancy() {
-    constexpr int occ = dwgrad_occ(W, WCO, WCI, SR, S, SDY);
-    return occ;
-}
 
-template <int W, int WCO, int WCI, int WPX, int SR, int S = 1, bool SDY = false>
-__global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S, SDY>())) dconv_wgrad_kernel(const DWArgs a) {
+template <int W, int WCO, int WCI, int WPX, int SR, int S>
+__global__ void __launch_bounds__(256, dwgrad_occ(W, WCO, WCI, SR, S)) dconv_wgrad_kernel(const DWArgs a) {
     constexpr int H = W, HW = H * W;                // output map
     constexpr int WI = S * W, HI = S * H;           // input map
     constexpr int SPX = SR * W;                     // pixels per stage
@@ -1039,16 +1020,16 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S, SDY
     static_assert(S == 1 || S == 2, "stride");
     static_assert(BM % COI == 0 && (SR % H == 0 || H % SR == 0), "stage geometry");
 
-    constexpr int SMEM = SDY ? DSZ + 2 * PSZ : 2 * BUF;
-    __shared__ float smem[SMEM];   // double-buffered [Dys | Ps] (SDY: [Dys | Ps0 | Ps1])
-    auto dbase = [](int bsel) { return SDY ? 0 : bsel * BUF; };
-    auto pbase = [](int bsel) { return SDY ? DSZ + bsel * PSZ : bsel * BUF + DSZ; };
+    constexpr int SMEM = 2 * BUF;
+    __shared__ float smem[SMEM];   // double-buffered [Dys | Ps]
+    auto dbase = [](int bsel) { return bsel * BUF; };
+    auto pbase = [](int bsel) { return bsel * BUF + DSZ; };
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wpx = wid % WPX, wci = (wid / WPX) % WCI, wco = wid / (WPX * WCI);
     int bx, by, bz;
-    xcd_block(a.xcd != 0, bx, by, bz);
+    block_xyz(bx, by, bz);
     const int split = bx, z = bz;
     const int ntile_ci = a.cin / BN;
     const int co0 = (by / ntile_ci) * BM, ci0 = (by % ntile_ci) * BN;
@@ -1169,15 +1150,7 @@ __global__ void __launch_bounds__(256, (dwgrad_occupancy<W, WCO, WCI, SR, S, SDY
                         acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[s], acc[s], 0, 0, 0);
                 }
             }
-            if (more) {
-                if constexpr (SDY) {  // the one dY buffer: every wave has finished reading it
-                    store_p(bsel ^ 1);
-                    __syncthreads();
-                    store_d(bsel ^ 1);
-                } else {
-                    store(bsel ^ 1);
-                }
-            }
+            if (more) store(bsel ^ 1);
             __syncthreads();
             bsel ^= 1;
         }
@@ -1298,7 +1271,7 @@ __global__ void __launch_bounds__(256, 3) dwgrad_q_kernel(const DWArgs a) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int cq = wid & 1, nq = wid >> 1;  // this wave's 16x16 quadrant (co half, ci half)
     int bx, by, bz;
-    xcd_block(a.xcd != 0, bx, by, bz);
+    block_xyz(bx, by, bz);
     const int split = bx, z = bz;
     const int ntile_ci = a.cin / 32;
     const int co0 = (by / ntile_ci) * 32, ci0 = (by % ntile_ci) * 32;
@@ -1478,7 +1451,7 @@ __global__ void __launch_bounds__(256) dconv_wgrad_small_kernel(const DWArgs a) 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wpx = __builtin_amdgcn_readfirstlane(tid >> 6);
     int bx, by, bz;
-    xcd_block(a.xcd != 0, bx, by, bz);
+    block_xyz(bx, by, bz);
     const int split = bx, z = bz;
     const int co0 = by * 32;
     const int cnt = a.counts ? a.counts[z] : a.batch;

@@ -61,6 +61,8 @@ SIGNATURES = {
     "fh_linear_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32, I32, I32, I32, P]),
     "fh_linear_bwd_fused": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, F32,
                                   P, I64, P, I32, I32, I32, I32, P]),
+    "fh_linear_bwd_fused_pool": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, I64,
+                                       P, I32, I32, I32, I32, I32, I32, I32, I32, P]),
     "fh_linear_head_ce": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, P, P, P, P,
                                 P, I64, P, I64, P, I64, P, I64, F32, I32, P, I32, I32, I32, I32,
                                 P]),

@@ -165,12 +165,15 @@ class PackedNet:
         # profiles/r02_c1/K2_fuse_pool1_fwd_ab.txt).  FH_FUSE_POOL1=0: two launches.
         # (DP-SGD's per-sample passes read the full-resolution maps: off there.)
         self.fuse_pool1 = os.environ.get("FH_FUSE_POOL1", "1") != "0"
-        # ... its backward half alone (conv1's weight gradient from pool1's gradient, the
-        # full-resolution gradient never written) works after either forward
-        # (measured 7 % slower on K2: the per-pixel gathers of argmax / pooled value / pooled
-        # gradient cost more than the full-resolution gradient pass; off unless
-        # FH_FUSE_POOL1_BWD=1 — the fused forward's backward is maxpool2_bwd_ymask + wgrad)
-        self.fuse_pool1_bwd = os.environ.get("FH_FUSE_POOL1_BWD", "0") == "1"
+        # ... and its backward half: conv1's weight gradient straight from pool1's gradient
+        # (fh_conv2d_c1_pool_wgrad; the 100 KB-per-image full-resolution gradient is never
+        # written or read).  r03: on the matrix-core conv1 WGRAD (two pooled values, two
+        # argmax bytes per staged quad) K2 1.362M -> 1.418 / 1.423M client-images/s,
+        # interleaved (profiles/r03_k2/; r02's VALU form lost 7 %).  FH_FUSE_POOL1_BWD=0: off.
+        self.fuse_pool1_bwd = os.environ.get("FH_FUSE_POOL1_BWD", "1") != "0"
+        # SimpleCNN: pool2's backward inside fc1's fused backward (fh_linear_bwd_fused_pool;
+        # FH_FUSE_POOL2_BWD=0: the pooled gradient + fh_maxpool2_bwd)
+        self.fuse_pool2_bwd = os.environ.get("FH_FUSE_POOL2_BWD", "1") != "0"
         self._pool1_fused = False
 
     # -------------------------------------------------------------- helpers
@@ -316,16 +319,21 @@ class PackedNet:
             mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
             ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
                             relu_out=self._fc_in, counts=cnt)
-        dp2 = A("dp2", 64, 7, 7)
-        if not (self.fused_linear_bwd and ops.linear_bwd_fused(
-                A("p2", 64, 7, 7), dh1, W(P_, "fc1.weight"), W(G, "fc1.weight"),
-                W(G, "fc1.bias"), dp2, n, B, 3136, 128, counts=cnt)):
-            ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B,
-                             3136, 128, counts=cnt)
-            ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
         p1, a2, da2, dp1, hp = self._simple_maps()
-        ops.maxpool2_bwd(dp2, A("i2", 64, 7, 7, dtype=torch.uint8), da2, n, B, 64, 14, 14,
-                         xin=a2, counts=cnt)
+        i2 = A("i2", 64, 7, 7, dtype=torch.uint8)
+        # fc1's backward writes pool2's INPUT gradient da2 directly (routed to the argmax,
+        # the ReLU mask = p2 > 0): no pooled gradient tensor, no maxpool2_bwd launch
+        if not (self.fused_linear_bwd and self.fuse_pool2_bwd and ops.linear_bwd_fused_pool(
+                A("p2", 64, 7, 7), dh1, W(P_, "fc1.weight"), W(G, "fc1.weight"),
+                W(G, "fc1.bias"), da2, i2, n, B, 64, 7, 7, 128, counts=cnt)):
+            dp2 = A("dp2", 64, 7, 7)
+            if not (self.fused_linear_bwd and ops.linear_bwd_fused(
+                    A("p2", 64, 7, 7), dh1, W(P_, "fc1.weight"), W(G, "fc1.weight"),
+                    W(G, "fc1.bias"), dp2, n, B, 3136, 128, counts=cnt)):
+                ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n,
+                                 B, 3136, 128, counts=cnt)
+                ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
+            ops.maxpool2_bwd(dp2, i2, da2, n, B, 64, 14, 14, xin=a2, counts=cnt)
         ops.conv2d_wgrad(p1, da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, hp, hp, 64,
                          3, 1, 1, counts=cnt)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,

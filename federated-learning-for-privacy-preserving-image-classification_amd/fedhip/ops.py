@@ -460,6 +460,28 @@ def linear_bwd_fused(x, dy, w, dw, db, dx, nclients, batch, in_f, out_f, mask=No
     return True
 
 
+def linear_bwd_fused_pool(x, dy, w, dw, db, dx, pidx, nclients, batch, C, OH, OW, out_f,
+                          counts=None):
+    """linear_bwd_fused of a layer fed by a flattened 2x2 max-pool output x [C][OH][OW]
+    (fh_linear_bwd_fused_pool): dx is the pool INPUT's gradient (planes dx.shape[-2:], map
+    2OH x 2OW top-left) routed to the argmax pidx where x > 0 — maxpool2_bwd's output, with
+    the pool's backward launch and the pooled gradient tensor gone.  False when the shape is
+    outside the fused kernel (nothing issued)."""
+    in_f = C * OH * OW
+    if not (batch <= 32 and in_f % _SKINNY_IN == 0 and out_f % 32 == 0 and dy.data_ptr() % 16 == 0
+            and dy.stride(0) % 4 == 0 and w.stride(0) % 4 == 0):
+        return False
+    xh, xw = dx.shape[-2], dx.shape[-1]
+    ev = PROBE.begin(f"linear_bwd:{in_f}->{out_f}")
+    call("fh_linear_bwd_fused_pool", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dw),
+         _cs(dw), ptr(db), _cs(db), ptr(dx), _cs(dx), ptr(pidx), _cs(pidx), _counts(counts),
+         nclients, batch, C, OH, OW, xh, xw, out_f, stream_handle())
+    PROBE.end(ev, 4.0 * nclients * batch * in_f * out_f,
+              _linear_bytes(nclients, batch, in_f, out_f, acts=3, weights=2) +
+              4.0 * nclients * batch * 3 * in_f, nclients)
+    return True
+
+
 def linear_head_ce(x, w, bias, targets, logits, dlogits, dw, db, dx, nclients, batch, in_f,
                    num_classes, loss_out=None, acc_loss=None, acc_correct=None, acc_seen=None,
                    reset=None, mask=None, p_drop=0.0, relu_in=False, counts=None):

@@ -194,6 +194,21 @@ int fh_linear_bwd_fused(const float* x, int64_t x_cs, const float* dy, int64_t d
                         const int32_t* counts, int32_t nclients, int32_t batch, int32_t in_f,
                         int32_t out_f, void* stream);
 
+/*
+ * fh_linear_bwd_fused_pool: fh_linear_bwd_fused for a layer whose input x is the flattened
+ * output of a 2x2 max-pool over ReLU'd maps [C][OH][OW] (SimpleCNN fc1,
+ * models_pytorch.py:91-95 — replaces that layer's backward + the pool's fh_maxpool2_bwd):
+ * dX is the gradient of the pool INPUT, planes xh x xw (map 2OH x 2OW top-left), the linear
+ * dgrad value routed to the window argmax pidx (dense [C][OH][OW]) where x > 0, zeros at the
+ * other window positions; elements outside the map untouched.
+ */
+int fh_linear_bwd_fused_pool(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                             const float* w, int64_t w_cs, float* dw, int64_t dw_cs, float* db,
+                             int64_t db_cs, float* dx, int64_t dx_cs, const uint8_t* pidx,
+                             int64_t pi_cs, const int32_t* counts, int32_t nclients, int32_t batch,
+                             int32_t C, int32_t OH, int32_t OW, int32_t xh, int32_t xw,
+                             int32_t out_f, void* stream);
+
 /* ---------------- BatchNorm2d (+ReLU, +residual add) ----------------------
  * x/y/res: [clients][batch][C][HW]; gamma/beta live in the per-client param
  * rows (stride p_cs); running stats stride r_cs (NULL: not tracked);

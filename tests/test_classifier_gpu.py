@@ -170,3 +170,40 @@ def test_linear_fwd_dropout_equals_two_launches(nc, in_f, out_f, mode):
     for z in range(nc):
         n = int(cnt[z])
         assert torch.equal(e1[z, :n], e2[z, :n]) and torch.equal(m1[z, :n], m2[z, :n])
+
+
+@pytest.mark.parametrize("nc,plane", [(3, 16), (1, 14), (33, 16)])
+def test_linear_bwd_fused_pool_equals_two_launches(nc, plane):
+    """fh_linear_bwd_fused_pool (SimpleCNN fc1 after pool2, models_pytorch.py:91-95) writes
+    the pool INPUT's gradient directly: bit-identical to fh_linear_bwd_fused (the pooled
+    gradient) + fh_maxpool2_bwd_ymask (routed to the argmax, ReLU mask = pooled output > 0),
+    the same dW / db, and the planes' elements outside the 14x14 map untouched."""
+    B, C, OH, OW, out_f = 32, 64, 7, 7, 128
+    in_f = C * OH * OW
+    cnt = _counts(nc, B, 11)
+    g = torch.Generator(device=DEV).manual_seed(nc)
+    # pooled ReLU output: non-negative with exact zeros (the mask matters)
+    x = torch.relu(torch.randn(nc, B, C, OH, OW, generator=g, device=DEV))
+    idx = torch.randint(0, 4, (nc, B, C, OH, OW), generator=g, device=DEV).to(torch.uint8)
+    dy = torch.randn(nc, B, out_f, generator=g, device=DEV)
+    w = torch.randn(nc, out_f, in_f, generator=g, device=DEV) * 0.02
+    dw1, db1 = torch.zeros(nc, out_f, in_f, device=DEV), torch.zeros(nc, out_f, device=DEV)
+    dw2, db2 = torch.zeros_like(dw1), torch.zeros_like(db1)
+    dp = torch.zeros(nc, B, in_f, device=DEV)
+    assert ops.linear_bwd_fused(x.view(nc, B, in_f), dy, w, dw1, db1, dp, nc, B, in_f, out_f,
+                                counts=cnt)
+    sentinel = 7.0  # outside the map: must stay untouched
+    da1 = torch.full((nc, B, C, plane, plane), sentinel, device=DEV)
+    da1[..., :14, :14] = 0.0
+    ops.maxpool2_bwd_ymask(dp.view(nc, B, C, OH, OW), idx, x, da1, nc, B, C, 14, 14, counts=cnt)
+    da2 = torch.full_like(da1, sentinel)
+    da2[..., :14, :14] = 0.0
+    assert ops.linear_bwd_fused_pool(x.view(nc, B, in_f), dy, w, dw2, db2, da2, idx, nc, B, C, OH,
+                                     OW, out_f, counts=cnt)
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw2) and torch.equal(db1, db2)
+    for z in range(nc):
+        n = int(cnt[z])
+        assert torch.equal(da1[z, :n], da2[z, :n])
+        if plane > 14:
+            assert bool((da2[z, :, :, 14:, :] == sentinel).all())

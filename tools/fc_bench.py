@@ -10,6 +10,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from fedhip import ops  # noqa: E402
 
 LAYERS = [(2048, 512), (512, 256), (256, 10)]
+if os.environ.get("FH_BENCH_LAYERS"):  # e.g. "3136x128,128x10" (SimpleCNN)
+    LAYERS = [tuple(int(v) for v in t.split("x")) for t in os.environ["FH_BENCH_LAYERS"].split(",")]
 
 
 def timeit(fn, it=30):
@@ -43,7 +45,8 @@ def main():
             t2 = timeit(lambda: ops.linear_dgrad(dy, w, dx, C, B, fi, fo))
             t3 = timeit(lambda: ops.linear_wgrad(x, dy, dw, db, C, B, fi, fo))
             tot += t1 + t2 + t3
-            line += f" | {fi}->{fo} {t1:6.1f} {t2:6.1f} {t3:6.1f}"
+            gbs = 4.0 * C * (B * fi + B * fo + fi * fo) / (t1 * 1e-6) / 1e9  # fwd algorithmic
+            line += f" | {fi}->{fo} {t1:6.1f} {t2:6.1f} {t3:6.1f} (fwd {gbs:5.0f} GB/s)"
         print(line + f" | total {tot:7.1f} us", flush=True)
 
 

@@ -14,7 +14,7 @@ fi
 [ $# -eq 0 ] && set -- "FH_NOOP=1"
 i=0
 for E in "$@"; do
-  env $E timeout -k 10 300 python bench.py --no-cpu-baseline --rounds-target 0 --no-instances --no-k2 --steps ${STEPS:-5} --warmup 1 > $OUT/bench_$i.json 2> $OUT/bench_$i.err
+  env $E timeout -k 10 300 python bench.py --config ${CONFIG:-KT} --no-cpu-baseline --rounds-target 0 --no-instances --no-k2 --steps ${STEPS:-5} --warmup 1 > $OUT/bench_$i.json 2> $OUT/bench_$i.err
   python -c "import json; d=json.load(open('$OUT/bench_$i.json')); print('$E', d['value'], d['ms_per_step'], d['round_frac'])" | tee -a $OUT/summary.txt
   i=$((i+1))
 done
