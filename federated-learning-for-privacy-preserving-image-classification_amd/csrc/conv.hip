@@ -1335,6 +1335,10 @@ static const int kDconvForceSplits = env_int("FH_DCONV_SPLITS", 0);  // sweeps: 
 static const int kDwgradForceSplits = env_int("FH_DWGRAD_SPLITS", 0);
 static const int kDconvCk32 = env_int("FH_DCONV_CK32", 8);  // sweeps: CK of the BM=32 tiles
 
+// split over input channels below kDconvSplitBelow workgroups, toward kDconvSplitTarget
+// (sweep knobs FH_DCONV_SPLIT_BELOW / FH_DCONV_SPLIT_TARGET; r02 defaults 512 / 1024)
+static const int kDconvSplitBelow = env_int("FH_DCONV_SPLIT_BELOW", 512);
+static const int kDconvSplitTarget = env_int("FH_DCONV_SPLIT_TARGET", 1024);
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false,
                         bool ck4 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
@@ -1350,8 +1354,8 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
     p.ck = (ck4 || p.bm == 128 || Cr <= 4) ? 4 : (p.bm == 32 && kDconvCk32 == 4) ? 4 : 8;
     const int64_t blocks = tn * ceil_div(M, p.bm) * nclients;
     const int chunks = (int)ceil_div(Cr, p.ck);
-    if ((kDconvForceSplits > 0 || blocks < fill(512)) && chunks > 1) {
-        int want = (int)std::min<int64_t>(ceil_div(fill(1024), blocks), chunks);
+    if ((kDconvForceSplits > 0 || blocks < fill(kDconvSplitBelow)) && chunks > 1) {
+        int want = (int)std::min<int64_t>(ceil_div(fill(kDconvSplitTarget), blocks), chunks);
         if (kDconvForceSplits > 0) want = std::min(kDconvForceSplits, chunks);
         const int per = (int)ceil_div(chunks, want);
         p.cchunk = per * p.ck;

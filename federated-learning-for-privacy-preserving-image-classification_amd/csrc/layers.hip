@@ -318,13 +318,52 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     const float* wz = w + z * w_cs;
     const int FP = F + 1;
     if constexpr (SMALLK) {
-        for (int e = tid; e < cnt * F; e += 256) {
-            const int b = e / F;
-            Xs[b * FP + (e - b * F)] = xz[e];
-        }
-        for (int e = tid; e < K * F; e += 256) {
-            const int k = e / F;
-            Ws[k * FP + (e - k * F)] = wz[e];
+        // float4 loads, all issued before the LDS stores (r03: the element loop waited for
+        // each load in turn — ~20 dependent global round trips per launch)
+        const bool v4 = (F & 3) == 0 && ((uintptr_t)xz & 15) == 0 && ((uintptr_t)wz & 15) == 0;
+        if (v4) {
+            constexpr int NX = 32 * FMAX / 4 / 256, NW = KMAX * FMAX / 4 / 256;
+            const int F4 = F / 4;
+            float4 xv[NX], wv[NW];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                const int e4 = tid + 256 * i;
+                xv[i] = e4 < cnt * F4 ? *reinterpret_cast<const float4*>(xz + 4 * e4)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int e4 = tid + 256 * i;
+                wv[i] = e4 < K * F4 ? *reinterpret_cast<const float4*>(wz + 4 * e4)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                const int e4 = tid + 256 * i;
+                if (e4 < cnt * F4) {
+                    const int b = e4 / F4, f = 4 * (e4 - b * F4);
+                    float* d = Xs + b * FP + f;
+                    d[0] = xv[i].x; d[1] = xv[i].y; d[2] = xv[i].z; d[3] = xv[i].w;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int e4 = tid + 256 * i;
+                if (e4 < K * F4) {
+                    const int k = e4 / F4, f = 4 * (e4 - k * F4);
+                    float* d = Ws + k * FP + f;
+                    d[0] = wv[i].x; d[1] = wv[i].y; d[2] = wv[i].z; d[3] = wv[i].w;
+                }
+            }
+        } else {
+            for (int e = tid; e < cnt * F; e += 256) {
+                const int b = e / F;
+                Xs[b * FP + (e - b * F)] = xz[e];
+            }
+            for (int e = tid; e < K * F; e += 256) {
+                const int k = e / F;
+                Ws[k * FP + (e - k * F)] = wz[e];
+            }
         }
         __syncthreads();
     }
@@ -460,13 +499,24 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     // 4. input gradient through Dropout + ReLU, this block's share: dx[b][f] = sum_k D[b][k] W[k][f]
     if (dx) {
         const int per = (cnt * F + S - 1) / S, e0 = part * per, e1 = min(cnt * F, e0 + per);
-        for (int e = e0 + tid; e < e1; e += 256) {
-            const int img = e / F, f = e - img * F;
-            float acc = 0.f;
-            for (int k = 0; k < K; ++k) acc = fmaf(D[img * K + k], Wt(k, f), acc);
-            if (mask) acc = mask[z * m_cs + e] ? acc * scale : 0.f;
-            if (relu_in && !(X(img, f) > 0.f)) acc = 0.f;
-            dx[z * dx_cs + e] = acc;
+        for (int eb = e0 + tid; eb < e1; eb += 4 * 256) {  // keep-mask bytes of 4 outputs first
+            uint8_t mk[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = eb + 256 * u;
+                mk[u] = (mask && e < e1) ? mask[z * m_cs + e] : 1;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = eb + 256 * u;
+                if (e >= e1) break;
+                const int img = e / F, f = e - img * F;
+                float acc = 0.f;
+                for (int k = 0; k < K; ++k) acc = fmaf(D[img * K + k], Wt(k, f), acc);
+                if (mask) acc = mk[u] ? acc * scale : 0.f;
+                if (relu_in && !(X(img, f) > 0.f)) acc = 0.f;
+                dx[z * dx_cs + e] = acc;
+            }
         }
     }
 }
