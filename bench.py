@@ -358,7 +358,7 @@ def rounds_to_target(dev, target, max_rounds, opt, lr, oracle_budget_s=150.0, si
                     "the HIP run's from Philox: equal in distribution only)"}
 
 
-def measured_traffic(tag, flops_per_launch=None):
+def measured_traffic(tag, flops_per_launch=None, workload=None):
     """HBM bytes per launch of a conv launch shape, from the newest committed PMC
     measurement (profiles/*/traffic.json, tools/traffic3.py: separate rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes of tools/traffic_probe.py, x2 FETCH correction), else
@@ -369,6 +369,17 @@ def measured_traffic(tag, flops_per_launch=None):
     here = os.path.dirname(os.path.abspath(__file__))
     def newest_first(f):  # profiles/r01_v13 after r01_v7: compare the digit runs as numbers
         return [int(p) if p.isdigit() else p for p in re.split(r"(\d+)", f)]
+    # r03: PMC passes over the bench's own timed launches (tools/bench_traffic.py), per
+    # launch shape of that workload — preferred when this run is that workload
+    for f in sorted(glob.glob(os.path.join(here, "profiles", "*", "bench_traffic.json")),
+                    key=newest_first, reverse=True):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        sh = t.get("shapes", {}).get(tag)
+        if sh and t.get("workload") == workload:
+            return int(round(sh["bytes_per_launch"]))
     for f in sorted(glob.glob(os.path.join(here, "profiles", "*", "traffic.json")),
                     key=newest_first, reverse=True):
         try:
@@ -376,6 +387,8 @@ def measured_traffic(tag, flops_per_launch=None):
         except (OSError, ValueError):
             continue
         fit = t.get("shapes", {}).get(tag, {}).get("fit")
+        if tag.startswith("conv_wgrad:") and tag.endswith("s1"):
+            continue  # r02 fits: the stride-1 WGRAD kernel was replaced in r03 (stale)
         if fit and flops_per_launch:
             return int(round(fit["bytes_at_zero_flops"] + fit["bytes_per_flop"] * flops_per_launch))
         if t.get("probe") == tag:
@@ -420,7 +433,7 @@ def summarize_instances(inst, buckets, peak):
     return rows, instances, by_bucket, conv_all
 
 
-def roofline_of(tag, n, t, f, b, peak, hbm=False):
+def roofline_of(tag, n, t, f, b, peak, hbm=False, workload=None):
     """The roofline object of one launch shape averaged over all its launches."""
     common = {"kernel": tag, "launches_timed": n, "avg_launch_ms": round(t / n, 4),
               "flops_per_launch": round(f / n), "bytes_per_launch": round(b / n),
@@ -433,7 +446,7 @@ def roofline_of(tag, n, t, f, b, peak, hbm=False):
                     frac=round(ach / HBM_PEAK_GBS, 4), traffic=None)
     ach = f / (t * 1e-3) / 1e12
     return dict(common, bound="mfma", achieved=round(ach, 2), peak=peak, unit="TFLOP/s",
-                frac=round(ach / peak, 4), traffic=measured_traffic(tag, f / n))
+                frac=round(ach / peak, 4), traffic=measured_traffic(tag, f / n, workload))
 
 
 _MAPS_THREAD = None
@@ -556,7 +569,7 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         # batches, tail steps); roofline_hbm: the same for the largest HBM-bound shape
         tag, v = rows[0]
         ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
-        roof = roofline_of(tag, *v, peak, hbm=v[2] <= ridge * v[3])
+        roof = roofline_of(tag, *v, peak, hbm=v[2] <= ridge * v[3], workload=key)
         hb = [(tg, vv) for tg, vv in rows if vv[2] <= ridge * vv[3]]
         if hb:
             roof_hbm = roofline_of(hb[0][0], *hb[0][1], peak, hbm=True)

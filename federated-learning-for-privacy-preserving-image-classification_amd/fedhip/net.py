@@ -171,9 +171,12 @@ class PackedNet:
         # argmax bytes per staged quad) K2 1.362M -> 1.418 / 1.423M client-images/s,
         # interleaved (profiles/r03_k2/; r02's VALU form lost 7 %).  FH_FUSE_POOL1_BWD=0: off.
         self.fuse_pool1_bwd = os.environ.get("FH_FUSE_POOL1_BWD", "1") != "0"
-        # SimpleCNN: pool2's backward inside fc1's fused backward (fh_linear_bwd_fused_pool;
-        # FH_FUSE_POOL2_BWD=0: the pooled gradient + fh_maxpool2_bwd)
-        self.fuse_pool2_bwd = os.environ.get("FH_FUSE_POOL2_BWD", "1") != "0"
+        # SimpleCNN: pool2's backward inside fc1's fused backward (fh_linear_bwd_fused_pool,
+        # bit-identical, tests/test_classifier_gpu.py).  Measured neutral on K2 (10-round
+        # rounds, interleaved x3: 1.382M on vs 1.402M off, within the K2 spread;
+        # profiles/r03_k2/K2_fuse_pool2_bwd_ab.txt): the skinny DGRAD epilogue's routed
+        # window stores cost what the maxpool2_bwd pass did.  Off unless FH_FUSE_POOL2_BWD=1.
+        self.fuse_pool2_bwd = os.environ.get("FH_FUSE_POOL2_BWD", "0") == "1"
         self._pool1_fused = False
 
     # -------------------------------------------------------------- helpers
