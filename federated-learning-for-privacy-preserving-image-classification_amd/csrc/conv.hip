@@ -2232,9 +2232,8 @@ extern "C" int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float*
 // weight stream, so one workgroup owns 32 input features and runs the 32 images as the
 // MFMA's other dimension, the out_f reduction split over its four waves and combined
 // through LDS in wave order; W arrives as 128-B rows, dY as float4 runs.  fc1 dgrad at 32
-// clients: 44 us vs 81 for the implicit GEMM, fc2 12 vs 27 (tools/fc_bench.py).  The same
-// layout for FWD lost (one dependent MFMA chain per wave over K/4: 123 vs 57 us) and
-// stays on the implicit GEMM.
+// clients: 44 us vs 81 for the implicit GEMM, fc2 12 vs 27 (tools/fc_bench.py).  FWD: see
+// linear_fwd_skinny_kernel below (round 3; round 1's attempt at it lost to the implicit GEMM).
 namespace fh {
 static const int kLinearSkinny = env_int("FH_LINEAR_SKINNY", 1);
 // A/B: FH_SKINNY32=0 keeps the skinny WGRAD / fused linear backward to in_f % 128 == 0 (the
@@ -2442,11 +2441,220 @@ linear_bwd_fused_kernel(const float* __restrict__ X, int64_t x_cs, const float* 
 static bool skinny_aligned(const void* p, int64_t cs) {
     return ((uintptr_t)p % 16 == 0) && cs % 4 == 0;
 }
+
+// Skinny linear FORWARD (batch <= 32 images per client, in_f % 32 == 0: SimpleCNN fc1
+// 3136->128, CIFAR10CNN fc1 2048->512 / fc2 512->256): y[img][o] = sum_k x[img][k] w[o][k]
+// (+ bias, ReLU, dropout).  A stream of W — each weight feeds at most 32 images — so the
+// operands go from global memory straight to registers, no LDS staging: per 32-k block a lane
+// loads 64 contiguous bytes of one x row (img = lane & 31) and one w row (o = lane & 31), two
+// lanes per 128-B line, and the block's 16 v_mfma_f32_32x32x2_f32 pair k = (k0 + 4q + j,
+// k0 + 16 + 4q + j) on the two lane halves.  A wave owns 32 outputs x all 32 images (one
+// accumulator); a workgroup = OT such output tiles x KG = 4 / OT k-groups over one k-chunk
+// (the k-groups take interleaved blocks, so the four waves read neighbouring pieces of the
+// same rows, and are combined through LDS in k-group order).  D blocks of loads stay in
+// flight ahead of the MFMAs (round 1's skinny FWD ran one dependent chain over all of K per
+// wave with nothing in flight: 123 vs 57 us).  The workgroups of one client sit on one XCD
+// (x read once per L2).  splits == 1: bias / ReLU / dropout in the epilogue; else a
+// [client][split][32][out_f] slab, summed in split order by linear_fwd_epilogue_kernel.
+template <int D, int OT>
+__global__ void __launch_bounds__(256)
+linear_fwd_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float* __restrict__ W,
+                         int64_t w_cs, const float* __restrict__ bias, int64_t b_cs,
+                         float* __restrict__ Y, int64_t y_cs, float* __restrict__ part,
+                         const int32_t* __restrict__ counts, int batch, int K, int M, int kbps,
+                         int relu, DropArgs drop) {
+    constexpr int KG = 4 / OT;
+    __shared__ float red[KG > 1 ? (KG - 1) * OT * 16 * 64 : 1];
+    const int gx = gridDim.x, gy = gridDim.y;  // x: splits, y: output groups, z: clients
+    const int N = gx * gy * gridDim.z;
+    int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    if ((N & 7) == 0) b = (b & 7) * (N >> 3) + (b >> 3);  // XCD-aware, see wgrad_skinny
+    const int s = b % gx, rest = b / gx, og = rest % gy, z = rest / gy;
+    const int cnt = counts ? counts[z] : batch;
+    if (cnt <= 0) return;  // workgroup-uniform
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int ot = wid % OT, kg = wid / OT;
+    const int r = lane & 31, h = lane >> 5;
+    const int o0 = (og * OT + ot) * 32;
+    const bool active = o0 < M;  // wave-uniform; inactive waves still meet the barrier
+    const int kb0 = s * kbps;
+    const int nkb = min(kbps, K / 32 - kb0);
+    const int nmine = nkb > kg ? (nkb - kg + KG - 1) / KG : 0;  // blocks kg, kg + KG, ...
+    // rows past the batch / the outputs read a valid row and are never stored: an A row
+    // only reaches its own D row, a B column only its own D column
+    const float* xk = X + z * x_cs + (int64_t)min(r, cnt - 1) * K + (int64_t)(kb0 + kg) * 32 + 16 * h;
+    const float* wk = W + z * w_cs + (int64_t)min(o0 + r, M - 1) * K + (int64_t)(kb0 + kg) * 32 + 16 * h;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    if (active) {
+        float4 xa[D][4], wa[D][4];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (d < nmine) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    xa[d][q] = *reinterpret_cast<const float4*>(xk + d * KG * 32 + 4 * q);
+                    wa[d][q] = *reinterpret_cast<const float4*>(wk + d * KG * 32 + 4 * q);
+                }
+            }
+        for (int b0 = 0; b0 < nmine; b0 += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int bb = b0 + d;
+                if (bb < nmine) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[d][q].x, wa[d][q].x, acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[d][q].y, wa[d][q].y, acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[d][q].z, wa[d][q].z, acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[d][q].w, wa[d][q].w, acc, 0, 0, 0);
+                    }
+                    if (bb + D < nmine) {
+                        const int64_t off = (int64_t)(bb + D) * KG * 32;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            xa[d][q] = *reinterpret_cast<const float4*>(xk + off + 4 * q);
+                            wa[d][q] = *reinterpret_cast<const float4*>(wk + off + 4 * q);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (KG > 1) {  // k-groups 1.. hand their sums to k-group 0, added in order
+        if (kg > 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) red[(((kg - 1) * OT + ot) * 16 + i) * 64 + lane] = acc[i];
+        }
+        __syncthreads();
+        if (kg > 0) return;
+#pragma unroll
+        for (int g = 1; g < KG; ++g)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] += red[(((g - 1) * OT + ot) * 16 + i) * 64 + lane];
+    }
+    const int o = o0 + r;
+    if (!active || o >= M) return;
+    if (gx == 1) {
+        const float bv = bias ? bias[z * b_cs + o] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int img = (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (img < cnt) {
+                float v = acc[i];
+                if (bias) v = v + bv;
+                if (relu) v = fmaxf(v, 0.f);
+                const int64_t e = (int64_t)img * M + o;
+                if (drop.mode) v = apply_dropout(drop, z, e, v);
+                Y[z * y_cs + e] = v;
+            }
+        }
+    } else {
+        float* pp = part + ((int64_t)z * gx + s) * 32 * M + o;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int img = (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (img < cnt) pp[(int64_t)img * M] = acc[i];
+        }
+    }
+}
+
+// linear_fwd_skinny's split reduction: y[z][e] = epilogue(sum_s part[z][s][e]), e = img*M + o
+// (splitk_epilogue_kernel's operations and order: slabs in split order, + bias, ReLU, dropout)
+__global__ void __launch_bounds__(256)
+linear_fwd_epilogue_kernel(const float* __restrict__ part, int splits, int M,
+                           float* __restrict__ Y, int64_t y_cs, const float* __restrict__ bias,
+                           int64_t b_cs, int relu, const int32_t* __restrict__ counts, int batch,
+                           DropArgs drop) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= cnt * M) return;
+    const float* p = part + (int64_t)z * splits * 32 * M + e;
+    const int64_t ss = (int64_t)32 * M;
+    float v = 0.f;
+    for (int i0 = 0; i0 < splits; i0 += 8) {
+        float t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = i0 + j < splits ? p[(i0 + j) * ss] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (i0 + j < splits) v += t[j];
+    }
+    if (bias) v = v + bias[z * b_cs + e % M];
+    if (relu) v = fmaxf(v, 0.f);
+    if (drop.mode) v = apply_dropout(drop, z, e, v);
+    Y[z * y_cs + e] = v;
+}
+
+// Split plan of linear_fwd_skinny: enough k-chunks that (output groups x clients x chunks)
+// reaches fill(kLfTarget) workgroups, each k-group of a chunk >= kLfMinKb 32-k blocks.
+static const int kLfTarget = env_int("FH_LF_TARGET", 512);   // sweeps (tools/r03_lf.sh)
+static const int kLfMinKb = env_int("FH_LF_MINKB", 4);
+static const int kLfDepth = env_int("FH_LF_DEPTH", 2);
+static const int kLfOt = env_int("FH_LF_OT", 1);  // output tiles per workgroup: 1, 2, 4
+
+static bool linear_fwd_skinny_ok(int batch, int in_f, int out_f) {
+    return kLinearSkinny && kLinearSkinny != 3 && batch > 0 && batch <= 32 && in_f > 0 &&
+           in_f % 32 == 0 && out_f > 0;
+}
+
+static void plan_lin_fwd(int nclients, int in_f, int out_f, int64_t target, int& splits,
+                         int& kbps) {
+    const int ot = (kLfOt == 2 || kLfOt == 4) ? kLfOt : 1;
+    const int kb = in_f / 32;
+    const int64_t tiles = (int64_t)ceil_div(out_f, 32 * ot) * std::max(nclients, 1);
+    int64_t want = ceil_div(target, tiles);
+    want = std::min<int64_t>(want, std::max(1, kb / (kLfMinKb * (4 / ot))));
+    want = std::max<int64_t>(want, 1);
+    kbps = (int)ceil_div(kb, want);
+    splits = (int)ceil_div(kb, kbps);
+}
+
+static int linear_fwd_skinny(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                             const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                             const int32_t* counts, int nclients, int batch, int in_f, int out_f,
+                             int relu, const DropArgs& drop, void* workspace, size_t ws_bytes,
+                             hipStream_t st) {
+    int splits, kbps;
+    plan_lin_fwd(nclients, in_f, out_f, fill(kLfTarget), splits, kbps);
+    const int ot = (kLfOt == 2 || kLfOt == 4) ? kLfOt : 1;
+    const dim3 grid((unsigned)splits, (unsigned)ceil_div(out_f, 32 * ot), (unsigned)nclients);
+    float* part = nullptr;
+    if (splits > 1) {
+        const size_t need = (size_t)nclients * splits * 32 * out_f * sizeof(float);
+        FH_REQUIRE(workspace && ws_bytes >= need, "linear_fwd: workspace %zu < %zu", ws_bytes, need);
+        part = (float*)workspace;
+    }
+#define FH_LFD(DD, OO)                                                                           \
+    if (kLfDepth == DD && ot == OO)                                                              \
+        FH_LAUNCH((linear_fwd_skinny_kernel<DD, OO>), grid, dim3(256), 0, st, x, x_cs, w, w_cs,  \
+                  bias, b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop);      \
+    else
+    FH_LFD(1, 1) FH_LFD(3, 1) FH_LFD(4, 1) FH_LFD(1, 2) FH_LFD(2, 2) FH_LFD(3, 2) FH_LFD(1, 4)
+    FH_LFD(2, 4) FH_LFD(3, 4)
+        FH_LAUNCH((linear_fwd_skinny_kernel<2, 1>), grid, dim3(256), 0, st, x, x_cs, w, w_cs,
+                  bias, b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop);
+#undef FH_LFD
+    if (splits > 1)
+        FH_LAUNCH(linear_fwd_epilogue_kernel, dim3((unsigned)ceil_div(32 * out_f, 256), nclients),
+                  dim3(256), 0, st, (const float*)part, splits, out_f, y, y_cs, bias, b_cs, relu,
+                  counts, batch, drop);
+    return FH_OK;
+}
 }  // namespace fh
 
 extern "C" size_t fh_linear_fwd_workspace(int32_t nclients, int32_t batch, int32_t in_f,
                                           int32_t out_f) {
-    return fh_conv2d_fwd_workspace(nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0);
+    size_t ws = fh_conv2d_fwd_workspace(nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0);
+    if (fh::linear_fwd_skinny_ok(batch, in_f, out_f) && nclients > 0) {
+        int splits, kbps;  // the whole-chip plan has the most splits of any fill fraction
+        fh::plan_lin_fwd(nclients, in_f, out_f, fh::kLfTarget, splits, kbps);
+        if (splits > 1)
+            ws = std::max(ws, (size_t)nclients * splits * 32 * out_f * sizeof(float));
+    }
+    return ws;
 }
 
 extern "C" size_t fh_linear_dgrad_workspace(int32_t nclients, int32_t batch, int32_t in_f,
@@ -2459,6 +2667,11 @@ extern "C" int fh_linear_fwd(const float* x, int64_t x_cs, const float* w, int64
                              const int32_t* counts, int32_t nclients, int32_t batch, int32_t in_f,
                              int32_t out_f, int32_t relu, void* workspace, size_t ws_bytes,
                              void* stream) {
+    if (fh::linear_fwd_skinny_ok(batch, in_f, out_f) && nclients > 0 && x && w && y &&
+        fh::skinny_aligned(x, x_cs) && fh::skinny_aligned(w, w_cs))
+        return fh::linear_fwd_skinny(x, x_cs, w, w_cs, bias, b_cs, y, y_cs, counts, nclients,
+                                     batch, in_f, out_f, relu, fh::DropArgs{}, workspace,
+                                     ws_bytes, fh::as_stream(stream));
     return fh_conv2d_fwd(x, x_cs, w, w_cs, bias, b_cs, y, y_cs, counts, nclients, batch, in_f, 1, 1,
                          out_f, 1, 1, 1, 0, relu, workspace, ws_bytes, stream);
 }
@@ -2487,6 +2700,11 @@ extern "C" int fh_linear_fwd_dropout(const float* x, int64_t x_cs, const float* 
     a.M = out_f; a.N = batch; a.K = in_f;
     const float keep = 1.0f - p_drop;
     a.drop = DropArgs{mask, m_cs, drop_mode, keep, 1.0f / keep, seed, seed_dev};
+    if (linear_fwd_skinny_ok(batch, in_f, out_f) && skinny_aligned(x, x_cs) &&
+        skinny_aligned(w, w_cs))
+        return linear_fwd_skinny(x, x_cs, w, w_cs, bias, b_cs, y, y_cs, counts, nclients, batch,
+                                 in_f, out_f, relu, a.drop, workspace, ws_bytes,
+                                 as_stream(stream));
     return run_mn<OP_FWD>(a, 1, 1, 1, nclients, workspace, ws_bytes, y, y_cs, bias, b_cs, relu, 0,
                           1, as_stream(stream), "linear_fwd_dropout");
 }

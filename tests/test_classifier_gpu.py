@@ -4,7 +4,9 @@
   dropout/ReLU backward of its input (reference: CIFAR10CNN fc3 models_pytorch.py:159-165,
   SimpleCNN fc2 :96-97, FederatedResNet fc :241-246; criterion training.py:193-203).
 * fh_linear_bwd_fused: a linear layer's wgrad + dgrad + the dropout/ReLU backward of its
-  input in one launch (the same MFMA bodies: bit-identical to the separate kernels)."""
+  input in one launch (the same MFMA bodies: bit-identical to the separate kernels).
+* fh_linear_fwd on the skinny FORWARD kernel (in_f % 32 == 0, <= 32 images): exact on
+  integer-valued operands for split and unsplit plans, ragged batches, partial output tiles."""
 import pytest
 import torch
 
@@ -145,7 +147,7 @@ def test_linear_bwd_fused_declines_unsupported_shapes():
 
 
 @pytest.mark.parametrize("nc,in_f,out_f", [(1, 2048, 512), (32, 2048, 512), (5, 512, 256),
-                                           (3, 3136, 128)])
+                                           (3, 3136, 128), (9, 128, 64)])
 @pytest.mark.parametrize("mode", [1, 2])
 def test_linear_fwd_dropout_equals_two_launches(nc, in_f, out_f, mode):
     """fh_linear_fwd_dropout == fh_dropout_fwd(fh_linear_fwd(x)), bit for bit, unsplit and
@@ -207,3 +209,26 @@ def test_linear_bwd_fused_pool_equals_two_launches(nc, plane):
         assert torch.equal(da1[z, :n], da2[z, :n])
         if plane > 14:
             assert bool((da2[z, :, :, 14:, :] == sentinel).all())
+
+
+@pytest.mark.parametrize("nc,B,in_f,out_f", [(1, 32, 2048, 512), (32, 32, 3136, 128),
+                                             (7, 17, 256, 100), (64, 20, 128, 96),
+                                             (3, 32, 512, 256), (2, 1, 96, 33)])
+def test_linear_fwd_skinny_exact(nc, B, in_f, out_f):
+    """Integer-valued x, w, bias (every partial sum exact in fp32): y equals the fp64 product
+    exactly, whatever the split plan (1 client: 32-k chunks; 128-in layers: one split),
+    ReLU applied, rows past each client's count untouched."""
+    g = torch.Generator().manual_seed(in_f + out_f)
+    x = torch.randint(-3, 4, (nc, B, in_f), generator=g).float()
+    w = torch.randint(-3, 4, (nc, out_f, in_f), generator=g).float()
+    b = torch.randint(-5, 6, (nc, out_f), generator=g).float()
+    cnt = _counts(nc, B, nc + in_f)
+    y = torch.full((nc, B, out_f), 7.0, device=DEV)
+    ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), y, nc, B, in_f, out_f, relu=True, counts=cnt)
+    torch.cuda.synchronize()
+    ref = torch.relu(torch.einsum("zbk,zok->zbo", x.double(), w.double()) + b.double()[:, None])
+    yc = y.cpu()
+    for z in range(nc):
+        n = int(cnt[z])
+        assert torch.equal(yc[z, :n].double(), ref[z, :n]), z
+        assert torch.all(yc[z, n:] == 7.0)

@@ -12,6 +12,7 @@ from fedhip import ops  # noqa: E402
 LAYERS = [(2048, 512), (512, 256), (256, 10)]
 if os.environ.get("FH_BENCH_LAYERS"):  # e.g. "3136x128,128x10" (SimpleCNN)
     LAYERS = [tuple(int(v) for v in t.split("x")) for t in os.environ["FH_BENCH_LAYERS"].split(",")]
+FWD_ONLY = os.environ.get("FH_BENCH_FWD_ONLY") == "1"
 
 
 def timeit(fn, it=30):
@@ -42,8 +43,11 @@ def main():
             dx = torch.empty_like(x)
             dw, db = torch.empty_like(w), torch.empty_like(b)
             t1 = timeit(lambda: ops.linear_fwd(x, w, b, y, C, B, fi, fo, relu=True))
-            t2 = timeit(lambda: ops.linear_dgrad(dy, w, dx, C, B, fi, fo))
-            t3 = timeit(lambda: ops.linear_wgrad(x, dy, dw, db, C, B, fi, fo))
+            if FWD_ONLY:  # kernel-trace sweeps of the forward (tools/lf_trace.py)
+                t2 = t3 = 0.0
+            else:
+                t2 = timeit(lambda: ops.linear_dgrad(dy, w, dx, C, B, fi, fo))
+                t3 = timeit(lambda: ops.linear_wgrad(x, dy, dw, db, C, B, fi, fo))
             tot += t1 + t2 + t3
             gbs = 4.0 * C * (B * fi + B * fo + fi * fo) / (t1 * 1e-6) / 1e9  # fwd algorithmic
             line += f" | {fi}->{fo} {t1:6.1f} {t2:6.1f} {t3:6.1f} (fwd {gbs:5.0f} GB/s)"
