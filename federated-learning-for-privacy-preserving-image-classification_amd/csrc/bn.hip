@@ -302,7 +302,7 @@ maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __re
         if (drop_mode) {
             uint8_t keep;
             if (drop_mode == 1) {
-                const uint4 rr = Philox::gen(seed, (uint64_t)z, (uint64_t)e[k]);
+                const uint4 rr = Philox::gen(seed, philox_row(seed_dev, z), (uint64_t)e[k]);
                 keep = u01(rr.x) <= keep_prob ? 1 : 0;
                 mask[z * m_cs + e[k]] = keep;
             } else {

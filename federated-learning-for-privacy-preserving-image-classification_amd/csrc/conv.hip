@@ -52,7 +52,7 @@ __device__ __forceinline__ float apply_dropout(const DropArgs& d, int z, int64_t
     uint8_t keep;
     if (d.mode == 1) {
         const uint64_t seed = d.seed + (d.seed_dev ? *d.seed_dev : 0ull);
-        const uint4 r = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
+        const uint4 r = Philox::gen(seed, philox_row(d.seed_dev, z), (uint64_t)e);
         keep = u01(r.x) <= d.keep ? 1 : 0;
         d.mask[z * d.m_cs + e] = keep;
     } else {

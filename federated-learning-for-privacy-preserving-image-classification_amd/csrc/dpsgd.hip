@@ -79,7 +79,7 @@ dpsgd_noise_kernel(float* __restrict__ grad, int64_t g_cs, int64_t n,
     for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nq;
          q += (int64_t)gridDim.x * blockDim.x) {
         float r[4];
-        gauss4(key, (uint64_t)z, (uint64_t)q, r);
+        gauss4(key, philox_row(seed_dev, z), (uint64_t)q, r);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int64_t j = q * 4 + u;

@@ -188,6 +188,14 @@ struct Philox {
         return c;
     }
 };
+// Philox row key of local row z.  seed_dev (nullable) points to the device key block
+// {step key, n_ids, id[0..n_ids)}: with n_ids != 0 row z draws under its GLOBAL client id, so a
+// client's dropout / augmentation / DP-SGD noise streams do not depend on the rank, lane or
+// slot it trains in; else under z (callers then salt the seed per lane and rank).
+__device__ __forceinline__ uint64_t philox_row(const uint64_t* seed_dev, int z) {
+    return (seed_dev != nullptr && seed_dev[1] != 0ull) ? seed_dev[2 + z] : (uint64_t)z;
+}
+
 // uniform in (0, 1]
 __device__ __forceinline__ float u01(uint32_t x) {
     return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);

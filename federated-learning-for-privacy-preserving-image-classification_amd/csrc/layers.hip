@@ -63,7 +63,7 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
         if (drop_mode) {
             uint8_t keep;
             if (drop_mode == 1) {
-                const uint4 r = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
+                const uint4 r = Philox::gen(seed, philox_row(seed_dev, z), (uint64_t)e);
                 keep = u01(r.x) <= keep_prob ? 1 : 0;
                 mask[z * m_cs + e] = keep;
             } else {
@@ -126,7 +126,7 @@ dropout_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict_
          e += (int64_t)gridDim.x * blockDim.x) {
         uint8_t keep;
         if (drop_mode == 1) {
-            const uint4 r = Philox::gen(seed, (uint64_t)z, (uint64_t)e);
+            const uint4 r = Philox::gen(seed, philox_row(seed_dev, z), (uint64_t)e);
             keep = u01(r.x) <= keep_prob ? 1 : 0;
             mask[z * m_cs + e] = keep;
         } else {
@@ -667,7 +667,7 @@ gather_u8_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ l
                 const uchar4 a = aug_in[z * aug_cs + b];
                 ci = a.x; cj = a.y; fl = a.z;
             } else {
-                const uint4 rr = Philox::gen(seed, (uint64_t)z, (uint64_t)b);
+                const uint4 rr = Philox::gen(seed, philox_row(seed_dev, z), (uint64_t)b);
                 const uint32_t span = 2u * (uint32_t)pad + 1u;
                 ci = pad > 0 ? (int)(((uint64_t)rr.x * span) >> 32) : 0;
                 cj = pad > 0 ? (int)(((uint64_t)rr.y * span) >> 32) : 0;

@@ -130,6 +130,7 @@ class PackedTrainer:
         for name in SlotStorage.FIELDS:
             setattr(self, name, getattr(storage, name)[row0:row0 + capacity])
         self.net.salt = (row0 * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        self.client_ids = None  # set_client_ids: global id per slot (Philox row keys)
         self.num_batches_tracked = [0] * capacity
         self.seg_offsets = torch.tensor(L.seg_offsets(), dtype=torch.int64, device=dev)
         self.opt_type, self.lr, self.opt_step = "sgd", 0.01, 0
@@ -197,6 +198,17 @@ class PackedTrainer:
         L = self.layout
         return {n: L.view(self.params, n)[slot].reshape(s).clone()
                 for n, s in zip(L.names, L.shapes)}
+
+    def set_client_ids(self, ids):
+        """Global client id of each slot: every step's device key block carries them
+        (fh_common.h philox_row), so a client's dropout / augmentation / DP-SGD noise draws
+        depend on (round seed, step, client id) only — not on the rank, lane or slot it
+        trains in.  The per-lane / per-rank salt is then not needed (and would break that)."""
+        ids = np.asarray(list(ids), dtype=np.int64).reshape(-1)
+        if ids.size != self.capacity or (ids < 0).any():
+            raise FedHipError(f"set_client_ids: need {self.capacity} non-negative ids")
+        self.client_ids = ids
+        self.net.salt = 0
 
     # ------------------------------------------------------------ optimizer
     def begin_round(self, optimizer_type="sgd", lr=0.01):
@@ -315,12 +327,15 @@ class PackedTrainer:
             if not ops.PROBE.all:  # "*": an instrumented round, every launch timed
                 ops.PROBE.enabled = arm
             net.seed = (st["seed"] * 1000003 + g) & 0x7FFFFFFF
-            net.seed_dev = None
+            # the step's device key block (just copied into cur): the same keys as the
+            # host-side seed, plus the slots' global client ids when set
+            net.seed_dev = views["seed"]
             self._gather(st["data"], st["labels"], views, n, st["sample_elems"])
             self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
                                 adam_dev=views["adam"])
             if arm and not ops.PROBE.all:
                 ops.PROBE.enabled = False
+            net.seed_dev = None
         self._after_step(n)
 
     def _step_rows(self, plan, shard_offsets, seed):
@@ -328,14 +343,16 @@ class PackedTrainer:
         current-step slot `cur` [R] and typed views into it:
           gidx  int64 [S, B]  absolute sample index of each batch slot
           counts int32 [S], reset int32 [S]
-          seed  int64 [1]     (seed * 1000003 + g) * 1000003  -> dropout key base
+          seed  int64 [2 + S] the Philox key block: (seed * 1000003 + g) * 1000003 (the
+                              dropout key base), n_ids (S, or 0 without set_client_ids),
+                              then the slots' global client ids
           adam  f32 [2]       {sqrt(1 - b2^t), -lr / (1 - b1^t)} for t = g + 1"""
         G, S, B = plan["G"], plan["counts"].shape[1], self.batch
         r8 = lambda b: (b + 7) // 8 * 8
         o_cnt = S * B * 8
         o_rst = o_cnt + r8(S * 4)
         o_seed = o_rst + r8(S * 4)
-        o_adam = o_seed + 8
+        o_adam = o_seed + 8 * (2 + S)
         R = (o_adam + 8 + 15) // 16 * 16  # 16-B rows (fh_copy_bytes)
         buf = np.zeros((G, R), dtype=np.uint8)
         off = np.asarray(shard_offsets, dtype=np.int64).reshape(1, S, 1)
@@ -344,7 +361,12 @@ class PackedTrainer:
         buf[:, o_rst:o_rst + 4 * S] = plan["reset"].numpy().astype(np.int32).view(np.uint8)
         keys = np.array([(((seed * 1000003 + g) & 0x7FFFFFFF) * 1000003) & 0xFFFFFFFFFFFFFFFF
                          for g in range(G)], dtype=np.uint64)
-        buf[:, o_seed:o_seed + 8] = keys.view(np.uint8).reshape(G, 8)
+        block = np.zeros((G, 2 + S), dtype=np.uint64)
+        block[:, 0] = keys
+        if self.client_ids is not None:
+            block[:, 1] = S
+            block[:, 2:] = self.client_ids[:S].astype(np.uint64)
+        buf[:, o_seed:o_adam] = block.view(np.uint8).reshape(G, 8 * (2 + S))
         adam = np.zeros((G, 2), dtype=np.float32)
         for g in range(G):
             step_size, bc2_sqrt = ops.adam_bias_corrections(g + 1, self.lr)
@@ -358,7 +380,7 @@ class PackedTrainer:
         views = dict(gidx=cur[:o_cnt].view(torch.int64).view(S, B),
                      counts=cur[o_cnt:o_cnt + 4 * S].view(torch.int32),
                      reset=cur[o_rst:o_rst + 4 * S].view(torch.int32),
-                     seed=cur[o_seed:o_seed + 8].view(torch.int64),
+                     seed=cur[o_seed:o_adam].view(torch.int64),
                      adam=cur[o_adam:o_adam + 8].view(torch.float32))
         return rows, cur, views
 

@@ -176,6 +176,15 @@ class LanedTrainer:
         self._own_streams.append(handle.value)
         return torch.cuda.ExternalStream(handle.value, device=self.device)
 
+    def set_client_ids(self, ids):
+        """Global client id per slot (PackedTrainer.set_client_ids, lane by lane): Philox
+        row keys independent of the lane / rank a client lands in."""
+        ids = list(ids)
+        if len(ids) != self.capacity:
+            raise ValueError(f"set_client_ids: need {self.capacity} ids")
+        for i, ln in enumerate(self.lanes):
+            ln.set_client_ids(ids[self.cut[i]:self.cut[i + 1]])
+
     # PackedTrainer surface used by RankRound / bench
     @property
     def probe_full(self):

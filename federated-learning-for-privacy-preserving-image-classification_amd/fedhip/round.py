@@ -59,6 +59,8 @@ class RankRound:
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.trainer = LanedTrainer(template_model, steps or [0], batch=batch, device=self.device,
                                     lanes=lanes, salt=self.rank)
+        if self.slots:  # dropout / augmentation keyed by global client id (not rank / lane)
+            self.trainer.set_client_ids(self.slots)
         self.transform = transform  # ops.DataTransform when the shards are raw uint8 images
         self.trainer.transform = transform
         L = self.trainer.layout

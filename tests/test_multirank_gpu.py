@@ -22,10 +22,9 @@ Checks (per round):
     difference can flip a max-pool near-tie, which re-routes a gradient:
     measured 2 % of the update for the largest client, so the bound is 5 % — batches
     drawn from another client's stream, or another client's noise, miss it by 100x.
-    The model runs with dropout off: dropout and augmentation Philox streams are keyed by
-    (rank salt, lane, slot row), not by the global client id, so with dropout on a client's
-    masks DO change with its placement (statistically equivalent, not identical; DESIGN.md
-    §7) — layout invariance is claimed for shuffling and DP noise only.
+    The model runs with the reference's dropout on: dropout (and augmentation) Philox
+    streams are keyed by the global client id (r03), so a client's masks are
+    the same in every layout too (tests/test_client_keys_gpu.py checks them directly).
 """
 import os
 
@@ -58,7 +57,7 @@ def _run_layout(rank, world, dp):
     dev = torch.device("cuda", 0)
     mine = lpt_assign(SIZES, world)[rank]
     torch.manual_seed(0)
-    model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.0).to(dev)
+    model = hm.ModelFactory.create_model("cifar10_cnn").to(dev)
     rr = RankRound(model, SIZES, mine, epochs=1, device=dev, lanes=1, shuffle_seed=77,
                    dp=DPConfig(epsilon=DP_EPS) if dp else None, dp_seed=5)
     xs, ys = zip(*[_client_data(k, SIZES[k]) for k in rr.slots])
