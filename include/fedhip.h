@@ -279,7 +279,7 @@ int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* pidx, int64
  *   linears fh_linear_persample_sqnorm (||dy_i||^2 (||x_i||^2 + with_bias))
  * then fh_dpsgd_clip_coef -> coef [clients][batch], fh_scale_rows scales each layer's
  * upstream gradient rows by coef before the ordinary WGRAD (clipped sum), and
- * fh_dpsgd_noise adds sigma*C/B * N(0,1) (Philox key seed + *seed_dev, seed_dev nullable).
+ * fh_dpsgd_noise adds sigma*C/B * N(0,1) (Philox key seed + seed_dev[0], rows keyed as below).
  * Replaces: nothing in the reference (its DP clips whole update deltas, privacy.py:107-144);
  * sigma follows its Gaussian-mechanism formula (privacy.py:209). */
 size_t fh_conv2d_persample_sqnorm_workspace(int32_t nclients, int32_t batch, int32_t cin,
@@ -306,8 +306,11 @@ int fh_dpsgd_noise(float* grad, int64_t g_cs, int64_t n, const int32_t* counts, 
 /* ---------------- MaxPool2d(2,2) (+ fused Dropout after it) ---------------
  * idx: uint8 window argmax [clients][batch][C][H/2][W/2]; drop_mode 0 none,
  * 1 generate keep-mask (Philox4x32-10 keyed by seed, slot, element) into mask,
- * 2 apply the caller's mask (parity).  The Philox key is seed + *seed_dev
- * (seed_dev nullable: a per-step device value for graph replay).
+ * 2 apply the caller's mask (parity).  The Philox key is seed + seed_dev[0]
+ * (seed_dev nullable: a per-step device key block for graph replay).  Every seed_dev of
+ * this header points to that block, {step key, n_ids, id[0..n_ids)} (uint64): with
+ * n_ids != 0 client row z draws under id[z] (its global client id) instead of z, so a
+ * client's dropout / augmentation / DP-SGD noise does not depend on its slot.
  * Backward writes all four window slots;
  * xin (nullable) = the pooled ReLU output, to apply the ReLU mask at the argmax. */
 int fh_maxpool2_fwd(const float* x, int64_t x_cs, float* y, int64_t y_cs, uint8_t* idx,
