@@ -605,13 +605,24 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         "instances": instances,
         "instances_by_clients": by_bucket,
     }
-    if world == 1 and rtt and args.rounds_target > 0:
-        out["rounds_to_target"] = rounds_to_target(dev, args.rounds_target, args.rounds_max,
-                                                   args.opt, args.lr)
-    if world == 1 and cpu and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, [train[k] for k in rr.slots], args.opt, args.lr)
+    # the host-CPU legs (oracle rounds-to-target, CPU baseline) run after every timed GPU
+    # leg of the process (host_legs): their torch CPU thread pool would otherwise still be
+    # spinning while a later config's rounds are issued from the host
+    out["_host"] = (cfg, [train[k] for k in rr.slots], world == 1 and rtt and args.rounds_target > 0,
+                    world == 1 and cpu and not args.no_cpu_baseline)
     del rr, data, lab
     torch.cuda.empty_cache()
+    return out
+
+
+def host_legs(out, args, dev):
+    """rounds_to_target and cpu_baseline of a run_config result (rank 0)."""
+    cfg, sizes, rtt, cpu = out.pop("_host")
+    if rtt:
+        out["rounds_to_target"] = rounds_to_target(dev, args.rounds_target, args.rounds_max,
+                                                   args.opt, args.lr)
+    if cpu:
+        out["cpu_baseline"] = cpu_baseline(cfg, sizes, args.opt, args.lr)
     return out
 
 
@@ -720,12 +731,14 @@ def main():
     if world == 1 and args.config == "KT" and not args.no_k2:
         k2 = run_config("K2", args, world, rank, dev, max(args.steps, 3), args.warmup)
         if k2 is not None:
+            host_legs(k2, args, dev)
             out["k2"] = {k: k2[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
                                            "warmup", "config", "achieved_tflops_step",
                                            "round_frac", "roofline", "roofline_hbm",
                                            "conv_linear_all_launches", "instances",
                                            "instances_by_clients", "cpu_baseline") if k in k2}
     if rank == 0:
+        host_legs(out, args, dev)
         # every FH_* knob in the environment (diagnostics / A-B switches): none is set in a
         # driver run; a line measured with one set says so here
         out["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("FH_")}

@@ -1631,6 +1631,12 @@ static DWPlan plan_c1_mfma(int batch, int h, int nclients) {
     return p;
 }
 
+// byte offset of the bias partials behind the weight partials [client][split][MN] of a
+// WGRAD slab (every WGRAD path lays its workspace out this way)
+static int64_t wslab_bias_off(int nclients, int splits, int64_t MN) {
+    return (int64_t)(((size_t)nclients * splits * MN * sizeof(float) + 255) / 256 * 256);
+}
+
 static size_t dwgrad_ws_bytes(const DWPlan& p, int nclients, int M, int N) {
     const size_t wb = (size_t)nclients * p.splits * M * N * sizeof(float);
     return ((wb + 255) / 256) * 256 + (size_t)nclients * p.splits * M * sizeof(float);
@@ -2033,7 +2039,12 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
                              void* workspace, size_t ws_bytes, const int32_t* counts,
                              int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
                              int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad,
-                             void* stream) {
+                             void* stream, int32_t* defer_splits = nullptr,
+                             int64_t* defer_boff = nullptr) {
+    // defer_splits (fh_conv2d_wgrad_deferred): a split plan leaves its partials in the
+    // workspace for the optimizer step to sum; the reduction launch is skipped
+    if (defer_splits) *defer_splits = 1;
+    if (defer_boff) *defer_boff = 0;
     int oh, ow;
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);
     if (rc) return rc;
@@ -2070,6 +2081,11 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
                       dy_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps,
                       (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0);
         FH_LAUNCH_CHECK("conv2d_wgrad c1 mfma");
+        if (defer_splits) {
+            *defer_splits = p.splits;
+            *defer_boff = wslab_bias_off(nclients, p.splits, cout * cin * kh * kw);
+            return FH_OK;
+        }
         if (const int _r = splitk_sum((const float*)part, dw, dw_cs, p.splits, cout * 9,
                                       (const float*)bpart, db, db_cs, cout, nclients, st))
             return _r;
@@ -2091,6 +2107,11 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
                   (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0);
         FH_LAUNCH_CHECK("conv2d_wgrad c1");
         const int MN = cout * 9;
+        if (defer_splits) {
+            *defer_splits = p.splits;
+            *defer_boff = wslab_bias_off(nclients, p.splits, cout * cin * kh * kw);
+            return FH_OK;
+        }
         if (const int _r = splitk_sum((const float*)part, dw, dw_cs, p.splits, MN, (const float*)bpart, db, db_cs, cout, nclients, st)) return _r;
         FH_LAUNCH_CHECK("conv2d_wgrad c1 reduce");
         return FH_OK;
@@ -2113,6 +2134,11 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         else FH_LAUNCH((dconv_wgrad_small_kernel<8, 3>), grid, dim3(256), 0, st, d);
         FH_LAUNCH_CHECK("conv2d_wgrad small-cin");
         const int MN = a.M * a.N;
+        if (defer_splits) {
+            *defer_splits = p.splits;
+            *defer_boff = wslab_bias_off(nclients, p.splits, cout * cin * kh * kw);
+            return FH_OK;
+        }
         if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)d.bias_part, db, db_cs, a.M, nclients, st)) return _r;
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
         return FH_OK;
@@ -2147,6 +2173,11 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         FH_LAUNCH_CHECK("conv2d_wgrad direct (quadrant waves)");
         if (p.splits == 1) return FH_OK;
         const int MN = a.M * a.N;
+        if (defer_splits) {
+            *defer_splits = p.splits;
+            *defer_boff = wslab_bias_off(nclients, p.splits, cout * cin * kh * kw);
+            return FH_OK;
+        }
         if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)d.bias_part, db, db_cs, a.M, nclients, st)) return _r;
         FH_LAUNCH_CHECK("conv2d_wgrad reduce");
         return FH_OK;
@@ -2168,6 +2199,11 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         else FH_LAUNCH((dconv_wgrad_kernel<8, 2, 1, 2, 8, 2>), grid, dim3(256), 0, st, d);
         FH_LAUNCH_CHECK("conv2d_wgrad direct s2");
         const int MN = a.M * a.N;
+        if (defer_splits) {
+            *defer_splits = p.splits;
+            *defer_boff = wslab_bias_off(nclients, p.splits, cout * cin * kh * kw);
+            return FH_OK;
+        }
         if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)d.bias_part, db, db_cs, a.M, nclients, st)) return _r;
         FH_LAUNCH_CHECK("conv2d_wgrad s2 reduce");
         return FH_OK;
@@ -2199,6 +2235,11 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
     if (rc) return rc;
     FH_LAUNCH_CHECK("conv2d_wgrad");
     const int MN = a.M * a.N;
+    if (defer_splits) {
+        *defer_splits = p.splits;
+        *defer_boff = wslab_bias_off(nclients, p.splits, cout * cin * kh * kw);
+        return FH_OK;
+    }
     if (const int _r = splitk_sum((const float*)workspace, dw, dw_cs, p.splits, MN, (const float*)a.bias_part, db, db_cs, a.M, nclients, st)) return _r;
     FH_LAUNCH_CHECK("conv2d_wgrad reduce");
     return FH_OK;
@@ -2212,6 +2253,20 @@ extern "C" int fh_conv2d_wgrad(const float* x, int64_t x_cs, const float* dy, in
     return conv2d_wgrad_impl(x, x_cs, nullptr, nullptr, 0, dy, dy_cs, dw, dw_cs, db, db_cs,
                              workspace, ws_bytes, counts, nclients, batch, cin, h, w_, cout, kh,
                              kw, stride, pad, stream);
+}
+
+extern "C" int fh_conv2d_wgrad_deferred(
+    const float* x, int64_t x_cs, const float* in_scale, const float* in_shift, int64_t aff_cs,
+    const float* dy, int64_t dy_cs, float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* slab,
+    size_t slab_bytes, const int32_t* counts, int32_t nclients, int32_t batch, int32_t cin,
+    int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad,
+    int32_t* splits_out, int64_t* bias_off_out, void* stream) {
+    FH_REQUIRE(splits_out && bias_off_out, "conv2d_wgrad_deferred: null output");
+    FH_REQUIRE((in_scale == nullptr) == (in_shift == nullptr),
+               "conv2d_wgrad_deferred: scale/shift pair");
+    return conv2d_wgrad_impl(x, x_cs, in_scale, in_shift, aff_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
+                             slab, slab_bytes, counts, nclients, batch, cin, h, w_, cout, kh, kw,
+                             stride, pad, stream, splits_out, bias_off_out);
 }
 
 extern "C" int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float* in_scale,

@@ -122,11 +122,232 @@ adam4_kernel(float4* __restrict__ p, const float4* __restrict__ g, float4* __res
     }
 }
 
+// ---- optimizer steps that finish split WGRAD reductions (r03) --------------------------
+// The row is cut into ranges: slab ranges (a convolution's weight or bias gradient still
+// split over pixel ranges, fh_conv2d_wgrad_deferred) and the plain ranges between them.
+// blockIdx.y = client, blockIdx.x walks the ranges' blocks (blk0 = a range's first block).
+// A slab block is conv.hip splitk_sum_kernel<G> line for line — a thread owns one float4 of
+// outputs and one of G contiguous split ranges, 8 loads in flight, the G range sums added in
+// range order through LDS, G chosen from the split count as splitk_sum does — so g has the
+// bits the separate reduction launch gave; g is stored and the update applied in place.
+// A plain block reads g and updates 1024 float4s.  The separate reduction launch, its write
+// of g and the optimizer's read of g disappear for every split layer.
+struct SlabRange {
+    int off4, len4;       // float4s within a row
+    const float4* slab;   // null: plain range
+    int splits, G, blk0, pad;
+};
+struct SlabRanges {
+    int n;
+    SlabRange r[2 * FH_MAX_GRAD_SLABS + 1];
+};
+struct OptScal {  // SGD: neg_lr, mom, wd, first | Adam: the adam_elem scalars
+    float neg_lr, mom, wd;
+    int first;
+    float decay_mul, one_m_b1, b2, one_m_b2, bc2_sqrt, eps, neg_step_size;
+    int decoupled;
+    const float* scal;  // Adam: device {bc2_sqrt, -step_size} or null
+};
+
+constexpr int kOptPlainPer = 1024;  // float4s per plain block
+
+template <bool ADAM>
+__device__ __forceinline__ void opt_update4(float4* p, float4* s1, float4* s2, int64_t i,
+                                            float4 gv, const OptScal& o, float bc2_sqrt,
+                                            float neg_step) {
+    const float4 pv = p[i];
+    float4 out;
+    if constexpr (!ADAM) {
+        const bool use_buf = o.mom != 0.f;
+        const float4 bv = (use_buf && !o.first) ? s1[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 b;
+        out.x = sgd_elem(pv.x, gv.x, bv.x, o.neg_lr, o.mom, o.wd, o.first, b.x);
+        out.y = sgd_elem(pv.y, gv.y, bv.y, o.neg_lr, o.mom, o.wd, o.first, b.y);
+        out.z = sgd_elem(pv.z, gv.z, bv.z, o.neg_lr, o.mom, o.wd, o.first, b.z);
+        out.w = sgd_elem(pv.w, gv.w, bv.w, o.neg_lr, o.mom, o.wd, o.first, b.w);
+        if (use_buf) s1[i] = b;
+    } else {
+        float4 mv = s1[i], vv = s2[i];
+#define FH_ADAM_LANE(c) out.c = adam_elem(pv.c, gv.c, mv.c, vv.c, o.wd, o.decay_mul, o.decoupled, \
+                                          o.one_m_b1, o.b2, o.one_m_b2, bc2_sqrt, o.eps, neg_step)
+        FH_ADAM_LANE(x); FH_ADAM_LANE(y); FH_ADAM_LANE(z); FH_ADAM_LANE(w);
+#undef FH_ADAM_LANE
+        s1[i] = mv;
+        s2[i] = vv;
+    }
+    p[i] = out;
+}
+
+template <bool ADAM>
+__global__ void __launch_bounds__(256)
+opt_slabs_kernel(float4* __restrict__ p, float4* __restrict__ g, float4* __restrict__ s1,
+                 float4* __restrict__ s2, int64_t row4, const SlabRanges rg, const OptScal o) {
+    __shared__ float4 red[256];
+    const int z = blockIdx.y, bx = blockIdx.x, t = threadIdx.x;
+    int k = 0;
+    for (int i = 1; i < rg.n; ++i)
+        if (rg.r[i].blk0 <= bx) k = i;
+    const SlabRange R = rg.r[k];
+    const int64_t base = (int64_t)z * row4 + R.off4;
+    const float bc2_sqrt = (ADAM && o.scal) ? o.scal[0] : o.bc2_sqrt;
+    const float neg_step = (ADAM && o.scal) ? o.scal[1] : o.neg_step_size;
+    if (R.slab == nullptr) {
+        const int i0 = (bx - R.blk0) * kOptPlainPer + t;
+#pragma unroll
+        for (int u = 0; u < kOptPlainPer / 256; ++u) {
+            const int i = i0 + 256 * u;
+            if (i < R.len4) opt_update4<ADAM>(p, s1, s2, base + i, g[base + i], o, bc2_sqrt, neg_step);
+        }
+        return;
+    }
+    const int G = R.G, C = 256 / G;
+    const int e = (bx - R.blk0) * C + t % C;
+    const int piece = t / C, splits = R.splits;
+    const int s0 = (int)((int64_t)splits * piece / G), s1e = (int)((int64_t)splits * (piece + 1) / G);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < R.len4) {
+        const float4* src = R.slab + (int64_t)z * splits * R.len4 + e;
+        for (int i0 = s0; i0 < s1e; i0 += 8) {
+            float4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                v[j] = i0 + j < s1e ? src[(int64_t)(i0 + j) * R.len4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (i0 + j < s1e) {
+                    acc.x += v[j].x;
+                    acc.y += v[j].y;
+                    acc.z += v[j].z;
+                    acc.w += v[j].w;
+                }
+        }
+    }
+    if (G > 1) {  // block-uniform
+        red[t] = acc;
+        __syncthreads();
+        if (piece != 0) return;
+        for (int q = 1; q < G; ++q) {
+            const float4 w = red[t + C * q];
+            acc.x += w.x;
+            acc.y += w.y;
+            acc.z += w.z;
+            acc.w += w.w;
+        }
+    }
+    if (e >= R.len4) return;
+    g[base + e] = acc;
+    opt_update4<ADAM>(p, s1, s2, base + e, acc, o, bc2_sqrt, neg_step);
+}
+
+// conv.hip splitk_sum's thread-group count for a split count (kept identical: same bits)
+static int slab_groups(int splits) {
+    int G = 1;
+    while (G < 16 && splits >= 16 * G) G *= 2;
+    return G;
+}
+
+// host: the ranges of a row (slab ranges + the plain gaps) and their block offsets
+static int build_ranges(const fh_grad_slab* slabs, int nslabs, int64_t row_len, SlabRanges& rg,
+                        int& blocks) {
+    FH_REQUIRE(nslabs >= 0 && nslabs <= FH_MAX_GRAD_SLABS, "step_slabs: %d slab ranges (max %d)",
+               nslabs, FH_MAX_GRAD_SLABS);
+    FH_REQUIRE(nslabs == 0 || slabs, "step_slabs: null slab array");
+    FH_REQUIRE(row_len % 4 == 0 && row_len / 4 < (1ll << 30), "step_slabs: row_len %lld",
+               (long long)row_len);
+    rg.n = 0;
+    blocks = 0;
+    int64_t pos = 0;
+    auto add = [&](int64_t off, int64_t len, const float* slab, int splits) {
+        SlabRange& r = rg.r[rg.n++];
+        r.off4 = (int)(off / 4);
+        r.len4 = (int)(len / 4);
+        r.slab = (const float4*)slab;
+        r.splits = splits;
+        r.G = slab ? slab_groups(splits) : 1;
+        r.blk0 = blocks;
+        r.pad = 0;
+        blocks += (int)(slab ? ceil_div(r.len4, 256 / r.G) : ceil_div(r.len4, kOptPlainPer));
+    };
+    for (int i = 0; i < nslabs; ++i) {
+        const fh_grad_slab& s = slabs[i];
+        FH_REQUIRE(s.off >= pos && s.len > 0 && s.off + s.len <= row_len && s.off % 4 == 0 &&
+                       s.len % 4 == 0 && s.slab && (uintptr_t)s.slab % 16 == 0 && s.splits >= 1,
+                   "step_slabs: bad slab range %d (off %lld len %lld splits %d)", i,
+                   (long long)s.off, (long long)s.len, s.splits);
+        if (s.off > pos) add(pos, s.off - pos, nullptr, 0);
+        add(s.off, s.len, s.slab, s.splits);
+        pos = s.off + s.len;
+    }
+    if (pos < row_len) add(pos, row_len - pos, nullptr, 0);
+    return FH_OK;
+}
+
 }  // namespace fh
 
 using namespace fh;
 
 static int grid_for(int64_t n) { return (int)std::min<int64_t>(ceil_div(n, 256), 4096); }
+
+extern "C" int fh_sgd_step_slabs(float* param, float* grad, float* momentum_buf,
+                                 int64_t row_stride, int64_t row_len, int32_t nclients,
+                                 const fh_grad_slab* slabs, int32_t nslabs, float lr,
+                                 float momentum, float weight_decay, int32_t first_step,
+                                 void* stream) {
+    FH_REQUIRE(nclients >= 0 && row_stride >= row_len && row_stride % 4 == 0,
+               "sgd_step_slabs: bad shape");
+    if (nclients == 0 || row_len == 0) return FH_OK;
+    FH_REQUIRE(param && grad && (momentum == 0.f || momentum_buf), "sgd_step_slabs: null pointer");
+    FH_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)momentum_buf) % 16 == 0,
+               "sgd_step_slabs: rows must be 16-B aligned");
+    SlabRanges rg;
+    int blocks = 0;
+    if (const int rc = build_ranges(slabs, nslabs, row_len, rg, blocks)) return rc;
+    OptScal o{};
+    o.neg_lr = -lr;
+    o.mom = momentum;
+    o.wd = weight_decay;
+    o.first = first_step;
+    FH_LAUNCH(opt_slabs_kernel<false>, dim3(blocks, nclients), dim3(256), 0, as_stream(stream),
+              (float4*)param, (float4*)grad, (float4*)momentum_buf, (float4*)nullptr,
+              row_stride / 4, rg, o);
+    FH_LAUNCH_CHECK("sgd_step_slabs");
+    return FH_OK;
+}
+
+extern "C" int fh_adam_step_slabs(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
+                                  int64_t row_stride, int64_t row_len, int32_t nclients,
+                                  const fh_grad_slab* slabs, int32_t nslabs, double lr,
+                                  double beta1, double beta2, double eps, double weight_decay,
+                                  int32_t decoupled, double step_size, double bc2_sqrt,
+                                  const float* scal_dev, void* stream) {
+    FH_REQUIRE(nclients >= 0 && row_stride >= row_len && row_stride % 4 == 0,
+               "adam_step_slabs: bad shape");
+    if (nclients == 0 || row_len == 0) return FH_OK;
+    FH_REQUIRE(param && grad && exp_avg && exp_avg_sq, "adam_step_slabs: null pointer");
+    FH_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) %
+                       16 == 0,
+               "adam_step_slabs: rows must be 16-B aligned");
+    SlabRanges rg;
+    int blocks = 0;
+    if (const int rc = build_ranges(slabs, nslabs, row_len, rg, blocks)) return rc;
+    // fh_adam_step's fp32 roundings of the double scalars
+    OptScal o{};
+    o.wd = (float)weight_decay;
+    o.decay_mul = (float)(1.0 - lr * weight_decay);
+    o.decoupled = decoupled;
+    o.one_m_b1 = (float)(1.0 - beta1);
+    o.b2 = (float)beta2;
+    o.one_m_b2 = (float)(1.0 - beta2);
+    o.bc2_sqrt = (float)bc2_sqrt;
+    o.eps = (float)eps;
+    o.neg_step_size = (float)(-step_size);
+    o.scal = scal_dev;
+    FH_LAUNCH(opt_slabs_kernel<true>, dim3(blocks, nclients), dim3(256), 0, as_stream(stream),
+              (float4*)param, (float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq,
+              row_stride / 4, rg, o);
+    FH_LAUNCH_CHECK("adam_step_slabs");
+    return FH_OK;
+}
 
 extern "C" int fh_sgd_step(float* param, const float* grad, float* momentum_buf, int64_t n,
                            float lr, float momentum, float weight_decay, int32_t first_step,

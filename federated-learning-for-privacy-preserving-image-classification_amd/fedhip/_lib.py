@@ -40,6 +40,9 @@ SIGNATURES = {
     "fh_dp_apply": (I32, [P, I64, P, I64, P, I64, I32, I64, P, P, P, P, I64, U64, P, P]),
     "fh_sgd_step": (I32, [P, P, P, I64, F32, F32, F32, I32, P]),
     "fh_adam_step": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, I32, F64, F64, P, P]),
+    "fh_sgd_step_slabs": (I32, [P, P, P, I64, I64, I32, P, I32, F32, F32, F32, I32, P]),
+    "fh_adam_step_slabs": (I32, [P, P, P, P, I64, I64, I32, P, I32, F64, F64, F64, F64, F64, I32,
+                                 F64, F64, P, P]),
     "fh_conv2d_fwd_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "fh_conv2d_dgrad_workspace": (SZ, [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "fh_conv2d_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, I32,
@@ -91,6 +94,8 @@ SIGNATURES = {
                                 I32, I32, I32, F32, F32, I32, P]),
     "fh_conv2d_fwd_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
                                    I32, I32, I32, I32, I32, I32, I32, I32, P, SZ, P]),
+    "fh_conv2d_wgrad_deferred": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32,
+                                       I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P]),
     "fh_conv2d_wgrad_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32,
                                      I32, I32, I32, I32, I32, I32, I32, I32, I32, P]),
     "fh_maxpool2_fwd_pitched": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32,

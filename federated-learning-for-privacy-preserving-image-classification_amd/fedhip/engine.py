@@ -145,6 +145,10 @@ class PackedTrainer:
             self._coef = torch.zeros(capacity, batch, device=dev)
         self.on_step = None
         self.pre_step = None
+        # split WGRAD reductions finished inside the optimizer launch (ops.GradSlabs);
+        # FH_DEFER_WGRAD=0 restores the separate reduction launches (A/B)
+        self.defer_wgrad_reduce = os.environ.get("FH_DEFER_WGRAD", "1") != "0"
+        self._slabs = None
         # Step graphs: every step after the first of a round is replayed from a HIP graph
         # captured once per (active slots, optimizer, lr, data); the per-step inputs (batch
         # indices, counts, epoch resets, dropout key, Adam bias corrections) are copied into
@@ -219,7 +223,19 @@ class PackedTrainer:
         self.state1.zero_()
         self.state2.zero_()
 
-    def _optimizer_launch(self, n, first, adam_dev=None):
+    def _optimizer_launch(self, n, first, adam_dev=None, slabs=None):
+        """slabs: the step's deferred WGRAD reductions (ops.GradSlabs), finished by the update."""
+        if slabs is not None:
+            if self.opt_type == "sgd":
+                ops.sgd_step_slabs(self.params, self.grads, self.state1, self.lr, 0.9, n,
+                                   slabs.ranges, first_step=first)
+            else:
+                adamw = self.opt_type == "adamw"
+                ops.adam_step_slabs(self.params, self.grads, self.state1, self.state2,
+                                    self.opt_step, self.lr, n, slabs.ranges,
+                                    weight_decay=0.01 if adamw else 0.0, decoupled=adamw,
+                                    scal_dev=adam_dev)
+            return
         cnt = n * self.Ppad
         if self.opt_type == "sgd":
             ops.sgd_step(self.params, self.grads, self.state1, self.lr, 0.9, first_step=first,
@@ -241,14 +257,14 @@ class PackedTrainer:
             # the last linear layer, the loss and that layer's backward: one launch
             net.forward(self.params, self.bufs, n, counts, train=True, head=False)
             net.head_ce(self.params, self.grads, n, counts, **ce)
-            net.backward(self.params, self.grads, n, counts)
-            self._optimizer_launch(n, first, adam_dev)
+            self._backward_and_update(n, counts, first, adam_dev)
             return
         net.forward(self.params, self.bufs, n, counts, train=True)
         ops.ce_fwd_bwd(net.logits, net.y, net.dlogits, n, self.batch, net.num_classes,
                        counts=counts, **ce)
         if self.dpsgd is None:
-            net.backward(self.params, self.grads, n, counts)
+            self._backward_and_update(n, counts, first, adam_dev)
+            return
         else:
             d = self.dpsgd
             net.backward_dpsgd(self.params, self.grads, n, counts, self._sq, self._coef,
@@ -256,6 +272,19 @@ class PackedTrainer:
                                noise_seed=net._seed(77 + 1000 * d.seed),
                                noise_seed_dev=net.seed_dev, P=self.layout.P)
         self._optimizer_launch(n, first, adam_dev)
+
+    def _backward_and_update(self, n, counts, first, adam_dev):
+        """Backward + optimizer; with defer_wgrad_reduce the split convolution weight
+        gradients are summed by the optimizer launch (ops.GradSlabs) — same bits."""
+        if not self.defer_wgrad_reduce:
+            self.net.backward(self.params, self.grads, n, counts)
+            self._optimizer_launch(n, first, adam_dev)
+            return
+        if self._slabs is None:
+            self._slabs = ops.GradSlabs(self.device)
+        with self._slabs.collect(self.grads) as slabs:
+            self.net.backward(self.params, self.grads, n, counts)
+        self._optimizer_launch(n, first, adam_dev, slabs=slabs)
 
     # ------------------------------------------------------------ one packed step
     def step(self, n, counts, reset=None):

@@ -371,21 +371,129 @@ def conv2d_c1_pool_wgrad(x, dpool, idx, y, dw, db, nclients, batch, h, wd, cout,
     return dw
 
 
+class FhGradSlab(ctypes.Structure):
+    """include/fedhip.h fh_grad_slab."""
+    _fields_ = [("off", ctypes.c_int64), ("len", ctypes.c_int64), ("slab", ctypes.c_void_p),
+                ("splits", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+MAX_GRAD_SLABS = 24  # FH_MAX_GRAD_SLABS
+
+
+class GradSlabs:
+    """Weight-gradient reductions a step leaves to its optimizer (r03).
+
+    While a trainer's backward runs inside ``with slabs.collect(grads):``, conv2d_wgrad
+    calls whose dW / db are views of the packed gradient rows go through
+    fh_conv2d_wgrad_deferred: a split plan keeps its per-split partial sums in this arena (a
+    region per layer, so they survive the rest of the backward) and records the row range;
+    ``ranges`` then go to sgd_step_slabs / adam_step_slabs, which sum them as the update's
+    first operation (the separate splitk_sum launch, its write of g and the optimizer's read
+    of g disappear).  The arena is grow-only; a superseded buffer stays alive because a
+    captured step may still address it."""
+
+    def __init__(self, device):
+        self.device = device
+        self.arena = torch.empty(0, dtype=torch.uint8, device=device)
+        self.retired = []
+        self.grads, self.off, self.ranges = None, 0, []
+
+    def collect(self, grads):
+        return _SlabScope(self, grads)
+
+    def take(self, nbytes):
+        nb = (int(nbytes) + 255) // 256 * 256
+        if self.off + nb > self.arena.numel():
+            self.retired.append(self.arena)
+            self.arena = torch.empty(max(2 * self.arena.numel(), 4 * nb, 16 << 20),
+                                     dtype=torch.uint8, device=self.device)
+            self.off = 0
+        p = self.arena.data_ptr() + self.off
+        self.off += nb
+        return p, nb
+
+    def row_range(self, t, length):
+        """Float offset of view t within the gradient rows (None if t is not such a view or
+        the range is not float4-aligned)."""
+        g = self.grads
+        if t is None or g is None or t.dim() < 1 or t.stride(0) != g.stride(0):
+            return None
+        off = (t.data_ptr() - g.data_ptr()) // 4
+        if off < 0 or off + length > g.stride(0) or off % 4 or length % 4:
+            return None
+        return off
+
+
+class _SlabScope:
+    def __init__(self, slabs, grads):
+        self.slabs, self.grads = slabs, grads
+
+    def __enter__(self):
+        global _DEFER
+        s = self.slabs
+        s.grads, s.off, s.ranges = self.grads, 0, []
+        _DEFER = s
+        return s
+
+    def __exit__(self, *exc):
+        global _DEFER
+        _DEFER = None
+        self.slabs.grads = None
+        return False
+
+
+_DEFER = None
+
+
+def _wgrad_deferred(d, x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts,
+                    in_affine):
+    """fh_conv2d_wgrad_deferred into the active GradSlabs arena; False when the layer cannot
+    defer (then the caller runs the reducing entry point)."""
+    n_w = cout * cin * k * k
+    off_w = d.row_range(dw, n_w)
+    off_b = d.row_range(db, cout) if db is not None else -1
+    if off_w is None or off_b is None or len(d.ranges) + 2 > MAX_GRAD_SLABS:
+        return False
+    key = ("fh_conv2d_wgrad_workspace", _FILL[0], nclients, batch, cin, h, wd, cout, k, k, stride,
+           pad)
+    need = _WS_SIZE.get(key)
+    if need is None:
+        need = _WS_SIZE[key] = load().fh_conv2d_wgrad_workspace(nclients, batch, cin, h, wd, cout,
+                                                                 k, k, stride, pad)
+    if need == 0:
+        return False
+    base, nb = d.take(need)
+    sc, sh = in_affine if in_affine is not None else (None, None)
+    splits, boff = ctypes.c_int32(), ctypes.c_int64()
+    call("fh_conv2d_wgrad_deferred", ptr(x), _cs(x), ptr(sc), ptr(sh),
+         _cs(sc) if sc is not None else 0, ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
+         base, nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
+         ctypes.byref(splits), ctypes.byref(boff), stream_handle())
+    if splits.value > 1:
+        d.ranges.append((off_w, n_w, base, splits.value))
+        if db is not None:
+            d.ranges.append((off_b, cout, base + boff.value, splits.value))
+    return True
+
+
 def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
                  in_affine=None):
-    """in_affine as in conv2d_fwd (fh_conv2d_wgrad_bnrelu)."""
-    ws, nb = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, cin, h, wd, cout, k,
-                     k, stride, pad)
+    """in_affine as in conv2d_fwd (fh_conv2d_wgrad_bnrelu).  Inside a GradSlabs scope the
+    split reduction is left to the optimizer step (fh_conv2d_wgrad_deferred)."""
     ev = PROBE.begin(_conv_tag("wgrad", cin, h, wd, cout, k, stride))
-    if in_affine is not None:
-        sc, sh = in_affine
-        call("fh_conv2d_wgrad_bnrelu", ptr(x), _cs(x), ptr(sc), ptr(sh), _cs(sc), ptr(dy),
-             _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db), ptr(ws), nb, _counts(counts), nclients,
-             batch, cin, h, wd, cout, k, k, stride, pad, stream_handle())
-    else:
-        call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db),
-             _cs(db), ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k,
-             stride, pad, stream_handle())
+    if _DEFER is None or not _wgrad_deferred(_DEFER, x, dy, dw, db, nclients, batch, cin, h, wd,
+                                             cout, k, stride, pad, counts, in_affine):
+        ws, nb = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, cin, h, wd, cout,
+                         k, k, stride, pad)
+        if in_affine is not None:
+            sc, sh = in_affine
+            call("fh_conv2d_wgrad_bnrelu", ptr(x), _cs(x), ptr(sc), ptr(sh), _cs(sc), ptr(dy),
+                 _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db), ptr(ws), nb, _counts(counts),
+                 nclients, batch, cin, h, wd, cout, k, k, stride, pad, stream_handle())
+        else:
+            call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db),
+                 _cs(db), ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k,
+                 stride, pad, stream_handle())
     PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad),
               _conv_bytes(nclients, batch, cin, h, wd, cout, k, stride, pad), nclients)
     return dw
@@ -597,6 +705,35 @@ def sgd_step(param, grad, buf, lr, momentum, weight_decay=0.0, first_step=False,
     n = param.numel() if n is None else n
     call("fh_sgd_step", ptr(param), ptr(grad), ptr(buf), n, float(lr), float(momentum),
          float(weight_decay), int(first_step), stream_handle())
+
+
+def _slab_array(ranges):
+    rs = sorted(ranges)
+    arr = (FhGradSlab * max(1, len(rs)))()
+    for i, (off, ln, p, sp) in enumerate(rs):
+        arr[i].off, arr[i].len, arr[i].slab, arr[i].splits = off, ln, p, sp
+    return arr, len(rs)
+
+
+def sgd_step_slabs(param, grad, buf, lr, momentum, nclients, ranges, weight_decay=0.0,
+                   first_step=False):
+    """fh_sgd_step over rows [0, nclients) finishing the deferred WGRAD reductions in
+    `ranges` (GradSlabs.ranges) first — the bits of conv2d_wgrad + sgd_step."""
+    arr, ns = _slab_array(ranges)
+    call("fh_sgd_step_slabs", ptr(param), ptr(grad), ptr(buf), param.stride(0), param.shape[1],
+         nclients, arr, ns, float(lr), float(momentum), float(weight_decay), int(first_step),
+         stream_handle())
+
+
+def adam_step_slabs(param, grad, exp_avg, exp_avg_sq, step, lr, nclients, ranges, beta1=0.9,
+                    beta2=0.999, eps=1e-8, weight_decay=0.0, decoupled=False, scal_dev=None):
+    """fh_adam_step (+ scal_dev) over rows [0, nclients) finishing `ranges` first."""
+    arr, ns = _slab_array(ranges)
+    step_size, bc2_sqrt = adam_bias_corrections(step, lr, beta1, beta2)
+    call("fh_adam_step_slabs", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq),
+         param.stride(0), param.shape[1], nclients, arr, ns, float(lr), float(beta1),
+         float(beta2), float(eps), float(weight_decay), int(decoupled), float(step_size),
+         float(bc2_sqrt), ptr(scal_dev), stream_handle())
 
 
 def adam_bias_corrections(step, lr, beta1=0.9, beta2=0.999):

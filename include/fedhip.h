@@ -106,6 +106,35 @@ int fh_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg
                  int32_t decoupled, double step_size, double bc2_sqrt, const float* scal_dev,
                  void* stream);
 
+/* Optimizer steps that finish split weight-gradient reductions (r03).  A convolution's
+ * weight gradient split over pixel ranges (fh_conv2d_wgrad_deferred) leaves per-split partial
+ * sums; the step sums them as its first operation instead of a separate reduction launch.
+ * Rows [0, nclients) of param / grad / state at stride row_stride, row_len floats each
+ * (row_len and row_stride multiples of 4, rows 16-B aligned).  Inside each slab range
+ * [off, off + len) of a row:  g = sum over s of slab[z][s][j - off], summed in the same
+ * order and with the same bits as fh_conv2d_wgrad's own reduction, and g is stored to grad;
+ * elsewhere g is read from grad.  Then every element gets the fh_sgd_step / fh_adam_step
+ * update (same bits).  slabs: HOST array (copied into the launch) of nslabs <=
+ * FH_MAX_GRAD_SLABS ranges, sorted, non-overlapping, off and len multiples of 4, each slab
+ * 16-B aligned with client stride splits * len. */
+#define FH_MAX_GRAD_SLABS 24
+typedef struct {
+    int64_t off;       /* first float of the range within a row */
+    int64_t len;       /* floats */
+    const float* slab; /* device [client][split][len] */
+    int32_t splits;
+    int32_t reserved;
+} fh_grad_slab;
+int fh_sgd_step_slabs(float* param, float* grad, float* momentum_buf, int64_t row_stride,
+                      int64_t row_len, int32_t nclients, const fh_grad_slab* slabs,
+                      int32_t nslabs, float lr, float momentum, float weight_decay,
+                      int32_t first_step, void* stream);
+int fh_adam_step_slabs(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
+                       int64_t row_stride, int64_t row_len, int32_t nclients,
+                       const fh_grad_slab* slabs, int32_t nslabs, double lr, double beta1,
+                       double beta2, double eps, double weight_decay, int32_t decoupled,
+                       double step_size, double bc2_sqrt, const float* scal_dev, void* stream);
+
 /* ---------------- convolution / linear (fp32 MFMA implicit GEMM) ----------
  * x: [clients][batch][cin][h][w]; w: [cout][cin][kh][kw] per client; y: [clients][batch][cout][oh][ow].
  * Supported: (kh,kw,stride) in {(3,3,1),(3,3,2),(1,1,1),(1,1,2)}, pad arbitrary. */
@@ -406,6 +435,18 @@ int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
                            size_t ws_bytes, const int32_t* counts, int32_t nclients,
                            int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
                            int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream);
+/* fh_conv2d_wgrad (in_scale / in_shift NULL) or fh_conv2d_wgrad_bnrelu without the final
+ * reduction: when the plan splits the pixel reduction (*splits_out > 1) the partial sums stay
+ * in `slab` (sized by fh_conv2d_wgrad_workspace) — weights [client][split][cout*cin*kh*kw] at
+ * byte 0, bias [client][split][cout] at byte *bias_off_out — for an optimizer step to finish
+ * (fh_sgd_step_slabs / fh_adam_step_slabs); *splits_out == 1: dw / db written directly. */
+int fh_conv2d_wgrad_deferred(const float* x, int64_t x_cs, const float* in_scale,
+                             const float* in_shift, int64_t aff_cs, const float* dy,
+                             int64_t dy_cs, float* dw, int64_t dw_cs, float* db, int64_t db_cs,
+                             void* slab, size_t slab_bytes, const int32_t* counts,
+                             int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
+                             int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad,
+                             int32_t* splits_out, int64_t* bias_off_out, void* stream);
 int fh_maxpool2_fwd_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
                            const float* in_shift, int64_t aff_cs, float* y, int64_t y_cs,
                            uint8_t* idx, int64_t i_cs, uint8_t* mask, int64_t m_cs,
