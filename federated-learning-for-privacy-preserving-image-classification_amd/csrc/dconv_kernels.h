@@ -119,8 +119,10 @@ struct DGeom {
 // BNB: the instance with the statistics epilogue — FWD the BatchNorm statistics, DGRAD the
 // BN-backward statistics (its registers would otherwise cost every instance an occupancy
 // step, e.g. DGRAD W=32 BM=32: 96 -> 114 VGPRs, 4 -> 3 waves per SIMD)
+// BM = 64: two waves per SIMD (the W=8 FWD statistics instance needed 260 registers, one
+// wave per SIMD; its 68 KB of LDS fit two workgroups per CU)
 template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC, int S = 1, bool BNB = false>
-__global__ void __launch_bounds__(256) dconv_kernel(const DConvArgs a) {
+__global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DConvArgs a) {
     using G = DGeom<W>;
     static_assert(S == 1 || (S == 2 && OP == OP_FWD), "stride 2: forward only");
     static_assert(!BNB || S == 1, "statistics epilogue: stride 1");
