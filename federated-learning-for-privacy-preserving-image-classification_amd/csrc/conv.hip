@@ -1339,6 +1339,13 @@ static const int kDconvCk32 = env_int("FH_DCONV_CK32", 8);  // sweeps: CK of the
 // (sweep knobs FH_DCONV_SPLIT_BELOW / FH_DCONV_SPLIT_TARGET; r02 defaults 512 / 1024)
 static const int kDconvSplitBelow = env_int("FH_DCONV_SPLIT_BELOW", 512);
 static const int kDconvSplitTarget = env_int("FH_DCONV_SPLIT_TARGET", 1024);
+// In-launch split sum (dconv_kernels.h DConvArgs::tickets, r03): the calling thread's zeroed
+// ticket counters (fh_set_split_tickets) and the split count the planner caps at so a last
+// arriver reads few partial tiles (FH_DCONV_INK=0: no cap, splitk_epilogue_kernel always)
+static thread_local int* g_tickets = nullptr;
+static thread_local int64_t g_ticket_n = 0;
+static const int kInkMaxSplits = env_int("FH_DCONV_INK", 4);
+
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false,
                         bool ck4 = false) {
     const int64_t tn = ceil_div((int64_t)batch * hw, 256);
@@ -1356,6 +1363,7 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
     const int chunks = (int)ceil_div(Cr, p.ck);
     if ((kDconvForceSplits > 0 || blocks < fill(kDconvSplitBelow)) && chunks > 1) {
         int want = (int)std::min<int64_t>(ceil_div(fill(kDconvSplitTarget), blocks), chunks);
+        if (kInkMaxSplits > 0) want = std::min(want, kInkMaxSplits);
         if (kDconvForceSplits > 0) want = std::min(kDconvForceSplits, chunks);
         const int per = (int)ceil_div(chunks, want);
         p.cchunk = per * p.ck;
@@ -1368,8 +1376,13 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
     return p;
 }
 
+// split slab: [z][split][M][Nfull] (splitk_epilogue_kernel) or the in-launch fragment slab
+// [tile][split][BM * 256] over the padded tile grid — the larger of the two
 static size_t dconv_ws_bytes(const DPlan& p, int nclients, int M, int batch, int hw) {
-    return p.splits > 1 ? (size_t)nclients * p.splits * M * batch * hw * sizeof(float) : 0;
+    if (p.splits <= 1) return 0;
+    const size_t mpad = (size_t)ceil_div(M, p.bm) * p.bm;
+    const size_t npad = (size_t)ceil_div((int64_t)batch * hw, 256) * 256;
+    return (size_t)nclients * p.splits * mpad * npad * sizeof(float);
 }
 
 template <int OP, int W, int S = 1, bool BNB = false>
@@ -1421,14 +1434,22 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     // float4 weight runs: 16-B aligned slices that never run past the tensor
     a.wvec = aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0);
     float* out = a.out;
-    if (p.splits > 1) a.out = (float*)ws;
     dim3 grid((unsigned)ceil_div(a.Nfull, 256), (unsigned)ceil_div(a.M, p.bm),
               (unsigned)(nclients * p.splits));
+    // the sum in the launch when this thread has ticket counters for every tile
+    const bool ink = p.splits > 1 && g_tickets != nullptr &&
+                     (int64_t)nclients * grid.x * grid.y <= g_ticket_n;
+    if (ink) {
+        a.slab = (float*)ws;
+        a.tickets = g_tickets;
+    } else if (p.splits > 1) {
+        a.out = (float*)ws;
+    }
     int rc;
     if constexpr (S == 2) {
         rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
-    } else if (a.bn_part && p.splits == 1) {  // the statistics epilogue instances
+    } else if (a.bn_part && (p.splits == 1 || ink)) {  // the statistics epilogue instances
         rc = w == 32 ? dconv_launch_w<OP, 32, 1, true>(p, grid, a, st)
            : w == 16 ? dconv_launch_w<OP, 16, 1, true>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 1, true>(p, grid, a, st);
@@ -1439,7 +1460,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     }
     if (rc) return rc;
     FH_LAUNCH_CHECK(name);
-    if (p.splits > 1) {
+    if (p.splits > 1 && !ink) {
         dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
@@ -1653,6 +1674,13 @@ extern "C" int fh_set_fill_fraction(float fraction) {
 }
 
 extern "C" float fh_get_fill_fraction(void) { return g_fill; }
+
+extern "C" int fh_set_split_tickets(int32_t* tickets, int64_t count) {
+    FH_REQUIRE(count >= 0 && (tickets != nullptr || count == 0), "set_split_tickets: bad args");
+    g_tickets = count > 0 ? (int*)tickets : nullptr;
+    g_ticket_n = count;
+    return FH_OK;
+}
 
 extern "C" size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
                                           int32_t w_, int32_t cout, int32_t kh, int32_t kw,

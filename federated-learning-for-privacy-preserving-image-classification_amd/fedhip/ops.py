@@ -35,12 +35,17 @@ def _counts(counts):
 
 
 class Workspace:
-    """Grow-only device scratch buffer (split-K partials)."""
+    """Grow-only device scratch buffer (split-K partials), plus the stream's zeroed ticket
+    counters for split direct convolutions summed inside their launch (fh_set_split_tickets;
+    allocated on first use outside a graph capture — a capture would record the zero fill)."""
+
+    TICKETS = 1 << 17
 
     def __init__(self, device):
         self.device = device
         self.buf = torch.empty(0, dtype=torch.uint8, device=device)
         self.retired = []
+        self.tickets = None
 
     def get(self, nbytes: int) -> torch.Tensor:
         if self.buf.numel() < nbytes:
@@ -153,12 +158,30 @@ def _linear_bytes(nclients, batch, in_f, out_f, acts=2, weights=1):
     return 4.0 * nclients * (batch * (acts - 1) * in_f + batch * out_f + weights * in_f * out_f)
 
 
+_TICKETS_SET = [None]
+# FH_SPLIT_TICKETS=1: split direct convolutions sum their partials inside the launch (ticket
+# counters per stream, write-through partials, the tile's last split adds them) instead of the
+# splitk_epilogue_kernel launch.  Bit-identical (tests/test_conv_gpu.py) but measured ~1 % slower
+# on KT than the separate launch at the same split cap (profiles/r03_s4/split_sum_ab.txt;
+# with a release fence per workgroup it was 4.5 % slower): off by default
+IN_LAUNCH_SPLIT_SUM = (os.environ.get("FH_DCONV_INK", "4") != "0" and
+                       os.environ.get("FH_SPLIT_TICKETS", "0") == "1")
+
+
 def _ws(device) -> Workspace:
     # one scratch buffer per (device, stream): lanes on different streams run concurrently
     key = (str(device), torch.cuda.current_stream(device).cuda_stream)
-    if key not in _WS:
-        _WS[key] = Workspace(device)
-    return _WS[key]
+    w = _WS.get(key)
+    if w is None:
+        w = _WS[key] = Workspace(device)
+    if w.tickets is None and not torch.cuda.is_current_stream_capturing():
+        w.tickets = torch.zeros(Workspace.TICKETS, dtype=torch.int32, device=device)
+        _TICKETS_SET[0] = None
+    if _TICKETS_SET[0] is not w:  # this stream's ticket counters for the launches that follow
+        t = w.tickets if IN_LAUNCH_SPLIT_SUM else None
+        call("fh_set_split_tickets", ptr(t), 0 if t is None else t.numel())
+        _TICKETS_SET[0] = w
+    return w
 
 
 _WS_SIZE: dict = {}
