@@ -457,16 +457,44 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const BNArgs a) {
     const float gm = n > 0 ? (float)(sg / (double)n) : 0.f;
     const float* xz = a.x + z * a.x_cs;
     float* dxz = a.dx + z * a.dx_cs;
+    auto apply4 = [&](float4 g, float4 xv) {
+        float4 r;
+        r.x = (((g.x - gm) - (xv.x - mean) * k) * invstd) * w;
+        r.y = (((g.y - gm) - (xv.y - mean) * k) * invstd) * w;
+        r.z = (((g.z - gm) - (xv.z - mean) * k) * invstd) * w;
+        r.w = (((g.w - gm) - (xv.w - mean) * k) * invstd) * w;
+        return r;
+    };
+    if (a.vec) {
+        // float4 path, two element quads per thread per iteration with every load issued
+        // before the first store (dx may alias nothing the loop reads, but the compiler
+        // cannot know: one quad per iteration left one HBM round trip per quad)
+        const int e0 = s * a.chunk, e1 = min((int)n, e0 + a.chunk);
+        const int64_t istride = (int64_t)a.C * a.HW, coff = (int64_t)c * a.HW;
+        for (int e = e0 + threadIdx.x * 4; e < e1; e += 2 * 256 * 4) {
+            const bool two = e + 256 * 4 < e1;
+            uint32_t img, p;
+            a.fd_hw.divmod(e, img, p);
+            const int64_t oa = img * istride + coff + p;
+            int64_t ob = oa;
+            if (two) {
+                a.fd_hw.divmod(e + 256 * 4, img, p);
+                ob = img * istride + coff + p;
+            }
+            const float4 xa = ld4(xz + oa), xb = ld4(xz + ob);
+            const float4 ua = upstream4(a, z, oa), ub = upstream4(a, z, ob);
+            const float4 ra = apply4(rm.apply4(ua, xa, oa), xa);
+            const float4 rb = apply4(rm.apply4(ub, xb, ob), xb);
+            st4(dxz + oa, ra);
+            if (two) st4(dxz + ob, rb);
+        }
+        return;
+    }
     for_slice(a, z, c, s, [&](int64_t o, int nv) {
         if (nv == 4) {
             const float4 xv = ld4(xz + o);
             const float4 g = rm.apply4(upstream4(a, z, o), xv, o);
-            float4 r;
-            r.x = (((g.x - gm) - (xv.x - mean) * k) * invstd) * w;
-            r.y = (((g.y - gm) - (xv.y - mean) * k) * invstd) * w;
-            r.z = (((g.z - gm) - (xv.z - mean) * k) * invstd) * w;
-            r.w = (((g.w - gm) - (xv.w - mean) * k) * invstd) * w;
-            st4(dxz + o, r);
+            st4(dxz + o, apply4(g, xv));
         } else {
             const float xv = xz[o];
             const float g = rm.keep(xv, o) ? upstream1(a, z, o) : 0.f;

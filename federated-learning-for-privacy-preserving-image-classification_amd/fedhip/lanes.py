@@ -80,6 +80,9 @@ def plan_lanes(slot_steps: Sequence[int], max_lanes: int = MAX_LANES, a: float =
     return [0] + _balanced(slot_steps, head, S, rest, a, b)
 
 
+_LANE_STREAMS: dict = {}
+
+
 class LanedTrainer:
     """PackedTrainer-compatible round driver over L concurrent lanes (see module doc)."""
 
@@ -150,7 +153,16 @@ class LanedTrainer:
         cu_env = os.environ.get("FH_LANE_CU")
         if not cu_env:  # torch-owned stream; the long lane 0 dispatches first by default
             prios = [int(v) for v in prio_env.split(",")] if prio_env else [-1, 0]
-            return torch.cuda.Stream(self.device, priority=prios[min(i, len(prios) - 1)])
+            prio = prios[min(i, len(prios) - 1)]
+            # one stream per (device, lane index, priority) for the whole process: HIP maps
+            # streams to its hardware queues (4 per process) in creation order, so a second
+            # LanedTrainer with fresh streams (the K2 line after KT in one bench process) could
+            # put two of its lanes on one queue and serialise them (K2 1.02M vs 1.46M alone)
+            key = (str(self.device), i, prio)
+            st = _LANE_STREAMS.get(key)
+            if st is None:
+                st = _LANE_STREAMS[key] = torch.cuda.Stream(self.device, priority=prio)
+            return st
         mask_words = None
         prio = 0
         if cu_env:
