@@ -1345,6 +1345,7 @@ static const int kDconvSplitTarget = env_int("FH_DCONV_SPLIT_TARGET", 1024);
 static thread_local int* g_tickets = nullptr;
 static thread_local int64_t g_ticket_n = 0;
 static const int kInkMaxSplits = env_int("FH_DCONV_INK", 4);
+static const int kDconvMinStages = env_int("FH_DCONV_MINSTAGES", 1);
 
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false,
                         bool ck4 = false) {
@@ -1364,6 +1365,9 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
     if ((kDconvForceSplits > 0 || blocks < fill(kDconvSplitBelow)) && chunks > 1) {
         int want = (int)std::min<int64_t>(ceil_div(fill(kDconvSplitTarget), blocks), chunks);
         if (kInkMaxSplits > 0) want = std::min(want, kInkMaxSplits);
+        // each split keeps >= kDconvMinStages stages: a split saves K-loop time, the
+        // reduction launch costs about a stage's worth of latency on a narrow grid
+        want = std::max(1, std::min(want, chunks / std::max(1, kDconvMinStages)));
         if (kDconvForceSplits > 0) want = std::min(kDconvForceSplits, chunks);
         const int per = (int)ceil_div(chunks, want);
         p.cchunk = per * p.ck;
@@ -1987,13 +1991,15 @@ extern "C" int fh_conv2d_c1_pool_fwd(const float* x, int64_t x_cs, const float* 
 // fh_conv2d_wgrad in one pass — the full-resolution gradient is never written; dpool and y
 // (the pooled ReLU output, whose sign is the mask at the argmax) in planes gh x gw.
 // Workspace: fh_conv2d_wgrad_workspace(nclients, batch, 1, h, w, cout, 3, 3, 1, 1).
-extern "C" int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float* dpool,
-                                       int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
-                                       const float* y, int64_t y_cs, float* dw, int64_t dw_cs,
-                                       float* db, int64_t db_cs, void* workspace,
-                                       size_t ws_bytes, const int32_t* counts, int32_t nclients,
-                                       int32_t batch, int32_t h, int32_t w_, int32_t cout,
-                                       int32_t gh, int32_t gw, void* stream) {
+static int c1_pool_wgrad_impl(const float* x, int64_t x_cs, const float* dpool, int64_t dp_cs,
+                              const uint8_t* idx, int64_t i_cs, const float* y, int64_t y_cs,
+                              float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
+                              size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                              int32_t batch, int32_t h, int32_t w_, int32_t cout, int32_t gh,
+                              int32_t gw, void* stream, int32_t* defer_splits,
+                              int64_t* defer_boff) {
+    if (defer_splits) *defer_splits = 1;
+    if (defer_boff) *defer_boff = 0;
     FH_REQUIRE(nclients >= 0 && batch > 0 && h >= 2 && w_ >= 2 && !(h & 1) && !(w_ & 1) &&
                gh >= h / 2 && gw >= w_ / 2, "conv2d_c1_pool_wgrad: bad shape");
     FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_wgrad: cout %d (32 or 64)", cout);
@@ -2020,6 +2026,11 @@ extern "C" int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float
                       dp_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps, idx, i_cs, y,
                       y_cs, gh, gw);
         FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad mfma");
+        if (defer_splits) {  // the optimizer step sums the chunks (fh_sgd_step_slabs)
+            *defer_splits = p.splits;
+            *defer_boff = wslab_bias_off(nclients, p.splits, cout * 9);
+            return FH_OK;
+        }
         if (const int _r = splitk_sum((const float*)part, dw, dw_cs, p.splits, cout * 9,
                                       (const float*)bpart, db, db_cs, cout, nclients, st))
             return _r;
@@ -2031,9 +2042,38 @@ extern "C" int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float
               p.splits, idx, i_cs, y, y_cs, gh, gw);
     FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad");
     const int MN = cout * 9;
+    if (defer_splits) {
+        *defer_splits = p.splits;
+        *defer_boff = wslab_bias_off(nclients, p.splits, MN);
+        return FH_OK;
+    }
     if (const int _r = splitk_sum((const float*)part, dw, dw_cs, p.splits, MN, (const float*)bpart, db, db_cs, cout, nclients, st)) return _r;
     FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad reduce");
     return FH_OK;
+}
+
+extern "C" int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float* dpool,
+                                       int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
+                                       const float* y, int64_t y_cs, float* dw, int64_t dw_cs,
+                                       float* db, int64_t db_cs, void* workspace,
+                                       size_t ws_bytes, const int32_t* counts, int32_t nclients,
+                                       int32_t batch, int32_t h, int32_t w_, int32_t cout,
+                                       int32_t gh, int32_t gw, void* stream) {
+    return c1_pool_wgrad_impl(x, x_cs, dpool, dp_cs, idx, i_cs, y, y_cs, dw, dw_cs, db, db_cs,
+                              workspace, ws_bytes, counts, nclients, batch, h, w_, cout, gh, gw,
+                              stream, nullptr, nullptr);
+}
+
+extern "C" int fh_conv2d_c1_pool_wgrad_deferred(
+    const float* x, int64_t x_cs, const float* dpool, int64_t dp_cs, const uint8_t* idx,
+    int64_t i_cs, const float* y, int64_t y_cs, float* dw, int64_t dw_cs, float* db, int64_t db_cs,
+    void* slab, size_t slab_bytes, const int32_t* counts, int32_t nclients, int32_t batch,
+    int32_t h, int32_t w_, int32_t cout, int32_t gh, int32_t gw, int32_t* splits_out,
+    int64_t* bias_off_out, void* stream) {
+    FH_REQUIRE(splits_out && bias_off_out, "conv2d_c1_pool_wgrad_deferred: null output");
+    return c1_pool_wgrad_impl(x, x_cs, dpool, dp_cs, idx, i_cs, y, y_cs, dw, dw_cs, db, db_cs, slab,
+                              slab_bytes, counts, nclients, batch, h, w_, cout, gh, gw, stream,
+                              splits_out, bias_off_out);
 }
 
 extern "C" size_t fh_conv2d_wgrad_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,

@@ -90,6 +90,9 @@ SIGNATURES = {
                                     I32, I32, I32, I32, P]),
     "fh_conv2d_c1_pool_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, SZ, P,
                                       I32, I32, I32, I32, I32, I32, I32, P]),
+    "fh_conv2d_c1_pool_wgrad_deferred": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P,
+                                               SZ, P, I32, I32, I32, I32, I32, I32, I32, P, P,
+                                               P]),
     "fh_bn_apply_tiles": (I32, [P, P, I64, P, I64, P, I64, P, P, I64, P, P, I64, P, P, P, I32,
                                 I32, I32, I32, F32, F32, I32, P]),
     "fh_conv2d_fwd_bnrelu": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,

@@ -166,6 +166,8 @@ _TICKETS_SET = [None]
 # with a release fence per workgroup it was 4.5 % slower): off by default
 IN_LAUNCH_SPLIT_SUM = (os.environ.get("FH_DCONV_INK", "4") != "0" and
                        os.environ.get("FH_SPLIT_TICKETS", "0") == "1")
+# ... or only for lanes planning for at most this share of the chip (narrow, latency-bound lanes)
+SPLIT_TICKETS_FILL = float(os.environ.get("FH_SPLIT_TICKETS_FILL", "0"))
 
 
 def _ws(device) -> Workspace:
@@ -178,7 +180,8 @@ def _ws(device) -> Workspace:
         w.tickets = torch.zeros(Workspace.TICKETS, dtype=torch.int32, device=device)
         _TICKETS_SET[0] = None
     if _TICKETS_SET[0] is not w:  # this stream's ticket counters for the launches that follow
-        t = w.tickets if IN_LAUNCH_SPLIT_SUM else None
+        on = IN_LAUNCH_SPLIT_SUM or _FILL[0] <= SPLIT_TICKETS_FILL
+        t = w.tickets if on else None
         call("fh_set_split_tickets", ptr(t), 0 if t is None else t.numel())
         _TICKETS_SET[0] = w
     return w
@@ -381,13 +384,30 @@ def conv2d_c1_pool_wgrad(x, dpool, idx, y, dw, db, nclients, batch, h, wd, cout,
     """conv2d_c1_pool_fwd's weight gradient from the pooled gradient dpool (planes like y):
     maxpool2_bwd(xin = the ReLU output) + conv2d_wgrad in one pass
     (fh_conv2d_c1_pool_wgrad)."""
-    ws, nb = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, 1, h, wd, cout, 3, 3,
-                     1, 1)
     gh, gw = dpool.shape[-2], dpool.shape[-1]
     ev = PROBE.begin(_conv_tag("wgrad", 1, h, wd, cout, 3, 1) + "+pool")
-    call("fh_conv2d_c1_pool_wgrad", ptr(x), _cs(x), ptr(dpool), _cs(dpool), ptr(idx), _cs(idx),
-         ptr(y), _cs(y), ptr(dw), _cs(dw), ptr(db), _cs(db), ptr(ws), nb, _counts(counts),
-         nclients, batch, h, wd, cout, gh, gw, stream_handle())
+    d = _DEFER
+    off_w = d.row_range(dw, cout * 9) if d is not None else None
+    off_b = (d.row_range(db, cout) if db is not None else -1) if d is not None else None
+    if off_w is not None and off_b is not None and len(d.ranges) + 2 <= MAX_GRAD_SLABS:
+        # inside a GradSlabs scope: the chunk sums are left to the optimizer step
+        need = load().fh_conv2d_wgrad_workspace(nclients, batch, 1, h, wd, cout, 3, 3, 1, 1)
+        base, nb = d.take(need)
+        splits, boff = ctypes.c_int32(), ctypes.c_int64()
+        call("fh_conv2d_c1_pool_wgrad_deferred", ptr(x), _cs(x), ptr(dpool), _cs(dpool), ptr(idx),
+             _cs(idx), ptr(y), _cs(y), ptr(dw), _cs(dw), ptr(db), _cs(db), base, nb,
+             _counts(counts), nclients, batch, h, wd, cout, gh, gw, ctypes.byref(splits),
+             ctypes.byref(boff), stream_handle())
+        if splits.value > 1:
+            d.ranges.append((off_w, cout * 9, base, splits.value))
+            if db is not None:
+                d.ranges.append((off_b, cout, base + boff.value, splits.value))
+    else:
+        ws, nb = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, 1, h, wd, cout, 3,
+                         3, 1, 1)
+        call("fh_conv2d_c1_pool_wgrad", ptr(x), _cs(x), ptr(dpool), _cs(dpool), ptr(idx),
+             _cs(idx), ptr(y), _cs(y), ptr(dw), _cs(dw), ptr(db), _cs(db), ptr(ws), nb,
+             _counts(counts), nclients, batch, h, wd, cout, gh, gw, stream_handle())
     pooled = nclients * batch * cout * (h // 2) * (wd // 2)  # dpool + y fp32, argmax uint8
     PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1),
               4.0 * nclients * (batch * h * wd + cout * 9) + 9.0 * pooled, nclients)

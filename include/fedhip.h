@@ -525,6 +525,15 @@ int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float* dpool, in
                             size_t ws_bytes, const int32_t* counts, int32_t nclients,
                             int32_t batch, int32_t h, int32_t w_, int32_t cout, int32_t gh,
                             int32_t gw, void* stream);
+/* fh_conv2d_c1_pool_wgrad without the final reduction (as fh_conv2d_wgrad_deferred): the
+ * per-chunk partials stay in `slab` for fh_sgd_step_slabs / fh_adam_step_slabs. */
+int fh_conv2d_c1_pool_wgrad_deferred(const float* x, int64_t x_cs, const float* dpool,
+                                     int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
+                                     const float* y, int64_t y_cs, float* dw, int64_t dw_cs,
+                                     float* db, int64_t db_cs, void* slab, size_t slab_bytes,
+                                     const int32_t* counts, int32_t nclients, int32_t batch,
+                                     int32_t h, int32_t w_, int32_t cout, int32_t gh, int32_t gw,
+                                     int32_t* splits_out, int64_t* bias_off_out, void* stream);
 /* fh_bn_fwd_train (its apply pass: y = [relu](bn(x) [+ res]), save_mean / save_invstd,
  * running statistics) from the tiles fh_conv2d_fwd_bnstats left — FederatedResNet's stem
  * bn1 and block bn2 + residual + ReLU (models_pytorch.py:189-194, :241-242), whose output the
