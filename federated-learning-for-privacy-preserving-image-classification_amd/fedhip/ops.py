@@ -159,15 +159,18 @@ def _linear_bytes(nclients, batch, in_f, out_f, acts=2, weights=1):
 
 
 _TICKETS_SET = [None]
-# FH_SPLIT_TICKETS=1: split direct convolutions sum their partials inside the launch (ticket
-# counters per stream, write-through partials, the tile's last split adds them) instead of the
-# splitk_epilogue_kernel launch.  Bit-identical (tests/test_conv_gpu.py) but measured ~1 % slower
-# on KT than the separate launch at the same split cap (profiles/r03_s4/split_sum_ab.txt;
-# with a release fence per workgroup it was 4.5 % slower): off by default
+# Split direct convolutions sum their partials inside the launch (ticket counters per stream,
+# write-through partials, the tile's last split adds them) instead of a splitk_epilogue_kernel
+# launch — bit-identical (tests/test_conv_gpu.py).  On for the lanes that plan for at most half
+# of the chip (FH_SPLIT_TICKETS_FILL, default 0.5: the narrow lanes, where nearly every split
+# launch happens): KT / K2 within noise of the separate launch there
+# (profiles/r03_s4/narrow_lane_knobs_ab.txt), while for every lane it measured ~1 % slower
+# (split_sum_ab.txt; 4.5 % with a release fence per workgroup).  FH_SPLIT_TICKETS=1: every lane,
+# FH_SPLIT_TICKETS_FILL=0: none.
 IN_LAUNCH_SPLIT_SUM = (os.environ.get("FH_DCONV_INK", "4") != "0" and
                        os.environ.get("FH_SPLIT_TICKETS", "0") == "1")
-# ... or only for lanes planning for at most this share of the chip (narrow, latency-bound lanes)
-SPLIT_TICKETS_FILL = float(os.environ.get("FH_SPLIT_TICKETS_FILL", "0"))
+SPLIT_TICKETS_FILL = (float(os.environ.get("FH_SPLIT_TICKETS_FILL", "0.5"))
+                      if os.environ.get("FH_DCONV_INK", "4") != "0" else 0.0)
 
 
 def _ws(device) -> Workspace:

@@ -291,13 +291,13 @@ def test_dgrad_s2_shortcut_declines_unsupported():
 
 
 def _with_in_launch_sum(on, fn):
-    prev = ops.IN_LAUNCH_SPLIT_SUM
-    ops.IN_LAUNCH_SPLIT_SUM = on
+    prev = ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL
+    ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL = on, 0.0
     ops._TICKETS_SET[0] = None
     try:
         return fn()
     finally:
-        ops.IN_LAUNCH_SPLIT_SUM = prev
+        ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL = prev
         ops._TICKETS_SET[0] = None
 
 

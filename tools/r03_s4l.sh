@@ -4,6 +4,7 @@
 set -e
 T=$1
 O=$GRAFT_REPO_ROOT/gpurun_out/$T; mkdir -p $O
+cd $GRAFT_REPO_ROOT && timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; tail -1 $O/gpu_tests.log
 cd /tmp && export TMPDIR=/tmp
 for ck in 8 4; do
   FH_DCONV_CK32=$ck timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/fs_ck$ck -o run -- python3 $GRAFT_REPO_ROOT/tools/fullstep.py cifar10_cnn 23 12 > $O/fs_ck$ck.log 2>&1
