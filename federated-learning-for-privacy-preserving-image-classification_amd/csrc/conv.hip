@@ -2585,7 +2585,7 @@ linear_fwd_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float*
                          int64_t w_cs, const float* __restrict__ bias, int64_t b_cs,
                          float* __restrict__ Y, int64_t y_cs, float* __restrict__ part,
                          const int32_t* __restrict__ counts, int batch, int K, int M, int kbps,
-                         int relu, DropArgs drop) {
+                         int relu, DropArgs drop, int* __restrict__ tickets) {
     constexpr int KG = 4 / OT;
     __shared__ float red[KG > 1 ? (KG - 1) * OT * 16 * 64 : 1];
     const int gx = gridDim.x, gy = gridDim.y;  // x: splits, y: output groups, z: clients
@@ -2673,6 +2673,50 @@ linear_fwd_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float*
                 Y[z * y_cs + e] = v;
             }
         }
+    } else if (tickets != nullptr) {
+        // the split sum inside the launch (r03): partials stored write-through (sc1), the
+        // 32-output tile's last split to take a ticket adds them in split order and finishes
+        // the epilogue (linear_fwd_epilogue_kernel's operations) — one wave per tile, so the
+        // hand-off needs no barrier: the wave drains its stores, lane 0 takes the ticket
+        float* slab = part + (int64_t)z * gx * 32 * M;
+        // 4-byte stores: relaxed agent-scope atomic stores are the sc1 form (Guideline 16 R1;
+        // a raw_buffer_store_b32 of the vector elements lost its per-element data here)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int img = (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (img < cnt)
+                __hip_atomic_store(slab + ((int64_t)s * 32 + img) * M + o, acc[i],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int last = 0;
+        if (lane == 0) {
+            int* ctr = tickets + ((int64_t)z * gy + og) * OT + ot;
+            const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = old == gx - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        last = __shfl(last, 0, 64);
+        if (!last) return;
+        const float bv = bias ? bias[z * b_cs + o] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int img = (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (img < cnt) {
+                const float* pp = slab + (int64_t)img * M + o;
+                float v = 0.f;
+                for (int q = 0; q < gx; ++q) v += pp[(int64_t)q * 32 * M];
+                if (bias) v = v + bv;
+                if (relu) v = fmaxf(v, 0.f);
+                const int64_t e = (int64_t)img * M + o;
+                if (drop.mode) v = apply_dropout(drop, z, e, v);
+                Y[z * y_cs + e] = v;
+            }
+        }
     } else {
         float* pp = part + ((int64_t)z * gx + s) * 32 * M + o;
 #pragma unroll
@@ -2750,17 +2794,20 @@ static int linear_fwd_skinny(const float* x, int64_t x_cs, const float* w, int64
         FH_REQUIRE(workspace && ws_bytes >= need, "linear_fwd: workspace %zu < %zu", ws_bytes, need);
         part = (float*)workspace;
     }
+    // the split sum in the launch when this thread has ticket counters for every output tile
+    int* tk = (splits > 1 && g_tickets != nullptr &&
+               (int64_t)nclients * grid.y * ot <= g_ticket_n) ? g_tickets : nullptr;
 #define FH_LFD(DD, OO)                                                                           \
     if (kLfDepth == DD && ot == OO)                                                              \
         FH_LAUNCH((linear_fwd_skinny_kernel<DD, OO>), grid, dim3(256), 0, st, x, x_cs, w, w_cs,  \
-                  bias, b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop);      \
+                  bias, b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop, tk);  \
     else
     FH_LFD(1, 1) FH_LFD(3, 1) FH_LFD(4, 1) FH_LFD(1, 2) FH_LFD(2, 2) FH_LFD(3, 2) FH_LFD(1, 4)
     FH_LFD(2, 4) FH_LFD(3, 4)
         FH_LAUNCH((linear_fwd_skinny_kernel<2, 1>), grid, dim3(256), 0, st, x, x_cs, w, w_cs,
-                  bias, b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop);
+                  bias, b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop, tk);
 #undef FH_LFD
-    if (splits > 1)
+    if (splits > 1 && tk == nullptr)
         FH_LAUNCH(linear_fwd_epilogue_kernel, dim3((unsigned)ceil_div(32 * out_f, 256), nclients),
                   dim3(256), 0, st, (const float*)part, splits, out_f, y, y_cs, bias, b_cs, relu,
                   counts, batch, drop);

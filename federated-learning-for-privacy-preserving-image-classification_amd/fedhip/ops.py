@@ -159,17 +159,18 @@ def _linear_bytes(nclients, batch, in_f, out_f, acts=2, weights=1):
 
 
 _TICKETS_SET = [None]
-# Split direct convolutions sum their partials inside the launch (ticket counters per stream,
-# write-through partials, the tile's last split adds them) instead of a splitk_epilogue_kernel
-# launch — bit-identical (tests/test_conv_gpu.py).  On for the lanes that plan for at most half
-# of the chip (FH_SPLIT_TICKETS_FILL, default 0.5: the narrow lanes, where nearly every split
-# launch happens): KT / K2 within noise of the separate launch there
-# (profiles/r03_s4/narrow_lane_knobs_ab.txt), while for every lane it measured ~1 % slower
-# (split_sum_ab.txt; 4.5 % with a release fence per workgroup).  FH_SPLIT_TICKETS=1: every lane,
-# FH_SPLIT_TICKETS_FILL=0: none.
+# Split direct convolutions and classifier forwards can sum their partials inside the launch
+# (ticket counters per stream, write-through partials, the tile's last split adds them in
+# split order) instead of a reduction launch — bit-identical (tests/test_conv_gpu.py,
+# tests/test_classifier_gpu.py) but not faster: every lane ~1 % slower on KT (dconv only,
+# profiles/r03_s4/split_sum_ab.txt; 4.5 % with a release fence per workgroup), the narrow lanes
+# only within noise (narrow_lane_knobs_ab.txt), and with the classifier forward's last arriver
+# reading its partials one dependent load at a time KT -3 % / K2 -6 % (in_launch_linear_ab.txt).
+# Off: FH_SPLIT_TICKETS=1 turns it on for every lane, FH_SPLIT_TICKETS_FILL=x for the lanes that
+# plan for at most that share of the chip.
 IN_LAUNCH_SPLIT_SUM = (os.environ.get("FH_DCONV_INK", "4") != "0" and
                        os.environ.get("FH_SPLIT_TICKETS", "0") == "1")
-SPLIT_TICKETS_FILL = (float(os.environ.get("FH_SPLIT_TICKETS_FILL", "0.5"))
+SPLIT_TICKETS_FILL = (float(os.environ.get("FH_SPLIT_TICKETS_FILL", "0"))
                       if os.environ.get("FH_DCONV_INK", "4") != "0" else 0.0)
 
 
