@@ -1330,7 +1330,7 @@ static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 64);
 static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 256);
 // RGB-layer wgrad target: 512 workgroups (42 -> 34 us at 32 clients, profiles/r01_v12)
 static const int kDwgradSmallBlocks = env_int("FH_DWGRAD_SMALL_BLOCKS", 512);
-static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 2);  // tools/tail_sweep.py
+static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 1);  // r03 s4 (tail_sweep.py: 2 in r01)
 static const int kDconvForceSplits = env_int("FH_DCONV_SPLITS", 0);  // sweeps: force splits
 static const int kDwgradForceSplits = env_int("FH_DWGRAD_SPLITS", 0);
 static const int kDconvCk32 = env_int("FH_DCONV_CK32", 8);  // sweeps: CK of the BM=32 tiles
@@ -1575,7 +1575,7 @@ static bool dwgrad_supported(int cin, int cout, int h, int w, int kh, int kw, in
 // (512: tools/r03_wgrad_ab.sh sweep, profiles/r03_dwq/).  KT against the r02 kernel (32x32x2
 // MFMAs, four pixel-waves, one 86 KB workgroup per CU): 270.3k / 272.1k vs 269.3k / 269.2k
 // client-images/s, interleaved.
-static const int kDwqBlocks = env_int("FH_DWQ_BLOCKS", 512);
+static const int kDwqBlocks = env_int("FH_DWQ_BLOCKS", 1024);
 // stage pixels: 128 = one buffer, stored between two barriers (default); 64 = two 64-pixel
 // buffers, the next stage stored half-way through this one's MFMAs, one barrier per stage
 // (FH_DWQ_SPX=64; measured within noise of 128, profiles/r03_dwq/)
