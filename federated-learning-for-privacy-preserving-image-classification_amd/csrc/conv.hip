@@ -1645,11 +1645,12 @@ static int conv_c1_chunks(int batch, int h, int w) {
 // conv1 WGRAD on the matrix cores (conv_c1_wgrad_mfma_kernel): 4-row stages, ~kC1MfmaBlocks
 // workgroups (the kernel is HBM-bound: many small workgroups keep loads in flight)
 static const int kC1MfmaBlocks = env_int("FH_C1_MFMA_BLOCKS", 1024);
+static const int kC1MinSps = env_int("FH_C1_MINSPS", 2);  // stages per chunk at least
 static bool conv_c1_mfma_ok(int h, int w) { return h % 4 == 0 && w % 4 == 0 && w <= 32; }
 static DWPlan plan_c1_mfma(int batch, int h, int nclients) {
     const int nst = batch * (h / 4);
     int want = (int)std::max<int64_t>(1, ceil_div(fill(kC1MfmaBlocks), std::max(nclients, 1)));
-    want = std::min(want, std::max(1, nst / 2));
+    want = std::min(want, std::max(1, nst / std::max(1, kC1MinSps)));
     DWPlan p{1, 1, 1, 4, 1, 1};
     p.sps = (int)ceil_div(nst, want);
     p.splits = (int)ceil_div(nst, p.sps);
