@@ -192,3 +192,39 @@ def test_plan_round_matches_loop_form(epochs):
     assert a["active"] == b["active"]
     for key in ("counts", "reset", "index"):
         assert a[key].dtype == b[key].dtype and torch.equal(a[key], b[key]), key
+
+
+def test_grad_slab_bookkeeping():
+    """ops.GradSlabs (deferred WGRAD reductions, r03): row ranges of gradient views, float4
+    alignment, a grow-only arena whose superseded buffers stay alive, sorted slab arrays."""
+    from fedhip import ops
+    grads = torch.zeros(3, 128)
+    s = ops.GradSlabs("cpu")
+    with s.collect(grads) as d:
+        assert ops._DEFER is d
+        assert d.row_range(grads[:, 8:8 + 36], 36) == 8
+        assert d.row_range(grads[:, 6:6 + 36], 36) is None          # offset not a float4
+        assert d.row_range(grads[:, 8:8 + 30], 30) is None          # length not a float4 multiple
+        assert d.row_range(torch.zeros(3, 36), 36) is None          # not a view of the rows
+        p1, n1 = d.take(100)
+        assert n1 == 256
+        first = d.arena
+        p2, _ = d.take(64 << 20)                                    # grows: a new arena
+        assert d.arena is not first and any(t is first for t in d.retired)
+        d.ranges += [(64, 8, 4096, 3), (8, 36, 8192, 2)]
+    assert ops._DEFER is None
+    arr, n = ops._slab_array(s.ranges)
+    assert n == 2 and (arr[0].off, arr[0].len, arr[0].splits) == (8, 36, 2)
+    assert (arr[1].off, arr[1].slab) == (64, 4096)
+
+
+def test_slab_step_validates_ranges_without_gpu():
+    """fh_sgd_step_slabs checks its ranges on the host before anything is launched."""
+    from fedhip import ops
+    bad = [[(2, 8, 4096, 2)], [(8, 6, 4096, 2)], [(60, 8, 4096, 2)], [(8, 8, 4100, 2)],
+           [(8, 8, 4096, 2), (12, 8, 8192, 2)]]
+    for r in bad:
+        arr, n = ops._slab_array(r)
+        with pytest.raises(_lib.FedHipError, match="bad slab range"):
+            _lib.call("fh_sgd_step_slabs", 4096, 4096, 4096, 64, 64, 1, arr, n, 0.1, 0.9, 0.0, 0,
+                      None)
