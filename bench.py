@@ -688,7 +688,126 @@ def run_dpsgd(args, dev, steps, warmup):
             "roofline_psnorm": [roofline_of(t, *v, peak, hbm=v[2] <= ridge * v[3])
                                 for t, v in ps],
             "conv_linear_all_launches": conv_all, "instances": instances,
-            "instances_by_clients": by_bucket}
+            "instances_by_clients": by_bucket, "_sizes": sizes}
+
+
+def cpu_baseline_dpsgd(sizes, lr=0.01, seconds=12.0, max_norm=1.0, eps=1.0, delta=1e-5):
+    """The K2-dpsgd round on the host cores: oracle/dpsgd_ref.py (explicit per-sample
+    gradients, per-sample clip to C, N(0, (sigma C)^2) noise with the reference's
+    Gaussian-mechanism sigma, privacy.py:209) over whole client shards of N(0,1) MNIST-shaped
+    data, batches of 32 with the partial last one, SGD, clients median shard first until
+    ~`seconds` of work.  Data generation is not timed."""
+    from oracle import dpsgd_ref, train_ref
+    host = host_cpu_info()
+    lim = [v for v in (host["physical_cores"], host["affinity_cpus"], host["cgroup_cpu_quota"])
+           if v]
+    threads = max(1, int(min(lim))) if lim else torch.get_num_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    init = train_ref.make_model("simple_cnn", 0)
+    gsd = {k: v.clone() for k, v in init.state_dict().items()}
+    sig = dpsgd_ref.sigma(eps, delta)
+    med = float(np.median(sizes))
+    imgs, busy, nclients = 0, 0.0, 0
+    for n in sorted(sizes, key=lambda v: (abs(v - med), v)):
+        if busy > seconds:
+            break
+        if n == 0:
+            continue
+        x = torch.randn(n, 1, 28, 28, generator=g)
+        y = torch.randint(0, 10, (n,), generator=g)
+        perm = torch.randperm(n, generator=g)
+        t0 = time.perf_counter()
+        m = train_ref.make_model("simple_cnn", None)
+        m.load_state_dict(gsd)
+        opt = train_ref.make_optimizer(m, "sgd", lr)
+        for j in range(0, n, 32):
+            idx = perm[j:j + 32]
+            noise = [torch.normal(0.0, sig * max_norm, p.shape) for p in m.parameters()]
+            dpsgd_ref.dpsgd_step(m, opt, x[idx], y[idx], max_norm, noise=noise)
+            imgs += len(idx)
+        busy += time.perf_counter() - t0
+        nclients += 1
+    torch.set_num_threads(prev)
+    return {"value": imgs / busy, "unit": "client-images/s", "cores": threads, "kind": "port",
+            "host": host,
+            "sample": f"{nclients} clients of K2-dpsgd ({imgs} client-images: whole shards, 1 "
+                      f"epoch, batch 32, per-sample clip C={max_norm} + Gaussian noise "
+                      f"sigma={sig:.3f}, sgd lr {lr}) in {busy:.1f}s (oracle/dpsgd_ref.py, "
+                      f"torch CPU, {threads} threads)"}
+
+
+MAX_LINE_BYTES = 4096   # the driver keeps an 8 KB stdout tail: the final line must fit in it
+_ROOF_KEYS = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
+              "avg_launch_ms", "launches_timed", "flops_per_launch", "bytes_per_launch")
+
+
+def _roof_short(r):
+    return None if r is None else {k: r[k] for k in _ROOF_KEYS if k in r}
+
+
+def _cpu_short(c):
+    if c is None:
+        return None
+    h = c.get("host") or {}
+    return {"value": round(c["value"], 1), "unit": c["unit"], "cores": c["cores"],
+            "kind": c["kind"], "sample": c["sample"],
+            "host": {k: h.get(k) for k in ("model", "physical_cores", "cgroup_cpu_quota")}}
+
+
+def compact(out):
+    """The ONE stdout line: the contract keys, the headline roofline objects, the CPU
+    baseline, a rounds-to-target summary and the K2 summary.  The per-launch-shape tables
+    (instances, instances_by_clients, conv_linear_all_launches) go to the detail file."""
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup",
+                                "ms_per_step", "higher_is_better", "scaling", "vs_baseline",
+                                "dtype", "data", "config", "achieved_tflops_step",
+                                "round_frac") if k in out}
+    line["roofline"] = _roof_short(out.get("roofline"))
+    if "roofline_hbm" in out:
+        line["roofline_hbm"] = _roof_short(out["roofline_hbm"])
+    ca = out.get("conv_linear_all_launches")
+    if ca:
+        line["conv_linear_all_launches_frac"] = ca["frac"]
+    line["cpu_baseline"] = _cpu_short(out.get("cpu_baseline"))
+    rt = out.get("rounds_to_target")
+    if rt:
+        line["rounds_to_target"] = {k: rt[k] for k in ("target", "rounds", "oracle_rounds",
+                                                        "max_rounds", "seconds")}
+    k2 = out.get("k2")
+    if k2:
+        line["k2"] = {"value": k2["value"], "unit": k2["unit"], "ms_per_step": k2["ms_per_step"],
+                      "steps": k2["steps"], "workload": k2["config"]["workload"],
+                      "round_frac": k2["round_frac"], "roofline": _roof_short(k2.get("roofline")),
+                      "roofline_hbm": _roof_short(k2.get("roofline_hbm")),
+                      "cpu_baseline": _cpu_short(k2.get("cpu_baseline"))}
+    line["env"] = out.get("env", {})
+    line["detail"] = out.get("detail_file")
+    s = json.dumps(line)
+    if len(s) > MAX_LINE_BYTES:  # never let the headline overflow the driver's tail
+        for k in ("data", "roofline_hbm", "detail"):
+            line.pop(k, None)
+            if "k2" in line:
+                line["k2"].pop(k, None)
+            if len(json.dumps(line)) <= MAX_LINE_BYTES:
+                break
+    return line
+
+
+def write_detail(out, path):
+    """Every field of the run (the full result incl. the per-launch-shape tables) as JSON."""
+    if not path:
+        return None
+    d = os.path.dirname(os.path.abspath(path))
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(path, "w") as fh:
+            json.dump(out, fh, indent=1)
+    except OSError as e:
+        log(f"detail file not written: {e}")
+        return None
+    return os.path.relpath(os.path.abspath(path), REPO)
 
 
 def main():
@@ -716,14 +835,20 @@ def main():
                     help="rehearsal: every rank on cuda:0 (multi-rank path on a 1-GPU box)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="concurrent client lanes per GPU (default: planner / FH_LANES)")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="JSON file for the full result (per-launch-shape tables); '' = none")
     args = ap.parse_args()
     world, rank, dev = setup(args)
     if args.config == "K2-dpsgd":
         if world != 1:
             raise SystemExit("K2-dpsgd: one GPU only")
         out = run_dpsgd(args, dev, args.steps, args.warmup)
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_dpsgd(out.pop("_sizes"), args.lr)
+        out.pop("_sizes", None)
         out["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("FH_")}
-        print(json.dumps(out), flush=True)
+        out["detail_file"] = write_detail(out, args.detail_out)
+        print(json.dumps(compact(out)), flush=True)
         return
     out = run_config(args.config, args, world, rank, dev, args.steps, args.warmup, rtt=True)
     # BASELINE.json's only 1-GPU config (K2: SimpleCNN, 32 Dirichlet(0.5) clients, update DP
@@ -732,17 +857,14 @@ def main():
         k2 = run_config("K2", args, world, rank, dev, max(args.steps, 3), args.warmup)
         if k2 is not None:
             host_legs(k2, args, dev)
-            out["k2"] = {k: k2[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
-                                           "warmup", "config", "achieved_tflops_step",
-                                           "round_frac", "roofline", "roofline_hbm",
-                                           "conv_linear_all_launches", "instances",
-                                           "instances_by_clients", "cpu_baseline") if k in k2}
+            out["k2"] = k2
     if rank == 0:
         host_legs(out, args, dev)
         # every FH_* knob in the environment (diagnostics / A-B switches): none is set in a
         # driver run; a line measured with one set says so here
         out["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("FH_")}
-        print(json.dumps(out), flush=True)
+        out["detail_file"] = write_detail(out, args.detail_out)
+        print(json.dumps(compact(out)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,0 +1,63 @@
+"""bench.py's final stdout line stays within what the driver keeps (r03: a 28 KB line
+overflowed the driver's 8 KB tail and the round had no parsed bench line).
+
+The stubs are the full result dicts of committed r03 runs (profiles/r03_s4z2/), i.e. the
+largest realistic inputs to bench.compact(): every per-launch-shape table included."""
+import json
+import os
+
+import pytest
+
+import bench
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONTRACT = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")
+
+
+def _stub(name):
+    d = json.load(open(os.path.join(REPO, "profiles", "r03_s4z2", name)))
+    d["detail_file"] = "gpurun_out/bench_detail.json"
+    return d
+
+
+@pytest.mark.parametrize("name", ["bench.json", "bench_K3.json", "bench_K2-dpsgd.json"])
+def test_compact_line_fits(name):
+    out = _stub(name)
+    assert len(json.dumps(out)) > 8192  # the full result would not fit
+    line = bench.compact(out)
+    s = json.dumps(line)
+    assert len(s) < bench.MAX_LINE_BYTES
+    for k in CONTRACT:
+        assert k in line, k
+    assert line["roofline"]["frac"] == out["roofline"]["frac"]
+    assert line["roofline"]["bound"] in ("hbm", "mfma")
+    assert "instances" not in s and "instances_by_clients" not in s
+
+
+def test_compact_line_carries_k2_and_baselines():
+    out = _stub("bench.json")
+    line = bench.compact(out)
+    assert line["cpu_baseline"]["value"] > 0 and line["cpu_baseline"]["cores"] >= 1
+    assert line["cpu_baseline"]["kind"] in ("port", "reference")
+    k2 = line["k2"]
+    for k in ("value", "ms_per_step", "round_frac", "roofline", "roofline_hbm", "cpu_baseline"):
+        assert k2.get(k) is not None, k
+    rt = line["rounds_to_target"]
+    assert rt["rounds"] == out["rounds_to_target"]["rounds"]
+
+
+def test_compact_line_trims_when_oversized():
+    out = _stub("bench.json")
+    out["data"] = "x" * 5000
+    line = bench.compact(out)
+    assert len(json.dumps(line)) <= bench.MAX_LINE_BYTES
+    assert line["value"] == out["value"] and line["roofline"]
+
+
+def test_write_detail_roundtrip(tmp_path):
+    out = _stub("bench.json")
+    p = tmp_path / "d" / "detail.json"
+    rel = bench.write_detail(out, str(p))
+    assert rel is not None
+    assert json.load(open(p))["instances"] == out["instances"]
