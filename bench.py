@@ -499,7 +499,7 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         algo, ratio = cfg["compression"]
         comp = CompressionConfig(algorithm=algo, sparsity_ratio=ratio)
     rr = RankRound(template, train, mine, epochs=cfg["epochs"], device=dev, dp=dp,
-                   lanes=args.lanes, transform=tf, compression=comp)
+                   lanes=args.lanes, transform=tf, compression=comp, exact=args.exact_fedavg)
     data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, rank, raw=raw)
     total_images = cfg["epochs"] * sum(train)
 
@@ -589,7 +589,7 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
                                f"{cfg['epochs']} local epoch(s), batch 32, {args.opt} lr {args.lr}, "
                                f"DP eps={cfg['dp']}, "
                                f"{'compression ' + str(cfg['compression']) + ', ' if cfg.get('compression') else ''}"
-                               f"FedAvg{' RCCL all-reduce' if world > 1 else ''}"
+                               f"FedAvg{(' exact all-gather' if args.exact_fedavg else ' RCCL all-reduce') if world > 1 else ''}"
                                + (f" [{world}/{cfg['config_gpus']} GPU slice of the "
                                   f"{cfg['clients'] * cfg['config_gpus']}-client config]"
                                   if cfg.get('config_gpus') else ""),
@@ -835,6 +835,8 @@ def main():
                     help="rehearsal: every rank on cuda:0 (multi-rank path on a 1-GPU box)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="concurrent client lanes per GPU (default: planner / FH_LANES)")
+    ap.add_argument("--exact-fedavg", action="store_true",
+                    help="N>1: all-gather + sequential FedAvg (bit-exact) instead of all-reduce")
     ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="JSON file for the full result (per-launch-shape tables); '' = none")
     args = ap.parse_args()

@@ -29,6 +29,7 @@ from __future__ import annotations
 import atexit
 import math
 import os
+import secrets
 import weakref
 from dataclasses import dataclass
 
@@ -67,7 +68,10 @@ class DPSGDConfig:
     epsilon: float = 1.0
     delta: float = 1e-5
     noise_multiplier: float = None
-    seed: int = 0
+    # None: a secret per-trainer key (secrets.randbits) is mixed into the noise stream, so
+    # knowing the round seed and client ids does not let anyone regenerate (and subtract)
+    # the noise; fix it only for tests and reproducible benchmarks
+    seed: int = None
 
     @property
     def sigma(self):
@@ -143,6 +147,8 @@ class PackedTrainer:
         if dpsgd is not None:
             self._sq = torch.zeros(capacity, batch, dtype=torch.float64, device=dev)
             self._coef = torch.zeros(capacity, batch, device=dev)
+            self._noise_key = (secrets.randbits(64) if dpsgd.seed is None
+                               else int(dpsgd.seed)) & 0xFFFFFFFFFFFFFFFF
         self.on_step = None
         self.pre_step = None
         # split WGRAD reductions finished inside the optimizer launch (ops.GradSlabs);
@@ -207,12 +213,14 @@ class PackedTrainer:
         """Global client id of each slot: every step's device key block carries them
         (fh_common.h philox_row), so a client's dropout / augmentation / DP-SGD noise draws
         depend on (round seed, step, client id) only — not on the rank, lane or slot it
-        trains in.  The per-lane / per-rank salt is then not needed (and would break that)."""
+        trains in.  The per-lane / per-rank salt is then left out of keys that go with a device
+        key block (it would break that); eager steps without one (PackedTrainer.step) key
+        rows by slot and keep the salt, so slot z of two lanes / ranks never shares a stream."""
         ids = np.asarray(list(ids), dtype=np.int64).reshape(-1)
         if ids.size != self.capacity or (ids < 0).any():
             raise FedHipError(f"set_client_ids: need {self.capacity} non-negative ids")
         self.client_ids = ids
-        self.net.salt = 0
+        self.net.ids_keyed = True
 
     # ------------------------------------------------------------ optimizer
     def begin_round(self, optimizer_type="sgd", lr=0.01):
@@ -269,7 +277,8 @@ class PackedTrainer:
             d = self.dpsgd
             net.backward_dpsgd(self.params, self.grads, n, counts, self._sq, self._coef,
                                d.max_grad_norm, d.sigma * d.max_grad_norm,
-                               noise_seed=net._seed(77 + 1000 * d.seed),
+                               noise_seed=(net._seed(77) + self._noise_key *
+                                           0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF,
                                noise_seed_dev=net.seed_dev, P=self.layout.P)
         self._optimizer_launch(n, first, adam_dev)
 

@@ -128,6 +128,7 @@ class PackedNet:
         self.seed = 0
         self.seed_dev = None  # device uint64 [1] = seed * 1000003 (graph replay)
         self.salt = 0  # per-lane key offset (a lane's slot 0 is not another lane's slot 0)
+        self.ids_keyed = False  # set_client_ids: device key blocks carry global client ids
         # CIFAR10CNN and ResNet training: BN apply + ReLU folded into the consumers (FH_FUSE_BN=0: off)
         self.fuse_bn = os.environ.get("FH_FUSE_BN", "1") != "0"
         # ... and the BN statistics taken by the producing conv's epilogue instead of a
@@ -200,7 +201,9 @@ class PackedNet:
         seed_dev set (graph replay) the per-step part lives on the device and the kernel
         adds it to the per-layer salt returned here."""
         if self.seed_dev is not None:
-            return (layer_id * 7919 + self.salt) & 0xFFFFFFFFFFFFFFFF
+            # rows keyed by global client id (philox_row): no lane / rank salt
+            salt = 0 if self.ids_keyed else self.salt
+            return (layer_id * 7919 + salt) & 0xFFFFFFFFFFFFFFFF
         return (self.seed * 1000003 + layer_id * 7919 + self.salt) & 0xFFFFFFFFFFFFFFFF
 
     def _drop_mode(self, train):

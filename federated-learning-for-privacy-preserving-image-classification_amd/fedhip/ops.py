@@ -439,6 +439,8 @@ class GradSlabs:
     of g disappear).  The arena is grow-only; a superseded buffer stays alive because a
     captured step may still address it."""
 
+    MIN_ARENA = 16 << 20  # bytes of the first arena (tests shrink it to force growth)
+
     def __init__(self, device):
         self.device = device
         self.arena = torch.empty(0, dtype=torch.uint8, device=device)
@@ -452,7 +454,7 @@ class GradSlabs:
         nb = (int(nbytes) + 255) // 256 * 256
         if self.off + nb > self.arena.numel():
             self.retired.append(self.arena)
-            self.arena = torch.empty(max(2 * self.arena.numel(), 4 * nb, 16 << 20),
+            self.arena = torch.empty(max(2 * self.arena.numel(), 4 * nb, self.MIN_ARENA),
                                      dtype=torch.uint8, device=self.device)
             self.off = 0
         p = self.arena.data_ptr() + self.off
@@ -461,9 +463,12 @@ class GradSlabs:
 
     def row_range(self, t, length):
         """Float offset of view t within the gradient rows (None if t is not such a view or
-        the range is not float4-aligned)."""
+        the range is not float4-aligned, or t is strided within a row: the optimizer sums
+        the partials into a contiguous run of the row)."""
         g = self.grads
         if t is None or g is None or t.dim() < 1 or t.stride(0) != g.stride(0):
+            return None
+        if t.dim() > 1 and not t[0].is_contiguous():
             return None
         off = (t.data_ptr() - g.data_ptr()) // 4
         if off < 0 or off + length > g.stride(0) or off % 4 or length % 4:

@@ -12,7 +12,11 @@ packed job, forms its partial FedAvg sum  S_r = sum_{k in r} fl32(w_k) x_k
 (w_k = n_k / sum_all n, host double, client-list order inside the rank), and
 one all_reduce(SUM) of the P-float vector over xGMI yields the new global
 model on every rank (no broadcast needed).  With one rank the sum is the
-reference's sequential loop, bit for bit.
+reference's sequential loop, bit for bit.  With more ranks the association of
+the all-reduce differs from that loop by a few ulp; ``exact=True`` instead
+all-gathers every client's row and runs the sequential FedAvg kernel over all
+clients in global client order on every rank (fedavg.py:278-285 bit for bit, at
+C x P floats of gather traffic per rank instead of one P-float all-reduce).
 """
 from __future__ import annotations
 
@@ -45,7 +49,7 @@ class RankRound:
     def __init__(self, template_model, all_train_sizes: Sequence[int], my_clients: Sequence[int],
                  epochs: int = 1, batch: int = 32, device="cuda", dp: Optional[DPConfig] = None,
                  group=None, lanes=None, compression=None, transform=None, dp_seed=None,
-                 shuffle_seed=None):
+                 shuffle_seed=None, exact=False):
         self.device = torch.device(device)
         self._template = template_model
         self.B, self.epochs, self.dp, self.group = batch, epochs, dp, group
@@ -111,6 +115,45 @@ class RankRound:
         if compression is not None:
             from .compress import SegmentPlan
             self._cplan = SegmentPlan(L.seg_offsets(), self.device)
+        self.exact = bool(exact) and self.distributed
+        if self.exact:
+            self._init_exact()
+
+    def _init_exact(self):
+        """Exact-mode FedAvg layout: every rank's client list (host, once), rows padded to
+        the largest rank's count, and the gather position of each global client."""
+        world = dist.get_world_size(self.group)
+        lists = [None] * world
+        dist.all_gather_object(lists, list(self.clients), group=self.group)
+        maxS = max(1, max(len(c) for c in lists))
+        pos = {}
+        for r, cl in enumerate(lists):
+            for i, k in enumerate(cl):
+                pos[k] = r * maxS + i
+        order = sorted(pos)  # global client order: the reference's sequential loop
+        self._x_world, self._x_maxS = world, maxS
+        self._x_w32 = torch.tensor([self.weights[k] for k in order], dtype=torch.float32,
+                                   device=self.device)
+        self._x_idx = torch.tensor([pos[k] for k in order], dtype=torch.int32, device=self.device)
+        self._x_mine = torch.tensor([self.slot_of[k] for k in self.clients], dtype=torch.int64,
+                                    device=self.device)
+        self._x_buf = {}
+
+    def _exact_fedavg(self, rows, n, out):
+        """out = sum over ALL clients, in global client order, of fl32(w_k) * row_k: this
+        rank's rows (client-list order, zero padded) all-gathered, then fh_fedavg_weighted_sum."""
+        world, maxS = self._x_world, self._x_maxS
+        buf = self._x_buf.get(n)
+        if buf is None:
+            buf = self._x_buf[n] = (torch.zeros(maxS, n, device=self.device),
+                                    torch.empty(world, maxS, n, device=self.device))
+        send, recv = buf
+        S = len(self.clients)
+        if S:
+            torch.index_select(rows[:, :n], 0, self._x_mine, out=send[:S])
+        dist.all_gather(list(recv.unbind(0)), send, group=self.group)
+        ops.fedavg_weighted_sum(recv.view(world * maxS, n), self._x_w32, out,
+                                row_index=self._x_idx, P=n)
 
     def client_shuffle_seed(self, seed: int, client: int) -> int:
         """Seed of the torch.Generator client `client` draws its round-`seed` batch
@@ -148,9 +191,15 @@ class RankRound:
             from .compress import compress_rows
             compress_rows(self._cplan, self.compression, tr.params, S,
                           base=self.global_flat.view(1, -1).expand(S, -1))
+        distributed = self.distributed
+        if self.exact:  # bit-exact multi-rank FedAvg: all-gather + one sequential sum
+            self._exact_fedavg(tr.params, self.P, self.global_flat)
+            if self.Q:
+                self._exact_fedavg(tr.bufs, self.Q, self.global_bufs)
+            self.round_index += 1
+            return metrics
         # FedAvg: this rank's partial sum in client-list order, then RCCL all-reduce.
         ops.fedavg_weighted_sum(tr.params, self.w32, self.partial, row_index=self.rows, P=self.P)
-        distributed = self.distributed
         if distributed:
             dist.all_reduce(self.partial, op=dist.ReduceOp.SUM, group=self.group)
         self.global_flat.copy_(self.partial)

@@ -125,3 +125,52 @@ def test_deferred_rounds_bit_identical(model_name, kw, shape, opt):
     assert a._slabs is not None and b._slabs is None
     for f in ("params", "grads", "state1", "state2", "bufs"):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
+
+
+def _laned_round(defer, sizes, cut, opt="sgd"):
+    from fedhip.lanes import LanedTrainer
+    torch.manual_seed(0)
+    model = hm.ModelFactory.create_model("cifar10_cnn", dropout_rate=0.3).to(DEV)
+    steps = [-(-n // 32) for n in sizes]
+    lt = LanedTrainer(model, steps, batch=32, device=DEV, cut=cut)
+    for ln in lt.lanes:
+        ln.defer_wgrad_reduce = defer
+    for k in range(len(sizes)):
+        lt.load_module_state(k, model)
+    g = torch.Generator().manual_seed(5)
+    data = torch.randn(sum(sizes), 3, 32, 32, generator=g).to(DEV)
+    labels = torch.randint(0, 10, (sum(sizes),), generator=g).to(DEV)
+    offs = [sum(sizes[:k]) for k in range(len(sizes))]
+    gen = torch.Generator().manual_seed(11)
+    for r in range(2):
+        lt.run_round(data, labels, offs, lt.make_plan(sizes, 1, generator=gen),
+                     optimizer_type=opt, lr=1e-3, seed=r)
+    torch.cuda.synchronize()
+    return lt
+
+
+def test_deferred_laned_program_rounds_bit_identical():
+    """The default KT / K2 path: a LanedTrainer (3 lanes on their own streams, step programs,
+    shared lane streams), deferral on vs off."""
+    sizes, cut = [300, 120, 100, 64, 33, 9], [0, 1, 4, 6]
+    a = _laned_round(True, sizes, cut)
+    b = _laned_round(False, sizes, cut)
+    assert all(ln.launch_mode == "program" for ln in a.lanes)
+    assert all(ln._slabs is not None for ln in a.lanes)
+    for f in ("params", "grads", "state1", "state2", "bufs"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_deferred_arena_growth_and_range_cap(monkeypatch):
+    """A deeper ResNet ([2,2,2]) with a 1 KB first arena (it grows mid-step, superseded
+    buffers kept alive for the captured steps) and a range cap of 6 (the layers past it fall
+    back to their own reduction launches): still bit-identical to deferral off."""
+    monkeypatch.setattr(ops.GradSlabs, "MIN_ARENA", 1 << 10)
+    monkeypatch.setattr(ops, "MAX_GRAD_SLABS", 6)
+    sizes = [70, 40, 9]
+    a = _round("federated_resnet", {}, (3, 32, 32), sizes, "sgd", defer=True)
+    b = _round("federated_resnet", {}, (3, 32, 32), sizes, "sgd", defer=False)
+    assert a._slabs.retired, "the arena never grew"
+    assert 0 < len(a._slabs.ranges) <= 6
+    for f in ("params", "grads", "state1", "bufs"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f

@@ -128,3 +128,22 @@ def test_dpsgd_refuses_batchnorm_models():
     eng.begin_round("sgd", 0.01)
     with pytest.raises(FedHipError, match="BatchNorm"):
         eng.step(1, torch.tensor([32], dtype=torch.int32, device=DEV))
+
+
+def test_dpsgd_noise_key_is_secret():
+    """Two trainers with the same public seeds (round seed, step, slot) draw different noise
+    unless the caller fixes DPSGDConfig.seed (a public key would let anyone
+    regenerate the noise and subtract it)."""
+    sizes = [32, 16]
+    counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
+    cfg = dict(max_grad_norm=1.0, noise_multiplier=1.0)
+    a, _, _ = _engine(sizes, DPSGDConfig(**cfg))
+    b, _, _ = _engine(sizes, DPSGDConfig(**cfg))
+    c, _, _ = _engine(sizes, DPSGDConfig(seed=5, **cfg))
+    d, _, _ = _engine(sizes, DPSGDConfig(seed=5, **cfg))
+    for e in (a, b, c, d):
+        e.step(2, counts)
+    torch.cuda.synchronize()
+    P = a.layout.P
+    assert not torch.equal(a.params[:, :P], b.params[:, :P])
+    assert torch.equal(c.params[:, :P], d.params[:, :P])

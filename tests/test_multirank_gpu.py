@@ -48,7 +48,7 @@ def _client_data(k, n):
     return torch.randn(n, 3, 32, 32, generator=g), torch.randint(0, 10, (n,), generator=g)
 
 
-def _run_layout(rank, world, dp):
+def _run_layout(rank, world, dp, exact=False):
     """Train SIZES' clients of `rank` for ROUNDS rounds; returns per-round results."""
     from fedhip.partition import lpt_assign
     from fedhip.round import DPConfig, RankRound
@@ -59,7 +59,7 @@ def _run_layout(rank, world, dp):
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model("cifar10_cnn").to(dev)
     rr = RankRound(model, SIZES, mine, epochs=1, device=dev, lanes=1, shuffle_seed=77,
-                   dp=DPConfig(epsilon=DP_EPS) if dp else None, dp_seed=5)
+                   dp=DPConfig(epsilon=DP_EPS) if dp else None, dp_seed=5, exact=exact)
     xs, ys = zip(*[_client_data(k, SIZES[k]) for k in rr.slots])
     data, labels = torch.cat(xs).to(dev), torch.cat(ys).to(dev)
     offs = np.cumsum([0] + [SIZES[k] for k in rr.slots][:-1]).tolist()
@@ -79,11 +79,11 @@ def _run_layout(rank, world, dp):
     return out
 
 
-def _rank_main(rank, world, port, dp, q):
+def _rank_main(rank, world, port, dp, q, exact=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        q.put((rank, _run_layout(rank, world, dp)))
+        q.put((rank, _run_layout(rank, world, dp, exact)))
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:  # surface the failure to the parent instead of hanging it
@@ -162,3 +162,35 @@ def test_bench_multirank_rehearsal():
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0
     assert out["config"]["clients"] == 64  # 32 clients per GPU, weak scaling
+
+
+def test_rankround_exact_mode_bitwise():
+    """RankRound(exact=True) over 2 ranks: all-gather of the client rows + the sequential
+    FedAvg kernel in global client order == the reference's one-loop sum over the same rows
+    (fedavg.py:278-285) bit for bit, for the parameters and the BN statistics, every round."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29720 + os.getpid() % 200
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, True, q, True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert not isinstance(res[r], str), f"rank {r} failed: {res[r]}"
+    total = sum(SIZES)
+    w = [n / total for n in SIZES]
+    for rnd in range(ROUNDS):
+        r0, r1 = res[0][rnd], res[1][rnd]
+        assert np.array_equal(r0["glob"], r1["glob"]) and np.array_equal(r0["gbufs"], r1["gbufs"])
+        rows = {**r0["rows"], **r1["rows"]}
+        bufs = {**r0["bufs"], **r1["bufs"]}
+        seq = fedavg_ref.weighted_average([rows[k] for k in range(len(SIZES))], w)
+        bseq = fedavg_ref.weighted_average([bufs[k] for k in range(len(SIZES))], w)
+        assert np.array_equal(r0["glob"].view(np.uint32), seq.astype(np.float32).view(np.uint32))
+        assert np.array_equal(r0["gbufs"].view(np.uint32), bseq.astype(np.float32).view(np.uint32))
+        if rnd + 1 < ROUNDS:  # the next round starts from the exact global model
+            assert np.array_equal(res[0][rnd + 1]["start"], r0["glob"])
