@@ -1317,35 +1317,19 @@ static bool dconv_supported(int h, int w, int kh, int kw, int stride, int pad) {
     return kh == 3 && kw == 3 && stride == 1 && pad == 1 && h == w && (w == 8 || w == 16 || w == 32);
 }
 
-// Tuning knobs (diagnostics; read once): FH_DCONV_BLOCKS = workgroups a larger BM must
-// still leave (default 1024), FH_DCONV_MAXBM caps BM, FH_DWGRAD_BLOCKS = wgrad split
-// target (default 1024), FH_DWGRAD_WPX forces the pixel-wave count (1, 2 or 4) when the
-// channel counts allow it.
-// defaults from the MI355X sweeps (tools/conv_sweep.py, CIFAR10CNN layers at 32 clients):
-// BM <= 64 once 512 workgroups are reached; wgrad with four pixel-waves per 32x32
-// (co, ci) tile and ~256 workgroups (one per CU at its 86 KB of LDS)
-static const int kDconvBlocks = env_int("FH_DCONV_BLOCKS", 512);
-static const int kDconvMaxBm = env_int("FH_DCONV_MAXBM", 64);
-// stride-2 WGRAD (dconv_wgrad_kernel<W, 2, 1, 2, .., S=2>): workgroup target per resident wave
-static const int kDwgradBlocks = env_int("FH_DWGRAD_BLOCKS", 256);
-// RGB-layer wgrad target: 512 workgroups (42 -> 34 us at 32 clients, profiles/r01_v12)
-static const int kDwgradSmallBlocks = env_int("FH_DWGRAD_SMALL_BLOCKS", 512);
-static const int kDwgradMinSps = env_int("FH_DWGRAD_MINSPS", 1);  // r03 s4 (tail_sweep.py: 2 in r01)
-static const int kDconvForceSplits = env_int("FH_DCONV_SPLITS", 0);  // sweeps: force splits
-static const int kDwgradForceSplits = env_int("FH_DWGRAD_SPLITS", 0);
-static const int kDconvCk32 = env_int("FH_DCONV_CK32", 8);  // sweeps: CK of the BM=32 tiles
-
-// split over input channels below kDconvSplitBelow workgroups, toward kDconvSplitTarget
-// (sweep knobs FH_DCONV_SPLIT_BELOW / FH_DCONV_SPLIT_TARGET; r02 defaults 512 / 1024)
-static const int kDconvSplitBelow = env_int("FH_DCONV_SPLIT_BELOW", 512);
-static const int kDconvSplitTarget = env_int("FH_DCONV_SPLIT_TARGET", 1024);
-// In-launch split sum (dconv_kernels.h DConvArgs::tickets, r03): the calling thread's zeroed
-// ticket counters (fh_set_split_tickets) and the split count the planner caps at so a last
-// arriver reads few partial tiles (FH_DCONV_INK=0: no cap, splitk_epilogue_kernel always)
-static thread_local int* g_tickets = nullptr;
-static thread_local int64_t g_ticket_n = 0;
-static const int kInkMaxSplits = env_int("FH_DCONV_INK", 4);
-static const int kDconvMinStages = env_int("FH_DCONV_MINSTAGES", 1);
+// Planner constants (MI355X sweeps: tools/conv_sweep.py on the CIFAR10CNN layers, r02 / r03
+// A/B in profiles/): BM <= 64 once 512 workgroups are reached; the direct kernels split over
+// input channels below 512 workgroups toward 1024, at most 4 splits (+0.5 % KT against no cap,
+// r03 s4); stride-2 WGRAD 256 workgroups per resident wave; RGB-layer WGRAD 512 workgroups
+// (42 -> 34 us at 32 clients, profiles/r01_v12).
+constexpr int kDconvBlocks = 512;
+constexpr int kDconvMaxBm = 64;
+constexpr int kDwgradBlocks = 256;
+constexpr int kDwgradSmallBlocks = 512;
+constexpr int kDwgradMinSps = 1;
+constexpr int kDconvSplitBelow = 512;
+constexpr int kDconvSplitTarget = 1024;
+constexpr int kDconvMaxSplits = 4;
 
 static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool force_bm32 = false,
                         bool ck4 = false) {
@@ -1359,16 +1343,12 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
             break;
         }
     }
-    p.ck = (ck4 || p.bm == 128 || Cr <= 4) ? 4 : (p.bm == 32 && kDconvCk32 == 4) ? 4 : 8;
+    p.ck = (ck4 || p.bm == 128 || Cr <= 4) ? 4 : 8;
     const int64_t blocks = tn * ceil_div(M, p.bm) * nclients;
     const int chunks = (int)ceil_div(Cr, p.ck);
-    if ((kDconvForceSplits > 0 || blocks < fill(kDconvSplitBelow)) && chunks > 1) {
+    if (blocks < fill(kDconvSplitBelow) && chunks > 1) {
         int want = (int)std::min<int64_t>(ceil_div(fill(kDconvSplitTarget), blocks), chunks);
-        if (kInkMaxSplits > 0) want = std::min(want, kInkMaxSplits);
-        // each split keeps >= kDconvMinStages stages: a split saves K-loop time, the
-        // reduction launch costs about a stage's worth of latency on a narrow grid
-        want = std::max(1, std::min(want, chunks / std::max(1, kDconvMinStages)));
-        if (kDconvForceSplits > 0) want = std::min(kDconvForceSplits, chunks);
+        want = std::max(1, std::min(want, kDconvMaxSplits));
         const int per = (int)ceil_div(chunks, want);
         p.cchunk = per * p.ck;
         p.splits = (int)ceil_div(Cr, p.cchunk);
@@ -1380,8 +1360,7 @@ static DPlan plan_dconv(int M, int Cr, int batch, int hw, int nclients, bool for
     return p;
 }
 
-// split slab: [z][split][M][Nfull] (splitk_epilogue_kernel) or the in-launch fragment slab
-// [tile][split][BM * 256] over the padded tile grid — the larger of the two
+// split slab: [z][split][M][Nfull] (splitk_epilogue_kernel), sized over the padded tile grid
 static size_t dconv_ws_bytes(const DPlan& p, int nclients, int M, int batch, int hw) {
     if (p.splits <= 1) return 0;
     const size_t mpad = (size_t)ceil_div(M, p.bm) * p.bm;
@@ -1440,20 +1419,12 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     float* out = a.out;
     dim3 grid((unsigned)ceil_div(a.Nfull, 256), (unsigned)ceil_div(a.M, p.bm),
               (unsigned)(nclients * p.splits));
-    // the sum in the launch when this thread has ticket counters for every tile
-    const bool ink = p.splits > 1 && g_tickets != nullptr &&
-                     (int64_t)nclients * grid.x * grid.y <= g_ticket_n;
-    if (ink) {
-        a.slab = (float*)ws;
-        a.tickets = g_tickets;
-    } else if (p.splits > 1) {
-        a.out = (float*)ws;
-    }
+    if (p.splits > 1) a.out = (float*)ws;
     int rc;
     if constexpr (S == 2) {
         rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
-    } else if (a.bn_part && (p.splits == 1 || ink)) {  // the statistics epilogue instances
+    } else if (a.bn_part && p.splits == 1) {  // the statistics epilogue instances
         rc = w == 32 ? dconv_launch_w<OP, 32, 1, true>(p, grid, a, st)
            : w == 16 ? dconv_launch_w<OP, 16, 1, true>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 1, true>(p, grid, a, st);
@@ -1464,7 +1435,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     }
     if (rc) return rc;
     FH_LAUNCH_CHECK(name);
-    if (p.splits > 1 && !ink) {
+    if (p.splits > 1) {
         dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
@@ -1586,7 +1557,7 @@ static DWPlan plan_dwq(int cout, int cin, int batch, int w, int nclients) {
     const int nst = (int)ceil_div((int64_t)batch * w * w, (int64_t)kDwqSpx);
     const int want = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(fill(kDwqBlocks), tiles)),
                                             std::max(1, nst / kDwgradMinSps));
-    p.sps = (int)ceil_div(nst, kDwgradForceSplits > 0 ? std::min(kDwgradForceSplits, nst) : want);
+    p.sps = (int)ceil_div(nst, want);
     p.splits = (int)ceil_div(nst, p.sps);
     return p;
 }
@@ -1679,13 +1650,6 @@ extern "C" int fh_set_fill_fraction(float fraction) {
 }
 
 extern "C" float fh_get_fill_fraction(void) { return g_fill; }
-
-extern "C" int fh_set_split_tickets(int32_t* tickets, int64_t count) {
-    FH_REQUIRE(count >= 0 && (tickets != nullptr || count == 0), "set_split_tickets: bad args");
-    g_tickets = count > 0 ? (int*)tickets : nullptr;
-    g_ticket_n = count;
-    return FH_OK;
-}
 
 extern "C" size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
                                           int32_t w_, int32_t cout, int32_t kh, int32_t kw,
@@ -2586,7 +2550,7 @@ linear_fwd_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float*
                          int64_t w_cs, const float* __restrict__ bias, int64_t b_cs,
                          float* __restrict__ Y, int64_t y_cs, float* __restrict__ part,
                          const int32_t* __restrict__ counts, int batch, int K, int M, int kbps,
-                         int relu, DropArgs drop, int* __restrict__ tickets) {
+                         int relu, DropArgs drop) {
     constexpr int KG = 4 / OT;
     __shared__ float red[KG > 1 ? (KG - 1) * OT * 16 * 64 : 1];
     const int gx = gridDim.x, gy = gridDim.y;  // x: splits, y: output groups, z: clients
@@ -2674,50 +2638,6 @@ linear_fwd_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float*
                 Y[z * y_cs + e] = v;
             }
         }
-    } else if (tickets != nullptr) {
-        // the split sum inside the launch (r03): partials stored write-through (sc1), the
-        // 32-output tile's last split to take a ticket adds them in split order and finishes
-        // the epilogue (linear_fwd_epilogue_kernel's operations) — one wave per tile, so the
-        // hand-off needs no barrier: the wave drains its stores, lane 0 takes the ticket
-        float* slab = part + (int64_t)z * gx * 32 * M;
-        // 4-byte stores: relaxed agent-scope atomic stores are the sc1 form (Guideline 16 R1;
-        // a raw_buffer_store_b32 of the vector elements lost its per-element data here)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int img = (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (img < cnt)
-                __hip_atomic_store(slab + ((int64_t)s * 32 + img) * M + o, acc[i],
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int last = 0;
-        if (lane == 0) {
-            int* ctr = tickets + ((int64_t)z * gy + og) * OT + ot;
-            const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = old == gx - 1;
-            if (last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        last = __shfl(last, 0, 64);
-        if (!last) return;
-        const float bv = bias ? bias[z * b_cs + o] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int img = (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (img < cnt) {
-                const float* pp = slab + (int64_t)img * M + o;
-                float v = 0.f;
-                for (int q = 0; q < gx; ++q) v += pp[(int64_t)q * 32 * M];
-                if (bias) v = v + bv;
-                if (relu) v = fmaxf(v, 0.f);
-                const int64_t e = (int64_t)img * M + o;
-                if (drop.mode) v = apply_dropout(drop, z, e, v);
-                Y[z * y_cs + e] = v;
-            }
-        }
     } else {
         float* pp = part + ((int64_t)z * gx + s) * 32 * M + o;
 #pragma unroll
@@ -2757,11 +2677,11 @@ linear_fwd_epilogue_kernel(const float* __restrict__ part, int splits, int M,
 }
 
 // Split plan of linear_fwd_skinny: enough k-chunks that (output groups x clients x chunks)
-// reaches fill(kLfTarget) workgroups, each k-group of a chunk >= kLfMinKb 32-k blocks.
-static const int kLfTarget = env_int("FH_LF_TARGET", 512);   // sweeps (tools/r03_lf.sh)
-static const int kLfMinKb = env_int("FH_LF_MINKB", 4);
-static const int kLfDepth = env_int("FH_LF_DEPTH", 2);
-static const int kLfOt = env_int("FH_LF_OT", 1);  // output tiles per workgroup: 1, 2, 4
+// reaches fill(kLfTarget) workgroups, each k-group of a chunk >= kLfMinKb 32-k blocks
+// (r03 sweeps, profiles/r03_lf/: target 512, 4 blocks, two blocks of loads in flight, one
+// output tile per workgroup)
+constexpr int kLfTarget = 512;
+constexpr int kLfMinKb = 4;
 
 static bool linear_fwd_skinny_ok(int batch, int in_f, int out_f) {
     return kLinearSkinny && kLinearSkinny != 3 && batch > 0 && batch <= 32 && in_f > 0 &&
@@ -2770,11 +2690,10 @@ static bool linear_fwd_skinny_ok(int batch, int in_f, int out_f) {
 
 static void plan_lin_fwd(int nclients, int in_f, int out_f, int64_t target, int& splits,
                          int& kbps) {
-    const int ot = (kLfOt == 2 || kLfOt == 4) ? kLfOt : 1;
     const int kb = in_f / 32;
-    const int64_t tiles = (int64_t)ceil_div(out_f, 32 * ot) * std::max(nclients, 1);
+    const int64_t tiles = (int64_t)ceil_div(out_f, 32) * std::max(nclients, 1);
     int64_t want = ceil_div(target, tiles);
-    want = std::min<int64_t>(want, std::max(1, kb / (kLfMinKb * (4 / ot))));
+    want = std::min<int64_t>(want, std::max(1, kb / (kLfMinKb * 4)));
     want = std::max<int64_t>(want, 1);
     kbps = (int)ceil_div(kb, want);
     splits = (int)ceil_div(kb, kbps);
@@ -2787,28 +2706,16 @@ static int linear_fwd_skinny(const float* x, int64_t x_cs, const float* w, int64
                              hipStream_t st) {
     int splits, kbps;
     plan_lin_fwd(nclients, in_f, out_f, fill(kLfTarget), splits, kbps);
-    const int ot = (kLfOt == 2 || kLfOt == 4) ? kLfOt : 1;
-    const dim3 grid((unsigned)splits, (unsigned)ceil_div(out_f, 32 * ot), (unsigned)nclients);
+    const dim3 grid((unsigned)splits, (unsigned)ceil_div(out_f, 32), (unsigned)nclients);
     float* part = nullptr;
     if (splits > 1) {
         const size_t need = (size_t)nclients * splits * 32 * out_f * sizeof(float);
         FH_REQUIRE(workspace && ws_bytes >= need, "linear_fwd: workspace %zu < %zu", ws_bytes, need);
         part = (float*)workspace;
     }
-    // the split sum in the launch when this thread has ticket counters for every output tile
-    int* tk = (splits > 1 && g_tickets != nullptr &&
-               (int64_t)nclients * grid.y * ot <= g_ticket_n) ? g_tickets : nullptr;
-#define FH_LFD(DD, OO)                                                                           \
-    if (kLfDepth == DD && ot == OO)                                                              \
-        FH_LAUNCH((linear_fwd_skinny_kernel<DD, OO>), grid, dim3(256), 0, st, x, x_cs, w, w_cs,  \
-                  bias, b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop, tk);  \
-    else
-    FH_LFD(1, 1) FH_LFD(3, 1) FH_LFD(4, 1) FH_LFD(1, 2) FH_LFD(2, 2) FH_LFD(3, 2) FH_LFD(1, 4)
-    FH_LFD(2, 4) FH_LFD(3, 4)
-        FH_LAUNCH((linear_fwd_skinny_kernel<2, 1>), grid, dim3(256), 0, st, x, x_cs, w, w_cs,
-                  bias, b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop, tk);
-#undef FH_LFD
-    if (splits > 1 && tk == nullptr)
+    FH_LAUNCH((linear_fwd_skinny_kernel<2, 1>), grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
+              b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop);
+    if (splits > 1)
         FH_LAUNCH(linear_fwd_epilogue_kernel, dim3((unsigned)ceil_div(32 * out_f, 256), nclients),
                   dim3(256), 0, st, (const float*)part, splits, out_f, y, y_cs, bias, b_cs, relu,
                   counts, batch, drop);

@@ -71,16 +71,6 @@ struct DConvArgs {
     const float* in2;
     const float* wt2;
     int64_t in2_cs, w2_cs;
-    // dconv_kernel split over reduction channels with the sum IN the launch (r03): tickets
-    // non-null -> each workgroup stores its partial tile to `slab` as [tile][split][BM/4][256]
-    // float4 fragments, takes a ticket on its tile's counter (agent-scope release / acquire,
-    // MI355X_MICROARCH.md inter-workgroup visibility) and the tile's last split to arrive adds
-    // the S partials in split order and runs the unsplit epilogue (bias, ReLU, BN statistics,
-    // accumulate) into `out`.  Counters are [client][gridY][gridX], zero between launches
-    // (the last arriver resets its own).  tickets null: `out` is the [z][split][M][Nfull] slab
-    // and splitk_epilogue_kernel finishes the sum.
-    float* slab;
-    int* tickets;
 };
 
 // Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
@@ -173,8 +163,7 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
     const int n0 = t * 256;
     // block-uniform: BN statistics of the stored values (FWD) / BN backward statistics of
     // the stored gradient (DGRAD)
-    const bool ink = a.splits > 1 && a.tickets != nullptr;  // in-launch split sum
-    const bool stats = BNB && a.bn_part != nullptr && (a.splits == 1 || ink);
+    const bool stats = BNB && a.bn_part != nullptr && a.splits == 1;
     if (n0 >= cnt * G::HW) {  // a tile past this client's images: zero statistics
         if (stats && tid < BM && m0 + tid < a.M) {
             double* q = a.bn_part + (((int64_t)z * a.M + m0 + tid) * a.bn_tiles + t) * 2;
@@ -374,98 +363,7 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
         }
     }
 
-    // ---- in-launch split sum: partial tiles through a fragment slab, last arriver sums ----
-    int nsplit = a.splits;
-    if (ink) {
-        constexpr int NQ = FM * FN * 4;  // float4 fragments per thread (= BM / 4)
-        float4* tile = reinterpret_cast<float4*>(a.slab) +
-                       (((int64_t)z * gridDim.y + by) * gridDim.x + bx) * a.splits * (NQ * 256);
-        // partials stored write-through (sc1: the buffer store's aux bit), so the hand-off needs
-        // no release fence — a release writes back every dirty line of the XCD's L2, the other
-        // lanes' included (cdna_hip_programming.md Guideline 16 R1)
-        typedef int v4i __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            tile, 0, a.splits * NQ * 256 * 16, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    __builtin_amdgcn_raw_buffer_store_b128(
-                        __builtin_bit_cast(v4i, make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1],
-                                                            acc[i][j][4 * q + 2],
-                                                            acc[i][j][4 * q + 3])),
-                        rs, ((split * NQ + (i * FN + j) * 4 + q) * 256 + tid) * 16, 0, 16);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-        __syncthreads();
-        int* flag = reinterpret_cast<int*>(smem);  // the one LDS array (no second __shared__)
-        if (tid == 0) {
-            int* ctr = a.tickets + ((int64_t)z * gridDim.y + by) * gridDim.x + bx;
-            const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-            const int last = old == a.splits - 1;
-            if (last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            flag[0] = last;
-        }
-        __syncthreads();
-        const bool last = flag[0] != 0;
-        __syncthreads();  // the epilogue reuses the LDS
-        if (!last) return;
-        // splits added in order from 0 (splitk_epilogue_kernel's sum: s = 0; s += part[i])
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        constexpr bool PAIR = NQ <= 8;  // two splits' loads in flight (registers allowing)
-        for (int s0 = 0; s0 < a.splits; s0 += PAIR ? 2 : 1) {
-            const bool two = PAIR && s0 + 1 < a.splits;  // block-uniform
-            float4 v0[NQ], v1[PAIR ? NQ : 1];
-#pragma unroll
-            for (int u = 0; u < NQ; ++u) v0[u] = tile[(s0 * NQ + u) * 256 + tid];
-            if constexpr (PAIR) {
-                if (two) {
-#pragma unroll
-                    for (int u = 0; u < NQ; ++u) v1[u] = tile[((s0 + 1) * NQ + u) * 256 + tid];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-                for (int j = 0; j < FN; ++j)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int u = (i * FN + j) * 4 + q;
-                        acc[i][j][4 * q] += v0[u].x;
-                        acc[i][j][4 * q + 1] += v0[u].y;
-                        acc[i][j][4 * q + 2] += v0[u].z;
-                        acc[i][j][4 * q + 3] += v0[u].w;
-                    }
-            if constexpr (PAIR) {
-                if (two) {
-#pragma unroll
-                    for (int i = 0; i < FM; ++i)
-#pragma unroll
-                        for (int j = 0; j < FN; ++j)
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                const int u = (i * FN + j) * 4 + q;
-                                acc[i][j][4 * q] += v1[u].x;
-                                acc[i][j][4 * q + 1] += v1[u].y;
-                                acc[i][j][4 * q + 2] += v1[u].z;
-                                acc[i][j][4 * q + 3] += v1[u].w;
-                            }
-                }
-            }
-        }
-        nsplit = 1;
-    }
+    const int nsplit = a.splits;
 
     // ---- epilogue: lanes = 32 consecutive pixels -> coalesced stores ----
     const int rbase = 4 * h;

@@ -35,17 +35,12 @@ def _counts(counts):
 
 
 class Workspace:
-    """Grow-only device scratch buffer (split-K partials), plus the stream's zeroed ticket
-    counters for split direct convolutions summed inside their launch (fh_set_split_tickets;
-    allocated on first use outside a graph capture — a capture would record the zero fill)."""
-
-    TICKETS = 1 << 17
+    """Grow-only device scratch buffer (split-K partials)."""
 
     def __init__(self, device):
         self.device = device
         self.buf = torch.empty(0, dtype=torch.uint8, device=device)
         self.retired = []
-        self.tickets = None
 
     def get(self, nbytes: int) -> torch.Tensor:
         if self.buf.numel() < nbytes:
@@ -158,36 +153,12 @@ def _linear_bytes(nclients, batch, in_f, out_f, acts=2, weights=1):
     return 4.0 * nclients * (batch * (acts - 1) * in_f + batch * out_f + weights * in_f * out_f)
 
 
-_TICKETS_SET = [None]
-# Split direct convolutions and classifier forwards can sum their partials inside the launch
-# (ticket counters per stream, write-through partials, the tile's last split adds them in
-# split order) instead of a reduction launch — bit-identical (tests/test_conv_gpu.py,
-# tests/test_classifier_gpu.py) but not faster: every lane ~1 % slower on KT (dconv only,
-# profiles/r03_s4/split_sum_ab.txt; 4.5 % with a release fence per workgroup), the narrow lanes
-# only within noise (narrow_lane_knobs_ab.txt), and with the classifier forward's last arriver
-# reading its partials one dependent load at a time KT -3 % / K2 -6 % (in_launch_linear_ab.txt).
-# Off: FH_SPLIT_TICKETS=1 turns it on for every lane, FH_SPLIT_TICKETS_FILL=x for the lanes that
-# plan for at most that share of the chip.
-IN_LAUNCH_SPLIT_SUM = (os.environ.get("FH_DCONV_INK", "4") != "0" and
-                       os.environ.get("FH_SPLIT_TICKETS", "0") == "1")
-SPLIT_TICKETS_FILL = (float(os.environ.get("FH_SPLIT_TICKETS_FILL", "0"))
-                      if os.environ.get("FH_DCONV_INK", "4") != "0" else 0.0)
-
-
 def _ws(device) -> Workspace:
     # one scratch buffer per (device, stream): lanes on different streams run concurrently
     key = (str(device), torch.cuda.current_stream(device).cuda_stream)
     w = _WS.get(key)
     if w is None:
         w = _WS[key] = Workspace(device)
-    if w.tickets is None and not torch.cuda.is_current_stream_capturing():
-        w.tickets = torch.zeros(Workspace.TICKETS, dtype=torch.int32, device=device)
-        _TICKETS_SET[0] = None
-    if _TICKETS_SET[0] is not w:  # this stream's ticket counters for the launches that follow
-        on = IN_LAUNCH_SPLIT_SUM or _FILL[0] <= SPLIT_TICKETS_FILL
-        t = w.tickets if on else None
-        call("fh_set_split_tickets", ptr(t), 0 if t is None else t.numel())
-        _TICKETS_SET[0] = w
     return w
 
 

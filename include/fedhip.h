@@ -551,12 +551,6 @@ int fh_bn_apply_tiles(const double* part, const float* x, int64_t x_cs, float* y
  * A client lane running concurrently with others asks for less (fedhip/lanes.py). */
 int fh_set_fill_fraction(float fraction);
 float fh_get_fill_fraction(void);
-/* Ticket counters for direct-convolution launches split over reduction channels (thread-
- * local, like the fill fraction): with count >= clients x tiles of a split launch, its
- * workgroups sum their partial tiles inside the launch — the last split of a tile to arrive
- * adds them in split order (device int32[count], zero on entry, left zero on exit) — instead
- * of a second reduction launch.  NULL / 0: the reduction launch. */
-int fh_set_split_tickets(int32_t* tickets, int64_t count);
 
 /* Lane streams (fedhip/lanes.py; replaces the reference's one-thread-per-client
  * concurrency, federated_simulation.py:309-318).  cu_mask (nullable; mask_words 32-bit

@@ -233,42 +233,3 @@ def test_linear_fwd_skinny_exact(nc, B, in_f, out_f):
         assert torch.equal(yc[z, :n].double(), ref[z, :n]), z
         assert torch.all(yc[z, n:] == 7.0)
 
-
-@pytest.mark.parametrize("nc,in_f,out_f", [(1, 2048, 512), (1, 3136, 128), (2, 512, 256),
-                                           (3, 3136, 128)])
-@pytest.mark.parametrize("drop", [False, True])
-def test_linear_fwd_split_sum_in_launch(nc, in_f, out_f, drop):
-    """The classifier forward's k-split summed inside the launch (ticket counters, the 32-output
-    tile's last split adds the partials: r03) equals the linear_fwd_epilogue_kernel launch bit for
-    bit — bias, ReLU, dropout mask generation — and leaves the counters at zero."""
-    B, p = 32, 0.3
-    cnt = _counts(nc, B, in_f + out_f)
-    g = torch.Generator(device=DEV).manual_seed(nc * in_f + out_f)
-    x = torch.randn(nc, B, in_f, generator=g, device=DEV)
-    w = torch.randn(nc, out_f, in_f, generator=g, device=DEV) * 0.05
-    b = torch.randn(nc, out_f, generator=g, device=DEV) * 0.1
-
-    def run(on):
-        prev = ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL
-        ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL = on, 0.0
-        ops._TICKETS_SET[0] = None
-        try:
-            y = torch.zeros(nc, B, out_f, device=DEV)
-            m = torch.zeros(nc, B, out_f, dtype=torch.uint8, device=DEV)
-            if drop:
-                ops.linear_fwd_dropout(x, w, b, y, m, nc, B, in_f, out_f, p, drop_mode=1, seed=5,
-                                       counts=cnt)
-            else:
-                ops.linear_fwd(x, w, b, y, nc, B, in_f, out_f, relu=True, counts=cnt)
-            torch.cuda.synchronize()
-            return y, m
-        finally:
-            ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL = prev
-            ops._TICKETS_SET[0] = None
-
-    (ya, ma), (yb, mb) = run(True), run(False)
-    for z in range(nc):
-        n = int(cnt[z])
-        assert torch.equal(ya[z, :n], yb[z, :n]) and torch.equal(ma[z, :n], mb[z, :n])
-    t = ops._ws(torch.device(DEV)).tickets
-    assert t is not None and int(t.abs().sum()) == 0

@@ -288,52 +288,3 @@ def test_dgrad_s2_shortcut_declines_unsupported():
     assert not ops.conv2d_dgrad_s2_shortcut(z(1, 2, 16, 4, 4, device=DEV), z(1, 16, 8, 3, 3, device=DEV),
                                             z(1, 2, 16, 4, 4, device=DEV), z(1, 16, 8, 1, 1, device=DEV),
                                             z(1, 2, 8, 8, 8, device=DEV), 1, 2, 8, 8, 8, 16)
-
-
-def _with_in_launch_sum(on, fn):
-    prev = ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL
-    ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL = on, 0.0
-    ops._TICKETS_SET[0] = None
-    try:
-        return fn()
-    finally:
-        ops.IN_LAUNCH_SPLIT_SUM, ops.SPLIT_TICKETS_FILL = prev
-        ops._TICKETS_SET[0] = None
-
-
-@pytest.mark.parametrize("C,B,cin,h,cout", [(1, 32, 64, 16, 64), (1, 32, 128, 8, 128),
-                                            (2, 27, 64, 8, 128), (1, 5, 32, 16, 64)])
-def test_split_sum_in_launch_matches_epilogue_launch(C, B, cin, h, cout):
-    """Direct 3x3 convolutions split over reduction channels (few clients): the partials
-    summed inside the launch by the tile's last split (ticket counters, r03) give the bits of
-    the separate splitk_epilogue_kernel launch — FWD with bias + ReLU, DGRAD accumulating,
-    the BN-statistics epilogue (fp64 tile partials: equal up to fp64 summation order), ragged
-    counts — and the counters are left at zero."""
-    g = torch.Generator().manual_seed(7)
-    x = torch.randn(C, B, cin, h, h, generator=g).to(DEV)
-    wt = (torch.randn(C, cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)).to(DEV)
-    bias = torch.randn(C, cout, generator=g).to(DEV)
-    dy = torch.randn(C, B, cout, h, h, generator=g).to(DEV)
-    base = torch.randn(C, B, cin, h, h, generator=g).to(DEV)
-    counts = torch.tensor([B - 3 * (i % 2) for i in range(C)], dtype=torch.int32, device=DEV)
-    tiles = ops.bnstats_tiles(B, h, h)
-
-    def run():
-        y = torch.zeros(C, B, cout, h, h, device=DEV)
-        ops.conv2d_fwd(x, wt, bias, y, C, B, cin, h, h, cout, 3, 1, 1, relu=True, counts=counts)
-        y2 = torch.zeros_like(y)
-        part = torch.zeros(C, cout, tiles, 2, dtype=torch.float64, device=DEV)
-        ops.conv2d_fwd(x, wt, bias, y2, C, B, cin, h, h, cout, 3, 1, 1, counts=counts,
-                       bn_stats=part)
-        dx = base.clone()
-        ops.conv2d_dgrad(dy, wt, dx, C, B, cin, h, h, cout, 3, 1, 1, counts=counts,
-                         accumulate=True)
-        torch.cuda.synchronize()
-        return y, y2, part, dx
-
-    a = _with_in_launch_sum(True, run)
-    b = _with_in_launch_sum(False, run)
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[3], b[3])
-    torch.testing.assert_close(a[2], b[2], rtol=1e-12, atol=1e-9)
-    w = ops._ws(torch.device(DEV))
-    assert w.tickets is not None and int(w.tickets.abs().sum()) == 0
