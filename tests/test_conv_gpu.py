@@ -288,3 +288,61 @@ def test_dgrad_s2_shortcut_declines_unsupported():
     assert not ops.conv2d_dgrad_s2_shortcut(z(1, 2, 16, 4, 4, device=DEV), z(1, 16, 8, 3, 3, device=DEV),
                                             z(1, 2, 16, 4, 4, device=DEV), z(1, 16, 8, 1, 1, device=DEV),
                                             z(1, 2, 8, 8, 8, device=DEV), 1, 2, 8, 8, 8, 16)
+
+
+@pytest.mark.parametrize("C,B,cin,h,cout", [(1, 32, 32, 32, 32), (1, 32, 64, 16, 64),
+                                            (1, 27, 32, 32, 32), (2, 32, 128, 8, 128),
+                                            (1, 9, 64, 8, 64)])
+def test_conv_lane_fill_exact(C, B, cin, h, cout):
+    """Narrow grids at a one-client lane's fill fraction (0.25: no split-K below 128
+    workgroups, fedhip/lanes.py): small-integer operands, so FWD, DGRAD and the two
+    statistics epilogues (BN forward sums of y; BN backward sums of the ReLU-masked gradient
+    and of (bn_x - mean) * g) must equal the fp64 reference exactly."""
+    g = torch.Generator().manual_seed(C * 1000 + B + cin + h)
+    x = torch.randint(-2, 3, (C, B, cin, h, h), generator=g).float()
+    wt = torch.randint(-2, 3, (C, cout, cin, 3, 3), generator=g).float()
+    bias = torch.randint(-2, 3, (C, cout), generator=g).float()
+    dy = torch.randint(-2, 3, (C, B, cout, h, h), generator=g).float()
+    bx = torch.randint(-3, 4, (C, B, cin, h, h), generator=g).float()    # BN input below
+    sc = torch.randint(1, 3, (C, cin), generator=g).float()
+    sh = torch.randint(-1, 2, (C, cin), generator=g).float()
+    mean = torch.randint(-1, 2, (C, cin), generator=g).float()
+    counts = torch.tensor([B - (i * 5) % 4 for i in range(C)], dtype=torch.int32)
+    cd = counts.to(DEV)
+    tiles = ops.bnstats_tiles(B, h, h)
+    y = torch.zeros(C, B, cout, h, h, device=DEV)
+    y1 = torch.zeros_like(y)
+    dx = torch.zeros(C, B, cin, h, h, device=DEV)
+    gx = torch.zeros_like(dx)
+    part = torch.zeros(C, cout, tiles, 2, dtype=torch.float64, device=DEV)
+    bpart = torch.zeros(C, cin, tiles, 2, dtype=torch.float64, device=DEV)
+    xd, wd, bd, dyd = x.to(DEV), wt.to(DEV), bias.to(DEV), dy.to(DEV)
+    ops.set_fill_fraction(0.25)
+    try:
+        ops.conv2d_fwd(xd, wd, bd, y, C, B, cin, h, h, cout, 3, 1, 1, counts=cd)
+        ops.conv2d_fwd(xd, wd, bd, y1, C, B, cin, h, h, cout, 3, 1, 1, counts=cd, bn_stats=part)
+        ops.conv2d_dgrad(dyd, wd, dx, C, B, cin, h, h, cout, 3, 1, 1, counts=cd)
+        ops.conv2d_dgrad(dyd, wd, gx, C, B, cin, h, h, cout, 3, 1, 1, counts=cd,
+                         bn_bwd=(bx.to(DEV), sc.to(DEV), sh.to(DEV), mean.to(DEV), bpart))
+    finally:
+        ops.set_fill_fraction(1.0)
+    torch.cuda.synchronize()
+    for z in range(C):
+        n = int(counts[z])
+        xr = x[z, :n].double().requires_grad_(True)
+        yr = F.conv2d(xr, wt[z].double(), bias[z].double(), padding=1)
+        yr.backward(dy[z, :n].double())
+        assert torch.equal(y[z, :n].cpu().double(), yr.detach()), f"fwd z={z}"
+        assert torch.equal(y1[z, :n].cpu().double(), yr.detach()), f"fwd+stats z={z}"
+        assert torch.equal(dx[z, :n].cpu().double(), xr.grad), f"dgrad z={z}"
+        ps = part[z].sum(dim=1).cpu()  # tiles summed: per channel (sum y, sum y^2)
+        assert torch.equal(ps[:, 0], yr.detach().sum(dim=(0, 2, 3))), f"bn sum z={z}"
+        assert torch.equal(ps[:, 1], (yr.detach() ** 2).sum(dim=(0, 2, 3))), f"bn sq z={z}"
+        on = (bx[z, :n].double() * sc[z].double().view(-1, 1, 1) +
+              sh[z].double().view(-1, 1, 1)) > 0
+        gr = torch.where(on, xr.grad, torch.zeros_like(xr.grad))
+        assert torch.equal(gx[z, :n].cpu().double(), gr), f"dgrad+bnstats z={z}"
+        bs = bpart[z].sum(dim=1).cpu()
+        assert torch.equal(bs[:, 0], gr.sum(dim=(0, 2, 3))), f"bn bwd sum z={z}"
+        dot = ((bx[z, :n].double() - mean[z].double().view(-1, 1, 1)) * gr).sum(dim=(0, 2, 3))
+        assert torch.equal(bs[:, 1], dot), f"bn bwd dot z={z}"

@@ -29,9 +29,23 @@ def run(op, cin, hw, cout, k, s, nc, reps, B=32):
     dx = torch.empty_like(x)
     dw = torch.empty_like(w)
     cnt = torch.full((nc,), B, dtype=torch.int32, device=dev)
+    tiles = ops.bnstats_tiles(B, oh, oh)
+    part = torch.zeros(nc, cout, tiles, 2, dtype=torch.float64, device=dev)
+    bpart = torch.zeros(nc, cin, tiles, 2, dtype=torch.float64, device=dev)
+    aff = (torch.rand(nc, cin, device=dev) + 0.5, torch.randn(nc, cin, device=dev))
+    mean = torch.randn(nc, cin, device=dev)
 
     def once():
-        if op == "fwd":
+        if op == "fwdbn":  # + BN statistics epilogue, input BN affine applied on load (KT)
+            ops.conv2d_fwd(x, w, None, y, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt,
+                           in_affine=aff, bn_stats=part)
+        elif op == "dgradbn":  # + BN backward statistics epilogue (KT's unpooled layers)
+            ops.conv2d_dgrad(dy, w, dx, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt,
+                             bn_bwd=(x, aff[0], aff[1], mean, bpart))
+        elif op == "wgradbn":  # input BN affine applied on load (KT)
+            ops.conv2d_wgrad(x, dy, dw, None, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt,
+                             in_affine=aff)
+        elif op == "fwd":
             ops.conv2d_fwd(x, w, None, y, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt)
         elif op == "dgrad":
             ops.conv2d_dgrad(dy, w, dx, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt)
@@ -57,7 +71,9 @@ def main():
     ap.add_argument("shapes", nargs="*")
     ap.add_argument("--clients", default="32,8,1")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--fill", type=float, default=1.0, help="split-K planner fill fraction")
     a = ap.parse_args()
+    ops.set_fill_fraction(a.fill)
     for sh in a.shapes or DEFAULT:
         op, cin, hw, cout, k, s = sh.split(":")
         for nc in [int(v) for v in a.clients.split(",")]:
