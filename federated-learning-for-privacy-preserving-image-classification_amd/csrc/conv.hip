@@ -1546,11 +1546,11 @@ static bool dwgrad_supported(int cin, int cout, int h, int w, int kh, int kw, in
 // (512: tools/r03_wgrad_ab.sh sweep, profiles/r03_dwq/).  KT against the r02 kernel (32x32x2
 // MFMAs, four pixel-waves, one 86 KB workgroup per CU): 270.3k / 272.1k vs 269.3k / 269.2k
 // client-images/s, interleaved.
-static const int kDwqBlocks = env_int("FH_DWQ_BLOCKS", 1024);
-// stage pixels: 128 = one buffer, stored between two barriers (default); 64 = two 64-pixel
-// buffers, the next stage stored half-way through this one's MFMAs, one barrier per stage
-// (FH_DWQ_SPX=64; measured within noise of 128, profiles/r03_dwq/)
-static const int kDwqSpx = env_int("FH_DWQ_SPX", 128) == 64 ? 64 : 128;
+constexpr int kDwqBlocks = 1024;
+// stage pixels: 128 = one buffer, stored between two barriers; the 64-pixel double-buffered
+// instance (the next stage stored half-way through this one's MFMAs) measured within noise of
+// it (profiles/r03_dwq/) and serves the per-image DP-SGD slabs of 8x8 maps (one image a stage)
+constexpr int kDwqSpx = 128;
 static DWPlan plan_dwq(int cout, int cin, int batch, int w, int nclients) {
     DWPlan p{1, 1, 4, kDwqSpx / w, 1, 1};
     const int64_t tiles = (int64_t)(cout / 32) * (cin / 32) * nclients;
@@ -2982,5 +2982,192 @@ extern "C" int fh_conv2d_persample_sqnorm(const float* x, int64_t x_cs, const fl
     FH_LAUNCH(conv_sq_reduce_kernel, dim3((unsigned)ceil_div(batch, 256), nclients),
                        dim3(256), 0, st, (const float*)workspace, tiles, batch, counts, sqnorm);
     FH_LAUNCH_CHECK("conv2d_persample_sqnorm reduce");
+    return FH_OK;
+}
+
+
+// ---- DP-SGD on the direct kernels (r04): per-image weight-gradient slabs -------------------
+// The direct WGRAD kernels split their pixel reduction into slabs [z][split][cout*cin*9] (+ bias
+// [z][split][cout] at wslab_bias_off); with one split per IMAGE the slab of split i is that
+// image's own gradient dW_i (of the batch-mean loss, i.e. g_i / B).  One WGRAD pass then gives
+// both what the clip needs — ||g_i||^2 = sum of squares of the image's slab rows, summed over
+// the layers (fh_persample_slab_sqnorm) — and, once the clip coefficients c_i are known, the
+// clipped sum sum_i c_i dW_i in image order (fh_persample_slab_wsum): no second WGRAD on rescaled
+// dY and no implicit-GEMM norm tiles.  SimpleCNN: conv2 on the padded 16x16 planes
+// (dwgrad_q_kernel, two 128-pixel stages = one image per split), conv1 from pool1's gradient
+// (conv_c1_wgrad_mfma_kernel<POOLED>, seven 4-row stages = one 28x28 image per split).
+static size_t persample_slab_bytes(int nclients, int batch, int per_w, int per_b) {
+    return (size_t)wslab_bias_off(nclients, batch, per_w) +
+           (size_t)nclients * batch * per_b * sizeof(float);
+}
+
+namespace fh {
+// sqnorm[z][i] += sum_j w[z][i][j]^2 + sum_j b[z][i][j]^2 (fp64, one workgroup per (i, z),
+// fixed order: per-thread strided partials, then block_sum_256)
+__global__ void __launch_bounds__(256)
+slab_sqnorm_kernel(const float* __restrict__ wpart, const float* __restrict__ bpart, int per_w,
+                   int per_b, const int32_t* __restrict__ counts, int batch,
+                   double* __restrict__ sqnorm) {
+    __shared__ double red[4];
+    const int i = blockIdx.x, z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    if (i >= cnt) return;  // block-uniform
+    const int64_t row = (int64_t)z * batch + i;
+    const float4* w4 = reinterpret_cast<const float4*>(wpart + row * per_w);
+    double s = 0.0;
+    for (int q = threadIdx.x; q < per_w / 4; q += 256) {
+        const float4 v = w4[q];
+        s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    if (bpart)
+        for (int q = threadIdx.x; q < per_b; q += 256) {
+            const double v = bpart[row * per_b + q];
+            s += v * v;
+        }
+    s = block_sum_256(s, red);
+    if (threadIdx.x == 0) sqnorm[row] += s;
+}
+
+// dw[z][j] = sum_{i < cnt} coef[z][i] * w[z][i][j] (float4 lanes; images in order, fl32
+// multiply then add — -ffp-contract=off); the same for the bias slab into db
+__global__ void __launch_bounds__(256)
+slab_wsum_kernel(const float* __restrict__ wpart, const float* __restrict__ bpart, int per_w,
+                 int per_b, const float* __restrict__ coef, const int32_t* __restrict__ counts,
+                 int batch, float* __restrict__ dw, int64_t dw_cs, float* __restrict__ db,
+                 int64_t db_cs) {
+    const int z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const float* cz = coef + (int64_t)z * batch;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    const int nq = per_w / 4;
+    if (q < nq) {
+        const float4* w4 = reinterpret_cast<const float4*>(wpart + (int64_t)z * batch * per_w) + q;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < cnt; ++i) {
+            const float c = cz[i];
+            const float4 v = w4[(int64_t)i * nq];
+            acc.x = acc.x + c * v.x;
+            acc.y = acc.y + c * v.y;
+            acc.z = acc.z + c * v.z;
+            acc.w = acc.w + c * v.w;
+        }
+        float* d = dw + z * dw_cs + 4 * q;
+        d[0] = acc.x;
+        d[1] = acc.y;
+        d[2] = acc.z;
+        d[3] = acc.w;
+    } else if (bpart && db && q - nq < per_b) {
+        const int j = q - nq;
+        float acc = 0.f;
+        for (int i = 0; i < cnt; ++i) acc = acc + cz[i] * bpart[((int64_t)z * batch + i) * per_b + j];
+        db[z * db_cs + j] = acc;
+    }
+}
+}  // namespace fh
+
+extern "C" size_t fh_conv2d_wgrad_persample_workspace(int32_t nclients, int32_t batch,
+                                                      int32_t cin, int32_t cout) {
+    if (nclients <= 0 || batch <= 0) return 0;
+    return persample_slab_bytes(nclients, batch, cout * cin * 9, cout);
+}
+
+extern "C" int fh_conv2d_wgrad_persample(const float* x, int64_t x_cs, const float* dy,
+                                         int64_t dy_cs, void* slab, size_t slab_bytes,
+                                         const int32_t* counts, int32_t nclients, int32_t batch,
+                                         int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                                         void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0, "conv2d_wgrad_persample: bad shape");
+    FH_REQUIRE(dwgrad_supported(cin, cout, h, w_, 3, 3, 1, 1),
+               "conv2d_wgrad_persample: 3x3/s1/p1 on a square 8/16/32 map, channels %% 32 "
+               "(got cin %d cout %d %dx%d)", cin, cout, h, w_);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && dy && slab, "conv2d_wgrad_persample: null pointer");
+    FH_REQUIRE((uintptr_t)x % 16 == 0 && (uintptr_t)dy % 16 == 0 && x_cs % 4 == 0 &&
+               dy_cs % 4 == 0, "conv2d_wgrad_persample: x / dy must be 16-B aligned");
+    const size_t need = fh_conv2d_wgrad_persample_workspace(nclients, batch, cin, cout);
+    FH_REQUIRE(slab_bytes >= need, "conv2d_wgrad_persample: slab %zu < %zu", slab_bytes, need);
+    const int N = cin * 9;
+    DWArgs d{};
+    d.x = x; d.dy = dy; d.x_cs = x_cs; d.dy_cs = dy_cs; d.counts = counts;
+    d.batch = batch; d.cin = cin; d.M = cout; d.N = N;
+    d.splits = batch;                                      // one split per image
+    const int spx = w_ == 8 ? 64 : 128;                    // a stage never straddles two images
+    d.stages_per_split = (w_ * w_) / spx;
+    d.part = (float*)slab;
+    d.bias_part = (float*)((char*)slab + wslab_bias_off(nclients, batch, cout * N));
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((unsigned)batch, (unsigned)((cout / 32) * (cin / 32)), (unsigned)nclients);
+    if (w_ == 32) FH_LAUNCH((dwgrad_q_kernel<32, 128, false>), grid, dim3(256), 0, st, d);
+    else if (w_ == 16) FH_LAUNCH((dwgrad_q_kernel<16, 128, false>), grid, dim3(256), 0, st, d);
+    else FH_LAUNCH((dwgrad_q_kernel<8, 64, true>), grid, dim3(256), 0, st, d);
+    FH_LAUNCH_CHECK("conv2d_wgrad_persample");
+    return FH_OK;
+}
+
+extern "C" int fh_conv2d_c1_pool_wgrad_persample(const float* x, int64_t x_cs, const float* dpool,
+                                                 int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
+                                                 const float* y, int64_t y_cs, void* slab,
+                                                 size_t slab_bytes, const int32_t* counts,
+                                                 int32_t nclients, int32_t batch, int32_t h,
+                                                 int32_t w_, int32_t cout, int32_t gh, int32_t gw,
+                                                 void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && h % 4 == 0 && w_ % 4 == 0 && w_ <= 32 &&
+               gh >= h / 2 && gw >= w_ / 2, "conv2d_c1_pool_wgrad_persample: bad shape");
+    FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_wgrad_persample: cout %d (32 or 64)", cout);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && dpool && idx && y && slab, "conv2d_c1_pool_wgrad_persample: null pointer");
+    FH_REQUIRE((uintptr_t)x % 16 == 0 && x_cs % 4 == 0,
+               "conv2d_c1_pool_wgrad_persample: x must be 16-B aligned");
+    const size_t need = fh_conv2d_wgrad_persample_workspace(nclients, batch, 1, cout);
+    FH_REQUIRE(slab_bytes >= need, "conv2d_c1_pool_wgrad_persample: slab %zu < %zu", slab_bytes,
+               need);
+    float* part = (float*)slab;
+    float* bpart = (float*)((char*)slab + wslab_bias_off(nclients, batch, cout * 9));
+    const int sps = h / 4;  // one image per split
+    const dim3 grid((unsigned)batch, (unsigned)nclients);
+    hipStream_t st = as_stream(stream);
+    if (cout == 32)
+        FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
+                  dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, gw);
+    else
+        FH_LAUNCH((conv_c1_wgrad_mfma_kernel<64, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
+                  dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, gw);
+    FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad_persample");
+    return FH_OK;
+}
+
+extern "C" int fh_persample_slab_sqnorm(const void* slab, int32_t per_w, int32_t per_b,
+                                        const int32_t* counts, int32_t nclients, int32_t batch,
+                                        double* sqnorm, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && per_w > 0 && per_w % 4 == 0 && per_b >= 0,
+               "persample_slab_sqnorm: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(slab && sqnorm, "persample_slab_sqnorm: null pointer");
+    const float* w = (const float*)slab;
+    const float* b = per_b ? (const float*)((const char*)slab + wslab_bias_off(nclients, batch, per_w))
+                           : nullptr;
+    FH_LAUNCH(slab_sqnorm_kernel, dim3((unsigned)batch, (unsigned)nclients), dim3(256), 0,
+              as_stream(stream), w, b, per_w, per_b, counts, batch, sqnorm);
+    FH_LAUNCH_CHECK("persample_slab_sqnorm");
+    return FH_OK;
+}
+
+extern "C" int fh_persample_slab_wsum(const void* slab, int32_t per_w, int32_t per_b,
+                                      const float* coef, const int32_t* counts, int32_t nclients,
+                                      int32_t batch, float* dw, int64_t dw_cs, float* db,
+                                      int64_t db_cs, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && per_w > 0 && per_w % 4 == 0 && per_b >= 0,
+               "persample_slab_wsum: bad shape");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(slab && coef && dw, "persample_slab_wsum: null pointer");
+    FH_REQUIRE(!per_b || db, "persample_slab_wsum: bias slab without db");
+    const float* w = (const float*)slab;
+    const float* b = per_b ? (const float*)((const char*)slab + wslab_bias_off(nclients, batch, per_w))
+                           : nullptr;
+    const int threads = per_w / 4 + per_b;
+    FH_LAUNCH(slab_wsum_kernel, dim3((unsigned)ceil_div(threads, 256), (unsigned)nclients),
+              dim3(256), 0, as_stream(stream), w, b, per_w, per_b, coef, counts, batch, dw, dw_cs,
+              db, db_cs);
+    FH_LAUNCH_CHECK("persample_slab_wsum");
     return FH_OK;
 }

@@ -139,11 +139,6 @@ class PackedTrainer:
         self.seg_offsets = torch.tensor(L.seg_offsets(), dtype=torch.int64, device=dev)
         self.opt_type, self.lr, self.opt_step = "sgd", 0.01, 0
         self.dpsgd = dpsgd
-        if dpsgd is not None:  # the per-sample passes read the dense maps and fc1's ReLU output
-            self.net.pad_maps = False
-            self.net.fused_dropout = False
-            self.net.fuse_pool1 = False
-            self.net.fuse_pool1_bwd = False
         if dpsgd is not None:
             self._sq = torch.zeros(capacity, batch, dtype=torch.float64, device=dev)
             self._coef = torch.zeros(capacity, batch, device=dev)

@@ -359,12 +359,16 @@ class PackedNet:
         ops.conv2d_wgrad(self.x, da1, W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 1, 28, 28, 32,
                          3, 1, 1, counts=cnt)
 
-    # ---------------- DP-SGD backward (per-sample clipping; dpsgd.hip)
+    # ---------------- DP-SGD backward (per-sample clipping; dpsgd.hip, conv.hip slabs)
     def backward_dpsgd(self, params, grads, n, counts, sqnorm, coef, max_norm, sigma_c,
                        noise_seed, noise_seed_dev=None, P=None):
-        """Backward with per-sample clipping + Gaussian noise.  Pass 1: the dgrad chain and
-        every layer's per-sample squared gradient norm; clip coefficients; pass 2: each
-        layer's WGRAD on its coefficient-scaled upstream gradient; noise on all grads.
+        """Backward with per-sample clipping + Gaussian noise (r04: on the direct kernels).
+        Pass 1: the dgrad chain (the training step's own kernels: padded 16x16 conv2 planes,
+        conv1 from pool1's gradient) and every layer's per-sample squared gradient norm —
+        linear layers by the rank-1 identity, conv layers from per-IMAGE weight-gradient
+        slabs (one WGRAD with one pixel split per image); clip coefficients.  Pass 2: the
+        clipped sums — conv layers as the coefficient-weighted sum of their slabs (no second
+        WGRAD), linear layers as WGRAD on coefficient-scaled rows; noise on all grads.
         Models with BatchNorm have no per-sample gradient (batch statistics couple the
         samples): like Opacus, DP-SGD is refused for them."""
         if self.family != "SimpleCNN":
@@ -373,6 +377,12 @@ class PackedNet:
             return
         A, B, W, K, cnt = self.A, self.batch, self.W, self.num_classes, counts
         P_, G = params, grads
+        p1, a2, da2, dp1, hp = self._simple_maps()
+        if hp != 16:
+            raise FedHipError("DP-SGD runs on the padded 16x16 conv2 planes (pad_maps)")
+        if getattr(self, "_ps", None) is None:
+            self._ps = (ops.PersampleSlab(self.device), ops.PersampleSlab(self.device))
+        s1, s2 = self._ps
         sqnorm[:n].zero_()
         # pass 1: dgrad chain + per-sample norms
         ops.linear_persample_sqnorm(self._fc_in, self.dlogits, sqnorm, n, B, 128, K, counts=cnt)
@@ -381,37 +391,31 @@ class PackedNet:
         dh1 = A("dh1", 128)
         mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
         ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
-                        relu_out=A("h1", 128), counts=cnt)
+                        relu_out=self._fc_in, counts=cnt)
         p2 = A("p2", 64, 7, 7)
         ops.linear_persample_sqnorm(p2, dh1, sqnorm, n, B, 3136, 128, counts=cnt)
         dp2 = A("dp2", 64, 7, 7)
         ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
-        da2 = A("da2", 64, 14, 14)
-        ops.maxpool2_bwd(dp2, A("i2", 64, 7, 7, dtype=torch.uint8), da2, n, B, 64, 14, 14,
-                         xin=A("a2", 64, 14, 14), counts=cnt)
-        p1 = A("p1", 32, 14, 14)
-        ops.conv2d_persample_sqnorm(p1, da2, sqnorm, n, B, 32, 14, 14, 64, 3, 1, 1, counts=cnt)
-        dp1 = A("dp1", 32, 14, 14)
-        ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, 14, 14, 64, 3, 1, 1,
+        i2 = A("i2", 64, 7, 7, dtype=torch.uint8)
+        ops.maxpool2_bwd(dp2, i2, da2, n, B, 64, 14, 14, xin=a2, counts=cnt)
+        ops.conv2d_wgrad_persample(p1, da2, s2, n, B, 32, hp, hp, 64, counts=cnt)
+        ops.slab_sqnorm(s2, sqnorm, counts=cnt)
+        ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt)
-        da1 = A("da1", 32, 28, 28)
-        ops.maxpool2_bwd(dp1, A("i1", 32, 14, 14, dtype=torch.uint8), da1, n, B, 32, 28, 28,
-                         xin=A("a1", 32, 28, 28), counts=cnt)
-        ops.conv2d_persample_sqnorm(self.x, da1, sqnorm, n, B, 1, 28, 28, 32, 3, 1, 1,
-                                    counts=cnt)
+        # conv1's per-image slabs from pool1's gradient (the pooled ReLU output p1 > 0 is the
+        # mask at each window's argmax, whether or not conv1's output was written)
+        ops.conv2d_c1_pool_wgrad_persample(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8),
+                                           p1, s1, n, B, 28, 28, 32, counts=cnt)
+        ops.slab_sqnorm(s1, sqnorm, counts=cnt)
         ops.dpsgd_clip_coef(sqnorm, coef, n, B, max_norm, counts=cnt)
-        # pass 2: clipped sums = WGRAD on coef-scaled upstream rows
+        # pass 2: clipped sums
         s = ops.scale_rows(self.dlogits, coef, A("s_dl", K), n, B, K, counts=cnt)
         ops.linear_wgrad(self._fc_in, s, W(G, "fc2.weight"), W(G, "fc2.bias"), n, B, 128, K,
                          counts=cnt)
         s = ops.scale_rows(dh1, coef, A("s_dh1", 128), n, B, 128, counts=cnt)
         ops.linear_wgrad(p2, s, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136, 128, counts=cnt)
-        s = ops.scale_rows(da2, coef, A("s_da2", 64, 14, 14), n, B, 64 * 196, counts=cnt)
-        ops.conv2d_wgrad(p1, s, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, 14, 14, 64,
-                         3, 1, 1, counts=cnt)
-        s = ops.scale_rows(da1, coef, A("s_da1", 32, 28, 28), n, B, 32 * 784, counts=cnt)
-        ops.conv2d_wgrad(self.x, s, W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 1, 28, 28,
-                         32, 3, 1, 1, counts=cnt)
+        ops.slab_wsum(s2, coef, W(G, "conv2.weight"), W(G, "conv2.bias"), counts=cnt)
+        ops.slab_wsum(s1, coef, W(G, "conv1.weight"), W(G, "conv1.bias"), counts=cnt)
         ops.dpsgd_noise(G, self.layout.P if P is None else P, n, B, sigma_c, seed=noise_seed,
                         seed_dev=noise_seed_dev, counts=cnt)
 

@@ -652,6 +652,64 @@ def linear_persample_sqnorm(x, dy, sqnorm, nclients, batch, in_f, out_f, with_bi
               _linear_bytes(nclients, batch, in_f, out_f, weights=0), nclients)
 
 
+class PersampleSlab:
+    """Per-image weight-gradient slab of one conv layer (DP-SGD, r04): filled by
+    conv2d_wgrad_persample / conv2d_c1_pool_wgrad_persample, read by slab_sqnorm (the clip
+    norms) and slab_wsum (the clipped sum).  Grow-only device buffer."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buf = torch.empty(0, dtype=torch.uint8, device=device)
+        self.per_w = self.per_b = self.nclients = self.batch = 0
+
+    def ensure(self, nclients, batch, cin, cout):
+        nb = load().fh_conv2d_wgrad_persample_workspace(nclients, batch, cin, cout)
+        if self.buf.numel() < nb:
+            self.buf = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        self.per_w, self.per_b = cout * cin * 9, cout
+        self.nclients, self.batch = nclients, batch
+        return nb
+
+
+def conv2d_wgrad_persample(x, dy, slab, nclients, batch, cin, h, wd, cout, counts=None):
+    """Per-image WGRAD slabs of a direct 3x3/s1/p1 conv (fh_conv2d_wgrad_persample)."""
+    nb = slab.ensure(nclients, batch, cin, cout)
+    ev = PROBE.begin(_conv_tag("pswgrad", cin, h, wd, cout, 3, 1))
+    call("fh_conv2d_wgrad_persample", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(slab.buf), nb,
+         _counts(counts), nclients, batch, cin, h, wd, cout, stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, 3, 1, 1),
+              _conv_bytes(nclients, batch, cin, h, wd, cout, 3, 1, 1) +
+              4.0 * nclients * batch * cout * (cin * 9 + 1), nclients)
+
+
+def conv2d_c1_pool_wgrad_persample(x, dpool, idx, y, slab, nclients, batch, h, wd, cout,
+                                   counts=None):
+    """Per-image WGRAD slabs of conv1 from pool1's gradient (fh_conv2d_c1_pool_wgrad_persample);
+    dpool / y in planes (gh, gw) = their last two dims."""
+    nb = slab.ensure(nclients, batch, 1, cout)
+    gh, gw = dpool.shape[-2], dpool.shape[-1]
+    ev = PROBE.begin(_conv_tag("pswgrad", 1, h, wd, cout, 3, 1) + "+pool")
+    call("fh_conv2d_c1_pool_wgrad_persample", ptr(x), _cs(x), ptr(dpool), _cs(dpool), ptr(idx),
+         _cs(idx), ptr(y), _cs(y), ptr(slab.buf), nb, _counts(counts), nclients, batch, h, wd,
+         cout, gh, gw, stream_handle())
+    pooled = nclients * batch * cout * (h // 2) * (wd // 2)
+    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1),
+              4.0 * nclients * batch * (h * wd + cout * 10) + 9.0 * pooled, nclients)
+
+
+def slab_sqnorm(slab, sqnorm, counts=None):
+    """sqnorm[z][i] += ||slab row (z, i)||^2 (weights + bias, fp64)."""
+    call("fh_persample_slab_sqnorm", ptr(slab.buf), slab.per_w, slab.per_b, _counts(counts),
+         slab.nclients, slab.batch, ptr(sqnorm), stream_handle())
+
+
+def slab_wsum(slab, coef, dw, db, counts=None):
+    """dw = sum_i coef[z][i] * slab[z][i] (image order), db from the bias slab."""
+    call("fh_persample_slab_wsum", ptr(slab.buf), slab.per_w, slab.per_b if db is not None else 0,
+         ptr(coef), _counts(counts), slab.nclients, slab.batch, ptr(dw), _cs(dw), ptr(db),
+         _cs(db), stream_handle())
+
+
 def dpsgd_clip_coef(sqnorm, coef, nclients, batch, max_norm, counts=None):
     call("fh_dpsgd_clip_coef", ptr(sqnorm), _counts(counts), nclients, batch, float(max_norm),
          ptr(coef), stream_handle())

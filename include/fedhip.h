@@ -323,6 +323,37 @@ int fh_linear_persample_sqnorm(const float* x, int64_t x_cs, const float* dy, in
                                int32_t with_bias, double* sqnorm, const int32_t* counts,
                                int32_t nclients, int32_t batch, int32_t in_f, int32_t out_f,
                                void* stream);
+/* DP-SGD on the direct kernels (r04): per-image weight-gradient slabs.  A direct WGRAD with one
+ * pixel split per image leaves slab [client][image][cout*cin*9] (the gradient of that image's
+ * share of the batch-mean loss, g_i / B) and the bias slab [client][image][cout] behind it at a
+ * 256-B aligned offset; fh_conv2d_wgrad_persample_workspace gives the slab bytes.
+ * fh_conv2d_wgrad_persample: 3x3/s1/p1 on square 8/16/32 maps, channels % 32 (SimpleCNN conv2
+ * on its padded 16x16 planes).  fh_conv2d_c1_pool_wgrad_persample: the single-input-channel
+ * conv1 from pool1's gradient (fh_conv2d_c1_pool_wgrad's routing), h % 4 == 0.
+ * fh_persample_slab_sqnorm: sqnorm[client][image] (fp64, [nclients][batch]) += the image's sum
+ * of squares over the slab (weights + bias; per_w % 4 == 0).  fh_persample_slab_wsum: dw =
+ * sum_{i < count} coef[client][i] * slab[client][i] in image order (fp32 multiply then add),
+ * db likewise from the bias slab (per_b = 0: no bias).  Together they replace the per-sample
+ * norm pass and the second WGRAD on coefficient-scaled rows (reference: per-sample clipping is
+ * not in the reference; its update clip is privacy.py:107-144, sigma privacy.py:209). */
+size_t fh_conv2d_wgrad_persample_workspace(int32_t nclients, int32_t batch, int32_t cin,
+                                           int32_t cout);
+int fh_conv2d_wgrad_persample(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                              void* slab, size_t slab_bytes, const int32_t* counts,
+                              int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w,
+                              int32_t cout, void* stream);
+int fh_conv2d_c1_pool_wgrad_persample(const float* x, int64_t x_cs, const float* dpool,
+                                      int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
+                                      const float* y, int64_t y_cs, void* slab, size_t slab_bytes,
+                                      const int32_t* counts, int32_t nclients, int32_t batch,
+                                      int32_t h, int32_t w, int32_t cout, int32_t gh, int32_t gw,
+                                      void* stream);
+int fh_persample_slab_sqnorm(const void* slab, int32_t per_w, int32_t per_b,
+                             const int32_t* counts, int32_t nclients, int32_t batch,
+                             double* sqnorm, void* stream);
+int fh_persample_slab_wsum(const void* slab, int32_t per_w, int32_t per_b, const float* coef,
+                           const int32_t* counts, int32_t nclients, int32_t batch, float* dw,
+                           int64_t dw_cs, float* db, int64_t db_cs, void* stream);
 int fh_dpsgd_clip_coef(const double* sqnorm, const int32_t* counts, int32_t nclients,
                        int32_t batch, double max_norm, float* coef, void* stream);
 int fh_scale_rows(const float* in, int64_t in_cs, const float* coef, const int32_t* counts,

@@ -147,3 +147,71 @@ def test_dpsgd_noise_key_is_secret():
     P = a.layout.P
     assert not torch.equal(a.params[:, :P], b.params[:, :P])
     assert torch.equal(c.params[:, :P], d.params[:, :P])
+
+
+def test_persample_conv_slabs_exact():
+    """fh_conv2d_wgrad_persample (one WGRAD pixel split per image, r04): each image's slab row
+    is that image's own weight / bias gradient, slab_sqnorm its squared norm and slab_wsum the
+    coefficient-weighted sum in image order — exact on small-integer operands and dyadic
+    coefficients (ragged counts: rows past a client's count are never read)."""
+    from fedhip import ops
+    import torch.nn.functional as F
+    C, B, cin, h, cout = 2, 7, 32, 16, 64
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(-2, 3, (C, B, cin, h, h), generator=g).float()
+    dy = torch.randint(-2, 3, (C, B, cout, h, h), generator=g).float()
+    counts = torch.tensor([7, 5], dtype=torch.int32)
+    coef = torch.tensor([[1.0, 0.5, 0.25, 1.0, 0.125, 0.5, 1.0]] * C)
+    slab = ops.PersampleSlab(DEV)
+    cd = counts.to(DEV)
+    ops.conv2d_wgrad_persample(x.to(DEV), dy.to(DEV), slab, C, B, cin, h, h, cout, counts=cd)
+    sq = torch.zeros(C, B, dtype=torch.float64, device=DEV)
+    ops.slab_sqnorm(slab, sq, counts=cd)
+    dw = torch.zeros(C, cout, cin, 3, 3, device=DEV)
+    db = torch.zeros(C, cout, device=DEV)
+    ops.slab_wsum(slab, coef.to(DEV), dw, db, counts=cd)
+    torch.cuda.synchronize()
+    nw = cout * cin * 9
+    boff = (C * B * nw * 4 + 255) // 256 * 256
+    wrows = slab.buf[:C * B * nw * 4].view(torch.float32).view(C, B, nw).cpu()
+    brows = slab.buf[boff:boff + C * B * cout * 4].view(torch.float32).view(C, B, cout).cpu()
+    for z in range(C):
+        accw = torch.zeros(cout, cin, 3, 3, dtype=torch.float64)
+        accb = torch.zeros(cout, dtype=torch.float64)
+        for i in range(int(counts[z])):
+            wr = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+            br = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+            F.conv2d(x[z, i:i + 1].double(), wr, br, padding=1).backward(dy[z, i:i + 1].double())
+            assert torch.equal(wrows[z, i].double(), wr.grad.reshape(-1)), (z, i)
+            assert torch.equal(brows[z, i].double(), br.grad), (z, i)
+            assert sq[z, i].item() == float((wr.grad ** 2).sum() + (br.grad ** 2).sum())
+            accw += coef[z, i].double() * wr.grad
+            accb += coef[z, i].double() * br.grad
+        assert torch.equal(dw[z].cpu().double(), accw), z
+        assert torch.equal(db[z].cpu().double(), accb), z
+
+
+def test_persample_c1_pool_slabs_sum_to_wgrad():
+    """conv1's per-image slabs from pool1's gradient sum (coefficients 1) to the ordinary
+    fused-pool conv1 weight gradient (fh_conv2d_c1_pool_wgrad) exactly, on integer data."""
+    from fedhip import ops
+    C, B, h = 2, 6, 28
+    g = torch.Generator().manual_seed(4)
+    x = torch.randint(-2, 3, (C, B, 1, h, h), generator=g).float().to(DEV)
+    dpool = torch.zeros(C, B, 32, 16, 16)
+    dpool[..., :14, :14] = torch.randint(-2, 3, (C, B, 32, 14, 14), generator=g).float()
+    yp = torch.zeros(C, B, 32, 16, 16)
+    yp[..., :14, :14] = torch.randint(-1, 2, (C, B, 32, 14, 14), generator=g).float()
+    idx = torch.randint(0, 4, (C, B, 32, 14, 14), generator=g).to(torch.uint8).to(DEV)
+    dpool, yp = dpool.to(DEV), yp.to(DEV)
+    cd = torch.tensor([6, 4], dtype=torch.int32, device=DEV)
+    slab = ops.PersampleSlab(DEV)
+    ops.conv2d_c1_pool_wgrad_persample(x, dpool, idx, yp, slab, C, B, h, h, 32, counts=cd)
+    dw = torch.zeros(C, 32, 1, 3, 3, device=DEV)
+    db = torch.zeros(C, 32, device=DEV)
+    ops.slab_wsum(slab, torch.ones(C, B, device=DEV), dw, db, counts=cd)
+    dw2, db2 = torch.zeros_like(dw), torch.zeros_like(db)
+    ops.conv2d_c1_pool_wgrad(x, dpool, idx, yp, dw2, db2, C, B, h, h, 32, counts=cd)
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    assert dw.abs().sum() > 0
