@@ -629,20 +629,25 @@ def host_legs(out, args, dev):
 def run_dpsgd(args, dev, steps, warmup):
     """`--config K2-dpsgd`: the K2 workload (SimpleCNN, 32 Dirichlet(0.5) clients, one
     local epoch) trained with per-sample DP-SGD (north_star extension, not in the
-    reference): every step clips each image's gradient to C = 1 by the per-image norm
-    passes (conv / linear per-sample square-norm tiles, fh_dpsgd_clip_coef, rows scaled
-    before the WGRADs) and adds N(0, (sigma C)^2) with the reference's Gaussian-mechanism
-    sigma (privacy.py:209, eps = 1, delta = 1e-5).  One lane (PackedTrainer), fp32 N(0,1)
-    data.  Algorithmic work per image: SimpleCNN's train FLOPs + 2 * MACs for the norms."""
-    from fedhip.engine import DPSGDConfig, PackedTrainer
+    reference): every step clips each image's gradient to C = 1 — linear layers by the
+    rank-1 norm identity, conv layers from per-image weight-gradient slabs whose
+    coefficient-weighted sum is the clipped gradient (r04) — and adds N(0, (sigma C)^2) with
+    the reference's Gaussian-mechanism sigma (privacy.py:209, eps = 1, delta = 1e-5).
+    Concurrent lanes as the other configs (fedhip/lanes.py), fp32 N(0,1) data.  Algorithmic
+    work per image: SimpleCNN's train FLOPs only — the conv norms come from the WGRAD product
+    itself and the linear norms are O(in + out) per image (r03 counted an extra WGRAD product
+    for the norms, 2 * MACs, which its implicit-GEMM norm pass did compute)."""
+    from fedhip.engine import DPSGDConfig
+    from fedhip.lanes import LanedTrainer
     cfg = CONFIGS["K2"]
     labels, train = build_clients(cfg, 1)
     order = sorted(range(len(train)), key=lambda k: (-train[k], k))
     sizes = [train[k] for k in order]
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
-    eng = PackedTrainer(model, capacity=len(sizes), batch=32, device=dev,
-                        dpsgd=DPSGDConfig(max_grad_norm=1.0, epsilon=1.0, delta=1e-5))
+    eng = LanedTrainer(model, [math.ceil(n / 32) for n in sizes], batch=32, device=dev,
+                       lanes=args.lanes,
+                       dpsgd=DPSGDConfig(max_grad_norm=1.0, epsilon=1.0, delta=1e-5))
     for k in range(len(sizes)):
         eng.load_module_state(k, model)
     g = torch.Generator(device=dev).manual_seed(1000)
@@ -661,16 +666,16 @@ def run_dpsgd(args, dev, steps, warmup):
     elapsed = time.perf_counter() - t0
     ops.PROBE.reset()
     ops.PROBE.tag, ops.PROBE.enabled = "*", True
-    eng.run_round(data, lab, offs, eng.make_plan(sizes, 1, generator=gen), args.opt, args.lr)
+    eng.run_round(data, lab, offs, eng.make_plan(sizes, 1, generator=gen), args.opt, args.lr,
+                  serialize=True)
     ops.PROBE.enabled = False
     peak = FP32_MFMA_PEAK_TFLOPS
     rows, instances, by_bucket, conv_all = summarize_instances(ops.PROBE.by_tag(),
                                                                ops.PROBE.by_tag_bucket(), peak)
     ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
-    ps = [(t, v) for t, v in rows if "psnorm" in t]
+    ps = [(t, v) for t, v in rows if "psnorm" in t or "pswgrad" in t]
     value = sum(sizes) * steps / elapsed
-    macs = (TRAIN_FLOPS["simple_cnn"] + 2 * 225_792) / 6  # MACs/img (first layer counted 4x)
-    fl = TRAIN_FLOPS["simple_cnn"] + 2 * macs
+    fl = TRAIN_FLOPS["simple_cnn"]
     return {"metric": "client-images/sec/node", "value": round(value, 1),
             "unit": "client-images/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
             "ms_per_step": round(1000 * elapsed / steps, 2), "higher_is_better": True,
@@ -679,8 +684,9 @@ def run_dpsgd(args, dev, steps, warmup):
                     "shard sizes from the reference partitioner restatement",
             "config": {"workload": f"K2-dpsgd: simple_cnn {len(sizes)} clients non_iid(a=0.5), 1 "
                                    f"local epoch, batch 32, per-sample DP-SGD C=1 eps=1 "
-                                   f"delta=1e-5, {args.opt} lr {args.lr} (one lane)",
-                       "clients": len(sizes), "images_per_round": sum(sizes)},
+                                   f"delta=1e-5, {args.opt} lr {args.lr}",
+                       "clients": len(sizes), "images_per_round": sum(sizes),
+                       "lanes": eng.cut},
             "achieved_tflops_step": round(value * fl / 1e12, 2),
             "round_frac": round(value * fl / 1e12 / peak, 4),
             "roofline": roofline_of(rows[0][0], *rows[0][1], peak,

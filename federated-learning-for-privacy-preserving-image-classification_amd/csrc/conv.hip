@@ -2452,7 +2452,9 @@ __device__ __forceinline__ void linear_wgrad_skinny_body(
         const float* __restrict__ X, int64_t x_cs, const float* __restrict__ dY, int64_t dy_cs,
         float* __restrict__ dW, int64_t dw_cs, float* __restrict__ db, int64_t db_cs,
         const int32_t* __restrict__ counts, int batch, int K, int M, int z, int kblock,
-        int mblock) {
+        int mblock, const float* __restrict__ rowscale = nullptr) {
+    // rowscale (nullable, [client][batch]): dY row b scaled by rowscale[z][b] on load — the
+    // fp32 products fh_scale_rows would store (DP-SGD's clipped linear-layer sums)
     const int m0 = mblock * 32;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int k0 = kblock * 128 + wid * 32;
@@ -2469,7 +2471,8 @@ __device__ __forceinline__ void linear_wgrad_skinny_body(
     for (int p = 0; p < 16; ++p) {
         const int b = 2 * p + h;
         const bool ok = b < cnt;
-        const float av = ok && mok ? yz[(int64_t)b * M] : 0.f;
+        float av = ok && mok ? yz[(int64_t)b * M] : 0.f;
+        if (rowscale && ok) av = rowscale[(int64_t)z * batch + b] * av;
         const float bv = ok ? xz[(int64_t)b * K] : 0.f;
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
     }
@@ -2481,7 +2484,9 @@ __device__ __forceinline__ void linear_wgrad_skinny_body(
     }
     if (db && kblock == 0 && wid == 0 && h == 0 && mok) {
         float v = 0.f;
-        for (int b = 0; b < cnt; ++b) v += yz[(int64_t)b * M];
+        for (int b = 0; b < cnt; ++b)
+            v += rowscale ? rowscale[(int64_t)z * batch + b] * yz[(int64_t)b * M]
+                          : yz[(int64_t)b * M];
         db[z * db_cs + m0 + r32] = v;
     }
 }
@@ -2490,7 +2495,8 @@ __global__ void __launch_bounds__(256)
 linear_wgrad_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float* __restrict__ dY,
                            int64_t dy_cs, float* __restrict__ dW, int64_t dw_cs,
                            float* __restrict__ db, int64_t db_cs,
-                           const int32_t* __restrict__ counts, int batch, int K, int M) {
+                           const int32_t* __restrict__ counts, int batch, int K, int M,
+                           const float* __restrict__ rowscale = nullptr) {
     // XCD-aware order: workgroups b and b + 8 share an XCD (round-robin dispatch), so the
     // logical workgroup L = (b % 8) * (N / 8) + b / 8 puts each client's tiles — which all
     // read that client's X and dY — on one XCD's L2 instead of all eight
@@ -2500,7 +2506,7 @@ linear_wgrad_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const floa
     if ((N & 7) == 0) b = (b & 7) * (N >> 3) + (b >> 3);
     const int kb = b % gx, rest = b / gx;
     linear_wgrad_skinny_body(X, x_cs, dY, dy_cs, dW, dw_cs, db, db_cs, counts, batch, K, M,
-                             rest / gy, kb, rest % gy);
+                             rest / gy, kb, rest % gy, rowscale);
 }
 
 // A whole linear backward in one launch: workgroups [0, nw) of each client are the skinny
@@ -2837,7 +2843,7 @@ static int linear_bwd_fused_impl(const float* x, int64_t x_cs, const float* dy, 
         FH_LAUNCH(linear_wgrad_skinny_kernel,
                   dim3((unsigned)kb, (unsigned)ceil_div(out_f, 32), nclients),
                   dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
-                  counts, batch, in_f, out_f);
+                  counts, batch, in_f, out_f, (const float*)nullptr);
         FH_LAUNCH_CHECK("linear_bwd_fused wgrad");
         if (in_f % 128 == 0)
             FH_LAUNCH(linear_dgrad_skinny_kernel<4>, dim3((unsigned)(in_f / 128), nclients),
@@ -2895,6 +2901,24 @@ extern "C" size_t fh_linear_wgrad_workspace(int32_t nclients, int32_t batch, int
     return fh_conv2d_wgrad_workspace(nclients, batch, in_f, 1, 1, out_f, 1, 1, 1, 0);
 }
 
+extern "C" int fh_linear_wgrad_rowscale(const float* x, int64_t x_cs, const float* dy,
+                                        int64_t dy_cs, const float* rowscale, float* dw,
+                                        int64_t dw_cs, float* db, int64_t db_cs,
+                                        const int32_t* counts, int32_t nclients, int32_t batch,
+                                        int32_t in_f, int32_t out_f, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && batch <= 32 && in_f > 0 && in_f % 32 == 0 &&
+                   out_f > 0, "linear_wgrad_rowscale: batch <= 32 and in_f %% 32 == 0 (got %d, %d)",
+               batch, in_f);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && dy && dw && rowscale, "linear_wgrad_rowscale: null pointer");
+    FH_LAUNCH(linear_wgrad_skinny_kernel,
+              dim3((unsigned)ceil_div(in_f, 128), (unsigned)ceil_div(out_f, 32), nclients),
+              dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs, counts,
+              batch, in_f, out_f, rowscale);
+    FH_LAUNCH_CHECK("linear_wgrad_rowscale");
+    return FH_OK;
+}
+
 extern "C" int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
                                float* dw, int64_t dw_cs, float* db, int64_t db_cs, void* workspace,
                                size_t ws_bytes, const int32_t* counts, int32_t nclients,
@@ -2904,7 +2928,7 @@ extern "C" int fh_linear_wgrad(const float* x, int64_t x_cs, const float* dy, in
         FH_LAUNCH(linear_wgrad_skinny_kernel,
                            dim3((unsigned)ceil_div(in_f, 128), (unsigned)ceil_div(out_f, 32), nclients),
                            dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
-                           counts, batch, in_f, out_f);
+                           counts, batch, in_f, out_f, (const float*)nullptr);
         FH_LAUNCH_CHECK("linear_wgrad skinny");
         return FH_OK;
     }

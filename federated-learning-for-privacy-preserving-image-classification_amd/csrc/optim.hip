@@ -151,6 +151,34 @@ struct OptScal {  // SGD: neg_lr, mom, wd, first | Adam: the adam_elem scalars
 
 constexpr int kOptPlainPer = 1024;  // float4s per plain block
 
+// DP-SGD (r04): the same launch finishes a per-sample-clipped step.  Slab ranges hold one
+// split per IMAGE (conv.hip fh_conv2d_wgrad_persample): g = sum_{i < count} coef[z][i] *
+// slab[z][i] in image order (fh_persample_slab_wsum's operations); then, on elements
+// [0, n_noise) of the row, g += (sigma_c / count) * N(0,1) with fh_dpsgd_noise's Philox keys
+// (key = seed + *seed_dev, row philox_row(seed_dev, z), counter = the row's float4 index) —
+// the bits of slab_wsum + dpsgd_noise + the optimizer step, in one pass.
+struct OptDp {
+    const float* coef;  // [client][batch]
+    const int32_t* counts;
+    int batch;
+    int64_t n_noise;
+    float sigma_c;
+    uint64_t seed;
+    const uint64_t* seed_dev;
+};
+
+__device__ __forceinline__ void dp_noise4(float4& g, const OptDp& d, uint64_t key, uint64_t row,
+                                          int64_t q, float s) {
+    if (s == 0.f) return;
+    float r[4];
+    gauss4(key, row, (uint64_t)q, r);
+    const int64_t j = 4 * q;
+    if (j < d.n_noise) g.x = g.x + s * r[0];
+    if (j + 1 < d.n_noise) g.y = g.y + s * r[1];
+    if (j + 2 < d.n_noise) g.z = g.z + s * r[2];
+    if (j + 3 < d.n_noise) g.w = g.w + s * r[3];
+}
+
 template <bool ADAM>
 __device__ __forceinline__ void opt_update4(float4* p, float4* s1, float4* s2, int64_t i,
                                             float4 gv, const OptScal& o, float bc2_sqrt,
@@ -178,10 +206,11 @@ __device__ __forceinline__ void opt_update4(float4* p, float4* s1, float4* s2, i
     p[i] = out;
 }
 
-template <bool ADAM>
+template <bool ADAM, bool DP = false>
 __global__ void __launch_bounds__(256)
 opt_slabs_kernel(float4* __restrict__ p, float4* __restrict__ g, float4* __restrict__ s1,
-                 float4* __restrict__ s2, int64_t row4, const SlabRanges rg, const OptScal o) {
+                 float4* __restrict__ s2, int64_t row4, const SlabRanges rg, const OptScal o,
+                 const OptDp d) {
     __shared__ float4 red[256];
     const int z = blockIdx.y, bx = blockIdx.x, t = threadIdx.x;
     int k = 0;
@@ -191,6 +220,43 @@ opt_slabs_kernel(float4* __restrict__ p, float4* __restrict__ g, float4* __restr
     const int64_t base = (int64_t)z * row4 + R.off4;
     const float bc2_sqrt = (ADAM && o.scal) ? o.scal[0] : o.bc2_sqrt;
     const float neg_step = (ADAM && o.scal) ? o.scal[1] : o.neg_step_size;
+    if constexpr (DP) {
+        const int cnt = d.counts ? d.counts[z] : d.batch;
+        const float s = cnt > 0 ? d.sigma_c / (float)cnt : 0.f;
+        const uint64_t key = d.seed + (d.seed_dev ? *d.seed_dev : 0ull);
+        const uint64_t row = philox_row(d.seed_dev, z);
+        if (R.slab == nullptr) {
+            const int i0 = (bx - R.blk0) * kOptPlainPer + t;
+#pragma unroll
+            for (int u = 0; u < kOptPlainPer / 256; ++u) {
+                const int i = i0 + 256 * u;
+                if (i < R.len4) {
+                    float4 gv = g[base + i];
+                    dp_noise4(gv, d, key, row, (int64_t)R.off4 + i, s);
+                    g[base + i] = gv;
+                    opt_update4<ADAM>(p, s1, s2, base + i, gv, o, bc2_sqrt, neg_step);
+                }
+            }
+            return;
+        }
+        const int e = (bx - R.blk0) * 256 + t;
+        if (e >= R.len4) return;
+        const float4* src = R.slab + (int64_t)z * R.splits * R.len4 + e;
+        const float* cz = d.coef + (int64_t)z * d.batch;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < cnt; ++i) {  // fh_persample_slab_wsum's order and operations
+            const float c = cz[i];
+            const float4 v = src[(int64_t)i * R.len4];
+            acc.x = acc.x + c * v.x;
+            acc.y = acc.y + c * v.y;
+            acc.z = acc.z + c * v.z;
+            acc.w = acc.w + c * v.w;
+        }
+        dp_noise4(acc, d, key, row, (int64_t)R.off4 + e, s);
+        g[base + e] = acc;
+        opt_update4<ADAM>(p, s1, s2, base + e, acc, o, bc2_sqrt, neg_step);
+        return;
+    }
     if (R.slab == nullptr) {
         const int i0 = (bx - R.blk0) * kOptPlainPer + t;
 #pragma unroll
@@ -248,7 +314,7 @@ static int slab_groups(int splits) {
 
 // host: the ranges of a row (slab ranges + the plain gaps) and their block offsets
 static int build_ranges(const fh_grad_slab* slabs, int nslabs, int64_t row_len, SlabRanges& rg,
-                        int& blocks) {
+                        int& blocks, bool per_image = false) {
     FH_REQUIRE(nslabs >= 0 && nslabs <= FH_MAX_GRAD_SLABS, "step_slabs: %d slab ranges (max %d)",
                nslabs, FH_MAX_GRAD_SLABS);
     FH_REQUIRE(nslabs == 0 || slabs, "step_slabs: null slab array");
@@ -263,7 +329,7 @@ static int build_ranges(const fh_grad_slab* slabs, int nslabs, int64_t row_len, 
         r.len4 = (int)(len / 4);
         r.slab = (const float4*)slab;
         r.splits = splits;
-        r.G = slab ? slab_groups(splits) : 1;
+        r.G = (slab && !per_image) ? slab_groups(splits) : 1;
         r.blk0 = blocks;
         r.pad = 0;
         blocks += (int)(slab ? ceil_div(r.len4, 256 / r.G) : ceil_div(r.len4, kOptPlainPer));
@@ -309,7 +375,7 @@ extern "C" int fh_sgd_step_slabs(float* param, float* grad, float* momentum_buf,
     o.first = first_step;
     FH_LAUNCH(opt_slabs_kernel<false>, dim3(blocks, nclients), dim3(256), 0, as_stream(stream),
               (float4*)param, (float4*)grad, (float4*)momentum_buf, (float4*)nullptr,
-              row_stride / 4, rg, o);
+              row_stride / 4, rg, o, OptDp{});
     FH_LAUNCH_CHECK("sgd_step_slabs");
     return FH_OK;
 }
@@ -344,8 +410,62 @@ extern "C" int fh_adam_step_slabs(float* param, float* grad, float* exp_avg, flo
     o.scal = scal_dev;
     FH_LAUNCH(opt_slabs_kernel<true>, dim3(blocks, nclients), dim3(256), 0, as_stream(stream),
               (float4*)param, (float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq,
-              row_stride / 4, rg, o);
+              row_stride / 4, rg, o, OptDp{});
     FH_LAUNCH_CHECK("adam_step_slabs");
+    return FH_OK;
+}
+
+extern "C" int fh_dpsgd_step_slabs(float* param, float* grad, float* state1, float* state2,
+                                   int64_t row_stride, int64_t row_len, int32_t nclients,
+                                   const fh_grad_slab* slabs, int32_t nslabs, const float* coef,
+                                   const int32_t* counts, int32_t batch, int64_t n_noise,
+                                   float sigma_c, uint64_t seed, const uint64_t* seed_dev,
+                                   int32_t adam, double lr, double momentum, double beta1,
+                                   double beta2, double eps, double weight_decay,
+                                   int32_t decoupled, int32_t first_step, double step_size,
+                                   double bc2_sqrt, const float* scal_dev, void* stream) {
+    FH_REQUIRE(nclients >= 0 && row_stride >= row_len && row_stride % 4 == 0 && batch > 0 &&
+                   n_noise >= 0 && n_noise <= row_len && sigma_c >= 0.f,
+               "dpsgd_step_slabs: bad shape");
+    if (nclients == 0 || row_len == 0) return FH_OK;
+    FH_REQUIRE(param && grad && coef && state1 && (!adam || state2),
+               "dpsgd_step_slabs: null pointer");
+    FH_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)state1 |
+                (adam ? (uintptr_t)state2 : 0)) % 16 == 0,
+               "dpsgd_step_slabs: rows must be 16-B aligned");
+    for (int i = 0; i < nslabs; ++i)
+        FH_REQUIRE(slabs[i].splits == batch, "dpsgd_step_slabs: slab %d has %d splits, not one "
+                   "per image (%d)", i, slabs[i].splits, batch);
+    SlabRanges rg;
+    int blocks = 0;
+    if (const int rc = build_ranges(slabs, nslabs, row_len, rg, blocks, true)) return rc;
+    OptScal o{};
+    OptDp d{coef, counts, batch, n_noise, sigma_c, seed, seed_dev};
+    hipStream_t st = as_stream(stream);
+    if (!adam) {
+        o.neg_lr = (float)-lr;
+        o.mom = (float)momentum;
+        o.wd = (float)weight_decay;
+        o.first = first_step;
+        FH_LAUNCH((opt_slabs_kernel<false, true>), dim3(blocks, nclients), dim3(256), 0, st,
+                  (float4*)param, (float4*)grad, (float4*)state1, (float4*)nullptr,
+                  row_stride / 4, rg, o, d);
+    } else {
+        o.wd = (float)weight_decay;
+        o.decay_mul = (float)(1.0 - lr * weight_decay);
+        o.decoupled = decoupled;
+        o.one_m_b1 = (float)(1.0 - beta1);
+        o.b2 = (float)beta2;
+        o.one_m_b2 = (float)(1.0 - beta2);
+        o.bc2_sqrt = (float)bc2_sqrt;
+        o.eps = (float)eps;
+        o.neg_step_size = (float)(-step_size);
+        o.scal = scal_dev;
+        FH_LAUNCH((opt_slabs_kernel<true, true>), dim3(blocks, nclients), dim3(256), 0, st,
+                  (float4*)param, (float4*)grad, (float4*)state1, (float4*)state2,
+                  row_stride / 4, rg, o, d);
+    }
+    FH_LAUNCH_CHECK("dpsgd_step_slabs");
     return FH_OK;
 }
 

@@ -268,14 +268,16 @@ class PackedTrainer:
         if self.dpsgd is None:
             self._backward_and_update(n, counts, first, adam_dev)
             return
-        else:
-            d = self.dpsgd
-            net.backward_dpsgd(self.params, self.grads, n, counts, self._sq, self._coef,
-                               d.max_grad_norm, d.sigma * d.max_grad_norm,
-                               noise_seed=(net._seed(77) + self._noise_key *
-                                           0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF,
-                               noise_seed_dev=net.seed_dev, P=self.layout.P)
-        self._optimizer_launch(n, first, adam_dev)
+        d = self.dpsgd
+        ranges = net.backward_dpsgd(self.params, self.grads, n, counts, self._sq, self._coef,
+                                    d.max_grad_norm)
+        # the conv layers' clipped sums, the noise and the update: one launch
+        ops.dpsgd_step_slabs(self.params, self.grads, self.state1, self.state2, n, ranges,
+                             self._coef, counts, self.batch, self.layout.P,
+                             d.sigma * d.max_grad_norm,
+                             (net._seed(77) + self._noise_key * 0xD1B54A32D192ED03)
+                             & 0xFFFFFFFFFFFFFFFF, seed_dev=net.seed_dev, opt=self.opt_type,
+                             lr=self.lr, step=self.opt_step, first_step=first, scal_dev=adam_dev)
 
     def _backward_and_update(self, n, counts, first, adam_dev):
         """Backward + optimizer; with defer_wgrad_reduce the split convolution weight

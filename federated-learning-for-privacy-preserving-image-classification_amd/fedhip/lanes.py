@@ -87,7 +87,7 @@ class LanedTrainer:
     """PackedTrainer-compatible round driver over L concurrent lanes (see module doc)."""
 
     def __init__(self, model, slot_steps: Sequence[int], batch=32, device="cuda",
-                 lanes=None, cut=None, salt=0):
+                 lanes=None, cut=None, salt=0, dpsgd=None):
         self.device = torch.device(device)
         S = len(slot_steps)
         if lanes is None:
@@ -112,7 +112,7 @@ class LanedTrainer:
         self.Ppad = ((self.layout.P + 63) // 64) * 64
         self.storage = SlotStorage(self.layout, self.Ppad, S, self.device)
         self.lanes = [PackedTrainer(model, cut[i + 1] - cut[i], batch, self.device,
-                                    storage=self.storage, row0=cut[i])
+                                    storage=self.storage, row0=cut[i], dpsgd=dpsgd)
                       for i in range(len(cut) - 1)]
         # dropout / augmentation Philox keys: per lane (row0) and per rank (salt), so no
         # two clients anywhere in the job share a stream

@@ -360,15 +360,16 @@ class PackedNet:
                          3, 1, 1, counts=cnt)
 
     # ---------------- DP-SGD backward (per-sample clipping; dpsgd.hip, conv.hip slabs)
-    def backward_dpsgd(self, params, grads, n, counts, sqnorm, coef, max_norm, sigma_c,
-                       noise_seed, noise_seed_dev=None, P=None):
-        """Backward with per-sample clipping + Gaussian noise (r04: on the direct kernels).
+    def backward_dpsgd(self, params, grads, n, counts, sqnorm, coef, max_norm):
+        """Backward with per-sample clipping (r04: on the direct kernels).
         Pass 1: the dgrad chain (the training step's own kernels: padded 16x16 conv2 planes,
         conv1 from pool1's gradient) and every layer's per-sample squared gradient norm —
         linear layers by the rank-1 identity, conv layers from per-IMAGE weight-gradient
         slabs (one WGRAD with one pixel split per image); clip coefficients.  Pass 2: the
-        clipped sums — conv layers as the coefficient-weighted sum of their slabs (no second
-        WGRAD), linear layers as WGRAD on coefficient-scaled rows; noise on all grads.
+        clipped sums of the linear layers as WGRAD on coefficient-scaled rows.  Returns the
+        conv layers' slab ranges [(row offset, length, slab pointer, images)]: their clipped
+        sums (the coefficient-weighted sum of the slabs — no second WGRAD) and the Gaussian
+        noise are the optimizer launch's (ops.dpsgd_step_slabs).
         Models with BatchNorm have no per-sample gradient (batch statistics couple the
         samples): like Opacus, DP-SGD is refused for them."""
         if self.family != "SimpleCNN":
@@ -408,16 +409,13 @@ class PackedNet:
                                            p1, s1, n, B, 28, 28, 32, counts=cnt)
         ops.slab_sqnorm(s1, sqnorm, counts=cnt)
         ops.dpsgd_clip_coef(sqnorm, coef, n, B, max_norm, counts=cnt)
-        # pass 2: clipped sums
-        s = ops.scale_rows(self.dlogits, coef, A("s_dl", K), n, B, K, counts=cnt)
-        ops.linear_wgrad(self._fc_in, s, W(G, "fc2.weight"), W(G, "fc2.bias"), n, B, 128, K,
-                         counts=cnt)
-        s = ops.scale_rows(dh1, coef, A("s_dh1", 128), n, B, 128, counts=cnt)
-        ops.linear_wgrad(p2, s, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136, 128, counts=cnt)
-        ops.slab_wsum(s2, coef, W(G, "conv2.weight"), W(G, "conv2.bias"), counts=cnt)
-        ops.slab_wsum(s1, coef, W(G, "conv1.weight"), W(G, "conv1.bias"), counts=cnt)
-        ops.dpsgd_noise(G, self.layout.P if P is None else P, n, B, sigma_c, seed=noise_seed,
-                        seed_dev=noise_seed_dev, counts=cnt)
+        # pass 2: the linear layers' clipped sums (dY rows scaled by c_i as they are loaded)
+        ops.linear_wgrad_rowscale(self._fc_in, self.dlogits, coef, W(G, "fc2.weight"),
+                                  W(G, "fc2.bias"), n, B, 128, K, counts=cnt)
+        ops.linear_wgrad_rowscale(p2, dh1, coef, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136,
+                                  128, counts=cnt)
+        return s1.ranges(G, W(G, "conv1.weight"), W(G, "conv1.bias")) + \
+            s2.ranges(G, W(G, "conv2.weight"), W(G, "conv2.bias"))
 
     # ---------------- CIFAR10CNN (models_pytorch.py:136-165)
     _CIFAR_CONVS = [  # name, cin, cout, hw, bn

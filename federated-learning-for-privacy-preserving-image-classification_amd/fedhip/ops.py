@@ -670,6 +670,15 @@ class PersampleSlab:
         self.nclients, self.batch = nclients, batch
         return nb
 
+    def ranges(self, grads, dw, db):
+        """fh_grad_slab ranges (row offset, length, slab pointer, images) of this layer's
+        weight and bias slabs inside the packed gradient rows (dpsgd_step_slabs)."""
+        g0 = grads.data_ptr()
+        boff = (self.nclients * self.batch * self.per_w * 4 + 255) // 256 * 256  # wslab_bias_off
+        base = self.buf.data_ptr()
+        return [((dw.data_ptr() - g0) // 4, self.per_w, base, self.batch),
+                ((db.data_ptr() - g0) // 4, self.per_b, base + boff, self.batch)]
+
 
 def conv2d_wgrad_persample(x, dy, slab, nclients, batch, cin, h, wd, cout, counts=None):
     """Per-image WGRAD slabs of a direct 3x3/s1/p1 conv (fh_conv2d_wgrad_persample)."""
@@ -708,6 +717,16 @@ def slab_wsum(slab, coef, dw, db, counts=None):
     call("fh_persample_slab_wsum", ptr(slab.buf), slab.per_w, slab.per_b if db is not None else 0,
          ptr(coef), _counts(counts), slab.nclients, slab.batch, ptr(dw), _cs(dw), ptr(db),
          _cs(db), stream_handle())
+
+
+def linear_wgrad_rowscale(x, dy, rowscale, dw, db, nclients, batch, in_f, out_f, counts=None):
+    """linear_wgrad on dY rows scaled by rowscale[z][b] on load (fh_linear_wgrad_rowscale)."""
+    ev = PROBE.begin(f"linear_wgrad:{in_f}->{out_f}")
+    call("fh_linear_wgrad_rowscale", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(rowscale), ptr(dw),
+         _cs(dw), ptr(db), _cs(db), _counts(counts), nclients, batch, in_f, out_f,
+         stream_handle())
+    PROBE.end(ev, 2.0 * nclients * batch * in_f * out_f,
+              _linear_bytes(nclients, batch, in_f, out_f), nclients)
 
 
 def dpsgd_clip_coef(sqnorm, coef, nclients, batch, max_norm, counts=None):
@@ -815,6 +834,23 @@ def adam_step_slabs(param, grad, exp_avg, exp_avg_sq, step, lr, nclients, ranges
          param.stride(0), param.shape[1], nclients, arr, ns, float(lr), float(beta1),
          float(beta2), float(eps), float(weight_decay), int(decoupled), float(step_size),
          float(bc2_sqrt), ptr(scal_dev), stream_handle())
+
+
+def dpsgd_step_slabs(param, grad, state1, state2, nclients, ranges, coef, counts, batch,
+                     n_noise, sigma_c, seed, seed_dev=None, opt="sgd", lr=0.01, step=1,
+                     first_step=False, momentum=0.9, scal_dev=None):
+    """fh_dpsgd_step_slabs: the per-image slab ranges' clipped sums (coef-weighted, image
+    order), Gaussian noise on [0, n_noise) of every row, then the SGD / Adam / AdamW update —
+    the bits of slab_wsum + dpsgd_noise + sgd_step / adam_step."""
+    arr, ns = _slab_array(ranges)
+    adam = opt in ("adam", "adamw")
+    step_size, bc2_sqrt = adam_bias_corrections(step, lr)
+    wd = 0.01 if opt == "adamw" else 0.0
+    call("fh_dpsgd_step_slabs", ptr(param), ptr(grad), ptr(state1), ptr(state2),
+         param.stride(0), param.shape[1], nclients, arr, ns, ptr(coef), _counts(counts), batch,
+         int(n_noise), float(sigma_c), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev), int(adam),
+         float(lr), float(momentum), 0.9, 0.999, 1e-8, wd, int(opt == "adamw"),
+         int(first_step), float(step_size), float(bc2_sqrt), ptr(scal_dev), stream_handle())
 
 
 def adam_bias_corrections(step, lr, beta1=0.9, beta2=0.999):

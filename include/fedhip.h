@@ -135,6 +135,30 @@ int fh_adam_step_slabs(float* param, float* grad, float* exp_avg, float* exp_avg
                        double beta2, double eps, double weight_decay, int32_t decoupled,
                        double step_size, double bc2_sqrt, const float* scal_dev, void* stream);
 
+/* DP-SGD step (r04): fh_sgd_step_slabs / fh_adam_step_slabs (adam != 0; decoupled = AdamW)
+ * for a per-sample-clipped step.  Each slab range holds one split per IMAGE (splits == batch,
+ * fh_conv2d_wgrad_persample's slab): g = sum_{i < counts[z]} coef[z][i] * slab[z][i] in image
+ * order; then elements [0, n_noise) of every row get g += (sigma_c / counts[z]) * N(0,1) with
+ * fh_dpsgd_noise's Philox keys (seed + *seed_dev, philox_row, the row's float4 index); g is
+ * stored and the update applied — the bits of fh_persample_slab_wsum + fh_dpsgd_noise + the
+ * optimizer step in one launch.  SGD uses lr / momentum / weight_decay / first_step, Adam lr /
+ * beta1 / beta2 / eps / weight_decay / step_size / bc2_sqrt / scal_dev as fh_adam_step. */
+/* fh_linear_wgrad on row-scaled dY: dy row b of client z multiplied by rowscale[z][b] as it is
+ * loaded (the products fh_scale_rows would store: same bits as scale_rows + linear_wgrad);
+ * DP-SGD's clipped linear-layer sums.  batch <= 32, in_f % 32 == 0. */
+int fh_linear_wgrad_rowscale(const float* x, int64_t x_cs, const float* dy, int64_t dy_cs,
+                             const float* rowscale, float* dw, int64_t dw_cs, float* db,
+                             int64_t db_cs, const int32_t* counts, int32_t nclients,
+                             int32_t batch, int32_t in_f, int32_t out_f, void* stream);
+int fh_dpsgd_step_slabs(float* param, float* grad, float* state1, float* state2,
+                        int64_t row_stride, int64_t row_len, int32_t nclients,
+                        const fh_grad_slab* slabs, int32_t nslabs, const float* coef,
+                        const int32_t* counts, int32_t batch, int64_t n_noise, float sigma_c,
+                        uint64_t seed, const uint64_t* seed_dev, int32_t adam, double lr,
+                        double momentum, double beta1, double beta2, double eps,
+                        double weight_decay, int32_t decoupled, int32_t first_step,
+                        double step_size, double bc2_sqrt, const float* scal_dev, void* stream);
+
 /* ---------------- convolution / linear (fp32 MFMA implicit GEMM) ----------
  * x: [clients][batch][cin][h][w]; w: [cout][cin][kh][kw] per client; y: [clients][batch][cout][oh][ow].
  * Supported: (kh,kw,stride) in {(3,3,1),(3,3,2),(1,1,1),(1,1,2)}, pad arbitrary. */

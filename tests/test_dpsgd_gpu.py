@@ -215,3 +215,63 @@ def test_persample_c1_pool_slabs_sum_to_wgrad():
     torch.cuda.synchronize()
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
     assert dw.abs().sum() > 0
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adamw"])
+def test_dpsgd_fused_step_bit_identical(opt):
+    """fh_dpsgd_step_slabs (r04) == slab_wsum of each per-image slab + dpsgd_noise over the
+    row + the plain optimizer step, bit for bit (params, grads, optimizer state), with ragged
+    counts and rows longer than the noised prefix."""
+    from fedhip import ops
+    C, B, cin, h, cout = 3, 9, 32, 16, 64
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(C, B, cin, h, h, generator=g).to(DEV)
+    dy = torch.randn(C, B, cout, h, h, generator=g).to(DEV)
+    cd = torch.tensor([9, 6, 1], dtype=torch.int32, device=DEV)
+    coef = torch.rand(C, B, generator=g).to(DEV)
+    slab = ops.PersampleSlab(DEV)
+    ops.conv2d_wgrad_persample(x, dy, slab, C, B, cin, h, h, cout, counts=cd)
+    nw = cout * cin * 9
+    off_w, off_b, P = 40, 40 + nw, 40 + nw + cout + 52
+    Ppad = (P + 60 + 63) // 64 * 64
+    out = []
+    for fused in (True, False):
+        gen = torch.Generator().manual_seed(5)
+        params = torch.randn(C, Ppad, generator=gen).to(DEV)
+        grads = torch.randn(C, Ppad, generator=gen).to(DEV)
+        s1 = torch.randn(C, Ppad, generator=gen).abs().to(DEV)
+        s2 = torch.randn(C, Ppad, generator=gen).abs().to(DEV)
+        dw, db = grads[:, off_w:off_w + nw], grads[:, off_b:off_b + cout]
+        if fused:
+            ops.dpsgd_step_slabs(params, grads, s1, s2, C, slab.ranges(grads, dw, db), coef, cd, B,
+                                 P, 2.5, seed=77, opt=opt, lr=0.01, step=3)
+        else:
+            ops.slab_wsum(slab, coef, dw, db, counts=cd)
+            ops.dpsgd_noise(grads, P, C, B, 2.5, seed=77, counts=cd)
+            if opt == "sgd":
+                ops.sgd_step(params, grads, s1, 0.01, 0.9, first_step=False)
+            else:
+                ops.adam_step(params, grads, s1, s2, 3, 0.01, weight_decay=0.01, decoupled=True)
+        torch.cuda.synchronize()
+        out.append((params, grads, s1, s2))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("in_f,out_f", [(3136, 128), (128, 10)])
+def test_linear_wgrad_rowscale_bit_identical(in_f, out_f):
+    """fh_linear_wgrad_rowscale == scale_rows + linear_wgrad, bit for bit (ragged counts)."""
+    from fedhip import ops
+    C, B = 3, 32
+    g = torch.Generator().manual_seed(in_f)
+    x = torch.randn(C, B, in_f, generator=g).to(DEV)
+    dy = torch.randn(C, B, out_f, generator=g).to(DEV)
+    coef = torch.rand(C, B, generator=g).to(DEV)
+    cd = torch.tensor([32, 17, 1], dtype=torch.int32, device=DEV)
+    dw1, db1 = torch.zeros(C, out_f, in_f, device=DEV), torch.zeros(C, out_f, device=DEV)
+    dw2, db2 = torch.zeros_like(dw1), torch.zeros_like(db1)
+    ops.linear_wgrad_rowscale(x, dy, coef, dw1, db1, C, B, in_f, out_f, counts=cd)
+    s = ops.scale_rows(dy, coef, torch.empty_like(dy), C, B, out_f, counts=cd)
+    ops.linear_wgrad(x, s, dw2, db2, C, B, in_f, out_f, counts=cd)
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw2) and torch.equal(db1, db2)
