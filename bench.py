@@ -840,7 +840,7 @@ def main():
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 (multi-rank path on a 1-GPU box)")
     ap.add_argument("--lanes", type=int, default=None,
-                    help="concurrent client lanes per GPU (default: planner / FH_LANES)")
+                    help="concurrent client lanes per GPU (default: the lane planner)")
     ap.add_argument("--exact-fedavg", action="store_true",
                     help="N>1: all-gather + sequential FedAvg (bit-exact) instead of all-reduce")
     ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),

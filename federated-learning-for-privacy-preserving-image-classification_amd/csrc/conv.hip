@@ -1124,15 +1124,9 @@ struct Plan {
 
 // FWD/DGRAD: split K only when the output tiling leaves most CUs idle (the
 // latency-bound tail of a round, when few clients are still training).
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return (v && *v) ? atoi(v) : dflt;
-}
-
-static const int kMnSplitBelow = env_int("FH_MN_SPLIT_BELOW", 192);  // sweeps (fc_bench.py)
-// diagnostics / A-B: FH_DGRAD_S2=0 sends stride-2 DGRAD back to the generic igemm
-static const int g_dgrad_s2_off = env_int("FH_DGRAD_S2", 1) == 0;
-static const int kMnTarget = env_int("FH_MN_TARGET", 768);
+constexpr int kMnSplitBelow = 192;  // sweeps (fc_bench.py)
+constexpr bool g_dgrad_s2_off = false;  // (r01 A/B switch, retired: phases always on)
+constexpr int kMnTarget = 768;
 
 static Plan plan_mn(int M, int N, int K, int nclients) {
     Plan p{pick_mn_tile(M, N), 1, K, M, N, K};
@@ -1261,7 +1255,7 @@ pack_dgrad_s2_kernel(const float* __restrict__ w, int64_t w_cs, float* __restric
 static size_t dgrad_s2_pack_bytes(int cin, int cout, int kh, int nclients) {
     return ((size_t)nclients * cin * cout * kh * kh * sizeof(float) + 255) / 256 * 256;
 }
-static const int g_dgrad_s2_pack = env_int("FH_DGRAD_S2_PACK", 1);  // A/B: 0 = gather W
+constexpr int g_dgrad_s2_pack = 1;  // A/B: 0 = gather W
 
 // GEMM per (client, phase): M = cin, N = batch * oh * ow, K <= cout * 4 (3x3) or cout (1x1)
 static Plan plan_dgrad_s2(int cin, int cout, int kh, int batch, int oh, int ow, int nclients) {
@@ -1451,7 +1445,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
 
 // 3x3 / stride 2 / pad 1 forward on square maps with an 8x8 or 16x16 output (ResNet
 // down-sampling blocks, 32->16 and 16->8): dconv_kernel<FWD, W_out, ..., S=2>
-static const int g_dconv_s2_off = env_int("FH_DCONV_S2", 1) == 0;  // A/B: back to igemm
+constexpr bool g_dconv_s2_off = false;  // A/B: back to igemm
 static bool dconv_s2_supported(int h, int w, int kh, int kw, int stride, int pad) {
     return !g_dconv_s2_off && kh == 3 && kw == 3 && stride == 2 && pad == 1 && h == w &&
            (w == 16 || w == 32);
@@ -1459,9 +1453,8 @@ static bool dconv_s2_supported(int h, int w, int kh, int kw, int stride, int pad
 
 // 3x3 / stride 2 / pad 1 DGRAD on square 32->16 and 16->8 maps (ResNet down-sampling blocks):
 // dconv_dgrad_s2_kernel<grid width, CK = 8>, 32 dX channels per workgroup, split over the
-// reduction channels (cout) on small grids; FH_DCONV_DGRAD_S2=0 sends it back to the
-// implicit-GEMM phases (A/B).
-static const int g_dconv_dgrad_s2_off = env_int("FH_DCONV_DGRAD_S2", 1) == 0;
+// reduction channels (cout) on small grids.
+constexpr bool g_dconv_dgrad_s2_off = false;
 static bool dconv_dgrad_s2_supported(int h, int w, int kh, int kw, int stride, int pad, int cin,
                                      int cout) {
     return !g_dconv_dgrad_s2_off && kh == 3 && kw == 3 && stride == 2 && pad == 1 && h == w &&
@@ -1469,8 +1462,8 @@ static bool dconv_dgrad_s2_supported(int h, int w, int kh, int kw, int stride, i
 }
 // split planning (sweeps): target workgroups (two fit a CU) and the fewest reduction channels a
 // split keeps (every split writes a slab the size of dX: few long splits beat many short ones)
-static const int kDs2Fill = env_int("FH_DS2_FILL", 256);
-static const int kDs2MinCh = env_int("FH_DS2_MINCH", 32);
+constexpr int kDs2Fill = 256;
+constexpr int kDs2MinCh = 32;
 static DPlan plan_dconv_dgrad_s2(int cin, int cout, int batch, int oh, int nclients) {
     DPlan p{32, 8, 1, cout};
     const int64_t blocks = ceil_div((int64_t)batch * oh * oh, 256) * ceil_div(cin, 32) * nclients;
@@ -1525,8 +1518,8 @@ static int run_dconv_dgrad_s2(DConvArgs a, int oh, int nclients, void* ws, size_
 }
 
 // 1x1 / stride 2 / pad 0 forward on square 32->16 and 16->8 maps (the ResNet projection
-// shortcut): pw_s2_fwd_kernel<output width, CK = 16>; FH_PW_S2=0: back to the implicit GEMM
-static const int g_pw_s2_off = env_int("FH_PW_S2", 1) == 0;
+// shortcut): pw_s2_fwd_kernel<output width, CK = 16>
+constexpr bool g_pw_s2_off = false;
 static bool pw_s2_supported(int h, int w, int kh, int kw, int stride, int pad, int cin) {
     return !g_pw_s2_off && kh == 1 && kw == 1 && stride == 2 && pad == 0 && h == w &&
            (w == 16 || w == 32) && cin % 16 == 0;
@@ -1583,8 +1576,7 @@ static DWPlan plan_dwgrad_small(int cout, int batch, int w, int nclients) {
 // 3x3 / stride 2 / pad 1 WGRAD on square 32->16 / 16->8 maps (ResNet down-sampling blocks):
 // dconv_wgrad_kernel<output width, WCO = 2, WCI = 1, WPX = 2, 64-pixel stages, S = 2> — 64 x 32
 // (co, ci) tiles, so each staged input patch (2*SEGR+1 rows) feeds twice the MFMAs;
-// FH_DWGRAD_S2=0: back to the implicit GEMM
-static const int g_dwgrad_s2_off = env_int("FH_DWGRAD_S2", 1) == 0;
+constexpr bool g_dwgrad_s2_off = false;
 static bool dwgrad_s2_supported(int cin, int cout, int h, int w, int kh, int kw, int stride,
                                 int pad) {
     return !g_dwgrad_s2_off && kh == 3 && kw == 3 && stride == 2 && pad == 1 && h == w &&
@@ -1604,8 +1596,7 @@ static DWPlan plan_dwgrad_s2(int cout, int cin, int batch, int wo, int nclients)
 }
 
 // single-input-channel 3x3 / s1 / p1 (SimpleCNN conv1): conv_c1_fwd_kernel / conv_c1_wgrad_kernel;
-// FH_CONV_C1=0: back to the implicit GEMM
-static const int g_conv_c1_off = env_int("FH_CONV_C1", 1) == 0;
+constexpr bool g_conv_c1_off = false;
 static bool conv_c1_supported(int cin, int cout, int kh, int kw, int stride, int pad) {
     return !g_conv_c1_off && cin == 1 && kh == 3 && kw == 3 && stride == 1 && pad == 1 &&
            (cout == 32 || cout == 64);
@@ -1615,8 +1606,8 @@ static int conv_c1_chunks(int batch, int h, int w) {
 }
 // conv1 WGRAD on the matrix cores (conv_c1_wgrad_mfma_kernel): 4-row stages, ~kC1MfmaBlocks
 // workgroups (the kernel is HBM-bound: many small workgroups keep loads in flight)
-static const int kC1MfmaBlocks = env_int("FH_C1_MFMA_BLOCKS", 1024);
-static const int kC1MinSps = env_int("FH_C1_MINSPS", 2);  // stages per chunk at least
+constexpr int kC1MfmaBlocks = 1024;
+constexpr int kC1MinSps = 2;  // stages per chunk at least
 static bool conv_c1_mfma_ok(int h, int w) { return h % 4 == 0 && w % 4 == 0 && w <= 32; }
 static DWPlan plan_c1_mfma(int batch, int h, int nclients) {
     const int nst = batch * (h / 4);
@@ -2323,10 +2314,8 @@ extern "C" int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float*
 // clients: 44 us vs 81 for the implicit GEMM, fc2 12 vs 27 (tools/fc_bench.py).  FWD: see
 // linear_fwd_skinny_kernel below (round 3; round 1's attempt at it lost to the implicit GEMM).
 namespace fh {
-static const int kLinearSkinny = env_int("FH_LINEAR_SKINNY", 1);
-// A/B: FH_SKINNY32=0 keeps the skinny WGRAD / fused linear backward to in_f % 128 == 0 (the
-// SimpleCNN fc1 WGRAD then runs on the implicit GEMM)
-static const int kSkinny32 = env_int("FH_SKINNY32", 1);
+constexpr int kLinearSkinny = 1;
+constexpr int kSkinny32 = 1;  // skinny WGRAD / fused backward for in_f % 32 (not only % 128)
 
 __device__ __forceinline__ float f4at(const float4& v, int q) {
     return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;

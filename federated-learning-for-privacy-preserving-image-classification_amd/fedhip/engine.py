@@ -146,9 +146,9 @@ class PackedTrainer:
                                else int(dpsgd.seed)) & 0xFFFFFFFFFFFFFFFF
         self.on_step = None
         self.pre_step = None
-        # split WGRAD reductions finished inside the optimizer launch (ops.GradSlabs);
-        # FH_DEFER_WGRAD=0 restores the separate reduction launches (A/B)
-        self.defer_wgrad_reduce = os.environ.get("FH_DEFER_WGRAD", "1") != "0"
+        # split WGRAD reductions finished inside the optimizer launch (ops.GradSlabs); False
+        # restores the separate reduction launches (tests compare the two bit for bit)
+        self.defer_wgrad_reduce = True
         self._slabs = None
         # Step graphs: every step after the first of a round is replayed from a HIP graph
         # captured once per (active slots, optimizer, lr, data); the per-step inputs (batch

@@ -25,7 +25,6 @@ on MI355X for CIFAR10CNN; at most 4 lanes (GPU_MAX_HW_QUEUES is 4).
 """
 from __future__ import annotations
 
-import ctypes
 import itertools
 import os
 import time
@@ -38,6 +37,8 @@ from .engine import PackedTrainer, SlotStorage, epochs_of, plan_round
 from .net import ParamLayout
 
 MAX_LANES = 3  # torch's own stream + 3 lanes = GPU_MAX_HW_QUEUES (4)
+# diagnostics (the only environment switch of the round path): per-lane GPU / host timelines
+HOST_TIMING = bool(os.environ.get("FH_HOST_TIMING"))
 
 
 def _lane_time(steps: Sequence[int], a: float, b: float) -> float:
@@ -90,12 +91,6 @@ class LanedTrainer:
                  lanes=None, cut=None, salt=0, dpsgd=None):
         self.device = torch.device(device)
         S = len(slot_steps)
-        if lanes is None:
-            env = os.environ.get("FH_LANES")
-            lanes = int(env) if env else None
-        env_cut = os.environ.get("FH_LANE_CUT")  # diagnostics: explicit cut, e.g. "0,1,12,32"
-        if cut is None and env_cut:
-            cut = [int(c) for c in env_cut.split(",")]
         if cut is not None:
             cut = list(cut)
             if cut[0] != 0 or cut[-1] != S or sorted(set(cut)) != cut:
@@ -118,13 +113,11 @@ class LanedTrainer:
         # two clients anywhere in the job share a stream
         for ln in self.lanes:
             ln.net.salt = (ln.net.salt + salt * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
-        self._own_streams = []
         if len(self.lanes) > 1:
             for i, ln in enumerate(self.lanes):
                 ln.stream = self._lane_stream(i)
                 ln.launch_mode = "program"  # csrc/program.hip: +1.3 % over graph replay
-        # split-K fill fraction per lane (ops.set_fill_fraction); FH_LANE_FILL = one value
-        # for every lane or one per lane (diagnostics)
+        # split-K fill fraction per lane (ops.set_fill_fraction)
         self.fill = [1.0] * len(self.lanes)
         if len(self.lanes) > 1:
             # concurrent lanes share the chip, so each plans its split-K for part of it:
@@ -136,57 +129,24 @@ class LanedTrainer:
             widest = max(range(len(sizes)), key=lambda i: (sizes[i], -i))
             for i, n in enumerate(sizes):
                 self.fill[i] = 0.25 if n == 1 else (0.75 if i == widest else 0.5)
-        env_fill = os.environ.get("FH_LANE_FILL")
-        if env_fill and len(self.lanes) > 1:
-            vals = [float(v) for v in env_fill.split(",")]
-            self.fill = vals * len(self.lanes) if len(vals) == 1 else vals
         for name in SlotStorage.FIELDS:
             setattr(self, name, getattr(self.storage, name))
         self.seg_offsets = self.lanes[0].seg_offsets
         self.net = self.lanes[0].net
 
     def _lane_stream(self, i):
-        """HIP stream of lane i.  Diagnostics: FH_LANE_PRIO = per-lane dispatch priorities
-        (e.g. "-1,0,0"); FH_LANE_CU = CUs reserved for lane 0 (the others get the rest),
-        FH_LANE_CU_LAYOUT = "spread" (every k-th mask bit) or "block" (the first bits)."""
-        prio_env = os.environ.get("FH_LANE_PRIO")
-        cu_env = os.environ.get("FH_LANE_CU")
-        if not cu_env:  # torch-owned stream; the long lane 0 dispatches first by default
-            prios = [int(v) for v in prio_env.split(",")] if prio_env else [-1, 0]
-            prio = prios[min(i, len(prios) - 1)]
-            # one stream per (device, lane index, priority) for the whole process: HIP maps
-            # streams to its hardware queues (4 per process) in creation order, so a second
-            # LanedTrainer with fresh streams (the K2 line after KT in one bench process) could
-            # put two of its lanes on one queue and serialise them (K2 1.02M vs 1.46M alone)
-            key = (str(self.device), i, prio)
-            st = _LANE_STREAMS.get(key)
-            if st is None:
-                st = _LANE_STREAMS[key] = torch.cuda.Stream(self.device, priority=prio)
-            return st
-        mask_words = None
-        prio = 0
-        if cu_env:
-            ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-            k = int(cu_env)
-            if os.environ.get("FH_LANE_CU_LAYOUT", "spread") == "block":
-                mine = set(range(k))
-            else:
-                step = ncu / k
-                mine = {int(j * step) for j in range(k)}
-            bits = mine if i == 0 else set(range(ncu)) - mine
-            words = [0] * ((ncu + 31) // 32)
-            for b in bits:
-                words[b // 32] |= 1 << (b % 32)
-            mask_words = (ctypes.c_uint32 * len(words))(*words)
-        if prio_env:
-            vals = [int(v) for v in prio_env.split(",")]
-            prio = vals[i] if i < len(vals) else vals[-1]
-        handle = ctypes.c_void_p()
-        with torch.cuda.device(self.device):
-            ops.call("fh_stream_create", prio, mask_words,
-                     len(mask_words) if mask_words is not None else 0, ctypes.byref(handle))
-        self._own_streams.append(handle.value)
-        return torch.cuda.ExternalStream(handle.value, device=self.device)
+        """HIP stream of lane i: the long lane 0 dispatches first (priority -1, +0.6 %); CU
+        masks and other priorities measured no better (profiles/r03_s4/KT_lane_prio_cu_sweep.txt).
+        One stream per (device, lane index, priority) for the whole process: HIP maps streams
+        to its hardware queues (4 per process) in creation order, so a second LanedTrainer with
+        fresh streams (the K2 line after KT in one bench process) could put two of its lanes on
+        one queue and serialise them (K2 1.02M vs 1.46M alone)."""
+        prio = -1 if i == 0 else 0
+        key = (str(self.device), i, prio)
+        st = _LANE_STREAMS.get(key)
+        if st is None:
+            st = _LANE_STREAMS[key] = torch.cuda.Stream(self.device, priority=prio)
+        return st
 
     def set_client_ids(self, ids):
         """Global client id per slot (PackedTrainer.set_client_ids, lane by lane): Philox
@@ -285,7 +245,7 @@ class LanedTrainer:
                 for j in order:
                     if j != i:
                         self.lanes[j].stream.wait_stream(self.lanes[i].stream)
-            tlog = [] if os.environ.get("FH_HOST_TIMING") else None
+            tlog = [] if HOST_TIMING else None
             for g in range(G):
                 for i in order:
                     ln, st, p = self.lanes[i], states[i], plans[i]
@@ -336,7 +296,7 @@ class LanedTrainer:
         out = []
         for ln, p in zip(self.lanes, plans):
             out += ln.collect_metrics(p, epochs_of(p))
-        if os.environ.get("FH_HOST_TIMING"):
+        if HOST_TIMING:
             import sys
             print(f"start_rounds+issue {1e3 * (t_c - t_r0):.1f} ms, collect (sync) "
                   f"{1e3 * (time.perf_counter() - t_c):.1f} ms", file=sys.stderr)

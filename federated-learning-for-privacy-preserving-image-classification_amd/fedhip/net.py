@@ -129,55 +129,55 @@ class PackedNet:
         self.seed_dev = None  # device uint64 [1] = seed * 1000003 (graph replay)
         self.salt = 0  # per-lane key offset (a lane's slot 0 is not another lane's slot 0)
         self.ids_keyed = False  # set_client_ids: device key blocks carry global client ids
-        # CIFAR10CNN and ResNet training: BN apply + ReLU folded into the consumers (FH_FUSE_BN=0: off)
-        self.fuse_bn = os.environ.get("FH_FUSE_BN", "1") != "0"
+        # CIFAR10CNN and ResNet training: BN apply + ReLU folded into the consumers
+        self.fuse_bn = True
         # ... and the BN statistics taken by the producing conv's epilogue instead of a
-        # second pass over its output (FH_BN_EPILOGUE=0: the separate statistics pass)
-        self.bn_epilogue = os.environ.get("FH_BN_EPILOGUE", "1") != "0"
+        # second pass over its output
+        self.bn_epilogue = True
         self._fused = False
         # training step: the last linear layer, the cross-entropy and that layer's backward
-        # in one launch (fh_linear_head_ce; FH_FUSED_HEAD=0: separate launches)
-        self.fused_head = os.environ.get("FH_FUSED_HEAD", "1") != "0"
-        # the BN finalize of a pooled layer inside the max-pool launch (FH_POOL_FINALIZE=0: off)
-        self.pool_finalize = os.environ.get("FH_POOL_FINALIZE", "1") != "0"
+        # in one launch (fh_linear_head_ce)
+        self.fused_head = True
+        # the BN finalize of a pooled layer inside the max-pool launch
+        self.pool_finalize = True
         # classifier backward: wgrad + dgrad + dropout/ReLU backward in one launch where
-        # the layer shape allows (fh_linear_bwd_fused; FH_FUSED_LINEAR_BWD=0: off)
-        self.fused_linear_bwd = os.environ.get("FH_FUSED_LINEAR_BWD", "1") != "0"
+        # the layer shape allows (fh_linear_bwd_fused)
+        self.fused_linear_bwd = True
         self._head_done = False
         self._head = True
         # SimpleCNN: the 14x14 conv runs on 16x16 planes (the map in the top-left corner,
         # a zero ring around it) so the direct 3x3 kernels take it instead of the implicit
-        # GEMM; the max-pools read / write the embedded maps (FH_PAD_MAPS=0: dense 14x14)
-        self.pad_maps = os.environ.get("FH_PAD_MAPS", "1") != "0"
-        # classifier dropout in the linear layer's forward epilogue (FH_FUSED_DROPOUT=0: its
-        # own launch); the pre-dropout ReLU output is then never written — every backward
-        # decides the ReLU on the dropped output (equal wherever the keep-mask is 1)
-        self.fused_dropout = os.environ.get("FH_FUSED_DROPOUT", "1") != "0"
+        # GEMM; the max-pools read / write the embedded maps
+        self.pad_maps = True
+        # classifier dropout in the linear layer's forward epilogue; the pre-dropout ReLU
+        # output is then never written — every backward decides the ReLU on the dropped
+        # output (equal wherever the keep-mask is 1)
+        self.fused_dropout = True
         # CIFAR10CNN backward: the ReLU mask and the BN backward statistics of bn1/bn3/bn5
         # taken in the epilogue of the next conv's dgrad (fh_conv2d_dgrad_bnstats), so the BN
-        # backward is its apply pass only (FH_BN_BWD_EPILOGUE=0: reduce + apply)
-        self.bn_bwd_epilogue = os.environ.get("FH_BN_BWD_EPILOGUE", "1") != "0"
+        # backward is its apply pass only
+        self.bn_bwd_epilogue = True
         # ResNet down-sampling blocks: conv1's and the projection shortcut's input gradients
-        # in one direct stride-2 launch (fh_conv2d_dgrad_s2_shortcut; FH_FUSED_SHORTCUT=0: two)
-        self.fused_shortcut = os.environ.get("FH_FUSED_SHORTCUT", "1") != "0"
+        # in one direct stride-2 launch (fh_conv2d_dgrad_s2_shortcut)
+        self.fused_shortcut = True
         # SimpleCNN training: conv1 -> ReLU -> pool1 in one launch (fh_conv2d_c1_pool_fwd; the
         # full-resolution conv1 output is never written) and pool1's backward masked by the
         # pooled output (maxpool2_bwd_ymask): bit-identical, K2 +3.5 % (interleaved x3,
-        # profiles/r02_c1/K2_fuse_pool1_fwd_ab.txt).  FH_FUSE_POOL1=0: two launches.
-        # (DP-SGD's per-sample passes read the full-resolution maps: off there.)
-        self.fuse_pool1 = os.environ.get("FH_FUSE_POOL1", "1") != "0"
+        # profiles/r02_c1/K2_fuse_pool1_fwd_ab.txt).  DP-SGD takes conv1's per-image slabs from
+        # pool1's gradient as well (r04).
+        self.fuse_pool1 = True
         # ... and its backward half: conv1's weight gradient straight from pool1's gradient
         # (fh_conv2d_c1_pool_wgrad; the 100 KB-per-image full-resolution gradient is never
         # written or read).  r03: on the matrix-core conv1 WGRAD (two pooled values, two
         # argmax bytes per staged quad) K2 1.362M -> 1.418 / 1.423M client-images/s,
-        # interleaved (profiles/r03_k2/; r02's VALU form lost 7 %).  FH_FUSE_POOL1_BWD=0: off.
-        self.fuse_pool1_bwd = os.environ.get("FH_FUSE_POOL1_BWD", "1") != "0"
+        # interleaved (profiles/r03_k2/; r02's VALU form lost 7 %).
+        self.fuse_pool1_bwd = True
         # SimpleCNN: pool2's backward inside fc1's fused backward (fh_linear_bwd_fused_pool,
         # bit-identical, tests/test_classifier_gpu.py).  Measured neutral on K2 (10-round
         # rounds, interleaved x3: 1.382M on vs 1.402M off, within the K2 spread;
         # profiles/r03_k2/K2_fuse_pool2_bwd_ab.txt): the skinny DGRAD epilogue's routed
-        # window stores cost what the maxpool2_bwd pass did.  Off unless FH_FUSE_POOL2_BWD=1.
-        self.fuse_pool2_bwd = os.environ.get("FH_FUSE_POOL2_BWD", "0") == "1"
+        # window stores cost what the maxpool2_bwd pass did.  Off.
+        self.fuse_pool2_bwd = False
         self._pool1_fused = False
 
     # -------------------------------------------------------------- helpers

@@ -311,16 +311,13 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
     return dx
 
 
-_DCONV_DGRAD_S2 = os.environ.get("FH_DCONV_DGRAD_S2", "1") != "0"
-
-
 def conv2d_dgrad_s2_shortcut(dy, w, dy_sc, w_sc, dx, nclients, batch, cin, h, wd, cout,
                              counts=None, accumulate=False):
     """A ResNet down-sampling block's input gradient in one launch: conv2d_dgrad(dy, w)
     (3x3/s2/p1) + conv2d_dgrad(dy_sc, w_sc) (the 1x1/s2 projection shortcut)
     (fh_conv2d_dgrad_s2_shortcut).  Returns False (nothing issued) outside the direct
     stride-2 kernel; the caller then issues the two dgrads."""
-    if not (_DCONV_DGRAD_S2 and h == wd and h in (16, 32) and cin % 32 == 0 and cout % 8 == 0
+    if not (h == wd and h in (16, 32) and cin % 32 == 0 and cout % 8 == 0
             and w.data_ptr() % 16 == 0 and w.stride(0) % 4 == 0 and dx.data_ptr() % 8 == 0
             and dx.stride(0) % 2 == 0 and dy_sc.data_ptr() % 16 == 0
             and dy_sc.stride(0) % 4 == 0):
@@ -570,7 +567,7 @@ def linear_wgrad(x, dy, dw, db, nclients, batch, in_f, out_f, counts=None):
 
 
 # ------------------------------------------------------------------ DP-SGD (per-sample clip)
-_SKINNY_IN = 32 if os.environ.get("FH_SKINNY32", "1") != "0" else 128
+_SKINNY_IN = 32
 
 
 def linear_bwd_fused(x, dy, w, dw, db, dx, nclients, batch, in_f, out_f, mask=None, p_drop=0.0,

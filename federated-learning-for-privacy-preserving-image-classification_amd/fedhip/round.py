@@ -32,10 +32,8 @@ import torch
 import torch.distributed as dist
 
 from . import ops
+from .lanes import HOST_TIMING as _HOST_TIMING  # diagnostics: per-round host split
 from .lanes import LanedTrainer
-
-
-_HOST_TIMING = bool(os.environ.get("FH_HOST_TIMING"))  # diagnostics: per-round host split
 
 
 @dataclass
