@@ -3149,6 +3149,105 @@ extern "C" int fh_conv2d_c1_pool_wgrad_persample(const float* x, int64_t x_cs, c
     return FH_OK;
 }
 
+namespace fh {
+constexpr int kNormSrcMax = 4;
+struct NormSrcs {
+    fh_linear_norm_src lin[kNormSrcMax];
+    int nlin;
+    const float* sw[kNormSrcMax];  // slab weights [z][i][per_w]
+    const float* sb[kNormSrcMax];  // slab bias [z][i][per_b] (nullable)
+    int per_w[kNormSrcMax], per_b[kNormSrcMax];
+    int nslab;
+};
+
+// One workgroup per (image, client): the image's squared gradient norm over every layer —
+// linear layers by the rank-1 identity ||dy_i||^2 (||x_i||^2 + bias), conv layers as the sum
+// of squares of the image's slab rows — in fp64, then its clip coefficient (clip_coef_kernel's
+// arithmetic).  Replaces the zero fill, the per-layer norm launches and the coefficient launch.
+__global__ void __launch_bounds__(256)
+dpsgd_norm_clip_kernel(const NormSrcs src, const int32_t* __restrict__ counts, int batch,
+                       double max_norm, double* __restrict__ sqnorm, float* __restrict__ coef) {
+    __shared__ double red[4];
+    const int i = blockIdx.x, z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    const int64_t row = (int64_t)z * batch + i;
+    if (i >= cnt) {  // block-uniform
+        if (threadIdx.x == 0) {
+            coef[row] = 0.f;
+            if (sqnorm) sqnorm[row] = 0.0;
+        }
+        return;
+    }
+    double total = 0.0;
+    for (int l = 0; l < src.nlin; ++l) {
+        const fh_linear_norm_src& L = src.lin[l];
+        const float* xr = L.x + z * L.x_cs + (int64_t)i * L.in_f;
+        const float* dr = L.dy + z * L.dy_cs + (int64_t)i * L.out_f;
+        double sx = 0.0, sd = 0.0;
+        for (int k = threadIdx.x; k < L.in_f; k += 256) sx += (double)xr[k] * (double)xr[k];
+        for (int k = threadIdx.x; k < L.out_f; k += 256) sd += (double)dr[k] * (double)dr[k];
+        sx = block_sum_256(sx, red);
+        sd = block_sum_256(sd, red);
+        total += sd * (sx + (L.with_bias ? 1.0 : 0.0));
+    }
+    for (int l = 0; l < src.nslab; ++l) {
+        const float4* w4 = reinterpret_cast<const float4*>(src.sw[l] + row * src.per_w[l]);
+        double sq = 0.0;
+        for (int q = threadIdx.x; q < src.per_w[l] / 4; q += 256) {
+            const float4 v = w4[q];
+            sq += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+        }
+        if (src.sb[l])
+            for (int q = threadIdx.x; q < src.per_b[l]; q += 256) {
+                const double v = src.sb[l][row * src.per_b[l] + q];
+                sq += v * v;
+            }
+        total += block_sum_256(sq, red);
+    }
+    if (threadIdx.x == 0) {
+        if (sqnorm) sqnorm[row] = total;
+        // ||g_i|| = B * ||g_i / B||  (the stored gradients are of the batch-mean loss)
+        const double norm = (double)cnt * sqrt(total);
+        coef[row] = norm > max_norm ? (float)(max_norm / norm) : 1.0f;
+    }
+}
+}  // namespace fh
+
+extern "C" int fh_dpsgd_norm_clip(const fh_linear_norm_src* lin, int32_t nlin,
+                                  const fh_slab_norm_src* slabs, int32_t nslab,
+                                  const int32_t* counts, int32_t nclients, int32_t batch,
+                                  double max_norm, double* sqnorm, float* coef, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && nlin >= 0 && nlin <= kNormSrcMax && nslab >= 0 &&
+                   nslab <= kNormSrcMax, "dpsgd_norm_clip: bad shape (%d linear, %d slab sources)",
+               nlin, nslab);
+    FH_REQUIRE(max_norm > 0.0, "dpsgd_norm_clip: max_norm must be > 0");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(coef && (nlin == 0 || lin) && (nslab == 0 || slabs), "dpsgd_norm_clip: null pointer");
+    NormSrcs s{};
+    s.nlin = nlin;
+    for (int l = 0; l < nlin; ++l) {
+        FH_REQUIRE(lin[l].x && lin[l].dy && lin[l].in_f > 0 && lin[l].out_f > 0,
+                   "dpsgd_norm_clip: bad linear source %d", l);
+        s.lin[l] = lin[l];
+    }
+    s.nslab = nslab;
+    for (int l = 0; l < nslab; ++l) {
+        FH_REQUIRE(slabs[l].slab && slabs[l].per_w > 0 && slabs[l].per_w % 4 == 0 &&
+                       slabs[l].per_b >= 0 && (uintptr_t)slabs[l].slab % 16 == 0,
+                   "dpsgd_norm_clip: bad slab source %d", l);
+        s.sw[l] = (const float*)slabs[l].slab;
+        s.sb[l] = slabs[l].per_b ? (const float*)((const char*)slabs[l].slab +
+                                                  wslab_bias_off(nclients, batch, slabs[l].per_w))
+                                 : nullptr;
+        s.per_w[l] = slabs[l].per_w;
+        s.per_b[l] = slabs[l].per_b;
+    }
+    FH_LAUNCH(dpsgd_norm_clip_kernel, dim3((unsigned)batch, (unsigned)nclients), dim3(256), 0,
+              as_stream(stream), s, counts, batch, max_norm, sqnorm, coef);
+    FH_LAUNCH_CHECK("dpsgd_norm_clip");
+    return FH_OK;
+}
+
 extern "C" int fh_persample_slab_sqnorm(const void* slab, int32_t per_w, int32_t per_b,
                                         const int32_t* counts, int32_t nclients, int32_t batch,
                                         double* sqnorm, void* stream) {

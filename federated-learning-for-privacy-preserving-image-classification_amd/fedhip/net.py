@@ -384,9 +384,7 @@ class PackedNet:
         if getattr(self, "_ps", None) is None:
             self._ps = (ops.PersampleSlab(self.device), ops.PersampleSlab(self.device))
         s1, s2 = self._ps
-        sqnorm[:n].zero_()
-        # pass 1: dgrad chain + per-sample norms
-        ops.linear_persample_sqnorm(self._fc_in, self.dlogits, sqnorm, n, B, 128, K, counts=cnt)
+        # pass 1: the dgrad chain and the conv layers' per-image slabs
         dd1 = A("dd1", 128)
         ops.linear_dgrad(self.dlogits, W(P_, "fc2.weight"), dd1, n, B, 128, K, counts=cnt)
         dh1 = A("dh1", 128)
@@ -394,21 +392,20 @@ class PackedNet:
         ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
                         relu_out=self._fc_in, counts=cnt)
         p2 = A("p2", 64, 7, 7)
-        ops.linear_persample_sqnorm(p2, dh1, sqnorm, n, B, 3136, 128, counts=cnt)
         dp2 = A("dp2", 64, 7, 7)
         ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
         i2 = A("i2", 64, 7, 7, dtype=torch.uint8)
         ops.maxpool2_bwd(dp2, i2, da2, n, B, 64, 14, 14, xin=a2, counts=cnt)
         ops.conv2d_wgrad_persample(p1, da2, s2, n, B, 32, hp, hp, 64, counts=cnt)
-        ops.slab_sqnorm(s2, sqnorm, counts=cnt)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt)
         # conv1's per-image slabs from pool1's gradient (the pooled ReLU output p1 > 0 is the
         # mask at each window's argmax, whether or not conv1's output was written)
         ops.conv2d_c1_pool_wgrad_persample(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8),
                                            p1, s1, n, B, 28, 28, 32, counts=cnt)
-        ops.slab_sqnorm(s1, sqnorm, counts=cnt)
-        ops.dpsgd_clip_coef(sqnorm, coef, n, B, max_norm, counts=cnt)
+        # every image's norm over all four layers and its clip coefficient: one launch
+        ops.dpsgd_norm_clip([(self._fc_in, self.dlogits, 128, K), (p2, dh1, 3136, 128)],
+                            [s2, s1], coef, n, B, max_norm, sqnorm=sqnorm, counts=cnt)
         # pass 2: the linear layers' clipped sums (dY rows scaled by c_i as they are loaded)
         ops.linear_wgrad_rowscale(self._fc_in, self.dlogits, coef, W(G, "fc2.weight"),
                                   W(G, "fc2.bias"), n, B, 128, K, counts=cnt)

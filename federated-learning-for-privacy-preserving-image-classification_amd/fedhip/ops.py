@@ -726,6 +726,35 @@ def linear_wgrad_rowscale(x, dy, rowscale, dw, db, nclients, batch, in_f, out_f,
               _linear_bytes(nclients, batch, in_f, out_f), nclients)
 
 
+class FhLinearNormSrc(ctypes.Structure):
+    """include/fedhip.h fh_linear_norm_src."""
+    _fields_ = [("x", ctypes.c_void_p), ("x_cs", ctypes.c_int64), ("dy", ctypes.c_void_p),
+                ("dy_cs", ctypes.c_int64), ("in_f", ctypes.c_int32), ("out_f", ctypes.c_int32),
+                ("with_bias", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class FhSlabNormSrc(ctypes.Structure):
+    """include/fedhip.h fh_slab_norm_src."""
+    _fields_ = [("slab", ctypes.c_void_p), ("per_w", ctypes.c_int32), ("per_b", ctypes.c_int32)]
+
+
+def dpsgd_norm_clip(linear, slabs, coef, nclients, batch, max_norm, sqnorm=None, counts=None):
+    """fh_dpsgd_norm_clip: every image's squared gradient norm over the linear sources
+    [(x, dy, in_f, out_f)] (rank-1 identity, with bias) and the PersampleSlab sources, and its
+    clip coefficient, in one launch."""
+    la = (FhLinearNormSrc * max(1, len(linear)))()
+    for i, (x, dy, fi, fo) in enumerate(linear):
+        la[i].x, la[i].x_cs, la[i].dy, la[i].dy_cs = ptr(x), _cs(x), ptr(dy), _cs(dy)
+        la[i].in_f, la[i].out_f, la[i].with_bias = fi, fo, 1
+    sa = (FhSlabNormSrc * max(1, len(slabs)))()
+    for i, s in enumerate(slabs):
+        sa[i].slab, sa[i].per_w, sa[i].per_b = s.buf.data_ptr(), s.per_w, s.per_b
+    ev = PROBE.begin("dpsgd_norm_clip")
+    call("fh_dpsgd_norm_clip", la, len(linear), sa, len(slabs), _counts(counts), nclients, batch,
+         float(max_norm), ptr(sqnorm), ptr(coef), stream_handle())
+    PROBE.end(ev, 0.0, 0.0, nclients)
+
+
 def dpsgd_clip_coef(sqnorm, coef, nclients, batch, max_norm, counts=None):
     call("fh_dpsgd_clip_coef", ptr(sqnorm), _counts(counts), nclients, batch, float(max_norm),
          ptr(coef), stream_handle())

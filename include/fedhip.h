@@ -143,6 +143,29 @@ int fh_adam_step_slabs(float* param, float* grad, float* exp_avg, float* exp_avg
  * stored and the update applied — the bits of fh_persample_slab_wsum + fh_dpsgd_noise + the
  * optimizer step in one launch.  SGD uses lr / momentum / weight_decay / first_step, Adam lr /
  * beta1 / beta2 / eps / weight_decay / step_size / bc2_sqrt / scal_dev as fh_adam_step. */
+/* DP-SGD clip coefficients in one launch (r04): for every (client, image < count) the squared
+ * norm of that image's gradient over all layers — linear sources by the rank-1 identity
+ * ||dy_i||^2 (||x_i||^2 + with_bias) (x [client][batch][in_f], dy [client][batch][out_f]),
+ * slab sources (fh_conv2d_wgrad_persample slabs: weights [client][image][per_w], bias behind
+ * them at the 256-B aligned offset) as the sum of squares of the image's rows — in fp64, then
+ * coef = min(1, max_norm / (count * sqrt(sum))) (the stored gradients are of the batch-mean
+ * loss); images >= count get coef 0.  sqnorm (nullable, fp64 [client][batch]) receives the sums.
+ * At most 4 sources of each kind.  Replaces fh_linear_persample_sqnorm / fh_persample_slab_sqnorm
+ * per layer + fh_dpsgd_clip_coef. */
+typedef struct {
+    const float* x;
+    int64_t x_cs;
+    const float* dy;
+    int64_t dy_cs;
+    int32_t in_f, out_f, with_bias, reserved;
+} fh_linear_norm_src;
+typedef struct {
+    const void* slab;
+    int32_t per_w, per_b;
+} fh_slab_norm_src;
+int fh_dpsgd_norm_clip(const fh_linear_norm_src* lin, int32_t nlin, const fh_slab_norm_src* slabs,
+                       int32_t nslab, const int32_t* counts, int32_t nclients, int32_t batch,
+                       double max_norm, double* sqnorm, float* coef, void* stream);
 /* fh_linear_wgrad on row-scaled dY: dy row b of client z multiplied by rowscale[z][b] as it is
  * loaded (the products fh_scale_rows would store: same bits as scale_rows + linear_wgrad);
  * DP-SGD's clipped linear-layer sums.  batch <= 32, in_f % 32 == 0. */

@@ -275,3 +275,38 @@ def test_linear_wgrad_rowscale_bit_identical(in_f, out_f):
     ops.linear_wgrad(x, s, dw2, db2, C, B, in_f, out_f, counts=cd)
     torch.cuda.synchronize()
     assert torch.equal(dw1, dw2) and torch.equal(db1, db2)
+
+
+def test_dpsgd_norm_clip_matches_per_layer_path():
+    """fh_dpsgd_norm_clip (r04: every image's norm over linear + slab sources and its clip
+    coefficient in one launch) == the per-layer norm launches + fh_dpsgd_clip_coef (fp64 sums
+    in another order: equal to 1e-12 relative; coefficients to fp32 rounding)."""
+    from fedhip import ops
+    C, B = 3, 12
+    g = torch.Generator().manual_seed(8)
+    cd = torch.tensor([12, 7, 1], dtype=torch.int32, device=DEV)
+    x1, d1 = torch.randn(C, B, 128, generator=g).to(DEV), torch.randn(C, B, 10, generator=g).to(DEV)
+    x2, d2 = torch.randn(C, B, 3136, generator=g).to(DEV), torch.randn(C, B, 128, generator=g).to(DEV)
+    s2 = ops.PersampleSlab(DEV)
+    ops.conv2d_wgrad_persample(torch.randn(C, B, 32, 16, 16, generator=g).to(DEV),
+                               torch.randn(C, B, 64, 16, 16, generator=g).to(DEV) * 1e-3, s2, C, B,
+                               32, 16, 16, 64, counts=cd)
+    sq_b = torch.zeros(C, B, dtype=torch.float64, device=DEV)
+    coef_b = torch.zeros(C, B, device=DEV)
+    ops.linear_persample_sqnorm(x1, d1, sq_b, C, B, 128, 10, counts=cd)
+    ops.linear_persample_sqnorm(x2, d2, sq_b, C, B, 3136, 128, counts=cd)
+    ops.slab_sqnorm(s2, sq_b, counts=cd)
+    norms = torch.cat([cd[z].item() * sq_b[z, :int(cd[z])].sqrt() for z in range(C)])
+    max_norm = float(norms.median())  # some images clipped, some not
+    ops.dpsgd_clip_coef(sq_b, coef_b, C, B, max_norm, counts=cd)
+    sq_a = torch.zeros(C, B, dtype=torch.float64, device=DEV)
+    coef_a = torch.zeros(C, B, device=DEV)
+    ops.dpsgd_norm_clip([(x1, d1, 128, 10), (x2, d2, 3136, 128)], [s2], coef_a, C, B, max_norm,
+                        sqnorm=sq_a, counts=cd)
+    torch.cuda.synchronize()
+    for z in range(C):
+        n = int(cd[z])
+        torch.testing.assert_close(sq_a[z, :n], sq_b[z, :n], rtol=1e-12, atol=0)
+        torch.testing.assert_close(coef_a[z, :n], coef_b[z, :n], rtol=2e-7, atol=0)
+        assert torch.all(coef_a[z, n:] == 0)
+    assert (coef_a < 1).any() and (coef_a == 1).any()  # both branches of the clip exercised
