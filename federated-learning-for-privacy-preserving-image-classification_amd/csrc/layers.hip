@@ -481,8 +481,9 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         }
     }
     const int S = gridDim.x;
-    // 3. weight gradient, this block's share: dW[k][f] = sum_b D[b][k] x[b][f]
-    {
+    // 3. weight gradient, this block's share: dW[k][f] = sum_b D[b][k] x[b][f] (dw null: the
+    // caller takes it elsewhere — DP-SGD clips it per image first)
+    if (dw) {
         const int per = (K * F + S - 1) / S, e0 = part * per, e1 = min(K * F, e0 + per);
         for (int e = e0 + tid; e < e1; e += 256) {
             const int k = e / F, f = e - k * F;
@@ -872,7 +873,8 @@ extern "C" int fh_linear_head_ce(const float* x, int64_t x_cs, const float* w, i
                in_f);
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "linear_head_ce: p=%g", p_drop);
     if (nclients == 0) return FH_OK;
-    FH_REQUIRE(x && w && targets && logits && dlogits && dw, "linear_head_ce: null pointer");
+    FH_REQUIRE(x && w && targets && logits && dlogits && (dw || !db),
+               "linear_head_ce: null pointer");
     const dim3 grid(kHeadBlocks, nclients);
     const float scale = 1.0f / (1.0f - p_drop);
     if (num_classes <= 16 && in_f <= 256)

@@ -262,9 +262,15 @@ class PackedTrainer:
             net.head_ce(self.params, self.grads, n, counts, **ce)
             self._backward_and_update(n, counts, first, adam_dev)
             return
-        net.forward(self.params, self.bufs, n, counts, train=True)
-        ops.ce_fwd_bwd(net.logits, net.y, net.dlogits, n, self.batch, net.num_classes,
-                       counts=counts, **ce)
+        if self.dpsgd is not None and net.fused_head and self.batch <= 32 and \
+                net.num_classes <= 16:
+            # the head without its weight gradient (clipped per image below)
+            net.forward(self.params, self.bufs, n, counts, train=True, head=False)
+            net.head_ce(self.params, self.grads, n, counts, wgrad=False, **ce)
+        else:
+            net.forward(self.params, self.bufs, n, counts, train=True)
+            ops.ce_fwd_bwd(net.logits, net.y, net.dlogits, n, self.batch, net.num_classes,
+                           counts=counts, **ce)
         if self.dpsgd is None:
             self._backward_and_update(n, counts, first, adam_dev)
             return

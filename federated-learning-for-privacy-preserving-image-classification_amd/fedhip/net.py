@@ -226,9 +226,10 @@ class PackedNet:
             self._fwd_resnet(params, bufs, n, counts, train)
         return self.logits
 
-    def head_ce(self, params, grads, n, counts, **ce):
+    def head_ce(self, params, grads, n, counts, wgrad=True, **ce):
         """Last linear layer + cross-entropy + its backward + the dropout/ReLU backward of
-        its input, one launch (after forward(head=False)); ce: ce_fwd_bwd's outputs."""
+        its input, one launch (after forward(head=False)); ce: ce_fwd_bwd's outputs.
+        wgrad=False: that layer's weight gradient is left out (DP-SGD clips it per image)."""
         self._head_done = True
         if n == 0:
             return
@@ -246,8 +247,8 @@ class PackedNet:
             x, F, wname, dx = A("feat", 256), 256, "fc", A("dfeat", 256)
             mask, relu = None, False
         ops.linear_head_ce(x, W(P_, f"{wname}.weight"), W(P_, f"{wname}.bias"), self.y,
-                           self.logits, self.dlogits, W(G, f"{wname}.weight"),
-                           W(G, f"{wname}.bias"), dx, n, B, F, K, mask=mask,
+                           self.logits, self.dlogits, W(G, f"{wname}.weight") if wgrad else None,
+                           W(G, f"{wname}.bias") if wgrad else None, dx, n, B, F, K, mask=mask,
                            p_drop=self.dropout_p, relu_in=relu, counts=counts, **ce)
 
     def backward(self, params, grads, n, counts):
@@ -384,13 +385,16 @@ class PackedNet:
         if getattr(self, "_ps", None) is None:
             self._ps = (ops.PersampleSlab(self.device), ops.PersampleSlab(self.device))
         s1, s2 = self._ps
-        # pass 1: the dgrad chain and the conv layers' per-image slabs
-        dd1 = A("dd1", 128)
-        ops.linear_dgrad(self.dlogits, W(P_, "fc2.weight"), dd1, n, B, 128, K, counts=cnt)
+        # pass 1: the dgrad chain and the conv layers' per-image slabs (the head launch already
+        # left dlogits and dh1, head_ce(wgrad=False))
         dh1 = A("dh1", 128)
-        mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
-        ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
-                        relu_out=self._fc_in, counts=cnt)
+        if not self._head_done:
+            dd1 = A("dd1", 128)
+            ops.linear_dgrad(self.dlogits, W(P_, "fc2.weight"), dd1, n, B, 128, K, counts=cnt)
+            mask = A("m1", 128, dtype=torch.uint8) if self._fc_in is not A("h1", 128) else None
+            ops.dropout_bwd(dd1, dh1, n, B, 128, mask=mask, p_drop=self.dropout_p,
+                            relu_out=self._fc_in, counts=cnt)
+        self._head_done = False
         p2 = A("p2", 64, 7, 7)
         dp2 = A("dp2", 64, 7, 7)
         ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)

@@ -72,7 +72,11 @@ def main():
     ap.add_argument("--clients", default="32,8,1")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--fill", type=float, default=1.0, help="split-K planner fill fraction")
+    ap.add_argument("--lib", default=None, help="A/B: load this libfedhip.so instead")
     a = ap.parse_args()
+    if a.lib:
+        from fedhip import _lib
+        _lib.load(a.lib)
     ops.set_fill_fraction(a.fill)
     for sh in a.shapes or DEFAULT:
         op, cin, hw, cout, k, s = sh.split(":")
