@@ -331,58 +331,30 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
             // ds_read immediate, and operands are double-buffered in registers: item j+1
             // is read while item j's MFMAs issue.
             constexpr int NI = 3 * (CK / 2);
-            // BATCH (r04): every operand of a kh row is read into registers before its MFMAs
-            // (36 floats at BM = 32), so a kh pays one LDS latency; the per-item register
-            // double buffer it replaces was re-scheduled by the compiler into ~8 exposed
-            // lgkmcnt(0) waits per kh.  Wide tiles (BM = 64: 60 operand floats at 252
-            // VGPRs) keep the per-item fetch.
-            constexpr bool BATCH = NI * (FM + FN) <= 40;
 #pragma unroll 1
             for (int kh = 0; kh < 3; ++kh) {
                 const float* Ab = &As[buf][a_lane + kh * 3 * CK * BMP];
                 const float* Pb = &Ps[buf][kh * PW];
-                if constexpr (BATCH) {
-                    float av[NI][FM], bv[NI][FN];
+                float av[2][FM], bv[2][FN];
+                auto fetch = [&](int j, int slot) {
+                    const int kw = j / (CK / 2), cp = j % (CK / 2);
 #pragma unroll
-                    for (int j = 0; j < NI; ++j) {
-                        const int kw = j / (CK / 2), cp = j % (CK / 2);
+                    for (int i = 0; i < FM; ++i)
+                        av[slot][i] = Ab[(kw * CK + 2 * cp) * BMP + i * 32];
 #pragma unroll
-                        for (int i = 0; i < FM; ++i)
-                            av[j][i] = Ab[(kw * CK + 2 * cp) * BMP + i * 32];
+                    for (int jj = 0; jj < FN; ++jj)
+                        bv[slot][jj] = Pb[b_lane[jj] + 2 * cp * CSTR + kw];
+                };
+                fetch(0, 0);
 #pragma unroll
-                        for (int jj = 0; jj < FN; ++jj)
-                            bv[j][jj] = Pb[b_lane[jj] + 2 * cp * CSTR + kw];
-                    }
+                for (int j = 0; j < NI; ++j) {
+                    if (j + 1 < NI) fetch(j + 1, (j + 1) & 1);
 #pragma unroll
-                    for (int j = 0; j < NI; ++j)
-#pragma unroll
-                        for (int i = 0; i < FM; ++i)
-#pragma unroll
-                            for (int jj = 0; jj < FN; ++jj)
-                                acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                                    av[j][i], bv[j][jj], acc[i][jj], 0, 0, 0);
-                } else {
-                    float av[2][FM], bv[2][FN];
-                    auto fetch = [&](int j, int slot) {
-                        const int kw = j / (CK / 2), cp = j % (CK / 2);
-#pragma unroll
-                        for (int i = 0; i < FM; ++i)
-                            av[slot][i] = Ab[(kw * CK + 2 * cp) * BMP + i * 32];
+                    for (int i = 0; i < FM; ++i)
 #pragma unroll
                         for (int jj = 0; jj < FN; ++jj)
-                            bv[slot][jj] = Pb[b_lane[jj] + 2 * cp * CSTR + kw];
-                    };
-                    fetch(0, 0);
-#pragma unroll
-                    for (int j = 0; j < NI; ++j) {
-                        if (j + 1 < NI) fetch(j + 1, (j + 1) & 1);
-#pragma unroll
-                        for (int i = 0; i < FM; ++i)
-#pragma unroll
-                            for (int jj = 0; jj < FN; ++jj)
-                                acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                                    av[j & 1][i], bv[j & 1][jj], acc[i][jj], 0, 0, 0);
-                    }
+                            acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                                av[j & 1][i], bv[j & 1][jj], acc[i][jj], 0, 0, 0);
                 }
             }
             if (more) store(buf ^ 1, c0 + CK);
