@@ -2456,12 +2456,15 @@ __device__ __forceinline__ void linear_wgrad_skinny_body(
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // row scales: lane l holds row l's (one coalesced load), image b's comes by a lane shuffle
+    const float rs_l = (rowscale && r32 < cnt) ? rowscale[(int64_t)z * batch + r32] : 1.f;
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
         const int b = 2 * p + h;
         const bool ok = b < cnt;
         float av = ok && mok ? yz[(int64_t)b * M] : 0.f;
-        if (rowscale && ok) av = rowscale[(int64_t)z * batch + b] * av;
+        const float rsb = __shfl(rs_l, b, 64);
+        if (rowscale && ok) av = rsb * av;
         const float bv = ok ? xz[(int64_t)b * K] : 0.f;
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
     }
