@@ -1,5 +1,5 @@
 """HBM traffic of the bench's own launches (r03): rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE
-passes (separate runs, tools/r03_pmc_crash.sh <tag> [--counter WRITE_SIZE]) of
+passes (separate runs, tools/evidence.sh stage m) of
 `bench.py --steps 1 --warmup 1 --no-instances --no-k2` (KT: the warmup and the timed round,
 lanes and step programs as timed), per launch SHAPE of bench.py's instrumented table:
 
@@ -10,7 +10,7 @@ summed over the shape's conv kernel and the split-K reduction dispatched right a
 same queue (a launch shape = one fedhip.ops call = kernel + reduction).  Shapes are recognised
 by kernel template (dwgrad_q_kernel<W,...>, dconv_kernel<OP, W, ...>) and, where two layers
 share a template (KT conv3 / conv4 at 16x16, conv5 / conv6 at 8x8), by their order inside
-a step (the backward issues the deeper layer first).  Average bytes per launch = the same
+a step (the forward issues the shallower layer first, the backward the deeper one).  Average bytes per launch = the same
 averaging as roofline.achieved (all launches of the shape).
 
 usage: python tools/bench_traffic.py <fetch_dir> <write_dir> <out.json>"""
@@ -50,7 +50,11 @@ def shape_of(name):
 KT = {("wgrad", 32, 0): "conv_wgrad:c32x32x32->32k3s1",
       ("wgrad", 16, 0): "conv_wgrad:c64x16x16->64k3s1", ("wgrad", 16, 1): "conv_wgrad:c32x16x16->64k3s1",
       ("wgrad", 8, 0): "conv_wgrad:c128x8x8->128k3s1", ("wgrad", 8, 1): "conv_wgrad:c64x8x8->128k3s1",
-      ("fwd", 32, 0): "conv_fwd:c32x32x32->32k3s1", ("dgrad", 32, 0): "conv_dgrad:c32x32x32->32k3s1"}
+      ("fwd", 32, 0): "conv_fwd:c32x32x32->32k3s1", ("dgrad", 32, 0): "conv_dgrad:c32x32x32->32k3s1",
+      ("fwd", 16, 0): "conv_fwd:c32x16x16->64k3s1", ("fwd", 16, 1): "conv_fwd:c64x16x16->64k3s1",
+      ("fwd", 8, 0): "conv_fwd:c64x8x8->128k3s1", ("fwd", 8, 1): "conv_fwd:c128x8x8->128k3s1",
+      ("dgrad", 16, 0): "conv_dgrad:c64x16x16->64k3s1", ("dgrad", 16, 1): "conv_dgrad:c32x16x16->64k3s1",
+      ("dgrad", 8, 0): "conv_dgrad:c128x8x8->128k3s1", ("dgrad", 8, 1): "conv_dgrad:c64x8x8->128k3s1"}
 
 
 def main(fd, wd, out):
@@ -68,7 +72,7 @@ def main(fd, wd, out):
                     continue
                 # occurrence of this template within the step: wgrad kernels of one width come
                 # in layer order (deeper first); forward / dgrad 32-wide kernels are unique
-                occ = seen[sh] % (2 if sh[1] in (16, 8) and sh[0] == "wgrad" else 1)
+                occ = seen[sh] % (2 if sh[1] in (16, 8) else 1)
                 seen[sh] += 1
                 tag = KT.get((sh[0], sh[1], occ))
                 if tag is None:
