@@ -1395,7 +1395,7 @@ static int dconv_launch_w(const DPlan& p, dim3 grid, const DConvArgs& a, hipStre
 
 template <int OP, int S = 1>
 static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes, int sp,
-                     hipStream_t st, const char* name) {
+                     hipStream_t st, const char* name, bool* pooled = nullptr) {
     DPlan p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients, false, S == 2);
     const bool aligned = ((uintptr_t)a.wt % 16 == 0) && a.w_cs % 4 == 0;
     if (!(aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0)) && p.bm != 32) {
@@ -1408,6 +1408,8 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     a.splits = p.splits;
     a.cchunk = p.cchunk;
     a.Nfull = a.batch * sp;
+    if (p.splits > 1) a.pool_y = nullptr;  // the pool then runs after the split reduction
+    if (pooled) *pooled = a.pool_y != nullptr;
     // float4 weight runs: 16-B aligned slices that never run past the tensor
     a.wvec = aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0);
     float* out = a.out;
@@ -1418,7 +1420,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     if constexpr (S == 2) {
         rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
-    } else if (a.bn_part && p.splits == 1) {  // the statistics epilogue instances
+    } else if ((a.bn_part || a.pool_y) && p.splits == 1) {  // the LDS-image epilogue instances
         rc = w == 32 ? dconv_launch_w<OP, 32, 1, true>(p, grid, a, st)
            : w == 16 ? dconv_launch_w<OP, 16, 1, true>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 1, true>(p, grid, a, st);
@@ -1801,6 +1803,51 @@ extern "C" int fh_conv2d_fwd_bnstats(const float* x, int64_t x_cs, const float* 
     return conv2d_fwd_impl(x, x_cs, in_scale, in_shift, aff_cs, w, w_cs, bias, b_cs, y, y_cs,
                            counts, nclients, batch, cin, h, w_, cout, 3, 3, 1, 1, 0, workspace,
                            ws_bytes, stream, bn_part);
+}
+
+extern "C" int fh_maxpool2_fwd_pitched(const float* x, int64_t x_cs, float* y, int64_t y_cs,
+                                       uint8_t* idx, int64_t i_cs, uint8_t* mask, int64_t m_cs,
+                                       const int32_t* counts, int32_t nclients, int32_t batch,
+                                       int32_t C, int32_t H, int32_t W, int32_t drop_mode,
+                                       float p_drop, uint64_t seed, const uint64_t* seed_dev,
+                                       int32_t xh, int32_t xw, int32_t yh, int32_t yw,
+                                       void* stream);  // layers.hip
+
+// conv (3x3 / s1 / p1) -> ReLU -> 2x2 max-pool of the top-left pool_hw x pool_hw map of each
+// h x w plane (SimpleCNN conv2 + pool2, models_pytorch.py:88-89, on 16x16 planes holding the
+// 14x14 map).  py / pidx: dense [img][cout][pool_hw/2][pool_hw/2] (maxpool2_fwd_kernel's values
+// and first-max argmax, bit for bit).  Unsplit launches pool in the conv's epilogue and never
+// write y; launches the planner splits over input channels write y (scratch, h x w planes) and
+// pool it after the split reduction.  The pool's backward therefore takes its ReLU mask from py
+// (fh_maxpool2_bwd_ymask): the pooled value IS the ReLU output at the argmax.
+extern "C" int fh_conv2d_fwd_relu_pool(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                                       const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                                       float* py, int64_t py_cs, uint8_t* pidx, int64_t pi_cs,
+                                       const int32_t* counts, int32_t nclients, int32_t batch,
+                                       int32_t cin, int32_t h, int32_t w_, int32_t cout,
+                                       int32_t pool_hw, void* workspace, size_t ws_bytes,
+                                       void* stream) {
+    int oh, ow;
+    int rc = conv_common_check(nclients, batch, cin, h, w_, cout, 3, 3, 1, 1, oh, ow);
+    if (rc) return rc;
+    FH_REQUIRE(dconv_supported(h, w_, 3, 3, 1, 1) && h <= 16, "conv2d_fwd_relu_pool: needs a "
+               "square 8 or 16 map (whole images per 256-pixel tile), got %dx%d", h, w_);
+    FH_REQUIRE(pool_hw >= 2 && pool_hw <= h && !(pool_hw & 1), "conv2d_fwd_relu_pool: pooled "
+               "map %d in a %d plane", pool_hw, h);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(x && w && y && py && pidx, "conv2d_fwd_relu_pool: null pointer");
+    DConvArgs d{};
+    d.in = x; d.wt = w; d.bias = bias; d.out = y;
+    d.in_cs = x_cs; d.w_cs = w_cs; d.b_cs = b_cs; d.out_cs = y_cs;
+    d.counts = counts; d.batch = batch; d.Cr = cin; d.M = cout; d.relu = 1;
+    d.pool_y = py; d.pool_idx = pidx; d.py_cs = py_cs; d.pix_cs = pi_cs; d.pool_hw = pool_hw;
+    bool fused = false;
+    rc = run_dconv<OP_FWD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
+                           "conv2d_fwd_relu_pool", &fused);
+    if (rc || fused) return rc;
+    return fh_maxpool2_fwd_pitched(y, y_cs, py, py_cs, pidx, pi_cs, nullptr, 0, counts, nclients,
+                                   batch, cout, pool_hw, pool_hw, 0, 0.f, 0, nullptr, h, w_,
+                                   pool_hw / 2, pool_hw / 2, stream);
 }
 
 extern "C" int fh_conv2d_dgrad(const float* dy, int64_t dy_cs, const float* w, int64_t w_cs,

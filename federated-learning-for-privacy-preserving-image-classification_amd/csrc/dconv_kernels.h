@@ -71,6 +71,14 @@ struct DConvArgs {
     const float* in2;
     const float* wt2;
     int64_t in2_cs, w2_cs;
+    // FWD, statistics-epilogue instance, unsplit, nullable: a 2x2 max-pool of the ReLU output's
+    // top-left pool_hw x pool_hw map (SimpleCNN's 14x14 conv2 on 16x16 planes), taken from the
+    // tile's image in LDS with maxpool2_fwd_kernel's first-max rule -> pool_y
+    // [img][M][pool_hw/2][pool_hw/2] and the argmax pool_idx (same layout); out is not written
+    float* pool_y;
+    uint8_t* pool_idx;
+    int64_t py_cs, pix_cs;
+    int pool_hw;
 };
 
 // Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
@@ -164,6 +172,7 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
     // block-uniform: BN statistics of the stored values (FWD) / BN backward statistics of
     // the stored gradient (DGRAD)
     const bool stats = BNB && a.bn_part != nullptr && a.splits == 1;
+    const bool pooled = BNB && OP == OP_FWD && a.pool_y != nullptr && a.splits == 1;
     if (n0 >= cnt * G::HW) {  // a tile past this client's images: zero statistics
         if (stats && tid < BM && m0 + tid < a.M) {
             double* q = a.bn_part + (((int64_t)z * a.M + m0 + tid) * a.bn_tiles + t) * 2;
@@ -536,13 +545,39 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
                         if (OP == OP_FWD) {
                             if (has_bias) v = v + bv_r[i][r];
                             if (a.relu) v = fmaxf(v, 0.f);
-                            if (stats) red[ml * kStatPitch + n - n0] = v;
+                            if (stats || pooled) red[ml * kStatPitch + n - n0] = v;
+                            if (pooled) continue;  // only the pooled map leaves the tile
                         } else if (a.accumulate) {
                             v = *q + v;
                         }
                         *q = v;
                     }
                 }
+        }
+    }
+    if constexpr (OP == OP_FWD && BNB && G::HW <= 256) {
+        if (pooled) {  // 2x2 max-pool of each whole image of the tile, from the LDS image
+            __syncthreads();
+            constexpr int IMGS = 256 / G::HW;
+            const int ph = a.pool_hw >> 1, per = ph * ph;
+            const int img_t = n0 / G::HW;
+            for (int e = tid; e < BM * IMGS * per; e += 256) {
+                const int ml = e / (IMGS * per), rem = e - ml * (IMGS * per);
+                const int li = rem / per, pp = rem - li * per;
+                const int oy = pp / ph, ox = pp - oy * ph;
+                const int m = m0 + ml, img = img_t + li;
+                if (m >= M || img >= cnt) continue;
+                const float* r = red + ml * kStatPitch + li * G::HW + (2 * oy) * W + 2 * ox;
+                const float v0 = r[0], v1 = r[1], v2 = r[W], v3 = r[W + 1];
+                float mx = v0;
+                int am = 0;
+                if (v1 > mx) { mx = v1; am = 1; }
+                if (v2 > mx) { mx = v2; am = 2; }
+                if (v3 > mx) { mx = v3; am = 3; }
+                const int64_t o = ((int64_t)img * M + m) * per + pp;
+                a.pool_y[z * a.py_cs + o] = mx;
+                a.pool_idx[z * a.pix_cs + o] = (uint8_t)am;
+            }
         }
     }
     if constexpr (OP == OP_FWD) {

@@ -77,6 +77,8 @@ SIGNATURES = {
     "fh_conv_bnstats_bytes": (SZ, [I32, I32, I32, I32, I32]),
     "fh_conv2d_fwd_bnstats": (I32, [P, I64, P, P, I64, P, I64, P, I64, P, I64, P, P, I32, I32,
                                     I32, I32, I32, I32, P, SZ, P]),
+    "fh_conv2d_fwd_relu_pool": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, I32,
+                                      I32, I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_maxpool2_fwd_bnfinalize": (I32, [P, P, P, I64, P, P, I64, P, P, P, P, I64, P, I64, P,
                                          I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32,
                                          F32, I32, F32, U64, P, P]),

@@ -178,7 +178,12 @@ class PackedNet:
         # profiles/r03_k2/K2_fuse_pool2_bwd_ab.txt): the skinny DGRAD epilogue's routed
         # window stores cost what the maxpool2_bwd pass did.  Off.
         self.fuse_pool2_bwd = False
+        # SimpleCNN (pad_maps): conv2 -> ReLU -> pool2 in one launch where the conv is unsplit
+        # (fh_conv2d_fwd_relu_pool: the pool taken from the tile image in LDS, the 16x16
+        # ReLU output never written); pool2's backward then masks by p2 (maxpool2_bwd_ymask)
+        self.fuse_pool2 = True
         self._pool1_fused = False
+        self._pool2_fused = False
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -292,9 +297,14 @@ class PackedNet:
             ops.conv2d_fwd(self.x, W(P_, "conv1.weight"), W(P_, "conv1.bias"), a1, n, B, 1, 28,
                            28, 32, 3, 1, 1, relu=True, counts=cnt)
             ops.maxpool2_fwd(a1, p1, i1, n, B, 32, 28, 28, counts=cnt)
-        ops.conv2d_fwd(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, n, B, 32, hp, hp, 64,
-                       3, 1, 1, relu=True, counts=cnt)
-        ops.maxpool2_fwd(a2, p2, i2, n, B, 64, 14, 14, counts=cnt)
+        self._pool2_fused = self.pad_maps and self.fuse_pool2
+        if self._pool2_fused:
+            ops.conv2d_fwd_relu_pool(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, p2, i2, n,
+                                     B, 32, hp, 64, 14, counts=cnt)
+        else:
+            ops.conv2d_fwd(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, n, B, 32, hp, hp,
+                           64, 3, 1, 1, relu=True, counts=cnt)
+            ops.maxpool2_fwd(a2, p2, i2, n, B, 64, 14, 14, counts=cnt)
         dm = self._drop_mode(train)
         x3 = h1
         if dm and self.fused_dropout:
@@ -340,7 +350,7 @@ class PackedNet:
                 ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n,
                                  B, 3136, 128, counts=cnt)
                 ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
-            ops.maxpool2_bwd(dp2, i2, da2, n, B, 64, 14, 14, xin=a2, counts=cnt)
+            self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
         ops.conv2d_wgrad(p1, da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, hp, hp, 64,
                          3, 1, 1, counts=cnt)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
@@ -359,6 +369,14 @@ class PackedNet:
                              xin=A("a1", 32, 28, 28), counts=cnt)
         ops.conv2d_wgrad(self.x, da1, W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 1, 28, 28, 32,
                          3, 1, 1, counts=cnt)
+
+    def _pool2_bwd(self, dp2, i2, a2, da2, n, cnt):
+        """pool2's backward; its ReLU mask from p2 when the forward fused the pool (a2 unwritten)."""
+        if self._pool2_fused:
+            ops.maxpool2_bwd_ymask(dp2, i2, self.A("p2", 64, 7, 7), da2, n, self.batch, 64, 14, 14,
+                                   counts=cnt)
+        else:
+            ops.maxpool2_bwd(dp2, i2, da2, n, self.batch, 64, 14, 14, xin=a2, counts=cnt)
 
     # ---------------- DP-SGD backward (per-sample clipping; dpsgd.hip, conv.hip slabs)
     def backward_dpsgd(self, params, grads, n, counts, sqnorm, coef, max_norm):
@@ -399,7 +417,7 @@ class PackedNet:
         dp2 = A("dp2", 64, 7, 7)
         ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
         i2 = A("i2", 64, 7, 7, dtype=torch.uint8)
-        ops.maxpool2_bwd(dp2, i2, da2, n, B, 64, 14, 14, xin=a2, counts=cnt)
+        self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
         ops.conv2d_wgrad_persample(p1, da2, s2, n, B, 32, hp, hp, 64, counts=cnt)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt)

@@ -282,6 +282,24 @@ def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad,
     return y
 
 
+def conv2d_fwd_relu_pool(x, w, bias, y, py, pidx, nclients, batch, cin, h, cout, pool_hw,
+                         counts=None):
+    """conv2d_fwd(relu=True) on h x h planes + maxpool2_fwd of each plane's top-left
+    pool_hw x pool_hw map into py / pidx (fh_conv2d_fwd_relu_pool): the pool runs in the conv's
+    epilogue when the launch is unsplit, so y is scratch (written only by split launches) and
+    the pool's backward masks by py (maxpool2_bwd_ymask)."""
+    require_device(x, "x")
+    ws, nb = _ws_for("fh_conv2d_fwd_workspace", x.device, nclients, batch, cin, h, h, cout, 3, 3,
+                     1, 1)
+    ev = PROBE.begin(_conv_tag("fwd", cin, h, h, cout, 3, 1))
+    call("fh_conv2d_fwd_relu_pool", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y),
+         _cs(y), ptr(py), _cs(py), ptr(pidx), _cs(pidx), _counts(counts), nclients, batch, cin, h,
+         h, cout, pool_hw, ptr(ws), nb, stream_handle())
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, h, cout, 3, 1, 1),
+              _conv_bytes(nclients, batch, cin, h, h, cout, 3, 1, 1), nclients)
+    return py
+
+
 def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
                  accumulate=False, bn_bwd=None):
     """bn_bwd = (bn_x, scale, shift, save_mean, part[, pidx, pmask, p_drop]): the input was

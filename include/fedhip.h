@@ -546,6 +546,19 @@ int fh_conv2d_fwd_bnstats(const float* x, int64_t x_cs, const float* in_scale,
                           double* bn_part, const int32_t* counts, int32_t nclients,
                           int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
                           void* workspace, size_t ws_bytes, void* stream);
+/* conv (3x3 / s1 / p1, bias) -> ReLU -> 2x2 max-pool of the top-left pool_hw x pool_hw map of
+ * each h x w plane (h = w = 8 or 16): SimpleCNN conv2 -> relu -> pool2 on the 16x16 planes that
+ * hold its 14x14 map (replaces conv2d_fwd + maxpool2_fwd of models_pytorch.py:88-89).  py /
+ * pidx: dense [img][cout][pool_hw/2][pool_hw/2], the values and first-max argmax of
+ * fh_maxpool2_fwd_pitched bit for bit.  y (h x w planes) is scratch: written only when the
+ * planner splits the launch over input channels; the pool's backward takes its ReLU mask from
+ * py (fh_maxpool2_bwd_ymask). */
+int fh_conv2d_fwd_relu_pool(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                            const float* bias, int64_t b_cs, float* y, int64_t y_cs, float* py,
+                            int64_t py_cs, uint8_t* pidx, int64_t pi_cs, const int32_t* counts,
+                            int32_t nclients, int32_t batch, int32_t cin, int32_t h, int32_t w_,
+                            int32_t cout, int32_t pool_hw, void* workspace, size_t ws_bytes,
+                            void* stream);
 /* fh_bn_finalize_tiles fused into the 2x2 max-pool (+dropout, drop_mode as fh_maxpool2_fwd)
  * of the BN-ReLU output (CIFAR10CNN conv -> bn -> relu -> pool -> dropout,
  * models_pytorch.py:139-155): the same outputs as fh_bn_finalize_tiles followed by
