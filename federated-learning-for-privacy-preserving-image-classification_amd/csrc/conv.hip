@@ -584,6 +584,17 @@ struct BnBwdEpi {
     int pw;  // pooled map width (the epilogue's map), x is 2pw wide
 };
 
+// FWD split-K epilogue with the 2x2 max-pool after the ReLU (fh_conv2d_fwd_relu_pool on a
+// split launch): planes of 256 pixels (one image per workgroup), the pool of the top-left
+// hw x hw map of each -> y [img][M][hw/2][hw/2] + argmax (maxpool2_fwd_kernel's rule); the
+// un-pooled output is not stored
+struct PoolEpi {
+    float* y;  // nullptr: off
+    uint8_t* idx;
+    int64_t y_cs, i_cs;
+    int hw, w;  // pooled map size, plane width
+};
+
 // FWD/DGRAD split-K epilogue: out[z][img][m][p] (=|+=) sum_s part[z][s][m][n] (+bias, relu).
 // bn_part (nullable): one fp64 pair per (client, channel, 256-pixel tile) as the unsplit
 // dconv epilogue writes it (dconv_kernels.h DConvArgs::bn_part): FWD the BatchNorm
@@ -594,12 +605,12 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
                        float* __restrict__ out, int64_t out_cs, const float* __restrict__ bias,
                        int64_t b_cs, int relu, int accumulate, const int32_t* __restrict__ counts,
                        int batch, int sp, double* __restrict__ bn_part, int bn_tiles,
-                       DropArgs drop, BnBwdEpi bb) {
+                       DropArgs drop, BnBwdEpi bb, PoolEpi pe) {
     const int z = blockIdx.z, m = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int n = blockIdx.x * 256 + threadIdx.x;
     const bool valid = n < cnt * sp;
-    if (!valid && bn_part == nullptr) return;
+    if (!valid && bn_part == nullptr) return;  // with pe.y (sp = 256): block-uniform
     float s = 0.f, d0f = 0.f, d1f = 0.f;
     if (valid) {
         const float* p = part + ((int64_t)z * splits * M + m) * Nfull + n;
@@ -636,7 +647,27 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
             d1f = (xv - bb.mean[z * M + m]) * g;
             if (!bb.pidx) s = g;
         }
-        *o = s;
+        if (!pe.y) *o = s;
+    }
+    if (pe.y) {  // block-uniform; the workgroup is one image's channel-m plane
+        __shared__ float pl[256];
+        pl[threadIdx.x] = s;
+        __syncthreads();
+        const int ph = pe.hw >> 1, per = ph * ph;
+        if ((int)threadIdx.x < per) {
+            const int oy = threadIdx.x / ph, ox = threadIdx.x - oy * ph;
+            const float* r = pl + (2 * oy) * pe.w + 2 * ox;
+            const float v0 = r[0], v1 = r[1], v2 = r[pe.w], v3 = r[pe.w + 1];
+            float mx = v0;
+            int am = 0;
+            if (v1 > mx) { mx = v1; am = 1; }
+            if (v2 > mx) { mx = v2; am = 2; }
+            if (v3 > mx) { mx = v3; am = 3; }
+            const int img = n / sp;
+            const int64_t o = ((int64_t)img * M + m) * per + threadIdx.x;
+            pe.y[z * pe.y_cs + o] = mx;
+            pe.idx[z * pe.i_cs + o] = (uint8_t)am;
+        }
     }
     if (bn_part != nullptr) {  // block-uniform
         __shared__ double red[2][4];
@@ -1213,7 +1244,7 @@ static int run_mn(ConvArgs a, int kh, int kw, int stride, int nclients, void* ws
         dim3 eg((unsigned)ceil_div(a.N, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.N, out, out_cs, bias, b_cs, relu, accum, a.counts, a.batch, sp,
-                           (double*)nullptr, 0, a.drop, BnBwdEpi{});
+                           (double*)nullptr, 0, a.drop, BnBwdEpi{}, PoolEpi{});
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -1408,7 +1439,9 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     a.splits = p.splits;
     a.cchunk = p.cchunk;
     a.Nfull = a.batch * sp;
-    if (p.splits > 1) a.pool_y = nullptr;  // the pool then runs after the split reduction
+    // split launches pool in the split reduction when each of its workgroups holds one whole
+    // image plane (sp = 256), else in a separate pass after it (the caller)
+    if (p.splits > 1 && sp != 256) a.pool_y = nullptr;
     if (pooled) *pooled = a.pool_y != nullptr;
     // float4 weight runs: 16-B aligned slices that never run past the tensor
     a.wvec = aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0);
@@ -1439,7 +1472,9 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
                            a.batch, sp, a.bn_part, a.bn_tiles, DropArgs{},
                            BnBwdEpi{OP == OP_FWD ? nullptr : a.bnx, a.bnx_cs, a.bn_scale,
                                     a.bn_shift, a.bns_cs, a.bn_mean, a.pidx, a.pmask, a.pi_cs,
-                                    a.pm_cs, a.pscale, w});
+                                    a.pm_cs, a.pscale, w},
+                           PoolEpi{OP == OP_FWD ? a.pool_y : nullptr, a.pool_idx, a.py_cs,
+                                   a.pix_cs, a.pool_hw, w});
         FH_LAUNCH_CHECK(name);
     }
     return FH_OK;
@@ -1513,7 +1548,7 @@ static int run_dconv_dgrad_s2(DConvArgs a, int oh, int nclients, void* ws, size_
         dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits, a.M,
                   a.Nfull, out, a.out_cs, nullptr, (int64_t)0, 0, a.accumulate, a.counts, a.batch,
-                  sp, nullptr, 0, DropArgs{}, BnBwdEpi{});
+                  sp, nullptr, 0, DropArgs{}, BnBwdEpi{}, PoolEpi{});
         FH_LAUNCH_CHECK("conv2d_dgrad direct s2 epilogue");
     }
     return FH_OK;
@@ -1816,10 +1851,11 @@ extern "C" int fh_maxpool2_fwd_pitched(const float* x, int64_t x_cs, float* y, i
 // conv (3x3 / s1 / p1) -> ReLU -> 2x2 max-pool of the top-left pool_hw x pool_hw map of each
 // h x w plane (SimpleCNN conv2 + pool2, models_pytorch.py:88-89, on 16x16 planes holding the
 // 14x14 map).  py / pidx: dense [img][cout][pool_hw/2][pool_hw/2] (maxpool2_fwd_kernel's values
-// and first-max argmax, bit for bit).  Unsplit launches pool in the conv's epilogue and never
-// write y; launches the planner splits over input channels write y (scratch, h x w planes) and
-// pool it after the split reduction.  The pool's backward therefore takes its ReLU mask from py
-// (fh_maxpool2_bwd_ymask): the pooled value IS the ReLU output at the argmax.
+// and first-max argmax, bit for bit).  Unsplit launches pool in the conv's epilogue, split
+// launches on 16x16 planes in the split reduction (splitk_epilogue_kernel, PoolEpi), neither
+// writes y; split launches on 8x8 planes write y (scratch) and pool it in a separate pass.  The
+// pool's backward therefore takes its ReLU mask from py (fh_maxpool2_bwd_ymask): the pooled
+// value IS the ReLU output at the argmax.
 extern "C" int fh_conv2d_fwd_relu_pool(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
                                        const float* bias, int64_t b_cs, float* y, int64_t y_cs,
                                        float* py, int64_t py_cs, uint8_t* pidx, int64_t pi_cs,

@@ -312,12 +312,27 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     __shared__ int ci[32];
     __shared__ double sl[4];
     __shared__ int sc[4];
+    // SMALLK: the targets, the bias and this block's share of the keep-mask, fetched with
+    // the operands at the start (r04: loaded where used they were three more dependent
+    // global round trips)
+    constexpr int MS = SMALLK ? 32 * FMAX / kHeadBlocks : 1;
+    __shared__ int64_t Ts[32];
+    __shared__ float Bs[KMAX];
+    __shared__ uint8_t Ms[MS];
     const int z = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
     const int cnt = counts ? counts[z] : batch;
     const float* xz = x + z * x_cs;
     const float* wz = w + z * w_cs;
     const int FP = F + 1;
+    const int S = gridDim.x;
+    const int dx_per = (cnt * F + S - 1) / S, dx_e0 = part * dx_per;
+    const int dx_e1 = min(cnt * F, dx_e0 + dx_per);
     if constexpr (SMALLK) {
+        if (tid < cnt) Ts[tid] = targets[z * t_cs + tid];
+        if (tid < K) Bs[tid] = bias ? bias[z * b_cs + tid] : 0.f;
+        if (mask && dx) {
+            for (int e = dx_e0 + tid; e < dx_e1; e += 256) Ms[e - dx_e0] = mask[z * m_cs + e];
+        }
         // float4 loads, all issued before the LDS stores (r03: the element loop waited for
         // each load in turn — ~20 dependent global round trips per launch)
         const bool v4 = (F & 3) == 0 && ((uintptr_t)xz & 15) == 0 && ((uintptr_t)wz & 15) == 0;
@@ -370,17 +385,41 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     auto X = [&](int b, int f) -> float { return SMALLK ? Xs[b * FP + f] : xz[(int64_t)b * F + f]; };
     auto Wt = [&](int k, int f) -> float { return SMALLK ? Ws[k * FP + f] : wz[(int64_t)k * F + f]; };
     // 1. logits
-    for (int o = tid; o < cnt * K; o += 256) {
-        const int img = o / K, k = o - img * K;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four chains: LDS latency overlaps
-        for (int f = 0; f < F; f += 4) {
-            a0 = fmaf(X(img, f), Wt(k, f), a0);
-            a1 = fmaf(X(img, f + 1), Wt(k, f + 1), a1);
-            a2 = fmaf(X(img, f + 2), Wt(k, f + 2), a2);
-            a3 = fmaf(X(img, f + 3), Wt(k, f + 3), a3);
+    if constexpr (SMALLK) {
+        // eight lanes per logit (f = q, q + 8, ...: neighbouring LDS words), two chains each,
+        // a fixed xor tree over the eight: ~cnt*K*8 / 256 short dot products per thread
+        // instead of one F-long chain
+        constexpr int Q = 8;
+        const int q = tid & (Q - 1);
+        for (int base = 0; base < cnt * K * Q; base += 256) {  // block-uniform trip count
+            const int it = base + tid, o = it / Q;
+            const bool ok = o < cnt * K;
+            const int img = ok ? o / K : 0, k = ok ? o - img * K : 0;
+            const float* xr = Xs + img * FP + q;
+            const float* wr = Ws + k * FP + q;
+            float a0 = 0.f, a1 = 0.f;
+            for (int f = 0; f < F; f += 2 * Q) {
+                a0 = fmaf(xr[f], wr[f], a0);
+                a1 = fmaf(xr[f + Q], wr[f + Q], a1);
+            }
+            float acc = a0 + a1;
+#pragma unroll
+            for (int o2 = 1; o2 < Q; o2 <<= 1) acc += __shfl_xor(acc, o2, 64);
+            if (ok && q == 0) L[img * K + k] = bias ? acc + Bs[k] : acc;
         }
-        const float acc = (a0 + a1) + (a2 + a3);
-        L[img * K + k] = bias ? acc + bias[z * b_cs + k] : acc;
+    } else {
+        for (int o = tid; o < cnt * K; o += 256) {
+            const int img = o / K, k = o - img * K;
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four chains: LDS latency overlaps
+            for (int f = 0; f < F; f += 4) {
+                a0 = fmaf(X(img, f), Wt(k, f), a0);
+                a1 = fmaf(X(img, f + 1), Wt(k, f + 1), a1);
+                a2 = fmaf(X(img, f + 2), Wt(k, f + 2), a2);
+                a3 = fmaf(X(img, f + 3), Wt(k, f + 3), a3);
+            }
+            const float acc = (a0 + a1) + (a2 + a3);
+            L[img * K + k] = bias ? acc + bias[z * b_cs + k] : acc;
+        }
     }
     __syncthreads();
     // 2. cross-entropy (ce_kernel's operations and fp64 sum order)
@@ -392,7 +431,7 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         const int g = tid >> 4, l = tid & 15;
         for (int img = g; img < cnt; img += 16) {
             const float* row = L + img * K;
-            const int tgt = (int)targets[z * t_cs + img];
+            const int tgt = SMALLK ? (int)Ts[img] : (int)targets[z * t_cs + img];
             const float v = l < K ? row[l] : -INFINITY;
             float mx = v;
             int amax = l < K ? l : K;
@@ -480,7 +519,6 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
             db[z * db_cs + tid] = v;
         }
     }
-    const int S = gridDim.x;
     // 3. weight gradient, this block's share: dW[k][f] = sum_b D[b][k] x[b][f] (dw null: the
     // caller takes it elsewhere — DP-SGD clips it per image first)
     if (dw) {
@@ -489,6 +527,7 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
             const int k = e / F, f = e - k * F;
             float a0 = 0.f, a1 = 0.f;
             int b = 0;
+#pragma unroll 4
             for (; b + 1 < cnt; b += 2) {
                 a0 = fmaf(D[b * K + k], X(b, f), a0);
                 a1 = fmaf(D[(b + 1) * K + k], X(b + 1, f), a1);
@@ -499,13 +538,13 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     }
     // 4. input gradient through Dropout + ReLU, this block's share: dx[b][f] = sum_k D[b][k] W[k][f]
     if (dx) {
-        const int per = (cnt * F + S - 1) / S, e0 = part * per, e1 = min(cnt * F, e0 + per);
+        const int e0 = dx_e0, e1 = dx_e1;
         for (int eb = e0 + tid; eb < e1; eb += 4 * 256) {  // keep-mask bytes of 4 outputs first
             uint8_t mk[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int e = eb + 256 * u;
-                mk[u] = (mask && e < e1) ? mask[z * m_cs + e] : 1;
+                mk[u] = (mask && e < e1) ? (SMALLK ? Ms[e - e0] : mask[z * m_cs + e]) : 1;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -513,7 +552,13 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
                 if (e >= e1) break;
                 const int img = e / F, f = e - img * F;
                 float acc = 0.f;
-                for (int k = 0; k < K; ++k) acc = fmaf(D[img * K + k], Wt(k, f), acc);
+                if constexpr (SMALLK) {  // unrolled: the LDS reads issue ahead of the chain
+#pragma unroll
+                    for (int k = 0; k < KMAX; ++k)
+                        if (k < K) acc = fmaf(D[img * K + k], Wt(k, f), acc);
+                } else {
+                    for (int k = 0; k < K; ++k) acc = fmaf(D[img * K + k], Wt(k, f), acc);
+                }
                 if (mask) acc = mk[u] ? acc * scale : 0.f;
                 if (relu_in && !(X(img, f) > 0.f)) acc = 0.f;
                 dx[z * dx_cs + e] = acc;
@@ -877,7 +922,7 @@ extern "C" int fh_linear_head_ce(const float* x, int64_t x_cs, const float* w, i
                "linear_head_ce: null pointer");
     const dim3 grid(kHeadBlocks, nclients);
     const float scale = 1.0f / (1.0f - p_drop);
-    if (num_classes <= 16 && in_f <= 256)
+    if (num_classes <= 16 && in_f <= 256 && in_f % 16 == 0)
         FH_LAUNCH(linear_head_ce_kernel<true>, grid, dim3(256), 0, as_stream(stream), x, x_cs, w,
                   w_cs, bias, b_cs, targets, t_cs, logits, l_cs, dlogits, d_cs, loss_out,
                   acc_loss, acc_correct, acc_seen, reset, dw, dw_cs, db, db_cs, dx, dx_cs, mask,

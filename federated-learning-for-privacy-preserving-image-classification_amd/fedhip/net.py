@@ -178,9 +178,10 @@ class PackedNet:
         # profiles/r03_k2/K2_fuse_pool2_bwd_ab.txt): the skinny DGRAD epilogue's routed
         # window stores cost what the maxpool2_bwd pass did.  Off.
         self.fuse_pool2_bwd = False
-        # SimpleCNN (pad_maps): conv2 -> ReLU -> pool2 in one launch where the conv is unsplit
-        # (fh_conv2d_fwd_relu_pool: the pool taken from the tile image in LDS, the 16x16
-        # ReLU output never written); pool2's backward then masks by p2 (maxpool2_bwd_ymask)
+        # SimpleCNN (pad_maps): conv2 -> ReLU -> pool2 without the pool launch
+        # (fh_conv2d_fwd_relu_pool: the pool taken from the tile image in LDS, or in the split
+        # reduction; the 16x16 ReLU output never written); pool2's backward then masks by p2
+        # (maxpool2_bwd_ymask).  K2 1.501M -> 1.564M (interleaved x2, profiles/r04_pool2/)
         self.fuse_pool2 = True
         self._pool1_fused = False
         self._pool2_fused = False
@@ -855,15 +856,20 @@ class PackedNet:
             p1, a2 = self._simple_maps()[:2]
             a2 = a2[..., :14, :14]
             a1 = A("a1", 32, 28, 28)
-            if self._pool1_fused:  # conv1's output not written: its value at each window's
-                # argmax is the pooled value (the backward uses no other element of it)
-                pooled = p1[..., :14, :14]
-                code = A("i1", 32, 14, 14, dtype=torch.uint8).long()
-                a1 = torch.zeros_like(a1)
+
+            def unpool(pooled, code, full):  # a conv output the fused pool never wrote: its
+                # value at each window's argmax is the pooled value (the backward uses no
+                # other element of it)
+                out = torch.zeros_like(full)
                 for dy in (0, 1):
                     for dx in (0, 1):
-                        a1[..., dy::2, dx::2] = torch.where(code == 2 * dy + dx, pooled,
-                                                            torch.zeros_like(pooled))
+                        out[..., dy::2, dx::2] = torch.where(code == 2 * dy + dx, pooled,
+                                                             torch.zeros_like(pooled))
+                return out
+            if self._pool1_fused:
+                a1 = unpool(p1[..., :14, :14], A("i1", 32, 14, 14, dtype=torch.uint8).long(), a1)
+            if self._pool2_fused:
+                a2 = unpool(A("p2", 64, 7, 7), A("i2", 64, 7, 7, dtype=torch.uint8).long(), a2)
             return [a1, a2, self._fc_in]  # dropped fc1 output: see fused_dropout
         if self.family == "CIFAR10CNN":
             if self._fused:  # BN outputs not materialised: the same fp32 ops on the host side

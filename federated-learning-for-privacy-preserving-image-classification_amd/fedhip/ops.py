@@ -286,8 +286,8 @@ def conv2d_fwd_relu_pool(x, w, bias, y, py, pidx, nclients, batch, cin, h, cout,
                          counts=None):
     """conv2d_fwd(relu=True) on h x h planes + maxpool2_fwd of each plane's top-left
     pool_hw x pool_hw map into py / pidx (fh_conv2d_fwd_relu_pool): the pool runs in the conv's
-    epilogue when the launch is unsplit, so y is scratch (written only by split launches) and
-    the pool's backward masks by py (maxpool2_bwd_ymask)."""
+    epilogue (unsplit) or its split reduction (16x16 planes), so y is scratch (written only by
+    split launches on 8x8 planes) and the pool's backward masks by py (maxpool2_bwd_ymask)."""
     require_device(x, "x")
     ws, nb = _ws_for("fh_conv2d_fwd_workspace", x.device, nclients, batch, cin, h, h, cout, 3, 3,
                      1, 1)

@@ -550,9 +550,10 @@ int fh_conv2d_fwd_bnstats(const float* x, int64_t x_cs, const float* in_scale,
  * each h x w plane (h = w = 8 or 16): SimpleCNN conv2 -> relu -> pool2 on the 16x16 planes that
  * hold its 14x14 map (replaces conv2d_fwd + maxpool2_fwd of models_pytorch.py:88-89).  py /
  * pidx: dense [img][cout][pool_hw/2][pool_hw/2], the values and first-max argmax of
- * fh_maxpool2_fwd_pitched bit for bit.  y (h x w planes) is scratch: written only when the
- * planner splits the launch over input channels; the pool's backward takes its ReLU mask from
- * py (fh_maxpool2_bwd_ymask). */
+ * fh_maxpool2_fwd_pitched bit for bit: pooled in the conv's epilogue (unsplit launches) or in
+ * the split-K reduction (16x16 planes).  y (h x w planes) is scratch, written only by split
+ * launches on 8x8 planes (pooled by a separate pass); the pool's backward takes its ReLU mask
+ * from py (fh_maxpool2_bwd_ymask). */
 int fh_conv2d_fwd_relu_pool(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
                             const float* bias, int64_t b_cs, float* y, int64_t y_cs, float* py,
                             int64_t py_cs, uint8_t* pidx, int64_t pi_cs, const int32_t* counts,

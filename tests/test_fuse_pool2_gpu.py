@@ -1,6 +1,6 @@
 """SimpleCNN conv2 -> ReLU -> pool2 in one launch (fh_conv2d_fwd_relu_pool, r04): the pool is
 taken in the direct conv's epilogue from the tile image in LDS when the launch is unsplit, and
-after the split reduction otherwise; the pool's backward masks by p2 (maxpool2_bwd_ymask).  The
+in the split reduction otherwise; the pool's backward masks by p2 (maxpool2_bwd_ymask).  The
 same fp32 values and first-max argmax as conv2d_fwd(relu) + maxpool2_fwd, so whole rounds are
 bit-identical to the two-launch path.  Reference: models_pytorch.py:88-89 (conv2 -> relu ->
 pool)."""
@@ -17,8 +17,8 @@ DEV = torch.device("cuda")
 
 @pytest.mark.parametrize("nc", [1, 3, 9, 20])
 def test_conv_relu_pool_op_matches_separate_launches(nc):
-    """nc = 1 / 3: the planner splits over input channels (pool after the reduction);
-    9 / 20: unsplit BM = 32 / 64 launches (pool in the epilogue)."""
+    """nc = 1 / 3: the planner splits over input channels (pool in the split reduction);
+    9 / 20: unsplit BM = 32 / 64 launches (pool in the conv's epilogue)."""
     B, H, cin, cout = 32, 16, 32, 64
     torch.manual_seed(nc)
     cnt = torch.tensor([B] + [int(v) for v in torch.randint(1, B + 1, (nc - 1,))],
@@ -79,7 +79,7 @@ def _round(fuse, opt, sizes, rounds=2):
 @pytest.mark.parametrize("opt", ["sgd", "adam"])
 def test_fused_pool2_rounds_bit_identical(opt):
     """12 ragged clients: the early steps run unsplit (pool in the epilogue), the tail steps
-    with few clients split (pool after the reduction) — both against the two-launch path."""
+    with few clients split (pool in the reduction) — both against the two-launch path."""
     sizes = [130, 100, 96, 75, 70, 64, 64, 50, 40, 33, 32, 9]
     a, ma = _round(True, opt, sizes)
     b, mb = _round(False, opt, sizes)

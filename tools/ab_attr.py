@@ -1,7 +1,8 @@
 """A/B of one PackedNet plan attribute on the bench (no environment knobs in the product):
-    python tools/ab_attr.py fuse_pool2=0 -- --config K2 --steps 10 --warmup 2
-sets the attribute on every PackedNet right after construction, then runs bench.main() with
-the arguments after `--`."""
+    python tools/ab_attr.py fuse_pool2=0 trainer.use_graphs=0 -- --config K2 --steps 10
+sets the attribute on every PackedNet (trainer.<attr>: every PackedTrainer) right after
+construction, then runs bench.main() with
+the arguments after `--`.  lib=<path> loads that libfedhip.so instead (tools/build_base_lib.sh)."""
 import os
 import sys
 
@@ -13,10 +14,18 @@ sys.path.insert(0, os.path.join(os.path.dirname(here),
 
 def main():
     cut = sys.argv.index("--")
-    sets = {}
+    sets, tsets, lib = {}, {}, None
     for kv in sys.argv[1:cut]:
-        k, v = kv.split("=")
-        sets[k] = bool(int(v))
+        k, v = kv.split("=", 1)
+        if k == "lib":
+            lib = v
+        elif k.startswith("trainer."):
+            tsets[k[len("trainer."):]] = bool(int(v))
+        else:
+            sets[k] = bool(int(v))
+    if lib:
+        from fedhip import _lib
+        _lib.load.__defaults__ = (lib,)
     from fedhip import net
     init = net.PackedNet.__init__
 
@@ -28,6 +37,17 @@ def main():
             setattr(self, k, v)
 
     net.PackedNet.__init__ = patched
+    from fedhip import engine
+    tinit = engine.PackedTrainer.__init__
+
+    def tpatched(self, *a, **kw):
+        tinit(self, *a, **kw)
+        for k, v in tsets.items():
+            if not hasattr(self, k):
+                raise AttributeError(f"PackedTrainer has no attribute {k}")
+            setattr(self, k, v)
+
+    engine.PackedTrainer.__init__ = tpatched
     sys.argv = [sys.argv[0]] + sys.argv[cut + 1:]
     import bench
     bench.main()
