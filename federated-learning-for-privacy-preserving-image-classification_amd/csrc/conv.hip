@@ -1453,7 +1453,9 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     if constexpr (S == 2) {
         rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
-    } else if ((a.bn_part || a.pool_y) && p.splits == 1) {  // the LDS-image epilogue instances
+    } else if ((a.bn_part || (a.pool_y && p.bm != 32)) && p.splits == 1) {
+        // the statistics-epilogue instances (and the pooled epilogue at BM = 64, whose tile
+        // image needs their LDS; at BM = 32 the plain instance pools in the K loop's LDS)
         rc = w == 32 ? dconv_launch_w<OP, 32, 1, true>(p, grid, a, st)
            : w == 16 ? dconv_launch_w<OP, 16, 1, true>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 1, true>(p, grid, a, st);

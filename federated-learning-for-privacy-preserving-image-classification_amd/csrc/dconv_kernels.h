@@ -172,7 +172,10 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
     // block-uniform: BN statistics of the stored values (FWD) / BN backward statistics of
     // the stored gradient (DGRAD)
     const bool stats = BNB && a.bn_part != nullptr && a.splits == 1;
-    const bool pooled = BNB && OP == OP_FWD && a.pool_y != nullptr && a.splits == 1;
+    // the pooled epilogue's [BM][kStatPitch] image fits in the K loop's LDS (the plain
+    // instance: BM = 32) or in the statistics image (the BNB instance)
+    constexpr bool POOL_LDS = BNB || LDS_MAIN >= BM * kStatPitch;
+    const bool pooled = POOL_LDS && OP == OP_FWD && a.pool_y != nullptr && a.splits == 1;
     if (n0 >= cnt * G::HW) {  // a tile past this client's images: zero statistics
         if (stats && tid < BM && m0 + tid < a.M) {
             double* q = a.bn_part + (((int64_t)z * a.M + m0 + tid) * a.bn_tiles + t) * 2;
@@ -555,7 +558,7 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
                 }
         }
     }
-    if constexpr (OP == OP_FWD && BNB && G::HW <= 256) {
+    if constexpr (OP == OP_FWD && POOL_LDS && G::HW <= 256) {
         if (pooled) {  // 2x2 max-pool of each whole image of the tile, from the LDS image
             __syncthreads();
             constexpr int IMGS = 256 / G::HW;

@@ -17,6 +17,8 @@
 
 namespace fh {
 
+typedef float hf32x4 __attribute__((ext_vector_type(4)));
+
 // ------------------------------------------------------------------ MaxPool 2x2 (+dropout)
 // x: [z][img][C][H][W] -> y: [z][img][C][H/2][W/2]; idx: window argmax (0..3, first max);
 // drop_mode 0: none; 1: generate keep-mask (Philox) into mask; 2: use caller mask.
@@ -284,9 +286,13 @@ ce_kernel(const float* __restrict__ logits, int64_t l_cs, const int64_t* __restr
 // the keep-mask is 1; elsewhere the gradient is 0 anyway).  Replaces the layer's forward
 // (+ split-K epilogue), ce, its wgrad, its dgrad and dropout_bwd.  batch <= 32.
 // Every block of a client stages x [cnt][F] (and, SMALLK, W [K][F]) in LDS with a +1 pitch,
-// recomputes the logits and the loss (a few hundred dot products), and then owns 1/S of the
-// dW and dX outputs; block 0 publishes logits, dlogits and the loss accumulators.  Dot
-// products are sequential fmaf chains (one thread per output), images / classes in order.
+// recomputes the logits and the loss, and then owns 1/S of the dW and dX outputs; block 0
+// publishes logits, dlogits and the loss accumulators.  SMALLK (<= 16 classes, F <= 256, the
+// BASELINE models' heads): the three products run on v_mfma_f32_16x16x4_f32 from the staged
+// LDS operands — logits as two 16-image tiles x two halves of F (one wave each), dW / dX as
+// 16-column tiles dealt round-robin to the S x 4 waves of the client (r04: the per-thread
+// fmaf chains made the launch ~20 us of dependent LDS round trips); else sequential fmaf
+// chains (one thread per output), images / classes in order.
 constexpr int kHeadBlocks = 4;
 template <bool SMALLK>
 __global__ void __launch_bounds__(256)
@@ -312,10 +318,9 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     __shared__ int ci[32];
     __shared__ double sl[4];
     __shared__ int sc[4];
-    // SMALLK: the targets, the bias and this block's share of the keep-mask, fetched with
-    // the operands at the start (r04: loaded where used they were three more dependent
-    // global round trips)
-    constexpr int MS = SMALLK ? 32 * FMAX / kHeadBlocks : 1;
+    // SMALLK: the targets, the bias and the keep-mask, fetched with the operands at the
+    // start (r04: loaded where used they were three more dependent global round trips)
+    constexpr int MS = SMALLK ? 32 * FMAX : 1;
     __shared__ int64_t Ts[32];
     __shared__ float Bs[KMAX];
     __shared__ uint8_t Ms[MS];
@@ -325,13 +330,29 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     const float* wz = w + z * w_cs;
     const int FP = F + 1;
     const int S = gridDim.x;
+    // block 0, thread 0: the running accumulators it updates at the end, loaded now
+    bool rs0 = false;
+    double al0 = 0.0;
+    int64_t ac0 = 0, as0 = 0;
+    if (part == 0 && tid == 0) {
+        rs0 = reset && reset[z];
+        if (acc_loss) al0 = acc_loss[z];
+        if (acc_correct) ac0 = acc_correct[z];
+        if (acc_seen) as0 = acc_seen[z];
+    }
     const int dx_per = (cnt * F + S - 1) / S, dx_e0 = part * dx_per;
     const int dx_e1 = min(cnt * F, dx_e0 + dx_per);
     if constexpr (SMALLK) {
         if (tid < cnt) Ts[tid] = targets[z * t_cs + tid];
         if (tid < K) Bs[tid] = bias ? bias[z * b_cs + tid] : 0.f;
         if (mask && dx) {
-            for (int e = dx_e0 + tid; e < dx_e1; e += 256) Ms[e - dx_e0] = mask[z * m_cs + e];
+            const uint8_t* mz = mask + z * m_cs;
+            if (((uintptr_t)mz & 3) == 0) {  // cnt * F % 16 == 0
+                for (int e = tid; e < cnt * F / 4; e += 256)
+                    reinterpret_cast<uint32_t*>(Ms)[e] = reinterpret_cast<const uint32_t*>(mz)[e];
+            } else {
+                for (int e = tid; e < cnt * F; e += 256) Ms[e] = mz[e];
+            }
         }
         // float4 loads, all issued before the LDS stores (r03: the element loop waited for
         // each load in turn — ~20 dependent global round trips per launch)
@@ -385,27 +406,35 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     auto X = [&](int b, int f) -> float { return SMALLK ? Xs[b * FP + f] : xz[(int64_t)b * F + f]; };
     auto Wt = [&](int k, int f) -> float { return SMALLK ? Ws[k * FP + f] : wz[(int64_t)k * F + f]; };
     // 1. logits
+    const int lane = tid & 63, wid = tid >> 6;
     if constexpr (SMALLK) {
-        // eight lanes per logit (f = q, q + 8, ...: neighbouring LDS words), two chains each,
-        // a fixed xor tree over the eight: ~cnt*K*8 / 256 short dot products per thread
-        // instead of one F-long chain
-        constexpr int Q = 8;
-        const int q = tid & (Q - 1);
-        for (int base = 0; base < cnt * K * Q; base += 256) {  // block-uniform trip count
-            const int it = base + tid, o = it / Q;
-            const bool ok = o < cnt * K;
-            const int img = ok ? o / K : 0, k = ok ? o - img * K : 0;
-            const float* xr = Xs + img * FP + q;
-            const float* wr = Ws + k * FP + q;
-            float a0 = 0.f, a1 = 0.f;
-            for (int f = 0; f < F; f += 2 * Q) {
-                a0 = fmaf(xr[f], wr[f], a0);
-                a1 = fmaf(xr[f + Q], wr[f + Q], a1);
-            }
-            float acc = a0 + a1;
+        // wave wid: image tile t (16 rows), half fh of F; D [img][16] holds the second half's
+        // partial products until the CE pass
+        const int mn = lane & 15, kk = lane >> 4, t = wid & 1, fh = wid >> 1, Fh = F >> 1;
+        const int ia = t * 16 + mn;
+        const bool arow = ia < cnt, bcol = mn < K;
+        const float* xa = Xs + ia * FP + fh * Fh + kk;
+        const float* wb = Ws + mn * FP + fh * Fh + kk;
+        hf32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int f = 0; f < Fh; f += 4)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(arow ? xa[f] : 0.f, bcol ? wb[f] : 0.f,
+                                                       acc, 0, 0, 0);
+        float* lp = fh ? D : L;
 #pragma unroll
-            for (int o2 = 1; o2 < Q; o2 <<= 1) acc += __shfl_xor(acc, o2, 64);
-            if (ok && q == 0) L[img * K + k] = bias ? acc + Bs[k] : acc;
+        for (int r = 0; r < 4; ++r) lp[(t * 16 + 4 * kk + r) * 16 + mn] = acc[r];
+        __syncthreads();
+        float lv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int o = tid + 256 * u;
+            const int img = o / K, k = o - img * K;
+            lv[u] = o < cnt * K ? L[img * 16 + k] + D[img * 16 + k] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int o = tid + 256 * u;
+            if (o < cnt * K) L[o] = bias ? lv[u] + Bs[o - (o / K) * K] : lv[u];
         }
     } else {
         for (int o = tid; o < cnt * K; o += 256) {
@@ -423,7 +452,6 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     }
     __syncthreads();
     // 2. cross-entropy (ce_kernel's operations and fp64 sum order)
-    const int lane = tid & 63, wid = tid >> 6;
     const float inv_n = cnt > 0 ? 1.0f / (float)cnt : 0.f;
     double lsum = 0.0;
     int corr = 0;
@@ -502,18 +530,24 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         if (tid == 0) {
             const double tot = sl[0] + sl[1] + sl[2] + sl[3];
             const float batch_loss = cnt > 0 ? (float)(tot / (double)cnt) : 0.f;
-            const bool rs = reset && reset[z];
             if (loss_out) loss_out[z] = batch_loss;
-            if (acc_loss) acc_loss[z] = (rs ? 0.0 : acc_loss[z]) + (double)batch_loss;
-            if (acc_correct)
-                acc_correct[z] = (rs ? 0 : acc_correct[z]) + sc[0] + sc[1] + sc[2] + sc[3];
-            if (acc_seen) acc_seen[z] = (rs ? 0 : acc_seen[z]) + cnt;
+            if (acc_loss) acc_loss[z] = (rs0 ? 0.0 : al0) + (double)batch_loss;
+            if (acc_correct) acc_correct[z] = (rs0 ? 0 : ac0) + sc[0] + sc[1] + sc[2] + sc[3];
+            if (acc_seen) acc_seen[z] = (rs0 ? 0 : as0) + cnt;
         }
         for (int o = tid; o < cnt * K; o += 256) {
             logits[z * l_cs + o] = L[o];
             dlogits[z * d_cs + o] = D[o];
         }
-        if (db && tid < K) {
+        if (SMALLK && db && wid == 0) {  // four image groups per class, then xor-combined
+            const int k = lane & 15, g = lane >> 4;
+            float v = 0.f;
+            if (k < K)
+                for (int b = g; b < cnt; b += 4) v += D[b * K + k];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            if (lane < K) db[z * db_cs + lane] = v;
+        } else if (db && tid < K) {
             float v = 0.f;
             for (int b = 0; b < cnt; ++b) v += D[b * K + tid];
             db[z * db_cs + tid] = v;
@@ -521,13 +555,30 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     }
     // 3. weight gradient, this block's share: dW[k][f] = sum_b D[b][k] x[b][f] (dw null: the
     // caller takes it elsewhere — DP-SGD clips it per image first)
-    if (dw) {
+    if (SMALLK && dw) {  // 16-column tiles of dW [K][F]; A = D^T (class x image), B = x
+        const int mn = lane & 15, kk = lane >> 4;
+        for (int tt = part + S * wid; tt < F / 16; tt += 4 * S) {
+            const int f0 = tt * 16;
+            hf32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int b0 = 0; b0 < cnt; b0 += 4) {
+                const int b = b0 + kk;
+                const bool ok = b < cnt;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ok && mn < K ? D[b * K + mn] : 0.f,
+                                                           ok ? Xs[b * FP + f0 + mn] : 0.f, acc,
+                                                           0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = 4 * kk + r;
+                if (k < K) dw[z * dw_cs + (int64_t)k * F + f0 + mn] = acc[r];
+            }
+        }
+    } else if (dw) {
         const int per = (K * F + S - 1) / S, e0 = part * per, e1 = min(K * F, e0 + per);
         for (int e = e0 + tid; e < e1; e += 256) {
             const int k = e / F, f = e - k * F;
             float a0 = 0.f, a1 = 0.f;
             int b = 0;
-#pragma unroll 4
             for (; b + 1 < cnt; b += 2) {
                 a0 = fmaf(D[b * K + k], X(b, f), a0);
                 a1 = fmaf(D[(b + 1) * K + k], X(b + 1, f), a1);
@@ -537,14 +588,38 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         }
     }
     // 4. input gradient through Dropout + ReLU, this block's share: dx[b][f] = sum_k D[b][k] W[k][f]
-    if (dx) {
+    if (SMALLK && dx) {  // tiles of 16 images x 16 columns of dX; A = D (image x class), B = W
+        const int mn = lane & 15, kk = lane >> 4;
+        for (int tt = part + S * wid; tt < 2 * (F / 16); tt += 4 * S) {
+            const int t = tt & 1, f0 = (tt >> 1) * 16;
+            if (t * 16 >= cnt) continue;  // wave-uniform
+            const int ia = t * 16 + mn;
+            hf32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int k0 = 0; k0 < K; k0 += 4) {
+                const int k = k0 + kk;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                    k < K && ia < cnt ? D[ia * K + k] : 0.f, k < K ? Ws[k * FP + f0 + mn] : 0.f,
+                    acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int img = t * 16 + 4 * kk + r, f = f0 + mn;
+                if (img < cnt) {
+                    float v = acc[r];
+                    if (mask) v = Ms[img * F + f] ? v * scale : 0.f;
+                    if (relu_in && !(Xs[img * FP + f] > 0.f)) v = 0.f;
+                    dx[z * dx_cs + (int64_t)img * F + f] = v;
+                }
+            }
+        }
+    } else if (dx) {
         const int e0 = dx_e0, e1 = dx_e1;
         for (int eb = e0 + tid; eb < e1; eb += 4 * 256) {  // keep-mask bytes of 4 outputs first
             uint8_t mk[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int e = eb + 256 * u;
-                mk[u] = (mask && e < e1) ? (SMALLK ? Ms[e - e0] : mask[z * m_cs + e]) : 1;
+                mk[u] = (mask && e < e1) ? mask[z * m_cs + e] : 1;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -552,13 +627,7 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
                 if (e >= e1) break;
                 const int img = e / F, f = e - img * F;
                 float acc = 0.f;
-                if constexpr (SMALLK) {  // unrolled: the LDS reads issue ahead of the chain
-#pragma unroll
-                    for (int k = 0; k < KMAX; ++k)
-                        if (k < K) acc = fmaf(D[img * K + k], Wt(k, f), acc);
-                } else {
-                    for (int k = 0; k < K; ++k) acc = fmaf(D[img * K + k], Wt(k, f), acc);
-                }
+                for (int k = 0; k < K; ++k) acc = fmaf(D[img * K + k], Wt(k, f), acc);
                 if (mask) acc = mk[u] ? acc * scale : 0.f;
                 if (relu_in && !(X(img, f) > 0.f)) acc = 0.f;
                 dx[z * dx_cs + e] = acc;

@@ -1,7 +1,7 @@
-# usage (GPU box): bash tools/ab_variants.sh <tag> "<configs>" "<tests>" "<variant>"... — bench
-# lines of each variant (tools/ab_attr.py arguments, e.g. "lib=ab_lib/base/libfedhip.so" or
-# "trainer.relocate_rows=0"; "-" = the tree as is), interleaved twice per config; the named
-# GPU tests first
+# usage (GPU box): [REPS=2] [STEPS=20] bash tools/ab_variants.sh <tag> "<configs>" "<tests>"
+# "<variant>"... — bench lines of each variant (tools/ab_attr.py arguments, e.g.
+# "lib=ab_lib/base/libfedhip.so" or "fuse_pool2=0"; "-" = the tree as is), interleaved REPS
+# times per config, STEPS timed rounds each; the named GPU tests first
 set -e
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$1; mkdir -p $O
@@ -11,11 +11,11 @@ if [ -n "$TESTS" ]; then
   tail -1 $O/tests.log
 fi
 for C in $CONFIGS; do
-  for rep in 1 2; do
+  for rep in $(seq 1 ${REPS:-2}); do
     i=0
     for v in "$@"; do
       i=$((i+1)); A=$v; [ "$v" = "-" ] && A=""
-      timeout -k 10 300 python tools/ab_attr.py $A -- --config $C --steps 20 --warmup 5 --no-cpu-baseline --rounds-target 0 --no-instances --no-k2 --detail-out '' > $O/${C}_v${i}_${rep}.json 2>> $O/ab.err
+      timeout -k 10 300 python tools/ab_attr.py $A -- --config $C --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline --rounds-target 0 --no-instances --no-k2 --detail-out '' > $O/${C}_v${i}_${rep}.json 2>> $O/ab.err
       python -c "import json; d=json.loads(open('$O/${C}_v${i}_${rep}.json').read().strip().splitlines()[-1]); print('$C', '[$v]', d['value'], d['ms_per_step'])" | tee -a $O/ab.txt
     done
   done

@@ -34,6 +34,9 @@ def run(op, cin, hw, cout, k, s, nc, reps, B=32):
     bpart = torch.zeros(nc, cin, tiles, 2, dtype=torch.float64, device=dev)
     aff = (torch.rand(nc, cin, device=dev) + 0.5, torch.randn(nc, cin, device=dev))
     mean = torch.randn(nc, cin, device=dev)
+    ph = (oh - 2) // 2  # fwdpool / fwdthenpool: the (hw-2)-map in the plane pooled (K2 conv2)
+    p2 = torch.empty(nc, B, cout, ph, ph, device=dev)
+    i2 = torch.empty(nc, B, cout, ph, ph, dtype=torch.uint8, device=dev)
 
     def once():
         if op == "fwdbn":  # + BN statistics epilogue, input BN affine applied on load (KT)
@@ -45,6 +48,13 @@ def run(op, cin, hw, cout, k, s, nc, reps, B=32):
         elif op == "wgradbn":  # input BN affine applied on load (KT)
             ops.conv2d_wgrad(x, dy, dw, None, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt,
                              in_affine=aff)
+        elif op == "fwdpool":  # conv -> ReLU -> 2x2 pool in one launch (fh_conv2d_fwd_relu_pool)
+            ops.conv2d_fwd_relu_pool(x, w, None, y, p2, i2, nc, B, cin, hw, cout, oh - 2,
+                                     counts=cnt)
+        elif op == "fwdthenpool":  # the same as conv(relu) + maxpool2_fwd launches
+            ops.conv2d_fwd(x, w, None, y, nc, B, cin, hw, hw, cout, k, s, pad, relu=True,
+                           counts=cnt)
+            ops.maxpool2_fwd(y, p2, i2, nc, B, cout, oh - 2, oh - 2, counts=cnt)
         elif op == "fwd":
             ops.conv2d_fwd(x, w, None, y, nc, B, cin, hw, hw, cout, k, s, pad, counts=cnt)
         elif op == "dgrad":
