@@ -37,16 +37,18 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int OH = H / 2, OW = W / 2;
-    const int64_t per_img = (int64_t)C * OH * OW;
-    const int64_t total = cnt * per_img;
+    // 32-bit unsigned index arithmetic (a client's batch is < 2^31 elements; the 64-bit
+    // divisions cost more than the pool itself)
+    const uint32_t per_img = (uint32_t)(C * OH * OW);
+    const uint32_t total = (uint32_t)cnt * per_img;
     const float* xb = x + z * x_cs;
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int ow = (int)(e % OW);
-        const int64_t t = e / OW;
-        const int oh = (int)(t % OH);
-        const int64_t plane = t / OH;  // img*C + c
-        const float* p = xb + plane * xh * xw + (2 * oh) * xw + 2 * ow;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += gridDim.x * blockDim.x) {
+        const uint32_t t = e / (uint32_t)OW;
+        const int ow = (int)(e - t * (uint32_t)OW);
+        const uint32_t plane = t / (uint32_t)OH;  // img*C + c
+        const int oh = (int)(t - plane * (uint32_t)OH);
+        const float* p = xb + (int64_t)plane * xh * xw + (2 * oh) * xw + 2 * ow;
         float v0 = p[0], v1 = p[1], v2 = p[xw], v3 = p[xw + 1];
         if (in_scale) {  // input = BN pre-activation: relu(x*scale + shift), bn_apply's ops
             const int c = (int)(plane % C);
@@ -73,7 +75,7 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
             }
             m = keep ? m * scale : 0.f;
         }
-        y[z * y_cs + plane * yh * yw + oh * yw + ow] = m;
+        y[z * y_cs + (int64_t)plane * yh * yw + oh * yw + ow] = m;
     }
 }
 
@@ -94,13 +96,14 @@ maxpool2_bwd_kernel(const float* __restrict__ dy, int64_t dy_cs, const uint8_t* 
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int OH = H / 2, OW = W / 2;
-    const int64_t total = cnt * (int64_t)C * OH * OW;
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int ow = (int)(e % OW);
-        const int64_t t = e / OW;
-        const int oh = (int)(t % OH);
-        const int64_t plane = t / OH;
+    const uint32_t total = (uint32_t)cnt * (uint32_t)(C * OH * OW);  // 32-bit: see the fwd
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += gridDim.x * blockDim.x) {
+        const uint32_t t = e / (uint32_t)OW;
+        const int ow = (int)(e - t * (uint32_t)OW);
+        const uint32_t pl = t / (uint32_t)OH;
+        const int oh = (int)(t - pl * (uint32_t)OH);
+        const int64_t plane = pl;
         float g = dy[z * dy_cs + plane * gh * gw + oh * gw + ow];
         if (mask) g = mask[z * m_cs + e] ? g * scale : 0.f;
         const int a = idx[z * i_cs + e];
@@ -766,16 +769,16 @@ gather_u8_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ l
                  const uint64_t* __restrict__ seed_dev) {
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
-    const int64_t plane = (int64_t)H * W, per = plane * C;
-    const int64_t total = (int64_t)cnt * per;
+    const uint32_t plane = (uint32_t)(H * W), per = plane * (uint32_t)C;
+    const uint32_t total = (uint32_t)cnt * per;  // 32-bit index arithmetic (< 2^31 per client)
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t b = e / per;
-        const int64_t r = e - b * per;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += gridDim.x * blockDim.x) {
+        const uint32_t b = e / per;
+        const uint32_t r = e - b * per;
         const int c = (int)(r / plane);
-        const int64_t p = r - (int64_t)c * plane;
-        const int yy = (int)(p / W), xx = (int)(p - (int64_t)yy * W);
+        const uint32_t p = r - (uint32_t)c * plane;
+        const int yy = (int)(p / (uint32_t)W), xx = (int)(p - (uint32_t)yy * (uint32_t)W);
         int ci = pad, cj = pad, fl = 0;
         if (pad > 0 || flip) {
             if (aug_in) {
