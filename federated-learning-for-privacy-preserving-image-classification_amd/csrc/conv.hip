@@ -2560,10 +2560,18 @@ __device__ __forceinline__ void linear_wgrad_skinny_body(
         if (m < M) wz[(int64_t)m * K] = acc[r];
     }
     if (db && kblock == 0 && wid == 0 && h == 0 && mok) {
+        // every image's term loaded first, then added in image order (the loop's loads had
+        // waited for each other: 32 dependent round trips in the kernel's tail — r04)
+        float t[32];
+#pragma unroll
+        for (int b = 0; b < 32; ++b)
+            t[b] = b < cnt ? (rowscale ? rowscale[(int64_t)z * batch + b] * yz[(int64_t)b * M]
+                                       : yz[(int64_t)b * M])
+                           : 0.f;
         float v = 0.f;
-        for (int b = 0; b < cnt; ++b)
-            v += rowscale ? rowscale[(int64_t)z * batch + b] * yz[(int64_t)b * M]
-                          : yz[(int64_t)b * M];
+#pragma unroll
+        for (int b = 0; b < 32; ++b)
+            if (b < cnt) v += t[b];
         db[z * db_cs + m0 + r32] = v;
     }
 }

@@ -1,5 +1,6 @@
 """Linear-layer (classifier) launch costs per client count: fwd / dgrad / wgrad of
-CIFAR10CNN's fc1-fc3 on packed clients (32 images each), HIP-event timed."""
+CIFAR10CNN's fc1-fc3 on packed clients (32 images each), HIP-event timed.
+[--lib path/libfedhip.so] times another build."""
 import os
 import sys
 
@@ -7,7 +8,10 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "federated-learning-for-privacy-preserving-image-classification_amd"))
-from fedhip import ops  # noqa: E402
+from fedhip import _lib, ops  # noqa: E402
+
+if "--lib" in sys.argv:  # A/B: time another libfedhip.so (tools/build_base_lib.sh)
+    _lib.load.__defaults__ = (sys.argv[sys.argv.index("--lib") + 1],)
 
 LAYERS = [(2048, 512), (512, 256), (256, 10)]
 if os.environ.get("FH_BENCH_LAYERS"):  # e.g. "3136x128,128x10" (SimpleCNN)
