@@ -367,6 +367,12 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
                         for (int jj = 0; jj < FN; ++jj)
                             acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(
                                 av[j & 1][i], bv[j & 1][jj], acc[i][jj], 0, 0, 0);
+                    // schedule: the next item's operand reads (DS read group), then this item's
+                    // MFMAs — one group per item, so each wait covers only the reads issued an
+                    // item earlier (r04: the compiler had paired items and waited on fresh reads;
+                    // per launch 1-4 %, the 8x8 FWD at 23 clients 16 %, profiles/r04_h/)
+                    if (j + 1 < NI) __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, FM * FN, 0);
                 }
             }
             if (more) store(buf ^ 1, c0 + CK);
