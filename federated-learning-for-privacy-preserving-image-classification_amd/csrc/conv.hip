@@ -770,13 +770,28 @@ conv_c1_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* __res
 // maxpool2_fwd_kernel does (strict >, window order) -> y (pooled planes yh x yw, the map in the
 // top-left corner) and the uint8 argmax idx; the full-resolution ReLU output is never written
 // (the backward's ReLU mask at the argmax is y > 0: conv_c1_wgrad_kernel<true>).
+// U8Src (non-null data): the input is read from the raw uint8 images instead of x — the
+// step's batch gather (fh_gather_u8: x = (u / 255 - mean) / std, no crop / flip, one channel)
+// folded into this launch: x is still written (each thread its own 2x2 window's pixels, for the
+// weight gradient's and the evaluation's reads) and so are the labels (r04, one launch less
+// per SimpleCNN step)
+struct U8Src {
+    const uint8_t* data;    // [N][H][W]
+    const int64_t* labels;  // [N]
+    const int64_t* gidx;    // [z][batch] sample of each batch slot
+    int64_t g_cs;
+    int64_t* ylab;          // [z][batch] labels out
+    int64_t yl_cs;
+    float mean, stdv;
+};
+
 template <int COUT>
 __global__ void __launch_bounds__(256)
 conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ w,
                         int64_t w_cs, const float* __restrict__ bias, int64_t b_cs,
                         float* __restrict__ y, int64_t y_cs, uint8_t* __restrict__ idx,
                         int64_t i_cs, const int32_t* __restrict__ counts, int batch, int H,
-                        int W, int yh, int yw) {
+                        int W, int yh, int yw, const U8Src src) {
     __shared__ float ws[COUT * 9], bs[COUT];
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
@@ -789,14 +804,35 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
     const int img = n / OHW, q = n - img * OHW, oh = q / OW, ow = q - oh * OW;
     const float* xi = x + z * x_cs + (int64_t)img * H * W;
     float t[4][4];  // input rows 2oh-1 .. 2oh+2, columns 2ow-1 .. 2ow+2 (zero padding)
+    if (src.data) {  // the gather folded in: gather_u8_kernel's operations on the raw bytes
+        const int64_t s = src.gidx[z * src.g_cs + img];
+        const uint8_t* si = src.data + s * H * W;
+        float* xo = const_cast<float*>(xi);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int yy = 2 * oh + i - 1, xx = 2 * ow + j - 1;
-            t[i][j] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) ? xi[yy * W + xx]
-                                                                               : 0.f;
-        }
+            for (int j = 0; j < 4; ++j) {
+                const int yy = 2 * oh + i - 1, xx = 2 * ow + j - 1;
+                float v = 0.f;
+                if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+                    const float u = __fdiv_rn((float)si[yy * W + xx], 255.f);
+                    v = __fdiv_rn(u - src.mean, src.stdv);
+                    if (i >= 1 && i <= 2 && j >= 1 && j <= 2) xo[yy * W + xx] = v;  // own window
+                }
+                t[i][j] = v;
+            }
+        if (q == 0) src.ylab[z * src.yl_cs + img] = src.labels[s];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int yy = 2 * oh + i - 1, xx = 2 * ow + j - 1;
+                t[i][j] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                              ? xi[yy * W + xx]
+                              : 0.f;
+            }
+    }
     float* yo = y + z * y_cs + (int64_t)img * COUT * yh * yw + oh * yw + ow;
     uint8_t* io = idx + z * i_cs + (int64_t)img * COUT * OHW + q;
 #pragma unroll 2
@@ -2020,11 +2056,43 @@ extern "C" int fh_conv2d_c1_pool_fwd(const float* x, int64_t x_cs, const float* 
     hipStream_t st = as_stream(stream);
     if (cout == 32)
         FH_LAUNCH(conv_c1_pool_fwd_kernel<32>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
-                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw);
+                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, U8Src{});
     else
         FH_LAUNCH(conv_c1_pool_fwd_kernel<64>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
-                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw);
+                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, U8Src{});
     FH_LAUNCH_CHECK("conv2d_c1_pool_fwd");
+    return FH_OK;
+}
+
+// fh_conv2d_c1_pool_fwd with the step's batch gather folded in (U8Src): x [z][batch][h][w] is
+// WRITTEN from the raw uint8 images data[gidx[z][b]] ([N][h][w], one channel) with
+// fh_gather_u8's normalisation (no crop / flip), and y_lab[z][b] = labels[gidx[z][b]] — the
+// same x / labels fh_gather_u8 would leave, bit for bit, and the same pooled output.
+extern "C" int fh_conv2d_c1_pool_fwd_u8(const uint8_t* data, const int64_t* labels,
+                                        const int64_t* gidx, int64_t g_cs, float mean, float stdv,
+                                        float* x, int64_t x_cs, int64_t* y_lab, int64_t yl_cs,
+                                        const float* w, int64_t w_cs, const float* bias,
+                                        int64_t b_cs, float* y, int64_t y_cs, uint8_t* idx,
+                                        int64_t i_cs, const int32_t* counts, int32_t nclients,
+                                        int32_t batch, int32_t h, int32_t w_, int32_t cout,
+                                        int32_t yh, int32_t yw, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0 && h >= 2 && w_ >= 2 && !(h & 1) && !(w_ & 1) &&
+               yh >= h / 2 && yw >= w_ / 2, "conv2d_c1_pool_fwd_u8: bad shape");
+    FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_fwd_u8: cout %d (32 or 64)", cout);
+    FH_REQUIRE(stdv != 0.f, "conv2d_c1_pool_fwd_u8: zero std");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(data && labels && gidx && x && y_lab && w && y && idx,
+               "conv2d_c1_pool_fwd_u8: null pointer");
+    const U8Src src{data, labels, gidx, g_cs, y_lab, yl_cs, mean, stdv};
+    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256), (unsigned)nclients);
+    hipStream_t st = as_stream(stream);
+    if (cout == 32)
+        FH_LAUNCH(conv_c1_pool_fwd_kernel<32>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
+                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, src);
+    else
+        FH_LAUNCH(conv_c1_pool_fwd_kernel<64>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
+                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, src);
+    FH_LAUNCH_CHECK("conv2d_c1_pool_fwd_u8");
     return FH_OK;
 }
 

@@ -88,6 +88,8 @@ SIGNATURES = {
                                           I32, I32, I32, I32, I32, P, SZ, P]),
     "fh_maxpool2_bwd_ymask": (I32, [P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32,
                                     I32, I32, I32, I32, P]),
+    "fh_conv2d_c1_pool_fwd_u8": (I32, [P, P, P, I64, F32, F32, P, I64, P, I64, P, I64, P, I64,
+                                       P, I64, P, I64, P, I32, I32, I32, I32, I32, I32, I32, P]),
     "fh_conv2d_c1_pool_fwd": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I32, I32, I32,
                                     I32, I32, I32, I32, P]),
     "fh_conv2d_c1_pool_wgrad": (I32, [P, I64, P, I64, P, I64, P, I64, P, I64, P, I64, P, SZ, P,

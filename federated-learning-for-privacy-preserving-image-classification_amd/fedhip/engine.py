@@ -372,8 +372,11 @@ class PackedTrainer:
             # host-side seed, plus the slots' global client ids when set
             net.seed_dev = views["seed"]
             self._gather(st["data"], st["labels"], views, n, st["sample_elems"])
-            self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
-                                adam_dev=views["adam"])
+            try:
+                self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
+                                    adam_dev=views["adam"])
+            finally:
+                net._src = None
             if arm and not ops.PROBE.all:
                 ops.PROBE.enabled = False
             net.seed_dev = None
@@ -432,6 +435,14 @@ class PackedTrainer:
         if data.dtype == torch.uint8:
             if self.transform is None:
                 raise FedHipError("uint8 images need a DataTransform (PackedTrainer.transform)")
+            tf = self.transform
+            if (net.family == "SimpleCNN" and net.fuse_input and net.fuse_pool1
+                    and data.dim() == 3 and len(tf.mean) == 1 and not tf.pad and not tf.flip
+                    and self.aug_record is None):
+                # the gather runs inside conv1's launch (net._fwd_simple); the caller clears
+                # _src once the step is issued / captured
+                net._src = (data, labels, views["gidx"], tf)
+                return
             ops.gather_u8(data, labels, views["gidx"], net.x, net.y, self.transform, n,
                           self.batch, counts=views["counts"], seed=net._seed(31),
                           seed_dev=net.seed_dev, aug_out=self.aug_record)
@@ -465,6 +476,7 @@ class PackedTrainer:
                     self._step_launches(n, views["counts"], views["reset"], first=False,
                                         adam_dev=views["adam"])
                 finally:
+                    net._src = None
                     if rec is not None:
                         prog = ops.Program.record_end(rec)
             net.seed_dev = None

@@ -185,6 +185,12 @@ class PackedNet:
         self.fuse_pool2 = True
         self._pool1_fused = False
         self._pool2_fused = False
+        # SimpleCNN training on raw uint8 images: the step's batch gather inside conv1's
+        # launch (fh_conv2d_c1_pool_fwd_u8; x and the labels are still written).  The trainer
+        # sets _src = (data, labels, gidx, transform) for the step it issues instead of the
+        # gather launch, and clears it after.
+        self.fuse_input = True
+        self._src = None
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -291,7 +297,12 @@ class PackedNet:
         h1, d1 = A("h1", 128), A("d1", 128)
         m1 = A("m1", 128, dtype=torch.uint8)
         self._pool1_fused = train and self.fuse_pool1
-        if self._pool1_fused:
+        if self._pool1_fused and self._src is not None:
+            data, labels, gidx, tf = self._src
+            ops.conv2d_c1_pool_fwd_u8(data, labels, gidx, tf, self.x, self.y,
+                                      W(P_, "conv1.weight"), W(P_, "conv1.bias"), p1, i1, n, B,
+                                      28, 28, 32, counts=cnt)
+        elif self._pool1_fused:
             ops.conv2d_c1_pool_fwd(self.x, W(P_, "conv1.weight"), W(P_, "conv1.bias"), p1, i1, n,
                                    B, 28, 28, 32, counts=cnt)
         else:

@@ -370,6 +370,25 @@ def conv2d_c1_pool_fwd(x, w, bias, y, idx, nclients, batch, h, wd, cout, counts=
     return y
 
 
+def conv2d_c1_pool_fwd_u8(data, labels, gidx, tf, x, y_lab, w, bias, y, idx, nclients, batch, h,
+                          wd, cout, counts=None):
+    """gather_u8 (no crop / flip, one channel) + conv2d_c1_pool_fwd in one launch
+    (fh_conv2d_c1_pool_fwd_u8): x and y_lab receive what gather_u8 would write, y / idx what
+    conv2d_c1_pool_fwd computes from that x."""
+    if data.dtype != torch.uint8 or data.dim() != 3 or len(tf.mean) != 1 or tf.pad or tf.flip:
+        raise FedHipError("conv2d_c1_pool_fwd_u8: one-channel uint8 [N, H, W] images, no crop / flip")
+    yh, yw = y.shape[-2], y.shape[-1]
+    ev = PROBE.begin(_conv_tag("fwd", 1, h, wd, cout, 3, 1) + "+pool")
+    call("fh_conv2d_c1_pool_fwd_u8", ptr(data), ptr(labels), ptr(gidx), _cs(gidx),
+         float(tf.mean[0]), float(tf.std[0]), ptr(x), _cs(x), ptr(y_lab), _cs(y_lab), ptr(w),
+         _cs(w), ptr(bias), _cs(bias), ptr(y), _cs(y), ptr(idx), _cs(idx), _counts(counts),
+         nclients, batch, h, wd, cout, yh, yw, stream_handle())
+    pooled = nclients * batch * cout * (h // 2) * (wd // 2)
+    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1),
+              nclients * (batch * h * wd + 4.0 * cout * 9) + 5.0 * pooled, nclients)
+    return y
+
+
 def conv2d_c1_pool_wgrad(x, dpool, idx, y, dw, db, nclients, batch, h, wd, cout, counts=None):
     """conv2d_c1_pool_fwd's weight gradient from the pooled gradient dpool (planes like y):
     maxpool2_bwd(xin = the ReLU output) + conv2d_wgrad in one pass

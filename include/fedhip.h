@@ -600,6 +600,20 @@ int fh_conv2d_c1_pool_fwd(const float* x, int64_t x_cs, const float* w, int64_t 
                           int64_t i_cs, const int32_t* counts, int32_t nclients, int32_t batch,
                           int32_t h, int32_t w_, int32_t cout, int32_t yh, int32_t yw,
                           void* stream);
+/* fh_conv2d_c1_pool_fwd with the step's batch gather folded in (r04): x [client][batch][h][w]
+ * is WRITTEN from the raw uint8 images data[gidx[client][b]] ([N][h][w], one channel) with
+ * fh_gather_u8's normalisation (x = (u / 255 - mean) / std; no crop / flip) and
+ * y_lab[client][b] = labels[gidx[client][b]] — fh_gather_u8's x and labels bit for bit — and
+ * the pooled output / argmax as fh_conv2d_c1_pool_fwd on that x.  Replaces gather +
+ * conv1 -> relu -> pool1 of SimpleCNN's training step (data_loader.py:298-301,
+ * models_pytorch.py:86-87). */
+int fh_conv2d_c1_pool_fwd_u8(const uint8_t* data, const int64_t* labels, const int64_t* gidx,
+                             int64_t g_cs, float mean, float stdv, float* x, int64_t x_cs,
+                             int64_t* y_lab, int64_t yl_cs, const float* w, int64_t w_cs,
+                             const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                             uint8_t* idx, int64_t i_cs, const int32_t* counts, int32_t nclients,
+                             int32_t batch, int32_t h, int32_t w_, int32_t cout, int32_t yh,
+                             int32_t yw, void* stream);
 /* fh_maxpool2_bwd (pitched planes: dy / y gh x gw, dx xh x xw) with the ReLU mask at the
  * argmax taken from the pooled output y (> 0), for a forward that never wrote the
  * full-resolution ReLU output (fh_conv2d_c1_pool_fwd); no dropout. */

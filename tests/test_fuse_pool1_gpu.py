@@ -85,3 +85,43 @@ def test_c1_pool_ops_match_separate_launches(nc, cout, plane):
     ops.conv2d_c1_pool_wgrad(x, dp, i, p, dw2, db2, nc, B, H, H, cout, counts=cnt)
     torch.cuda.synchronize()
     assert torch.equal(dw1, dw2) and torch.equal(db1, db2)
+
+
+def _u8_round(fuse_input, opt, sizes, rounds=2, graphs=True):
+    torch.manual_seed(0)
+    model = hm.ModelFactory.create_model("simple_cnn", dropout_rate=0.25).to(DEV)
+    S = len(sizes)
+    eng = PackedTrainer(model, capacity=S, batch=32, device=DEV)
+    eng.net.fuse_input = fuse_input
+    eng.use_graphs = graphs
+    eng.transform = ops.DataTransform.mnist()
+    for k in range(S):
+        eng.load_module_state(k, model)
+    g = torch.Generator().manual_seed(5)
+    data = torch.randint(0, 256, (sum(sizes), 28, 28), generator=g, dtype=torch.uint8).to(DEV)
+    labels = torch.randint(0, 10, (sum(sizes),), generator=g).to(DEV)
+    offs = [sum(sizes[:k]) for k in range(S)]
+    gen = torch.Generator().manual_seed(11)
+    metrics = []
+    for r in range(rounds):
+        plan = eng.make_plan(sizes, 1, generator=gen)
+        metrics.append(eng.run_round(data, labels, offs, plan, optimizer_type=opt, lr=1e-2,
+                                     seed=r))
+    torch.cuda.synchronize()
+    return eng, metrics
+
+
+@pytest.mark.parametrize("opt,graphs", [("sgd", True), ("adam", True), ("sgd", False)])
+def test_gather_in_conv1_rounds_bit_identical(opt, graphs):
+    """r04: the uint8 batch gather inside conv1's launch (fh_conv2d_c1_pool_fwd_u8) leaves the
+    same x / labels as fh_gather_u8 and the same rounds (graph replay and eager)."""
+    sizes = [130, 70, 33, 9]
+    a, ma = _u8_round(True, opt, sizes, graphs=graphs)
+    b, mb = _u8_round(False, opt, sizes, graphs=graphs)
+    assert a.net._src is None and b.net._src is None
+    assert torch.equal(a.net.x, b.net.x) and torch.equal(a.net.y, b.net.y)
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.state1, b.state1)
+    for ra, rb in zip(ma, mb):
+        for x, y in zip(ra, rb):
+            assert (x.loss, x.accuracy) == (y.loss, y.accuracy)
