@@ -1,7 +1,7 @@
 """A/B of one PackedNet plan attribute on the bench (no environment knobs in the product):
     python tools/ab_attr.py fuse_pool2=0 trainer.use_graphs=0 -- --config K2 --steps 10
-sets the attribute on every PackedNet (trainer.<attr>: every PackedTrainer) right after
-construction, then runs bench.main() with
+sets the attribute on every PackedNet (trainer.<attr>: every PackedTrainer; fillI=F: lane I's
+split-K fill fraction) right after construction, then runs bench.main() with
 the arguments after `--`.  lib=<path> loads that libfedhip.so instead (tools/build_base_lib.sh)."""
 import os
 import sys
@@ -14,11 +14,13 @@ sys.path.insert(0, os.path.join(os.path.dirname(here),
 
 def main():
     cut = sys.argv.index("--")
-    sets, tsets, lib = {}, {}, None
+    sets, tsets, fills, lib = {}, {}, {}, None
     for kv in sys.argv[1:cut]:
         k, v = kv.split("=", 1)
         if k == "lib":
             lib = v
+        elif k.startswith("fill"):  # fillI=F: lane I's split-K fill fraction (LanedTrainer.fill)
+            fills[int(k[4:])] = float(v)
         elif k.startswith("trainer."):
             tsets[k[len("trainer."):]] = bool(int(v))
         else:
@@ -48,6 +50,16 @@ def main():
             setattr(self, k, v)
 
     engine.PackedTrainer.__init__ = tpatched
+    from fedhip import lanes
+    linit = lanes.LanedTrainer.__init__
+
+    def lpatched(self, *a, **kw):
+        linit(self, *a, **kw)
+        for i, f in fills.items():
+            if i < len(self.fill):
+                self.fill[i] = f
+
+    lanes.LanedTrainer.__init__ = lpatched
     sys.argv = [sys.argv[0]] + sys.argv[cut + 1:]
     import bench
     bench.main()
