@@ -2989,10 +2989,12 @@ static int linear_bwd_fused_impl(const float* x, int64_t x_cs, const float* dy, 
     }
     const int kb = (int)ceil_div(in_f, 128);  // WGRAD k-blocks (spare waves return)
     const int nw = kb * (int)ceil_div(out_f, 32);
-    if (kLinearSkinny != 2 && (int64_t)kb * nclients >= fill(256)) {
+    if (kLinearSkinny != 2 && in_f % 128 == 0 && (int64_t)kb * nclients >= fill(256)) {
         // wide launches: the two roles as two kernels — in one grid every WGRAD workgroup
         // would carry the DGRAD role's 48 KB of LDS and stream dW at 3 workgroups per CU
-        // (fc1 at 32 clients: 190 us fused vs ~105 us as two launches)
+        // (fc1 at 32 clients: 190 us fused vs ~105 us as two launches).  SimpleCNN's fc1
+        // (in_f = 3136, one 32-feature DGRAD tile per workgroup) stays one launch at every
+        // width (r04: one launch less per K2 step)
         FH_LAUNCH(linear_wgrad_skinny_kernel,
                   dim3((unsigned)kb, (unsigned)ceil_div(out_f, 32), nclients),
                   dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs,
