@@ -1460,6 +1460,47 @@ static int dconv_launch_w(const DPlan& p, dim3 grid, const DConvArgs& a, hipStre
     return FH_E_UNSUPPORTED;
 }
 
+// Dual-role layer backward (dconv_wgrad_dual_kernel).  fh_conv_pair(mode > 0) arms the next
+// WGRAD on this thread: when it plans the quadrant-wave kernel with 128-pixel stages and its
+// dW needs no reduction launch of its own (one split, or a deferred slab), the launch is held
+// here and issued together with the next direct DGRAD on the same stream and map width
+// (BM = 32, CK = 8 plan) as one grid.  Anything else flushes it as its own launch first;
+// fh_conv_pair(0) flushes and disarms.  mode 1: WGRAD workgroups first, 2: DGRAD first.
+struct PendingWgrad {
+    bool on = false;
+    int w = 0, mode = 1;
+    dim3 grid;
+    DWArgs d{};
+    hipStream_t st = nullptr;
+};
+thread_local int g_pair_mode = 0;
+thread_local PendingWgrad g_pend;
+
+static int flush_pending_wgrad() {
+    if (!g_pend.on) return FH_OK;
+    g_pend.on = false;
+    const PendingWgrad& q = g_pend;
+    if (q.w == 32) FH_LAUNCH((dwgrad_q_kernel<32, 128, false>), q.grid, dim3(256), 0, q.st, q.d);
+    else if (q.w == 16) FH_LAUNCH((dwgrad_q_kernel<16, 128, false>), q.grid, dim3(256), 0, q.st, q.d);
+    else FH_LAUNCH((dwgrad_q_kernel<8, 128, false>), q.grid, dim3(256), 0, q.st, q.d);
+    FH_LAUNCH_CHECK("conv2d_wgrad direct (held)");
+    return FH_OK;
+}
+
+template <int W, bool BNB>
+static int launch_dual(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_t st) {
+    (void)p;
+    const PendingWgrad& q = g_pend;
+    const int64_t nw = (int64_t)q.grid.x * q.grid.y * q.grid.z;
+    const int64_t nd = (int64_t)grid.x * grid.y * grid.z;
+    FH_REQUIRE(nw + nd < (1ll << 31), "dual conv backward: grid %lld + %lld", (long long)nw,
+               (long long)nd);
+    FH_LAUNCH((dconv_wgrad_dual_kernel<W, BNB>), dim3((unsigned)(nw + nd)), dim3(256), 0, st,
+              q.d, (int)q.grid.x, (int)q.grid.y, (int)nw, a, (int)grid.x, (int)grid.y,
+              (int)nd, q.mode == 1 ? 1 : 0);
+    return FH_OK;
+}
+
 template <int OP, int S = 1>
 static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes, int sp,
                      hipStream_t st, const char* name, bool* pooled = nullptr) {
@@ -1486,7 +1527,28 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
               (unsigned)(nclients * p.splits));
     if (p.splits > 1) a.out = (float*)ws;
     int rc;
-    if constexpr (S == 2) {
+    bool dual = false;
+    if constexpr (OP == OP_DGRAD && S == 1) {
+        if (g_pend.on) {
+            if (g_pend.st == st && g_pend.w == w && p.bm == 32 && p.ck == 8 && a.wvec) {
+                const bool bnb = a.bn_part && p.splits == 1;
+                rc = w == 32 ? (bnb ? launch_dual<32, true>(p, grid, a, st)
+                                    : launch_dual<32, false>(p, grid, a, st))
+                   : w == 16 ? (bnb ? launch_dual<16, true>(p, grid, a, st)
+                                    : launch_dual<16, false>(p, grid, a, st))
+                             : (bnb ? launch_dual<8, true>(p, grid, a, st)
+                                    : launch_dual<8, false>(p, grid, a, st));
+                g_pend.on = false;
+                if (rc) return rc;
+                dual = true;
+            } else if (const int fr = flush_pending_wgrad()) {
+                return fr;
+            }
+        }
+    }
+    if (dual) {
+        rc = FH_OK;
+    } else if constexpr (S == 2) {
         rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
     } else if ((a.bn_part || (a.pool_y && p.bm != 32)) && p.splits == 1) {
@@ -1716,6 +1778,16 @@ extern "C" int fh_set_fill_fraction(float fraction) {
 }
 
 extern "C" float fh_get_fill_fraction(void) { return g_fill; }
+
+extern "C" int fh_conv_pair(int32_t mode) {
+    FH_REQUIRE(mode >= 0 && mode <= 2, "conv_pair: mode %d", mode);
+    if (mode > 0) {
+        g_pair_mode = mode;
+        return FH_OK;
+    }
+    g_pair_mode = 0;
+    return flush_pending_wgrad();
+}
 
 extern "C" size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
                                           int32_t w_, int32_t cout, int32_t kh, int32_t kw,
@@ -2220,6 +2292,8 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
                              int64_t* defer_boff = nullptr) {
     // defer_splits (fh_conv2d_wgrad_deferred): a split plan leaves its partials in the
     // workspace for the optimizer step to sum; the reduction launch is skipped
+    const int pair = g_pair_mode;  // fh_conv_pair arms one call
+    g_pair_mode = 0;
     if (defer_splits) *defer_splits = 1;
     if (defer_boff) *defer_boff = 0;
     int oh, ow;
@@ -2342,6 +2416,14 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
             if (w_ == 32) FH_LAUNCH((dwgrad_q_kernel<32, 64, true>), grid, dim3(256), 0, st, d);
             else if (w_ == 16) FH_LAUNCH((dwgrad_q_kernel<16, 64, true>), grid, dim3(256), 0, st, d);
             else FH_LAUNCH((dwgrad_q_kernel<8, 64, true>), grid, dim3(256), 0, st, d);
+        } else if (pair && (p.splits == 1 || defer_splits)) {  // held for the next DGRAD
+            if (const int fr = flush_pending_wgrad()) return fr;
+            g_pend.w = w_;
+            g_pend.mode = pair;
+            g_pend.grid = grid;
+            g_pend.d = d;
+            g_pend.st = st;
+            g_pend.on = true;
         } else {
             if (w_ == 32) FH_LAUNCH((dwgrad_q_kernel<32, 128, false>), grid, dim3(256), 0, st, d);
             else if (w_ == 16) FH_LAUNCH((dwgrad_q_kernel<16, 128, false>), grid, dim3(256), 0, st, d);

@@ -129,8 +129,23 @@ struct DGeom {
 // step, e.g. DGRAD W=32 BM=32: 96 -> 114 VGPRs, 4 -> 3 waves per SIMD)
 // BM = 64: two waves per SIMD (the W=8 FWD statistics instance needed 260 registers, one
 // wave per SIMD; its 68 KB of LDS fit two workgroups per CU)
+// LDS floats of one dconv workgroup (the stage buffers, or the statistics image when larger)
+template <int OP, int W, int BM, int CK, int S, bool BNB>
+constexpr int dconv_lds_floats() {
+    using G = DGeom<W>;
+    constexpr int PRS = S == 1 ? G::SEGR + 2 : 2 * G::SEGR + 1;
+    constexpr int PW = S * W + 2, PR = G::NI * PRS;
+    constexpr int CSTR = S == 1 ? PR * PW : ((PR * PW) | 1);
+    constexpr int MAIN = 2 * 9 * CK * (BM + 1) + 2 * CK * CSTR;
+    constexpr int STAT = !BNB ? 0 : BM * kStatPitch + (OP == OP_DGRAD ? 3 * BM : 0);
+    return STAT > MAIN ? STAT : MAIN;
+}
+
+// the workgroup body; smem holds dconv_lds_floats() floats (dconv_kernel's own array, or
+// the array a dual-role launch shares with a WGRAD body: dconv_wgrad_dual_kernel)
 template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC, int S = 1, bool BNB = false>
-__global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DConvArgs a) {
+__device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int bx, int by,
+                                           int bz) {
     using G = DGeom<W>;
     static_assert(S == 1 || (S == 2 && OP == OP_FWD), "stride 2: forward only");
     static_assert(!BNB || S == 1, "statistics epilogue: stride 1");
@@ -155,15 +170,13 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
     constexpr int LDS_MAIN = 2 * KS * BMP + 2 * PE;
     constexpr int LDS_STAT = !BNB ? 0 : BM * kStatPitch + (OP == OP_DGRAD ? 3 * BM : 0);
     constexpr int LDS_N = LDS_STAT > LDS_MAIN ? LDS_STAT : LDS_MAIN;
-    __shared__ float smem[LDS_N];
+    static_assert(LDS_N == dconv_lds_floats<OP, W, BM, CK, S, BNB>(), "dconv LDS size");
     float (*As)[KS * BMP] = reinterpret_cast<float (*)[KS * BMP]>(smem);
     float (*Ps)[PE] = reinterpret_cast<float (*)[PE]>(smem + 2 * KS * BMP);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WAVES_N, wn = wid % WAVES_N;
-    int bx, by, bz;
-    block_xyz(bx, by, bz);
     const int z = bz / a.splits;
     const int split = bz - z * a.splits;
     const int cnt = a.counts ? a.counts[z] : a.batch;
@@ -617,6 +630,14 @@ __global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DCon
             }
         }
     }
+}
+
+template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC, int S = 1, bool BNB = false>
+__global__ void __launch_bounds__(256, BM == 64 ? 2 : 1) dconv_kernel(const DConvArgs a) {
+    __shared__ float smem[dconv_lds_floats<OP, W, BM, CK, S, BNB>()];
+    int bx, by, bz;
+    block_xyz(bx, by, bz);
+    dconv_body<OP, W, BM, WAVES_M, CK, WVEC, S, BNB>(a, smem, bx, by, bz);
 }
 
 // ---------------------------------------------------------------------------
@@ -1297,7 +1318,8 @@ constexpr int dwq_lds_floats(int W, int SPX, bool DB) {
 }
 
 template <int W, int SPX, bool DB>
-__global__ void __launch_bounds__(256, 3) dwgrad_q_kernel(const DWArgs a) {
+__device__ __forceinline__ void dwgrad_q_body(const DWArgs& a, float* smem, int bx, int by,
+                                              int bz) {
     constexpr int H = W, HW = H * W;
     constexpr int SR = SPX / W;
     constexpr int SEGR = SR < H ? SR : H, NI = SR / SEGR;
@@ -1313,13 +1335,10 @@ __global__ void __launch_bounds__(256, 3) dwgrad_q_kernel(const DWArgs a) {
     static_assert(SR % SEGR == 0 && (SR <= H || SR % H == 0), "stage geometry");
     static_assert(!DB || SR % 2 == 0 || SR == 1, "half-stage store point");
     static_assert(dwq_lds_floats(W, SPX, DB) * 4 <= 160 * 1024 / 3, "three workgroups per CU");
-    __shared__ float smem[dwq_lds_floats(W, SPX, DB)];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int cq = wid & 1, nq = wid >> 1;  // this wave's 16x16 quadrant (co half, ci half)
-    int bx, by, bz;
-    block_xyz(bx, by, bz);
     const int split = bx, z = bz;
     const int ntile_ci = a.cin / 32;
     const int co0 = (by / ntile_ci) * 32, ci0 = (by % ntile_ci) * 32;
@@ -1470,6 +1489,39 @@ __global__ void __launch_bounds__(256, 3) dwgrad_q_kernel(const DWArgs a) {
         } else {
             a.bias_part[slab + co0 + tid] = v;
         }
+    }
+}
+
+template <int W, int SPX, bool DB>
+__global__ void __launch_bounds__(256, 3) dwgrad_q_kernel(const DWArgs a) {
+    __shared__ float smem[dwq_lds_floats(W, SPX, DB)];
+    int bx, by, bz;
+    block_xyz(bx, by, bz);
+    dwgrad_q_body<W, SPX, DB>(a, smem, bx, by, bz);
+}
+
+// A layer's WGRAD (dwgrad_q, 128-pixel stages) and DGRAD (dconv, BM = 32, CK = 8) read the
+// same output gradient and write disjoint outputs: one launch runs both, the nw workgroups
+// of the WGRAD grid (wx, wy, z) first (wfirst) or after the nd of the DGRAD grid (dx, dy, z),
+// each x-fastest as in its own launch.  The layer's backward is then one dependent step instead of
+// two, and the two grids fill each other's tails.
+template <int W, bool BNB>
+__global__ void __launch_bounds__(256, 3)
+    dconv_wgrad_dual_kernel(const DWArgs wa, int wx, int wy, int nw, const DConvArgs da, int dx,
+                            int dy, int nd, int wfirst) {
+    constexpr int LW = dwq_lds_floats(W, 128, false);
+    constexpr int LD = dconv_lds_floats<OP_DGRAD, W, 32, 8, 1, BNB>();
+    __shared__ float smem[LW > LD ? LW : LD];
+    const int b = blockIdx.x;
+    const bool isw = wfirst ? b < nw : b >= nd;
+    if (isw) {
+        const int q = wfirst ? b : b - nd;
+        const int bz = q / (wx * wy), r = q - bz * wx * wy;
+        dwgrad_q_body<W, 128, false>(wa, smem, r % wx, r / wx, bz);
+    } else {
+        const int q = wfirst ? b - nw : b;
+        const int bz = q / (dx * dy), r = q - bz * dx * dy;
+        dconv_body<OP_DGRAD, W, 32, 1, 8, true, 1, BNB>(da, smem, r % dx, r / dx, bz);
     }
 }
 

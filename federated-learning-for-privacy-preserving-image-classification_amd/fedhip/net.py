@@ -191,6 +191,11 @@ class PackedNet:
         # gather launch, and clears it after.
         self.fuse_input = True
         self._src = None
+        # CIFAR10CNN / ResNet 3x3 layers: a layer's WGRAD and its DGRAD in one dual-role launch
+        # (fh_conv_pair, dconv_wgrad_dual_kernel; 1 = WGRAD workgroups first, 2 = DGRAD first,
+        # 0 = two launches).  KT 276.1k (r04 library) / 275.4k (0) -> 285.9k (1) / 287.4k (2),
+        # interleaved x2 (profiles/r04_dual/)
+        self.dual_bwd = 2
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -651,6 +656,8 @@ class PackedNet:
                 aff = self._bn_affine(convs[i - 1][4], ci)
             else:
                 xin = A(f"r_{convs[i - 1][0]}", ci, hw, hw)
+            if i > 0:
+                ops.conv_pair(self.dual_bwd)  # held for this layer's DGRAD below
             ops.conv2d_wgrad(xin, dc, W(G, f"{cv}.weight"), W(G, f"{cv}.bias"), n, B, ci, hw, hw,
                              co, 3, 1, 1, counts=cnt, in_affine=aff)
             if i == 0:
@@ -677,6 +684,7 @@ class PackedNet:
                           self._bn_save(pbn, ci)[0], bn_tiles)
                 ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), A(f"dr_{pcv}", ci, hw, hw), n, B, ci,
                                  hw, hw, co, 3, 1, 1, counts=cnt, bn_bwd=bb)
+            ops.conv_pair(0)
 
     # ---------------- FederatedResNet (models_pytorch.py:230-246, block :189-194)
     def _fwd_resnet(self, P_, bufs, n, cnt, train):
@@ -798,6 +806,7 @@ class PackedNet:
             a = A(f"{pf}.a", co, ho, ho)
             aff1 = self._bn_affine(f"{pf}.bn1", co) if self._fused else None
             ar = a if self._fused else A(f"{pf}.ar", co, ho, ho)
+            ops.conv_pair(self.dual_bwd)  # held for conv2's DGRAD below
             ops.conv2d_wgrad(ar, db, W(G, f"{pf}.conv2.weight"), None, n, B, co, ho, ho, co, 3, 1, 1,
                              counts=cnt, in_affine=aff1)
             dar = A(f"{pf}.dar", co, ho, ho)
@@ -808,12 +817,14 @@ class PackedNet:
                 tiles = self._bn_part(f"{pf}.bn1.bwd", co, ho)
                 ops.conv2d_dgrad(db, W(P_, f"{pf}.conv2.weight"), dar, n, B, co, ho, ho, co, 3, 1,
                                  1, counts=cnt, bn_bwd=(a, *aff1, sm1, tiles))
+                ops.conv_pair(0)
                 ops.bn_bwd_tiles(tiles, dar, a, W(P_, f"{pf}.bn1.weight"), sm1, si1, da,
                                  W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co,
                                  ho * ho, counts=cnt)
             else:
                 ops.conv2d_dgrad(db, W(P_, f"{pf}.conv2.weight"), dar, n, B, co, ho, ho, co, 3, 1,
                                  1, counts=cnt)
+                ops.conv_pair(0)
                 ops.bn_bwd(dar, None, a, W(P_, f"{pf}.bn1.weight"), sm1, si1, da,
                            W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co, ho * ho,
                            relu=True, counts=cnt, beta=W(P_, f"{pf}.bn1.bias"))

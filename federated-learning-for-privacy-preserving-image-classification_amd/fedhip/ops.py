@@ -231,6 +231,13 @@ def set_fill_fraction(fraction: float):
         _FILL[0] = float(fraction)
 
 
+def conv_pair(mode: int):
+    """mode 1 / 2: hold the next conv2d_wgrad's direct launch for the following conv2d_dgrad
+    (one dual-role grid; 1 = WGRAD workgroups first, 2 = DGRAD first); 0: issue anything
+    still held and disarm (fh_conv_pair).  Per calling thread."""
+    call("fh_conv_pair", int(mode))
+
+
 def _ws_for(fn_name, device, *args):
     """Scratch for a split-K launch; the size query is cached per shape (and fill)."""
     key = (fn_name, _FILL[0]) + args

@@ -658,6 +658,14 @@ int fh_bn_apply_tiles(const double* part, const float* x, int64_t x_cs, float* y
 int fh_set_fill_fraction(float fraction);
 float fh_get_fill_fraction(void);
 
+/* Dual-role layer backward (CIFAR10CNN / ResNet 3x3 layers, the WGRAD + DGRAD pair of
+ * models_pytorch.py's autograd backward).  mode 1 or 2 arms the CALLING THREAD's next
+ * fh_conv2d_wgrad* call: a direct quadrant-wave WGRAD whose dW needs no reduction launch is
+ * held and issued in one grid with the next direct DGRAD on the same stream (1: WGRAD
+ * workgroups first, 2: DGRAD first), else on its own before it.  mode 0 issues anything still
+ * held and disarms; call it after the pair's DGRAD. */
+int fh_conv_pair(int32_t mode);
+
 /* Lane streams (fedhip/lanes.py; replaces the reference's one-thread-per-client
  * concurrency, federated_simulation.py:309-318).  cu_mask (nullable; mask_words 32-bit
  * words, bit i = CU i) restricts the stream to those CUs (hipExtStreamCreateWithCUMask);

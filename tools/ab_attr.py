@@ -22,9 +22,9 @@ def main():
         elif k.startswith("fill"):  # fillI=F: lane I's split-K fill fraction (LanedTrainer.fill)
             fills[int(k[4:])] = float(v)
         elif k.startswith("trainer."):
-            tsets[k[len("trainer."):]] = bool(int(v))
+            tsets[k[len("trainer."):]] = int(v)
         else:
-            sets[k] = bool(int(v))
+            sets[k] = int(v)
     if lib:
         from fedhip import _lib
         _lib.load.__defaults__ = (lib,)
