@@ -368,10 +368,12 @@ class PackedNet:
                                  B, 3136, 128, counts=cnt)
                 ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
             self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
+        ops.conv_pair(self.dual_bwd)  # conv2's WGRAD held for its DGRAD: one launch
         ops.conv2d_wgrad(p1, da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, hp, hp, 64,
                          3, 1, 1, counts=cnt)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt)
+        ops.conv_pair(0)
         if self.fuse_pool1_bwd:
             ops.conv2d_c1_pool_wgrad(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8), p1,
                                      W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 28, 28, 32,

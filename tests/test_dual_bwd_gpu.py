@@ -61,7 +61,7 @@ def test_held_wgrad_flushed_without_dgrad():
         assert torch.equal(u, v)
 
 
-def _round(model_name, kw, sizes, opt, mode, defer=True, rounds=2):
+def _round(model_name, kw, sizes, opt, mode, defer=True, rounds=2, shape=(3, 32, 32)):
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model(model_name, **kw).to(DEV)
     S = len(sizes)
@@ -71,7 +71,7 @@ def _round(model_name, kw, sizes, opt, mode, defer=True, rounds=2):
     for k in range(S):
         eng.load_module_state(k, model)
     g = torch.Generator().manual_seed(5)
-    data = torch.randn(sum(sizes), 3, 32, 32, generator=g).to(DEV)
+    data = torch.randn(sum(sizes), *shape, generator=g).to(DEV)
     labels = torch.randint(0, 10, (sum(sizes),), generator=g).to(DEV)
     offs = [sum(sizes[:k]) for k in range(S)]
     gen = torch.Generator().manual_seed(11)
@@ -87,12 +87,14 @@ def _round(model_name, kw, sizes, opt, mode, defer=True, rounds=2):
     ("cifar10_cnn", {"dropout_rate": 0.5}, "adam", True),
     ("cifar10_cnn", {"dropout_rate": 0.5}, "sgd", False),
     ("federated_resnet", {"num_blocks": [1, 1, 1]}, "sgd", True),
+    ("simple_cnn", {"dropout_rate": 0.25}, "adam", True),
 ])
 def test_dual_rounds_bit_identical(model_name, kw, opt, defer):
     sizes = [100, 70, 40, 9]
-    b = _round(model_name, kw, sizes, opt, 0, defer)
+    shape = (1, 28, 28) if model_name == "simple_cnn" else (3, 32, 32)
+    b = _round(model_name, kw, sizes, opt, 0, defer, shape=shape)
     for mode in (1, 2):
-        a = _round(model_name, kw, sizes, opt, mode, defer)
+        a = _round(model_name, kw, sizes, opt, mode, defer, shape=shape)
         for f in ("params", "grads", "state1", "state2", "bufs"):
             assert torch.equal(getattr(a, f), getattr(b, f)), (mode, f)
 
