@@ -234,8 +234,9 @@ def set_fill_fraction(fraction: float):
 def conv_pair(mode: int):
     """mode 1 / 2: hold the next conv2d_wgrad's direct launch for the following conv2d_dgrad
     (one dual-role grid; 1 = WGRAD workgroups first, 2 = DGRAD first); 0: issue anything
-    still held and disarm (fh_conv_pair).  Per calling thread."""
-    call("fh_conv_pair", int(mode))
+    still held and disarm (fh_conv_pair).  Per calling thread.  Instrumented rounds (PROBE
+    enabled) keep the two launches apart, so each is timed against its own work."""
+    call("fh_conv_pair", 0 if PROBE.enabled else int(mode))
 
 
 def _ws_for(fn_name, device, *args):
