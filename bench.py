@@ -845,7 +845,13 @@ def main():
                     help="N>1: all-gather + sequential FedAvg (bit-exact) instead of all-reduce")
     ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="JSON file for the full result (per-launch-shape tables); '' = none")
+    ap.add_argument("--separate-conv-bwd", action="store_true",
+                    help="each layer's WGRAD and DGRAD as two launches (no dual-role launch): "
+                         "the PMC traffic passes (tools/bench_traffic.py) attribute per kernel")
     args = ap.parse_args()
+    if args.separate_conv_bwd:
+        from fedhip import ops as _ops
+        _ops.set_conv_pairing(False)
     world, rank, dev = setup(args)
     if args.config == "K2-dpsgd":
         if world != 1:

@@ -231,12 +231,21 @@ def set_fill_fraction(fraction: float):
         _FILL[0] = float(fraction)
 
 
+_PAIRING = [True]
+
+
+def set_conv_pairing(on: bool):
+    """False: conv_pair arms nothing (every WGRAD and DGRAD its own launch; bench.py
+    --separate-conv-bwd for per-kernel PMC traffic)."""
+    _PAIRING[0] = bool(on)
+
+
 def conv_pair(mode: int):
     """mode 1 / 2: hold the next conv2d_wgrad's direct launch for the following conv2d_dgrad
     (one dual-role grid; 1 = WGRAD workgroups first, 2 = DGRAD first); 0: issue anything
     still held and disarm (fh_conv_pair).  Per calling thread.  Instrumented rounds (PROBE
     enabled) keep the two launches apart, so each is timed against its own work."""
-    call("fh_conv_pair", 0 if PROBE.enabled else int(mode))
+    call("fh_conv_pair", int(mode) if _PAIRING[0] and not PROBE.enabled else 0)
 
 
 def _ws_for(fn_name, device, *args):

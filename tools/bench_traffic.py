@@ -1,6 +1,7 @@
 """HBM traffic of the bench's own launches (r03): rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE
 passes (separate runs, tools/evidence.sh stage m) of
-`bench.py --steps 1 --warmup 1 --no-instances --no-k2` (KT: the warmup and the timed round,
+`bench.py --steps 1 --warmup 1 --no-instances --no-k2 --separate-conv-bwd` (each layer's WGRAD
+and DGRAD as their own dispatches, not the dual-role launch; KT: the warmup and the timed round,
 lanes and step programs as timed), per launch SHAPE of bench.py's instrumented table:
 
   bytes(launch) = 2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE   (KiB counters; MI355X_MICROARCH.md
