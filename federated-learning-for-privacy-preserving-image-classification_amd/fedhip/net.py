@@ -196,6 +196,9 @@ class PackedNet:
         # 0 = two launches).  KT 276.1k (r04 library) / 275.4k (0) -> 285.9k (1) / 287.4k (2),
         # interleaved x2 (profiles/r04_dual/)
         self.dual_bwd = 2
+        # ... and each stride-1 ResNet block's conv1 pair (its DGRAD accumulates onto the
+        # identity shortcut's gradient): K3 +0.5 %, K4 +0.8 % (x2, profiles/r04_dual/)
+        self.dual_resnet_conv1 = True
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -831,6 +834,10 @@ class PackedNet:
                            W(G, f"{pf}.bn1.weight"), W(G, f"{pf}.bn1.bias"), n, B, co, ho * ho,
                            relu=True, counts=cnt, beta=W(P_, f"{pf}.bn1.bias"))
             xin = b["xin"]
+            # conv1's WGRAD held for its DGRAD below (stride 1, identity shortcut)
+            pair1 = s == 1 and not b["proj"] and self.dual_resnet_conv1
+            if pair1:
+                ops.conv_pair(self.dual_bwd)
             ops.conv2d_wgrad(xin, da, W(G, f"{pf}.conv1.weight"), None, n, B, ci, hi, hi, co, 3, s, 1,
                              counts=cnt)
             if b["proj"]:
@@ -851,6 +858,8 @@ class PackedNet:
                                  1, s, 0, counts=cnt)
             ops.conv2d_dgrad(da, W(P_, f"{pf}.conv1.weight"), din, n, B, ci, hi, hi, co, 3, s, 1,
                              counts=cnt, accumulate=True)
+            if pair1:
+                ops.conv_pair(0)
         # stem: bn1 (relu) then conv1 weight grad
         dstem = A("dstem", 64, 32, 32)
         dc0 = A("dc_stem", 64, 32, 32)
