@@ -1780,7 +1780,12 @@ extern "C" int fh_set_fill_fraction(float fraction) {
 extern "C" float fh_get_fill_fraction(void) { return g_fill; }
 
 extern "C" int fh_conv_pair(int32_t mode) {
-    FH_REQUIRE(mode >= 0 && mode <= 2, "conv_pair: mode %d", mode);
+    FH_REQUIRE(mode >= -1 && mode <= 2, "conv_pair: mode %d", mode);
+    if (mode < 0) {  // error paths: drop a held launch unissued
+        g_pair_mode = 0;
+        g_pend.on = false;
+        return FH_OK;
+    }
     if (mode > 0) {
         g_pair_mode = mode;
         return FH_OK;

@@ -377,6 +377,7 @@ class PackedTrainer:
                                     adam_dev=views["adam"])
             finally:
                 net._src = None
+                ops.conv_pair_reset()  # no-op unless the step raised between a pair's calls
             if arm and not ops.PROBE.all:
                 ops.PROBE.enabled = False
             net.seed_dev = None
@@ -477,6 +478,7 @@ class PackedTrainer:
                                         adam_dev=views["adam"])
                 finally:
                     net._src = None
+                    ops.conv_pair_reset()
                     if rec is not None:
                         prog = ops.Program.record_end(rec)
             net.seed_dev = None

@@ -248,6 +248,11 @@ def conv_pair(mode: int):
     call("fh_conv_pair", int(mode) if _PAIRING[0] and not PROBE.enabled else 0)
 
 
+def conv_pair_reset():
+    """Disarm and drop a held WGRAD launch unissued (fh_conv_pair(-1)): a step's error path."""
+    call("fh_conv_pair", -1)
+
+
 def _ws_for(fn_name, device, *args):
     """Scratch for a split-K launch; the size query is cached per shape (and fill)."""
     key = (fn_name, _FILL[0]) + args

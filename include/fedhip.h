@@ -663,7 +663,8 @@ float fh_get_fill_fraction(void);
  * fh_conv2d_wgrad* call: a direct quadrant-wave WGRAD whose dW needs no reduction launch is
  * held and issued in one grid with the next direct DGRAD on the same stream (1: WGRAD
  * workgroups first, 2: DGRAD first), else on its own before it.  mode 0 issues anything still
- * held and disarms; call it after the pair's DGRAD. */
+ * held and disarms; call it after the pair's DGRAD.  mode -1 disarms and drops a held launch
+ * unissued (a caller's error path). */
 int fh_conv_pair(int32_t mode);
 
 /* Lane streams (fedhip/lanes.py; replaces the reference's one-thread-per-client

@@ -127,3 +127,26 @@ def test_dual_laned_program_rounds_bit_identical():
     assert all(ln.launch_mode == "program" for ln in a.lanes)
     for f in ("params", "grads", "state1", "state2", "bufs"):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_reset_drops_held_wgrad():
+    """fh_conv_pair(-1) (a step's error path) drops the held WGRAD unissued and disarms."""
+    nc, B, c, hw = 2, 32, 64, 16
+    x = torch.randn(nc, B * c * hw * hw, device=DEV)
+    dy = torch.randn(nc, B * c * hw * hw, device=DEV)
+    dw = torch.full((nc, c * c * 9), 7.0, device=DEV)
+    db = torch.full((nc, c), 7.0, device=DEV)
+    ops.set_fill_fraction(0.001)
+    try:
+        h = ops.Program.record_begin()
+        ops.conv_pair(2)
+        ops.conv2d_wgrad(x, dy, dw, db, nc, B, c, hw, hw, c, 3, 1, 1)
+        ops.conv_pair_reset()
+        ops.conv_pair(0)
+        prog = ops.Program.record_end(h)
+    finally:
+        ops.set_fill_fraction(1.0)
+    torch.cuda.synchronize()
+    assert prog.kernels == 0
+    prog.release()
+    assert bool((dw == 7.0).all()) and bool((db == 7.0).all())
