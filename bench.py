@@ -93,10 +93,15 @@ def setup(args):
     return world, rank, torch.device("cuda", local)
 
 
-def build_clients(cfg, world, seed=0):
-    """Weak scaling: clients-per-GPU fixed; the synthetic dataset scales with N."""
-    C = cfg["clients"] * world
-    N = cfg["samples"] * world
+def build_clients(cfg, world, seed=0, strong=False):
+    """Weak scaling: clients-per-GPU fixed; the synthetic dataset scales with N.  Strong
+    scaling (--strong): the config's whole client set (KT: 32 clients over 50k images; K3-K5:
+    their 64 / 128 / 256 clients over 50k), fixed whatever N, LPT-sharded over the ranks — the
+    reference's fixed client set (federated_simulation.py:309-318) averaged once per round
+    (fedavg.py:267-289)."""
+    mult = cfg.get("config_gpus", 1) if strong else world
+    C = cfg["clients"] * mult
+    N = cfg["samples"] * mult
     labels = np.random.default_rng(seed).integers(0, cfg["classes"], size=N)
     import random
     random.seed(seed)
@@ -122,6 +127,18 @@ def make_rank_data(cfg, train_sizes, my_slots, device, seed, raw=True):
     labels = torch.randint(0, cfg["classes"], (total,), generator=g, device=device)
     offs = np.cumsum([0] + [train_sizes[k] for k in my_slots][:-1]).tolist()
     return data, labels, offs
+
+
+def shard_report(train, assign, epochs, batch=32):
+    """Per-rank load of a round: the clients' sequential local steps bound any
+    split of a fixed client set — a rank cannot finish before its longest client's
+    epochs * ceil(n / 32) dependent steps, however few clients it holds."""
+    steps = [epochs * math.ceil(n / batch) for n in train]
+    ranks = [{"clients": len(a), "images": epochs * sum(train[k] for k in a),
+              "client_steps": sum(steps[k] for k in a),
+              "longest_client_steps": max((steps[k] for k in a), default=0)} for a in assign]
+    return {"ranks": ranks, "longest_client_steps": max(steps, default=0),
+            "total_client_steps": sum(steps)}
 
 
 def flops_key(cfg):
@@ -165,24 +182,68 @@ def host_cpu_info():
             "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(cfg, train_sizes, opt="sgd", lr=0.01, seconds=12.0):
-    """The reference's client round on the host cores — oracle/ (the CPU restatement pinned
-    bit-exact to the reference LocalTrainer / privacy / compression / FedAvg): clients of
-    this workload in order, each its whole shard of synthetic uint8 images through the
-    reference loaders' per-sample transforms (data_loader.py:298-306, 454-458), batches of 32
-    in a shuffled order with the partial last one, a fresh optimizer (training.py:89), the
-    config's local epochs, then its update DP (privacy.py:284-311, torch.normal noise) and
-    compression when the config has them, and the FedAvg of the sampled clients
-    (fedavg.py:267-289).  Clients are taken median shard size first (a representative
-    sample) until ~`seconds` of this work; the sample's client-images / its wall time is
-    the baseline.  Data generation is not timed."""
-    from oracle import compress_ref, data_ref, fedavg_ref, privacy_ref, train_ref
+def _cpu_threads():
+    """One thread per physical core this job may use: min(physical cores, affinity, cgroup
+    quota) — the box's share of its host, not the whole machine's core count."""
     host = host_cpu_info()
-    # one thread per physical core this job may use: min(physical cores, affinity, cgroup
-    # quota) — the box's share of its host, not the whole machine's core count
     lim = [v for v in (host["physical_cores"], host["affinity_cpus"], host["cgroup_cpu_quota"])
            if v]
-    threads = max(1, int(min(lim))) if lim else torch.get_num_threads()
+    return host, (max(1, int(min(lim))) if lim else torch.get_num_threads())
+
+
+def timed_passes(run_client, sizes, seconds, passes=3):
+    """BASELINE.md §2 / SURVEY.md §8d: one warm-up client (untimed: first-touch allocations,
+    oneDNN primitive creation), then the same client sample timed `passes` times; the
+    baseline is the median pass.  The sample is the clients median shard size first, as many
+    as the warm-up client's rate says fit in ~`seconds` per pass.  run_client(i, n) trains
+    client i of `sizes` and returns its client-images and its result row; run_client.prepare(i)
+    generates client i's data (untimed) and run_client.finish(rows, ns) runs once per pass
+    (FedAvg)."""
+    med = float(np.median(sizes))
+    order = [i for i in sorted(range(len(sizes)), key=lambda i: (abs(sizes[i] - med), sizes[i]))
+             if sizes[i] > 0]
+    run_client.prepare(order[0])
+    t0 = time.perf_counter()
+    imgs0, _ = run_client(order[0])
+    rate = imgs0 / max(time.perf_counter() - t0, 1e-6)
+    sample, budget = [], 0.0
+    for i in order:
+        sample.append(i)
+        budget += sizes[i] * run_client.epochs / rate
+        if budget >= seconds:
+            break
+    for i in sample:  # data generated before the timed passes, reused by every pass
+        run_client.prepare(i)
+    rates, secs = [], []
+    for _ in range(passes):
+        imgs, busy, rows, ns = 0, 0.0, [], []
+        for i in sample:
+            t0 = time.perf_counter()
+            n_i, row = run_client(i)
+            busy += time.perf_counter() - t0
+            imgs += n_i
+            rows.append(row)
+            ns.append(n_i)
+        t0 = time.perf_counter()
+        run_client.finish(rows, ns)
+        busy += time.perf_counter() - t0
+        rates.append(imgs / busy)
+        secs.append(busy)
+    return sorted(rates)[len(rates) // 2], rates, len(sample), imgs, secs
+
+
+def cpu_baseline(cfg, train_sizes, opt="sgd", lr=0.01, seconds=5.0):
+    """The reference's client round on the host cores — oracle/ (the CPU restatement pinned
+    bit-exact to the reference LocalTrainer / privacy / compression / FedAvg): clients of
+    this workload, each its whole shard of synthetic uint8 images through the reference
+    loaders' per-sample transforms (data_loader.py:298-306, 454-458), batches of 32 in a
+    shuffled order with the partial last one, a fresh optimizer (training.py:89), the
+    config's local epochs, then its update DP (privacy.py:284-311, torch.normal noise) and
+    compression when the config has them, and the FedAvg of the sampled clients
+    (fedavg.py:267-289).  timed_passes: one warm-up client, then the median of 3 timed passes
+    over a fixed client sample.  Data generation is not timed."""
+    from oracle import compress_ref, data_ref, fedavg_ref, privacy_ref, train_ref
+    host, threads = _cpu_threads()
     prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
@@ -191,28 +252,31 @@ def cpu_baseline(cfg, train_sizes, opt="sgd", lr=0.01, seconds=12.0):
     model = train_ref.make_model(cfg["model"], 0, **cfg["kw"])
     gsd = {k: v.clone() for k, v in model.state_dict().items()}
     gvec = [p.detach().numpy().copy() for p in model.parameters()]
-    rows, ns, imgs, busy, nclients = [], [], 0, 0.0, 0
-    med = float(np.median(train_sizes))
-    for n in sorted(train_sizes, key=lambda v: (abs(v - med), v)):
-        if busy > seconds:
-            break
-        if n == 0:
-            continue
-        raw = rng.integers(0, 256, (n, h, w) if c == 1 else (n, h, w, c), dtype=np.uint8)
-        labels = torch.from_numpy(rng.integers(0, cfg["classes"], n))
-        draws = rng.integers(0, 2 * tf.pad + 1, (cfg["epochs"], n, 2))
-        flips = rng.integers(0, 2, (cfg["epochs"], n)).astype(bool) & tf.flip
-        perms = [rng.permutation(n) for _ in range(cfg["epochs"])]
-        t0 = time.perf_counter()
+    data = {}
+
+    def client_data(i):
+        if i not in data:  # generated once, outside the timed region, reused by every pass
+            n = train_sizes[i]
+            raw = rng.integers(0, 256, (n, h, w) if c == 1 else (n, h, w, c), dtype=np.uint8)
+            labels = torch.from_numpy(rng.integers(0, cfg["classes"], n))
+            draws = rng.integers(0, 2 * tf.pad + 1, (cfg["epochs"], n, 2))
+            flips = rng.integers(0, 2, (cfg["epochs"], n)).astype(bool) & tf.flip
+            perms = [rng.permutation(n) for _ in range(cfg["epochs"])]
+            data[i] = (n, raw, labels, draws, flips, perms)
+        return data[i]
+
+    def run_client(i):
+        n, raw, labels, draws, flips, perms = data[i]
         m = train_ref.make_model(cfg["model"], None, **cfg["kw"])
         m.load_state_dict(gsd)
         optm = train_ref.make_optimizer(m, opt, lr)
+        imgs = 0
         for e in range(cfg["epochs"]):
             for j in range(0, n, 32):
                 idx = perms[e][j:j + 32]
-                x = np.ascontiguousarray(np.stack([data_ref.transform(raw[i], tf.mean, tf.std, tf.pad,
-                                                 int(draws[e, i, 0]), int(draws[e, i, 1]),
-                                                 bool(flips[e, i])) for i in idx]))
+                x = np.ascontiguousarray(np.stack([data_ref.transform(raw[i_], tf.mean, tf.std, tf.pad,
+                                                 int(draws[e, i_, 0]), int(draws[e, i_, 1]),
+                                                 bool(flips[e, i_])) for i_ in idx]))
                 train_ref.train_step(m, optm, torch.from_numpy(x), labels[idx])
                 imgs += len(idx)
         local = [p.detach().numpy() for p in m.parameters()]
@@ -227,22 +291,23 @@ def cpu_baseline(cfg, train_sizes, opt="sgd", lr=0.01, seconds=12.0):
             _, ratio = cfg["compression"]
             local = [(gp + compress_ref.topk_dense((lp - gp).astype(np.float32), ratio))
                      .astype(np.float32) for lp, gp in zip(local, gvec)]
-        rows.append(np.concatenate([v.reshape(-1) for v in local]))
-        ns.append(cfg["epochs"] * n)
-        nclients += 1
-        busy += time.perf_counter() - t0
-    t0 = time.perf_counter()
-    fedavg_ref.weighted_average(rows, fedavg_ref.calculate_sample_weights(ns))
-    busy += time.perf_counter() - t0
+        return imgs, np.concatenate([v.reshape(-1) for v in local])
+
+    run_client.epochs = cfg["epochs"]
+    run_client.prepare = client_data
+    run_client.finish = lambda rows, ns: fedavg_ref.weighted_average(
+        rows, fedavg_ref.calculate_sample_weights(ns))
+    value, rates, nclients, imgs, secs = timed_passes(run_client, train_sizes, seconds)
     torch.set_num_threads(prev_threads)
     extras = ", update DP" if cfg["dp"] else ""
     extras += ", top-k compression" if cfg.get("compression") else ""
-    return {"value": imgs / busy, "unit": "client-images/s", "cores": threads, "kind": "port",
-            "host": host,
-            "sample": f"{nclients} clients of this workload ({imgs} client-images: whole "
-                      f"shards, {cfg['epochs']} local epoch(s), per-sample host transforms, "
-                      f"batch 32, {opt} lr {lr}{extras}, FedAvg of the sample) in "
-                      f"{busy:.1f}s (oracle/*.py, torch CPU, {threads} threads)"}
+    return {"value": value, "unit": "client-images/s", "cores": threads, "kind": "port",
+            "host": host, "passes": [round(r, 1) for r in rates],
+            "sample": f"median of 3 passes ({', '.join(f'{r:.0f}' for r in rates)}/s) after one "
+                      f"warm-up client; a pass = {nclients} clients of this workload ({imgs} "
+                      f"client-images: whole shards, {cfg['epochs']} local epoch(s), per-sample "
+                      f"host transforms, batch 32, {opt} lr {lr}{extras}, FedAvg of the sample) "
+                      f"in {float(np.median(secs)):.1f}s (oracle/*.py, torch CPU, {threads} threads)"}
 
 
 def proxy_prototypes(classes=10):
@@ -482,7 +547,7 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     synchronize on both sides, max over ranks), then one instrumented round.  Returns the
     rank-0 result dict (None on other ranks)."""
     cfg = CONFIGS[key]
-    labels, train = build_clients(cfg, world)
+    labels, train = build_clients(cfg, world, strong=args.strong)
     C = len(train)
     assign = lpt_assign(train, world)
     mine = assign[rank]
@@ -503,15 +568,10 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, rank, raw=raw)
     total_images = cfg["epochs"] * sum(train)
 
-    # launch probe: dominant conv kernel (the largest-FLOP 3x3 fwd launch of the model)
-    probe_tag = args.probe or {
-        "cifar10_cnn": "conv_dgrad:c32x32x32->32k3s1",
-        "simple_cnn": "conv_dgrad:c32x14x14->64k3s1",
-        "federated_resnet": "conv_dgrad:c64x32x32->64k3s1"}[cfg["model"]]
+    # the timed rounds run exactly as the driver's: no probe armed (every step after a round's
+    # first replays its captured step program); the roofline comes from the instrumented round
     ops.PROBE.reset()
-    ops.PROBE.tag, ops.PROBE.enabled = probe_tag, False
-    # timed rounds: full-width full-batch steps run eagerly with the probe armed (the
-    # engine replays every other step from its captured graph)
+    ops.PROBE.tag, ops.PROBE.enabled = None, False
     rr.trainer.probe_full = False
 
     gen = torch.Generator().manual_seed(7)
@@ -523,7 +583,6 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    rr.trainer.probe_full = True
     t0 = time.perf_counter()
     for s in range(steps):
         rr.run(data, lab, offs, args.opt, args.lr, seed=100 + s, generator=gen)
@@ -532,16 +591,15 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    rr.trainer.probe_full = False
-    ops.PROBE.enabled = False
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    probe = ops.PROBE.summary()
     # one instrumented round (untimed, every step eager, the lanes one after another so a
     # launch never shares the chip with another lane's): HIP events around EVERY conv /
-    # linear launch — every client count, ragged and tail steps included
+    # linear launch — every client count, ragged and tail steps included.  Launches are the
+    # timed rounds' launches: each layer's WGRAD + DGRAD pair is the one dual-role grid
+    # (conv_bwd_dual:<shape>, timed against both roles' FLOPs)
     inst = buckets = None
     if not args.no_instances:
         ops.PROBE.reset()
@@ -555,12 +613,6 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     value = total_images * steps / elapsed
     fl = TRAIN_FLOPS[flops_key(cfg)]
     peak = FP32_MFMA_PEAK_TFLOPS
-    full = None
-    if probe:
-        ach = probe["flops_per_launch"] / (probe["avg_ms"] * 1e-3) / 1e12
-        full = {"kernel": probe_tag, "achieved": round(ach, 2), "frac": round(ach / peak, 4),
-                "launches_timed": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4),
-                "note": "full-width full-batch launches of the timed rounds only"}
     roof = roof_hbm = instances = by_bucket = conv_all = None
     if inst:
         rows, instances, by_bucket, conv_all = summarize_instances(inst, buckets, peak)
@@ -573,18 +625,25 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         hb = [(tg, vv) for tg, vv in rows if vv[2] <= ridge * vv[3]]
         if hb:
             roof_hbm = roofline_of(hb[0][0], *hb[0][1], peak, hbm=True)
+        for r in [roof, roof_hbm] + instances:
+            if r and ops.PROBE.exec_ratio.get(r.get("kernel", r.get("launch"))):
+                # the kernel runs this layer's map inside zero-ringed planes: FLOPs above are
+                # the algorithmic ones, the kernel executes this factor more
+                r["executed_over_algorithmic"] = ops.PROBE.exec_ratio[r.get("kernel", r.get("launch"))]
     out = {
         "metric": "client-images/sec/node", "value": round(value, 1),
         "unit": "client-images/s", "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": round(1000 * elapsed / steps, 2),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None, "dtype": "f32",
         "data": ("synthetic uint8 CIFAR/MNIST-shaped images resident in HBM, the "
                  "reference loaders' transforms (crop/flip/normalise) applied on the chip "
                  "each step" if raw else "synthetic N(0,1) CIFAR/MNIST-shaped fp32 tensors "
                  "resident in HBM") + "; Dirichlet shard sizes from the reference "
                 "partitioner restatement",
         "config": {"workload": f"{key}: {cfg['model']} {C} clients "
-                               f"({cfg['clients']}/GPU), {cfg['strategy']}"
+                               f"({'fixed, LPT-sharded' if args.strong else str(cfg['clients']) + '/GPU'}), "
+                               f"{cfg['strategy']}"
                                f"{'(a=' + str(cfg['alpha']) + ')' if cfg['strategy'] == 'non_iid' else ''}, "
                                f"{cfg['epochs']} local epoch(s), batch 32, {args.opt} lr {args.lr}, "
                                f"DP eps={cfg['dp']}, "
@@ -592,7 +651,7 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
                                f"FedAvg{(' exact all-gather' if args.exact_fedavg else ' RCCL all-reduce') if world > 1 else ''}"
                                + (f" [{world}/{cfg['config_gpus']} GPU slice of the "
                                   f"{cfg['clients'] * cfg['config_gpus']}-client config]"
-                                  if cfg.get('config_gpus') else ""),
+                                  if cfg.get('config_gpus') and not args.strong else ""),
                    "clients": C, "images_per_round": total_images, "batch": 32,
                    "parallelism": f"client-packed x{world} GPU",
                    "lanes": rr.trainer.cut},
@@ -600,10 +659,10 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         "round_frac": round(value * fl / 1e12 / peak, 4),
         "roofline": roof,
         "roofline_hbm": roof_hbm,
-        "roofline_full_width_probe": full,
         "conv_linear_all_launches": conv_all,
         "instances": instances,
         "instances_by_clients": by_bucket,
+        "shards": shard_report(train, assign, cfg["epochs"]),
     }
     # the host-CPU legs (oracle rounds-to-target, CPU baseline) run after every timed GPU
     # leg of the process (host_legs): their torch CPU thread pool would otherwise still be
@@ -697,34 +756,30 @@ def run_dpsgd(args, dev, steps, warmup):
             "instances_by_clients": by_bucket, "_sizes": sizes}
 
 
-def cpu_baseline_dpsgd(sizes, lr=0.01, seconds=12.0, max_norm=1.0, eps=1.0, delta=1e-5):
+def cpu_baseline_dpsgd(sizes, lr=0.01, seconds=5.0, max_norm=1.0, eps=1.0, delta=1e-5):
     """The K2-dpsgd round on the host cores: oracle/dpsgd_ref.py (explicit per-sample
     gradients, per-sample clip to C, N(0, (sigma C)^2) noise with the reference's
     Gaussian-mechanism sigma, privacy.py:209) over whole client shards of N(0,1) MNIST-shaped
-    data, batches of 32 with the partial last one, SGD, clients median shard first until
-    ~`seconds` of work.  Data generation is not timed."""
+    data, batches of 32 with the partial last one, SGD; timed_passes (one warm-up client, the
+    median of 3 passes over a fixed client sample).  Data generation is not timed."""
     from oracle import dpsgd_ref, train_ref
-    host = host_cpu_info()
-    lim = [v for v in (host["physical_cores"], host["affinity_cpus"], host["cgroup_cpu_quota"])
-           if v]
-    threads = max(1, int(min(lim))) if lim else torch.get_num_threads()
+    host, threads = _cpu_threads()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     init = train_ref.make_model("simple_cnn", 0)
     gsd = {k: v.clone() for k, v in init.state_dict().items()}
     sig = dpsgd_ref.sigma(eps, delta)
-    med = float(np.median(sizes))
-    imgs, busy, nclients = 0, 0.0, 0
-    for n in sorted(sizes, key=lambda v: (abs(v - med), v)):
-        if busy > seconds:
-            break
-        if n == 0:
-            continue
-        x = torch.randn(n, 1, 28, 28, generator=g)
-        y = torch.randint(0, 10, (n,), generator=g)
-        perm = torch.randperm(n, generator=g)
-        t0 = time.perf_counter()
+    data = {}
+
+    def prepare(i):
+        if i not in data:
+            n = sizes[i]
+            data[i] = (n, torch.randn(n, 1, 28, 28, generator=g),
+                       torch.randint(0, 10, (n,), generator=g), torch.randperm(n, generator=g))
+
+    def run_client(i):
+        n, x, y, perm = data[i]
         m = train_ref.make_model("simple_cnn", None)
         m.load_state_dict(gsd)
         opt = train_ref.make_optimizer(m, "sgd", lr)
@@ -732,16 +787,20 @@ def cpu_baseline_dpsgd(sizes, lr=0.01, seconds=12.0, max_norm=1.0, eps=1.0, delt
             idx = perm[j:j + 32]
             noise = [torch.normal(0.0, sig * max_norm, p.shape) for p in m.parameters()]
             dpsgd_ref.dpsgd_step(m, opt, x[idx], y[idx], max_norm, noise=noise)
-            imgs += len(idx)
-        busy += time.perf_counter() - t0
-        nclients += 1
+        return n, None
+
+    run_client.epochs, run_client.prepare = 1, prepare
+    run_client.finish = lambda rows, ns: None
+    value, rates, nclients, imgs, secs = timed_passes(run_client, sizes, seconds)
     torch.set_num_threads(prev)
-    return {"value": imgs / busy, "unit": "client-images/s", "cores": threads, "kind": "port",
-            "host": host,
-            "sample": f"{nclients} clients of K2-dpsgd ({imgs} client-images: whole shards, 1 "
-                      f"epoch, batch 32, per-sample clip C={max_norm} + Gaussian noise "
-                      f"sigma={sig:.3f}, sgd lr {lr}) in {busy:.1f}s (oracle/dpsgd_ref.py, "
-                      f"torch CPU, {threads} threads)"}
+    return {"value": value, "unit": "client-images/s", "cores": threads, "kind": "port",
+            "host": host, "passes": [round(r, 1) for r in rates],
+            "sample": f"median of 3 passes ({', '.join(f'{r:.0f}' for r in rates)}/s) after one "
+                      f"warm-up client; a pass = {nclients} clients of K2-dpsgd ({imgs} "
+                      f"client-images: whole shards, 1 epoch, batch 32, per-sample clip "
+                      f"C={max_norm} + Gaussian noise sigma={sig:.3f}, sgd lr "
+                      f"{lr}) in {float(np.median(secs)):.1f}s (oracle/dpsgd_ref.py, torch CPU, "
+                      f"{threads} threads)"}
 
 
 MAX_LINE_BYTES = 4096   # the driver keeps an 8 KB stdout tail: the final line must fit in it
@@ -798,6 +857,19 @@ def compact(out):
                 line["k2"].pop(k, None)
             if len(json.dumps(line)) <= MAX_LINE_BYTES:
                 break
+    # still too long: shorten the free-text fields, longest first, then drop the k2 block
+    texts = [(line.get("config") or {}, "workload"), (line.get("cpu_baseline") or {}, "sample"),
+             (line.get("k2") or {}, "workload"), ((line.get("k2") or {}).get("cpu_baseline") or {},
+                                                   "sample")]
+    for d, k in sorted(texts, key=lambda dk: -len(str(dk[0].get(dk[1], "")))):
+        if len(json.dumps(line)) <= MAX_LINE_BYTES:
+            break
+        if isinstance(d.get(k), str) and len(d[k]) > 80:
+            d[k] = d[k][:77] + "..."
+    if len(json.dumps(line)) > MAX_LINE_BYTES:
+        line.pop("k2", None)
+    if len(json.dumps(line)) > MAX_LINE_BYTES:
+        line.pop("env", None)
     return line
 
 
@@ -824,7 +896,6 @@ def main():
     ap.add_argument("--config", default="KT", choices=sorted(CONFIGS) + ["K2-dpsgd"])
     ap.add_argument("--opt", default="sgd")
     ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--probe", default=None, help="conv launch tag to time (default: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-instances", action="store_true",
                     help="skip the instrumented per-launch-shape round")
@@ -841,6 +912,9 @@ def main():
                     help="rehearsal: every rank on cuda:0 (multi-rank path on a 1-GPU box)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="concurrent client lanes per GPU (default: the lane planner)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: the config's whole client set (KT 32, K3 64, K4 128, K5 "
+                         "256 clients) fixed whatever N, LPT-sharded over the ranks")
     ap.add_argument("--exact-fedavg", action="store_true",
                     help="N>1: all-gather + sequential FedAvg (bit-exact) instead of all-reduce")
     ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),

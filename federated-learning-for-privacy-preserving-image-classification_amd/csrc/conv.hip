@@ -783,6 +783,8 @@ struct U8Src {
     int64_t* ylab;          // [z][batch] labels out
     int64_t yl_cs;
     float mean, stdv;
+    float* xo;              // x written (the kernel's x parameter is read-only: not read here)
+    int64_t xo_cs;
 };
 
 template <int COUT>
@@ -807,7 +809,7 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
     if (src.data) {  // the gather folded in: gather_u8_kernel's operations on the raw bytes
         const int64_t s = src.gidx[z * src.g_cs + img];
         const uint8_t* si = src.data + s * H * W;
-        float* xo = const_cast<float*>(xi);
+        float* xo = src.xo + z * src.xo_cs + (int64_t)img * H * W;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1475,6 +1477,7 @@ struct PendingWgrad {
 };
 thread_local int g_pair_mode = 0;
 thread_local PendingWgrad g_pend;
+thread_local int64_t g_dual_launches = 0;  // fh_conv_pair_status (instrumentation)
 
 static int flush_pending_wgrad() {
     if (!g_pend.on) return FH_OK;
@@ -1498,6 +1501,7 @@ static int launch_dual(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_
     FH_LAUNCH((dconv_wgrad_dual_kernel<W, BNB>), dim3((unsigned)(nw + nd)), dim3(256), 0, st,
               q.d, (int)q.grid.x, (int)q.grid.y, (int)nw, a, (int)grid.x, (int)grid.y,
               (int)nd, q.mode == 1 ? 1 : 0);
+    ++g_dual_launches;
     return FH_OK;
 }
 
@@ -1792,6 +1796,13 @@ extern "C" int fh_conv_pair(int32_t mode) {
     }
     g_pair_mode = 0;
     return flush_pending_wgrad();
+}
+
+extern "C" int fh_conv_pair_status(int32_t* held, int64_t* dual_launches) {
+    FH_REQUIRE(held && dual_launches, "conv_pair_status: null pointer");
+    *held = g_pend.on ? 1 : 0;
+    *dual_launches = g_dual_launches;
+    return FH_OK;
 }
 
 extern "C" size_t fh_conv2d_fwd_workspace(int32_t nclients, int32_t batch, int32_t cin, int32_t h,
@@ -2160,7 +2171,7 @@ extern "C" int fh_conv2d_c1_pool_fwd_u8(const uint8_t* data, const int64_t* labe
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(data && labels && gidx && x && y_lab && w && y && idx,
                "conv2d_c1_pool_fwd_u8: null pointer");
-    const U8Src src{data, labels, gidx, g_cs, y_lab, yl_cs, mean, stdv};
+    const U8Src src{data, labels, gidx, g_cs, y_lab, yl_cs, mean, stdv, x, x_cs};
     dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256), (unsigned)nclients);
     hipStream_t st = as_stream(stream);
     if (cout == 32)

@@ -150,6 +150,7 @@ SIGNATURES = {
     "fh_set_fill_fraction": (I32, [F32]),
     "fh_get_fill_fraction": (F32, []),
     "fh_conv_pair": (I32, [I32]),
+    "fh_conv_pair_status": (I32, [P, P]),
     "fh_stream_create": (I32, [I32, P, I32, P]),
     "fh_stream_destroy": (I32, [P]),
     "fh_record_begin": (I32, [P]),

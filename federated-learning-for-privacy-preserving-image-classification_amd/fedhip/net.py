@@ -320,7 +320,7 @@ class PackedNet:
         self._pool2_fused = self.pad_maps and self.fuse_pool2
         if self._pool2_fused:
             ops.conv2d_fwd_relu_pool(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, p2, i2, n,
-                                     B, 32, hp, 64, 14, counts=cnt)
+                                     B, 32, hp, 64, 14, counts=cnt, alg_hw=14)
         else:
             ops.conv2d_fwd(p1, W(P_, "conv2.weight"), W(P_, "conv2.bias"), a2, n, B, 32, hp, hp,
                            64, 3, 1, 1, relu=True, counts=cnt)
@@ -373,9 +373,9 @@ class PackedNet:
             self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
         ops.conv_pair(self.dual_bwd)  # conv2's WGRAD held for its DGRAD: one launch
         ops.conv2d_wgrad(p1, da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, hp, hp, 64,
-                         3, 1, 1, counts=cnt)
+                         3, 1, 1, counts=cnt, alg_hw=14)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
-                         counts=cnt)
+                         counts=cnt, alg_hw=14)
         ops.conv_pair(0)
         if self.fuse_pool1_bwd:
             ops.conv2d_c1_pool_wgrad(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8), p1,
@@ -440,9 +440,9 @@ class PackedNet:
         ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
         i2 = A("i2", 64, 7, 7, dtype=torch.uint8)
         self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
-        ops.conv2d_wgrad_persample(p1, da2, s2, n, B, 32, hp, hp, 64, counts=cnt)
+        ops.conv2d_wgrad_persample(p1, da2, s2, n, B, 32, hp, hp, 64, counts=cnt, alg_hw=14)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
-                         counts=cnt)
+                         counts=cnt, alg_hw=14)
         # conv1's per-image slabs from pool1's gradient (the pooled ReLU output p1 > 0 is the
         # mask at each window's argmax, whether or not conv1's output was written)
         ops.conv2d_c1_pool_wgrad_persample(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8),

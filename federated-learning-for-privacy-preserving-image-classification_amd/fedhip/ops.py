@@ -67,6 +67,12 @@ class LaunchProbe:
         self.enabled = False
         self.records = []
         self.seen = {}
+        # a WGRAD launch libfedhip holds for the next DGRAD (fh_conv_pair): (shape, flops,
+        # bytes) — its work is timed inside that DGRAD's window as one dual-role launch
+        self.held = None
+        # launch shapes whose kernels execute more than their algorithmic work (SimpleCNN's
+        # 14x14 conv2 on padded 16x16 planes): tag -> executed / algorithmic FLOPs
+        self.exec_ratio = {}
 
     @property
     def all(self):
@@ -90,17 +96,18 @@ class LaunchProbe:
         ev.record()
         return (tag, ev)
 
-    def end(self, h, flops, nbytes=0.0, clients=0):
+    def end(self, h, flops, nbytes=0.0, clients=0, tag=None):
         """flops / nbytes: the launch's algorithmic work — every operand read
-        and every result written once; clients: its active-client count (bench.py buckets)."""
+        and every result written once; clients: its active-client count (bench.py buckets);
+        tag: record under this launch shape instead of begin()'s."""
         if h is None:
             return
         e2 = torch.cuda.Event(enable_timing=True)
         e2.record()
-        self.records.append((h[0], h[1], e2, flops, nbytes, clients))
+        self.records.append((tag or h[0], h[1], e2, flops, nbytes, clients))
 
     def reset(self):
-        self.records, self.seen = [], {}
+        self.records, self.seen, self.held = [], {}, None
 
     def summary(self):
         torch.cuda.synchronize()
@@ -243,9 +250,60 @@ def set_conv_pairing(on: bool):
 def conv_pair(mode: int):
     """mode 1 / 2: hold the next conv2d_wgrad's direct launch for the following conv2d_dgrad
     (one dual-role grid; 1 = WGRAD workgroups first, 2 = DGRAD first); 0: issue anything
-    still held and disarm (fh_conv_pair).  Per calling thread.  Instrumented rounds (PROBE
-    enabled) keep the two launches apart, so each is timed against its own work."""
-    call("fh_conv_pair", int(mode) if _PAIRING[0] and not PROBE.enabled else 0)
+    still held and disarm (fh_conv_pair).  Per calling thread.  An instrumented round (PROBE
+    tag "*") pairs exactly as the timed rounds do and times the dual launch against both
+    roles' work ("conv_bwd_dual:..."); a single-shape probe keeps the two launches apart."""
+    if PROBE.enabled and not PROBE.all:
+        mode = 0
+    if mode == 0 and PROBE.held is not None:  # the held WGRAD issues here, on its own
+        tag, fl, nb, nc = PROBE.held
+        PROBE.held = None
+        ev = PROBE.begin(tag)
+        call("fh_conv_pair", 0)
+        PROBE.end(ev, fl, nb, nc)
+        return
+    call("fh_conv_pair", int(mode) if _PAIRING[0] else 0)
+
+
+def _pair_status():
+    """(held, dual launches issued) of this thread (fh_conv_pair_status)."""
+    held, duals = ctypes.c_int32(), ctypes.c_int64()
+    call("fh_conv_pair_status", ctypes.byref(held), ctypes.byref(duals))
+    return held.value, duals.value
+
+
+def _probe_wgrad_end(ev, tag, flops, nbytes, nclients):
+    """PROBE.end for a WGRAD call — unless libfedhip held its launch for the next DGRAD,
+    whose window then times both (_probe_dgrad_end)."""
+    if ev is not None and _pair_status()[0]:
+        PROBE.held = (tag, flops, nbytes, nclients)
+        return
+    PROBE.end(ev, flops, nbytes, nclients)
+
+
+def _probe_dgrad_begin(tag):
+    ev = PROBE.begin(tag)
+    return ev, (_pair_status()[1] if ev is not None and PROBE.held is not None else None)
+
+
+def _probe_dgrad_end(ev, duals0, flops, nbytes, nclients):
+    """PROBE.end for a DGRAD call.  With a WGRAD held before it, the window contains the
+    dual-role launch (recorded as conv_bwd_dual:<shape>, FLOPs / bytes = both roles') or the
+    held WGRAD issued on its own ahead of the DGRAD (conv_bwd_seq:<shape>, both launches)."""
+    if ev is None or duals0 is None:
+        PROBE.end(ev, flops, nbytes, nclients)
+        return
+    held, duals = _pair_status()
+    if held:  # not this DGRAD's pair (another path): the WGRAD is still waiting
+        PROBE.end(ev, flops, nbytes, nclients)
+        return
+    wtag, wfl, wnb, _ = PROBE.held
+    PROBE.held = None
+    kind = "conv_bwd_dual:" if duals > duals0 else "conv_bwd_seq:"
+    dtag = kind + wtag.split(":", 1)[1]
+    if wtag in PROBE.exec_ratio:
+        PROBE.exec_ratio[dtag] = PROBE.exec_ratio[wtag]
+    PROBE.end(ev, flops + wfl, nbytes + wnb, nclients, tag=dtag)
 
 
 def conv_pair_reset():
@@ -266,6 +324,21 @@ def _ws_for(fn_name, device, *args):
 
 
 # ------------------------------------------------------------------ conv / linear
+def _alg_map(h, wd, alg_hw, k, stride, pad):
+    """The map size a launch's algorithmic work is counted on: alg_hw when the kernel runs
+    the layer's map inside larger zero-ringed planes (SimpleCNN's 14x14 conv2 on 16x16
+    planes), else (h, wd)."""
+    if alg_hw is None or alg_hw == h:
+        return h, wd
+    return alg_hw, alg_hw
+
+
+def _note_exec(tag, h, wd, ah, aw):
+    """PROBE.exec_ratio[tag] = executed / algorithmic FLOPs of a padded-plane launch shape."""
+    if (h, wd) != (ah, aw) and PROBE.enabled:
+        PROBE.exec_ratio[tag] = round(h * wd / float(ah * aw), 4)
+
+
 def _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad):
     oh = (h + 2 * pad - k) // stride + 1
     ow = (wd + 2 * pad - k) // stride + 1
@@ -305,7 +378,7 @@ def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad,
 
 
 def conv2d_fwd_relu_pool(x, w, bias, y, py, pidx, nclients, batch, cin, h, cout, pool_hw,
-                         counts=None):
+                         counts=None, alg_hw=None):
     """conv2d_fwd(relu=True) on h x h planes + maxpool2_fwd of each plane's top-left
     pool_hw x pool_hw map into py / pidx (fh_conv2d_fwd_relu_pool): the pool runs in the conv's
     epilogue (unsplit) or its split reduction (16x16 planes), so y is scratch (written only by
@@ -313,17 +386,20 @@ def conv2d_fwd_relu_pool(x, w, bias, y, py, pidx, nclients, batch, cin, h, cout,
     require_device(x, "x")
     ws, nb = _ws_for("fh_conv2d_fwd_workspace", x.device, nclients, batch, cin, h, h, cout, 3, 3,
                      1, 1)
-    ev = PROBE.begin(_conv_tag("fwd", cin, h, h, cout, 3, 1))
+    ah, _ = _alg_map(h, h, alg_hw, 3, 1, 1)
+    tag = _conv_tag("fwd", cin, ah, ah, cout, 3, 1)
+    _note_exec(tag, h, h, ah, ah)
+    ev = PROBE.begin(tag)
     call("fh_conv2d_fwd_relu_pool", ptr(x), _cs(x), ptr(w), _cs(w), ptr(bias), _cs(bias), ptr(y),
          _cs(y), ptr(py), _cs(py), ptr(pidx), _cs(pidx), _counts(counts), nclients, batch, cin, h,
          h, cout, pool_hw, ptr(ws), nb, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, h, cout, 3, 1, 1),
-              _conv_bytes(nclients, batch, cin, h, h, cout, 3, 1, 1), nclients)
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, ah, ah, cout, 3, 1, 1),
+              _conv_bytes(nclients, batch, cin, ah, ah, cout, 3, 1, 1), nclients)
     return py
 
 
 def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
-                 accumulate=False, bn_bwd=None):
+                 accumulate=False, bn_bwd=None, alg_hw=None):
     """bn_bwd = (bn_x, scale, shift, save_mean, part[, pidx, pmask, p_drop]): the input was
     relu(BN(bn_x)) with that BN's affine (scale, shift); dx receives the ReLU-masked gradient
     g and part the BN backward statistics for bn_bwd_tiles (fh_conv2d_dgrad_bnstats,
@@ -332,7 +408,10 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
     is bn_bwd_pool_tiles."""
     ws, nb = _ws_for("fh_conv2d_dgrad_workspace", dy.device, nclients, batch, cin, h, wd, cout, k,
                      k, stride, pad)
-    ev = PROBE.begin(_conv_tag("dgrad", cin, h, wd, cout, k, stride))
+    ah, aw = _alg_map(h, wd, alg_hw, k, stride, pad)
+    tag = _conv_tag("dgrad", cin, ah, aw, cout, k, stride)
+    _note_exec(tag, h, wd, ah, aw)
+    ev, duals0 = _probe_dgrad_begin(tag)
     if bn_bwd is not None:
         if accumulate or (k, stride, pad) != (3, 1, 1):
             raise FedHipError("conv2d_dgrad(bn_bwd=...): 3x3/s1/p1 without accumulate only")
@@ -346,8 +425,8 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
         call("fh_conv2d_dgrad", ptr(dy), _cs(dy), ptr(w), _cs(w), ptr(dx), _cs(dx),
              _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
              int(accumulate), ptr(ws), nb, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad),
-              _conv_bytes(nclients, batch, cin, h, wd, cout, k, stride, pad), nclients)
+    _probe_dgrad_end(ev, duals0, _conv_flops(nclients, batch, cin, ah, aw, cout, k, stride, pad),
+                     _conv_bytes(nclients, batch, cin, ah, aw, cout, k, stride, pad), nclients)
     return dx
 
 
@@ -556,10 +635,13 @@ def _wgrad_deferred(d, x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stri
 
 
 def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pad, counts=None,
-                 in_affine=None):
+                 in_affine=None, alg_hw=None):
     """in_affine as in conv2d_fwd (fh_conv2d_wgrad_bnrelu).  Inside a GradSlabs scope the
     split reduction is left to the optimizer step (fh_conv2d_wgrad_deferred)."""
-    ev = PROBE.begin(_conv_tag("wgrad", cin, h, wd, cout, k, stride))
+    ah, aw = _alg_map(h, wd, alg_hw, k, stride, pad)
+    tag = _conv_tag("wgrad", cin, ah, aw, cout, k, stride)
+    _note_exec(tag, h, wd, ah, aw)
+    ev = PROBE.begin(tag)
     if _DEFER is None or not _wgrad_deferred(_DEFER, x, dy, dw, db, nclients, batch, cin, h, wd,
                                              cout, k, stride, pad, counts, in_affine):
         ws, nb = _ws_for("fh_conv2d_wgrad_workspace", x.device, nclients, batch, cin, h, wd, cout,
@@ -573,8 +655,8 @@ def conv2d_wgrad(x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stride, pa
             call("fh_conv2d_wgrad", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db),
                  _cs(db), ptr(ws), nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k,
                  stride, pad, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, k, stride, pad),
-              _conv_bytes(nclients, batch, cin, h, wd, cout, k, stride, pad), nclients)
+    _probe_wgrad_end(ev, tag, _conv_flops(nclients, batch, cin, ah, aw, cout, k, stride, pad),
+                     _conv_bytes(nclients, batch, cin, ah, aw, cout, k, stride, pad), nclients)
     return dw
 
 
@@ -716,12 +798,17 @@ class PersampleSlab:
     def __init__(self, device):
         self.device = device
         self.buf = torch.empty(0, dtype=torch.uint8, device=device)
+        self.retired = []
         self.per_w = self.per_b = self.nclients = self.batch = 0
 
     def ensure(self, nclients, batch, cin, cout):
         nb = load().fh_conv2d_wgrad_persample_workspace(nclients, batch, cin, cout)
         if self.buf.numel() < nb:
-            self.buf = torch.empty(nb, dtype=torch.uint8, device=self.device)
+            # superseded buffers stay alive: a step graph / program captured at a smaller
+            # client count still addresses the old slab (as Workspace.get / GradSlabs.take)
+            self.retired.append(self.buf)
+            self.buf = torch.empty(max(nb, 2 * self.buf.numel()), dtype=torch.uint8,
+                                   device=self.device)
         self.per_w, self.per_b = cout * cin * 9, cout
         self.nclients, self.batch = nclients, batch
         return nb
@@ -736,14 +823,18 @@ class PersampleSlab:
                 ((db.data_ptr() - g0) // 4, self.per_b, base + boff, self.batch)]
 
 
-def conv2d_wgrad_persample(x, dy, slab, nclients, batch, cin, h, wd, cout, counts=None):
+def conv2d_wgrad_persample(x, dy, slab, nclients, batch, cin, h, wd, cout, counts=None,
+                           alg_hw=None):
     """Per-image WGRAD slabs of a direct 3x3/s1/p1 conv (fh_conv2d_wgrad_persample)."""
     nb = slab.ensure(nclients, batch, cin, cout)
-    ev = PROBE.begin(_conv_tag("pswgrad", cin, h, wd, cout, 3, 1))
+    ah, aw = _alg_map(h, wd, alg_hw, 3, 1, 1)
+    tag = _conv_tag("pswgrad", cin, ah, aw, cout, 3, 1)
+    _note_exec(tag, h, wd, ah, aw)
+    ev = PROBE.begin(tag)
     call("fh_conv2d_wgrad_persample", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(slab.buf), nb,
          _counts(counts), nclients, batch, cin, h, wd, cout, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, cin, h, wd, cout, 3, 1, 1),
-              _conv_bytes(nclients, batch, cin, h, wd, cout, 3, 1, 1) +
+    PROBE.end(ev, _conv_flops(nclients, batch, cin, ah, aw, cout, 3, 1, 1),
+              _conv_bytes(nclients, batch, cin, ah, aw, cout, 3, 1, 1) +
               4.0 * nclients * batch * cout * (cin * 9 + 1), nclients)
 
 

@@ -127,8 +127,14 @@ class RankRound:
         pos = {}
         for r, cl in enumerate(lists):
             for i, k in enumerate(cl):
+                if k in pos:  # the all-reduce path would count it twice, this one once
+                    raise ops.FedHipError(f"exact FedAvg: client {k} is listed by more than "
+                                          f"one rank")
                 pos[k] = r * maxS + i
         order = sorted(pos)  # global client order: the reference's sequential loop
+        if order != list(range(len(self.all_sizes))):
+            raise ops.FedHipError(f"exact FedAvg: the ranks' client lists cover {len(order)} "
+                                  f"of {len(self.all_sizes)} clients")
         self._x_world, self._x_maxS = world, maxS
         self._x_w32 = torch.tensor([self.weights[k] for k in order], dtype=torch.float32,
                                    device=self.device)
@@ -195,6 +201,7 @@ class RankRound:
             if self.Q:
                 self._exact_fedavg(tr.bufs, self.Q, self.global_bufs)
             self.round_index += 1
+            self._host_timing(_t)
             return metrics
         # FedAvg: this rank's partial sum in client-list order, then RCCL all-reduce.
         ops.fedavg_weighted_sum(tr.params, self.w32, self.partial, row_index=self.rows, P=self.P)
@@ -207,12 +214,15 @@ class RankRound:
             if distributed:
                 dist.all_reduce(self.global_bufs, op=dist.ReduceOp.SUM, group=self.group)
         self.round_index += 1
+        self._host_timing(_t)
+        return metrics
+
+    def _host_timing(self, _t):
         if _t:
             torch.cuda.synchronize(self.device)
             _t.append(time.perf_counter())
             print("round host ms: plan %.1f, run_round %.1f, dp/fedavg+sync %.1f" % tuple(
                 1e3 * (b - a) for a, b in zip(_t, _t[1:])), file=sys.stderr)
-        return metrics
 
     def evaluate(self, data, labels, template_model=None):
         """Eval-mode metrics of the current global model on a device-resident test set

@@ -666,6 +666,10 @@ float fh_get_fill_fraction(void);
  * held and disarms; call it after the pair's DGRAD.  mode -1 disarms and drops a held launch
  * unissued (a caller's error path). */
 int fh_conv_pair(int32_t mode);
+/* The calling thread's pairing state, for instrumentation (bench.py's per-launch timing
+ * attributes a dual launch to both roles' work): *held = 1 while a WGRAD launch is held for
+ * the next DGRAD, *dual_launches = dual-role grids this thread has issued so far. */
+int fh_conv_pair_status(int32_t* held, int64_t* dual_launches);
 
 /* Lane streams (fedhip/lanes.py; replaces the reference's one-thread-per-client
  * concurrency, federated_simulation.py:309-318).  cu_mask (nullable; mask_words 32-bit

@@ -61,3 +61,39 @@ def test_write_detail_roundtrip(tmp_path):
     rel = bench.write_detail(out, str(p))
     assert rel is not None
     assert json.load(open(p))["instances"] == out["instances"]
+
+
+def test_compact_line_trims_long_free_text():
+    """long workload / cpu_baseline sample strings must not push the line past
+    the budget either (the pop loop alone only drops data / roofline_hbm / detail)."""
+    out = _stub("bench.json")
+    out["config"]["workload"] = "w" * 3000
+    out["cpu_baseline"]["sample"] = "s" * 3000
+    out["k2"]["config"]["workload"] = "k" * 3000
+    line = bench.compact(out)
+    assert len(json.dumps(line)) <= bench.MAX_LINE_BYTES
+    assert line["value"] == out["value"] and line["roofline"]["frac"] == out["roofline"]["frac"]
+    assert line["cpu_baseline"]["value"] > 0
+
+
+def test_shard_report_bounds_strong_scaling():
+    """--strong: the per-rank report names the longest client's sequential steps, which bound
+    any rank's round however the fixed client set is split."""
+    from fedhip.partition import lpt_assign
+    train = [4200, 1300, 900, 33, 32, 31, 1]
+    for world in (1, 2, 4):
+        rep = bench.shard_report(train, lpt_assign(train, world), epochs=2)
+        assert rep["longest_client_steps"] == 2 * 132
+        assert rep["total_client_steps"] == sum(2 * -(-n // 32) for n in train)
+        assert sum(r["clients"] for r in rep["ranks"]) == len(train)
+        assert max(r["longest_client_steps"] for r in rep["ranks"]) == 2 * 132
+
+
+def test_strong_client_set_is_fixed():
+    for key in ("KT", "K3"):
+        cfg = bench.CONFIGS[key]
+        sizes = [bench.build_clients(cfg, w, strong=True)[1] for w in (1, 2, 8)]
+        assert sizes[0] == sizes[1] == sizes[2]
+        assert len(sizes[0]) == cfg["clients"] * cfg.get("config_gpus", 1)
+    weak = bench.build_clients(bench.CONFIGS["KT"], 2)[1]
+    assert len(weak) == 64

@@ -228,3 +228,29 @@ def test_slab_step_validates_ranges_without_gpu():
         with pytest.raises(_lib.FedHipError, match="bad slab range"):
             _lib.call("fh_sgd_step_slabs", 4096, 4096, 4096, 64, 64, 1, arr, n, 0.1, 0.9, 0.0, 0,
                       None)
+
+
+def test_persample_slab_keeps_superseded_buffers():
+    """PersampleSlab.ensure grows its buffer for more clients; the old buffer stays
+    alive (a DP-SGD step program captured at a smaller client count still addresses it)."""
+    from fedhip import ops
+    s = ops.PersampleSlab("cpu")
+    nb2 = s.ensure(2, 32, 32, 64)
+    first = s.buf
+    assert first.numel() >= nb2 > 0
+    assert s.ensure(1, 32, 32, 64) <= first.numel() and s.buf is first  # no growth
+    nb8 = s.ensure(8, 32, 32, 64)
+    assert s.buf is not first and s.buf.numel() >= max(nb8, 2 * first.numel())
+    assert any(t is first for t in s.retired)
+
+
+def test_conv_pair_status_without_gpu():
+    """fh_conv_pair_status (instrumentation of the dual-role launch): nothing held, no dual
+    launch issued on a fresh thread; disarming is host-only."""
+    import ctypes
+    _lib.call("fh_conv_pair", -1)
+    held, duals = ctypes.c_int32(7), ctypes.c_int64(7)
+    _lib.call("fh_conv_pair_status", ctypes.byref(held), ctypes.byref(duals))
+    assert held.value == 0 and duals.value == 0
+    with pytest.raises(_lib.FedHipError):
+        _lib.call("fh_conv_pair_status", None, None)

@@ -1,8 +1,8 @@
-"""HBM traffic of the bench's own launches (r03): rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE
-passes (separate runs, tools/evidence.sh stage m) of
-`bench.py --steps 1 --warmup 1 --no-instances --no-k2 --separate-conv-bwd` (each layer's WGRAD
-and DGRAD as their own dispatches, not the dual-role launch; KT: the warmup and the timed round,
-lanes and step programs as timed), per launch SHAPE of bench.py's instrumented table:
+"""HBM traffic of the bench's own launches (r03; r05: the timed launches as they run): rocprofv3
+--pmc FETCH_SIZE and WRITE_SIZE passes (separate runs, tools/evidence.sh stage m) of
+`bench.py --steps 1 --warmup 1 --no-instances --no-k2` (KT: the warmup and the timed round,
+lanes, step programs and dual-role WGRAD + DGRAD launches as timed; add --separate-conv-bwd to
+the bench for per-role numbers), per launch SHAPE of bench.py's instrumented table:
 
   bytes(launch) = 2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE   (KiB counters; MI355X_MICROARCH.md
                   §HBM: FETCH_SIZE reports half the bytes of a wide coalesced read)
@@ -41,6 +41,9 @@ def shape_of(name):
     m = re.match(r"fh::dwgrad_q_kernel<(\d+),", n)
     if m:
         return ("wgrad", int(m.group(1)))
+    m = re.match(r"fh::dconv_wgrad_dual_kernel<(\d+),", n)
+    if m:
+        return ("dual", int(m.group(1)))
     m = re.match(r"fh::dconv_kernel<(\d), (\d+), (\d+), \d+, (\d+),", n)
     if m and int(m.group(4)) == 8:  # CK = 8: not the RGB first layer (Cr = 3 -> CK = 4)
         return ("fwd" if m.group(1) == "0" else "dgrad", int(m.group(2)))
@@ -55,7 +58,11 @@ KT = {("wgrad", 32, 0): "conv_wgrad:c32x32x32->32k3s1",
       ("fwd", 16, 0): "conv_fwd:c32x16x16->64k3s1", ("fwd", 16, 1): "conv_fwd:c64x16x16->64k3s1",
       ("fwd", 8, 0): "conv_fwd:c64x8x8->128k3s1", ("fwd", 8, 1): "conv_fwd:c128x8x8->128k3s1",
       ("dgrad", 16, 0): "conv_dgrad:c64x16x16->64k3s1", ("dgrad", 16, 1): "conv_dgrad:c32x16x16->64k3s1",
-      ("dgrad", 8, 0): "conv_dgrad:c128x8x8->128k3s1", ("dgrad", 8, 1): "conv_dgrad:c64x8x8->128k3s1"}
+      ("dgrad", 8, 0): "conv_dgrad:c128x8x8->128k3s1", ("dgrad", 8, 1): "conv_dgrad:c64x8x8->128k3s1",
+      # the dual-role WGRAD + DGRAD grid of a layer's backward (deeper layer first)
+      ("dual", 32, 0): "conv_bwd_dual:c32x32x32->32k3s1",
+      ("dual", 16, 0): "conv_bwd_dual:c64x16x16->64k3s1", ("dual", 16, 1): "conv_bwd_dual:c32x16x16->64k3s1",
+      ("dual", 8, 0): "conv_bwd_dual:c128x8x8->128k3s1", ("dual", 8, 1): "conv_bwd_dual:c64x8x8->128k3s1"}
 
 
 def main(fd, wd, out):

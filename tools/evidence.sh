@@ -8,9 +8,8 @@
 #      (--separate-conv-bwd): per-kernel averages of the dual-role launch's two roles
 #   k  the K3 / K4 / K5 / K2-dpsgd lines (+ their detail files)
 #   m  separate rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of the KT bench -> the
-#      per-launch-shape HBM traffic of the timed launches (tools/bench_traffic.py); run with
-#      --separate-conv-bwd, so WGRAD and DGRAD are their own dispatches (same kernel bodies
-#      as the dual-role launch's two roles)
+#      per-launch-shape HBM traffic of the timed launches as they run, dual-role WGRAD + DGRAD
+#      grids included (tools/bench_traffic.py)
 # default stages "tsb".  Every GPU step has its own time limit and the chain stops at the
 # first failure (set -e).
 set -e
@@ -57,8 +56,8 @@ if [[ $ST == *q* ]]; then  # the same kernel trace with WGRAD / DGRAD as separat
 fi
 if [[ $ST == *m* ]]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --rounds-target 0 --steps 1 --warmup 1 --no-instances --no-k2 --separate-conv-bwd --detail-out '' > $O/pmc_fetch.json 2> $O/pmc_fetch.log
-  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --no-cpu-baseline --rounds-target 0 --steps 1 --warmup 1 --no-instances --no-k2 --separate-conv-bwd --detail-out '' > $O/pmc_write.json 2> $O/pmc_write.log
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --rounds-target 0 --steps 1 --warmup 1 --no-instances --no-k2 --detail-out '' > $O/pmc_fetch.json 2> $O/pmc_fetch.log
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --no-cpu-baseline --rounds-target 0 --steps 1 --warmup 1 --no-instances --no-k2 --detail-out '' > $O/pmc_write.json 2> $O/pmc_write.log
   python3 $R/tools/bench_traffic.py $O/pmc_fetch $O/pmc_write $O/bench_traffic.json > $O/bench_traffic.log 2>&1 || true
   tail -5 $O/bench_traffic.log
   cd $R
