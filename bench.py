@@ -514,6 +514,26 @@ def roofline_of(tag, n, t, f, b, peak, hbm=False, workload=None):
                 frac=round(ach / peak, 4), traffic=measured_traffic(tag, f / n, workload))
 
 
+def timed_roofline(tag, inst_row, timed, steps, peak, ridge, workload, hbm=False):
+    """The roofline object of a launch shape from its launches in the TIMED rounds:
+    `timed` = (launches, total ms, dropped) of fh_timing_collect; the algorithmic FLOPs /
+    bytes per launch from the instrumented round's row (launches, ms, flops, bytes)."""
+    if not timed or not timed[0]:
+        return None
+    n_t, ms_t, dropped = timed
+    n_i, _, f_i, b_i = inst_row
+    fpl, bpl = f_i / n_i, b_i / n_i
+    r = roofline_of(tag, n_t, ms_t, fpl * n_t, bpl * n_t, peak, hbm=hbm, workload=workload)
+    r["measured"] = ("HIP events on the lane stream around every launch of this shape in the "
+                     "timed rounds (lanes concurrent, step programs as timed); algorithmic work "
+                     "per launch from the instrumented round")
+    r["launches_per_round"] = round(n_t / max(steps, 1), 2)
+    r["instrumented_launches_per_round"] = n_i
+    if dropped:
+        r["untimed_launches"] = dropped
+    return r
+
+
 _MAPS_THREAD = None
 
 
@@ -577,8 +597,37 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     gen = torch.Generator().manual_seed(7)
     if os.environ.get("FH_DUMP_MAPS"):
         dump_maps_periodically(os.environ["FH_DUMP_MAPS"])
+    # launch-group tags on from the first capture: each step program knows which of its
+    # kernels form which launch shape; every lane replays its steps as a program
+    ops.PROBE.tagging = True
+    for ln in rr.trainer.lanes:
+        ln.launch_mode = "program"
     for w in range(warmup):
         rr.run(data, lab, offs, args.opt, args.lr, seed=w, generator=gen)
+    torch.cuda.synchronize()
+    # one instrumented round (untimed, every step eager, the lanes one after another so a
+    # launch never shares the chip with another lane's): HIP events around EVERY conv /
+    # linear launch — every client count, ragged and tail steps included.  Launches are the
+    # timed rounds' launches: each layer's WGRAD + DGRAD pair is the one dual-role grid
+    # (conv_bwd_dual:<shape>, timed against both roles' FLOPs).  It picks the roofline launch
+    # shapes, which the timed rounds then time on their own streams.
+    inst = buckets = rows = None
+    peak = FP32_MFMA_PEAK_TFLOPS
+    ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    timed_tags = []
+    if not args.no_instances:
+        ops.PROBE.reset()
+        ops.PROBE.tag, ops.PROBE.enabled = "*", True
+        rr.run(data, lab, offs, args.opt, args.lr, seed=999, generator=gen, serialize_lanes=True)
+        ops.PROBE.enabled = False
+        inst = ops.PROBE.by_tag()
+        buckets = ops.PROBE.by_tag_bucket()
+        rows = summarize_instances(inst, buckets, peak)[0]
+        timed_tags = [rows[0][0]]
+        hb = [tg for tg, vv in rows if vv[2] <= ridge * vv[3]]
+        if hb and hb[0] not in timed_tags:
+            timed_tags.append(hb[0])
+        ops.timing_enable(timed_tags, reserve=max(4096, 2 * steps * max(v[0] for v in inst.values())))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -591,41 +640,38 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    timed = {t: ops.timing_collect(t) for t in timed_tags}
+    ops.timing_enable([])
+    ops.PROBE.tagging = False
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    # one instrumented round (untimed, every step eager, the lanes one after another so a
-    # launch never shares the chip with another lane's): HIP events around EVERY conv /
-    # linear launch — every client count, ragged and tail steps included.  Launches are the
-    # timed rounds' launches: each layer's WGRAD + DGRAD pair is the one dual-role grid
-    # (conv_bwd_dual:<shape>, timed against both roles' FLOPs)
-    inst = buckets = None
-    if not args.no_instances:
-        ops.PROBE.reset()
-        ops.PROBE.tag, ops.PROBE.enabled = "*", True
-        rr.run(data, lab, offs, args.opt, args.lr, seed=999, generator=gen, serialize_lanes=True)
-        ops.PROBE.enabled = False
-        inst = ops.PROBE.by_tag()
-        buckets = ops.PROBE.by_tag_bucket()
     if rank != 0:
         return None
     value = total_images * steps / elapsed
     fl = TRAIN_FLOPS[flops_key(cfg)]
-    peak = FP32_MFMA_PEAK_TFLOPS
     roof = roof_hbm = instances = by_bucket = conv_all = None
+    roof_iso = roof_hbm_iso = None
     if inst:
         rows, instances, by_bucket, conv_all = summarize_instances(inst, buckets, peak)
-        # the roofline kernel: the launch shape with the largest share of the round's
-        # conv/linear time, averaged over ALL its launches (every client count, ragged
-        # batches, tail steps); roofline_hbm: the same for the largest HBM-bound shape
-        tag, v = rows[0]
-        ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
-        roof = roofline_of(tag, *v, peak, hbm=v[2] <= ridge * v[3], workload=key)
-        hb = [(tg, vv) for tg, vv in rows if vv[2] <= ridge * vv[3]]
+        # the roofline kernel: the launch shape with the largest share of the instrumented
+        # round's conv/linear time; roofline_hbm: the largest HBM-bound shape.  Their
+        # numbers: every launch of the shape in the TIMED rounds, HIP events on its lane's
+        # stream (lanes concurrent, as timed), algorithmic FLOPs / bytes per launch from the
+        # instrumented round (the same launches: same clients, shard sizes and plan shape).
+        # The *_isolated objects: the instrumented round's own timing (lanes serialised).
+        by = dict(rows)
+        tag = timed_tags[0]
+        v = by[tag]
+        roof_iso = roofline_of(tag, *v, peak, hbm=v[2] <= ridge * v[3], workload=key)
+        roof = timed_roofline(tag, v, timed.get(tag), steps, peak, ridge, key) or roof_iso
+        hb = [tg for tg in timed_tags[1:]] or ([tag] if v[2] <= ridge * v[3] else [])
         if hb:
-            roof_hbm = roofline_of(hb[0][0], *hb[0][1], peak, hbm=True)
-        for r in [roof, roof_hbm] + instances:
+            roof_hbm_iso = roofline_of(hb[0], *by[hb[0]], peak, hbm=True)
+            roof_hbm = timed_roofline(hb[0], by[hb[0]], timed.get(hb[0]), steps, peak, ridge,
+                                      None, hbm=True) or roof_hbm_iso
+        for r in [roof, roof_hbm, roof_iso, roof_hbm_iso] + instances:
             if r and ops.PROBE.exec_ratio.get(r.get("kernel", r.get("launch"))):
                 # the kernel runs this layer's map inside zero-ringed planes: FLOPs above are
                 # the algorithmic ones, the kernel executes this factor more
@@ -659,6 +705,8 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         "round_frac": round(value * fl / 1e12 / peak, 4),
         "roofline": roof,
         "roofline_hbm": roof_hbm,
+        "roofline_isolated": roof_iso,
+        "roofline_hbm_isolated": roof_hbm_iso,
         "conv_linear_all_launches": conv_all,
         "instances": instances,
         "instances_by_clients": by_bucket,
@@ -756,6 +804,64 @@ def run_dpsgd(args, dev, steps, warmup):
             "instances_by_clients": by_bucket, "_sizes": sizes}
 
 
+def predict_strong(key, args, dev, worlds, steps, warmup):
+    """Strong-scaling prediction on one GPU: the config's fixed client set is
+    LPT-sharded over N ranks exactly as `--strong --gpus N` would shard it, and each rank's
+    share is timed here as its own RankRound (lanes as planned for that share, the rank's
+    partial FedAvg; no collective — KT's one 5.9 MB all-reduce is ~0.1 ms over xGMI).  The
+    N-GPU round cannot be shorter than its slowest rank, so the predicted N-GPU round time
+    is max over ranks and the speed-up over N = 1 is t(1) / max_r t(r)."""
+    cfg = CONFIGS[key]
+    _, train = build_clients(cfg, 1, strong=True)
+    torch.manual_seed(0)
+    template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
+    dp = DPConfig(epsilon=cfg["dp"]) if cfg["dp"] else None
+    tf = ops.DataTransform.mnist() if cfg["shape"][0] == 1 else ops.DataTransform.cifar10()
+    comp = None
+    if cfg.get("compression"):
+        from fedhip.compress import CompressionConfig
+        comp = CompressionConfig(algorithm=cfg["compression"][0],
+                                 sparsity_ratio=cfg["compression"][1])
+    res = {}
+    for world in worlds:
+        assign = lpt_assign(train, world)
+        per = []
+        for r in range(world):
+            rr = RankRound(template, train, assign[r], epochs=cfg["epochs"], device=dev, dp=dp,
+                           lanes=args.lanes, transform=tf, compression=comp)
+            data, lab, offs = make_rank_data(cfg, train, rr.slots, dev, r)
+            gen = torch.Generator().manual_seed(7)
+            for w in range(warmup):
+                rr.run(data, lab, offs, args.opt, args.lr, seed=w, generator=gen)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for s_ in range(steps):
+                rr.run(data, lab, offs, args.opt, args.lr, seed=100 + s_, generator=gen)
+            torch.cuda.synchronize()
+            per.append(1e3 * (time.perf_counter() - t0) / steps)
+            del rr, data, lab
+            torch.cuda.empty_cache()
+        rep = shard_report(train, assign, cfg["epochs"])
+        res[world] = {"rank_ms": [round(v, 2) for v in per], "round_ms": round(max(per), 2),
+                      "slowest_rank": int(np.argmax(per)),
+                      "clients_per_rank": [r_["clients"] for r_ in rep["ranks"]],
+                      "longest_client_steps_per_rank": [r_["longest_client_steps"]
+                                                        for r_ in rep["ranks"]]}
+        log(f"predict-strong {key} N={world}: rank ms {res[world]['rank_ms']}")
+    base = res[worlds[0]]["round_ms"] if worlds[0] == 1 else None
+    images = cfg["epochs"] * sum(train)
+    for world, v in res.items():
+        v["client_images_per_s"] = round(images / (v["round_ms"] * 1e-3), 1)
+        if base:
+            v["speedup_over_1"] = round(base / v["round_ms"], 3)
+    return {"metric": "client-images/sec/node (strong-scaling prediction)", "config": key,
+            "clients": len(train), "images_per_round": images,
+            "longest_client_steps": max(cfg["epochs"] * math.ceil(n / 32) for n in train),
+            "method": "each rank's LPT share of the fixed client set timed as its own RankRound "
+                      "on one MI355X; predicted N-GPU round = slowest rank (no collective "
+                      "time)", "steps": steps, "warmup": warmup, "worlds": res}
+
+
 def cpu_baseline_dpsgd(sizes, lr=0.01, seconds=5.0, max_norm=1.0, eps=1.0, delta=1e-5):
     """The K2-dpsgd round on the host cores: oracle/dpsgd_ref.py (explicit per-sample
     gradients, per-sample clip to C, N(0, (sigma C)^2) noise with the reference's
@@ -830,6 +936,11 @@ def compact(out):
                                 "dtype", "data", "config", "achieved_tflops_step",
                                 "round_frac") if k in out}
     line["roofline"] = _roof_short(out.get("roofline"))
+    if out.get("roofline_isolated") and line["roofline"]:
+        # the same launch shape timed alone (instrumented round, lanes serialised)
+        line["roofline"]["isolated_frac"] = out["roofline_isolated"]["frac"]
+    if line["roofline"] and (out.get("roofline") or {}).get("executed_over_algorithmic"):
+        line["roofline"]["executed_over_algorithmic"] = out["roofline"]["executed_over_algorithmic"]
     if "roofline_hbm" in out:
         line["roofline_hbm"] = _roof_short(out["roofline_hbm"])
     ca = out.get("conv_linear_all_launches")
@@ -844,7 +955,14 @@ def compact(out):
     if k2:
         line["k2"] = {"value": k2["value"], "unit": k2["unit"], "ms_per_step": k2["ms_per_step"],
                       "steps": k2["steps"], "workload": k2["config"]["workload"],
-                      "round_frac": k2["round_frac"], "roofline": _roof_short(k2.get("roofline")),
+                      "round_frac": k2["round_frac"],
+                      "roofline": dict(_roof_short(k2.get("roofline")) or {},
+                                       **({"isolated_frac": k2["roofline_isolated"]["frac"]}
+                                          if k2.get("roofline_isolated") else {}),
+                                       **({"executed_over_algorithmic":
+                                           k2["roofline"]["executed_over_algorithmic"]}
+                                          if (k2.get("roofline") or {}).get(
+                                              "executed_over_algorithmic") else {})) or None,
                       "roofline_hbm": _roof_short(k2.get("roofline_hbm")),
                       "cpu_baseline": _cpu_short(k2.get("cpu_baseline"))}
     line["env"] = out.get("env", {})
@@ -915,6 +1033,9 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the config's whole client set (KT 32, K3 64, K4 128, K5 "
                          "256 clients) fixed whatever N, LPT-sharded over the ranks")
+    ap.add_argument("--predict-strong", default="",
+                    help="comma list of GPU counts (e.g. 1,2,4,8): time each rank's LPT share "
+                         "of the fixed client set on this one GPU (strong-scaling prediction)")
     ap.add_argument("--exact-fedavg", action="store_true",
                     help="N>1: all-gather + sequential FedAvg (bit-exact) instead of all-reduce")
     ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
@@ -927,6 +1048,13 @@ def main():
         from fedhip import ops as _ops
         _ops.set_conv_pairing(False)
     world, rank, dev = setup(args)
+    if args.predict_strong:
+        if world != 1:
+            raise SystemExit("--predict-strong: one process, one GPU")
+        worlds = [int(v) for v in args.predict_strong.split(",")]
+        out = predict_strong(args.config, args, dev, worlds, args.steps, args.warmup)
+        print(json.dumps(out), flush=True)
+        return
     if args.config == "K2-dpsgd":
         if world != 1:
             raise SystemExit("K2-dpsgd: one GPU only")

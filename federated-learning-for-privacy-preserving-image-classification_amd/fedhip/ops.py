@@ -84,7 +84,30 @@ class LaunchProbe:
     # the launch itself, not the host's issue time (the spin is outside the window)
     lead_cycles = 120_000
 
+    # r05 launch-group tags: with `tagging` on, every probed call is bracketed by
+    # fh_tag_begin / fh_tag_end, so a recorded step program knows which of its kernels form
+    # which launch shape, and bench.py times one shape over the TIMED rounds with HIP events
+    # on the launch stream (fh_timing_enable / fh_timing_collect, csrc/program.hip)
+    tagging = False
+    _ids: dict = {}
+    _open = False
+
+    def tag_id(self, tag):
+        i = self._ids.get(tag)
+        if i is None:
+            i = self._ids[tag] = len(self._ids) + 1
+        return i
+
+    def close(self):
+        """End the open launch group (fh_tag_end), if any."""
+        if self._open:
+            self._open = False
+            call("fh_tag_end")
+
     def begin(self, tag):
+        if self.tagging:
+            call("fh_tag_begin", self.tag_id(tag))
+            self._open = True
         if not self.enabled:
             return None
         self.seen[tag] = self.seen.get(tag, 0) + 1
@@ -100,6 +123,7 @@ class LaunchProbe:
         """flops / nbytes: the launch's algorithmic work — every operand read
         and every result written once; clients: its active-client count (bench.py buckets);
         tag: record under this launch shape instead of begin()'s."""
+        self.close()
         if h is None:
             return
         e2 = torch.cuda.Event(enable_timing=True)
@@ -259,8 +283,10 @@ def conv_pair(mode: int):
         tag, fl, nb, nc = PROBE.held
         PROBE.held = None
         ev = PROBE.begin(tag)
-        call("fh_conv_pair", 0)
-        PROBE.end(ev, fl, nb, nc)
+        try:
+            call("fh_conv_pair", 0)
+        finally:
+            PROBE.end(ev, fl, nb, nc)
         return
     call("fh_conv_pair", int(mode) if _PAIRING[0] else 0)
 
@@ -277,38 +303,57 @@ def _probe_wgrad_end(ev, tag, flops, nbytes, nclients):
     whose window then times both (_probe_dgrad_end)."""
     if ev is not None and _pair_status()[0]:
         PROBE.held = (tag, flops, nbytes, nclients)
+        PROBE.close()
         return
     PROBE.end(ev, flops, nbytes, nclients)
 
 
 def _probe_dgrad_begin(tag):
+    """PROBE.begin for a DGRAD call, plus the dual-launch count when a WGRAD is held for it."""
     ev = PROBE.begin(tag)
-    return ev, (_pair_status()[1] if ev is not None and PROBE.held is not None else None)
+    if (ev is None or PROBE.held is None) and not PROBE.tagging:
+        return ev, None
+    held, duals = _pair_status()
+    return ev, (duals if held else None)
 
 
-def _probe_dgrad_end(ev, duals0, flops, nbytes, nclients):
-    """PROBE.end for a DGRAD call.  With a WGRAD held before it, the window contains the
-    dual-role launch (recorded as conv_bwd_dual:<shape>, FLOPs / bytes = both roles') or the
-    held WGRAD issued on its own ahead of the DGRAD (conv_bwd_seq:<shape>, both launches)."""
-    if ev is None or duals0 is None:
+def _probe_dgrad_end(ev, duals0, flops, nbytes, nclients, tag):
+    """PROBE.end for a DGRAD call.  With a WGRAD held before it, the call issued the dual-role
+    launch (recorded as conv_bwd_dual:<shape>, FLOPs / bytes = both roles') or the held WGRAD
+    on its own ahead of the DGRAD (conv_bwd_seq:<shape>, both launches); tagging renames the
+    launch group the same way."""
+    if duals0 is None:
         PROBE.end(ev, flops, nbytes, nclients)
         return
     held, duals = _pair_status()
     if held:  # not this DGRAD's pair (another path): the WGRAD is still waiting
         PROBE.end(ev, flops, nbytes, nclients)
         return
+    dtag = ("conv_bwd_dual:" if duals > duals0 else "conv_bwd_seq:") + tag.split(":", 1)[1]
+    if PROBE.tagging:
+        call("fh_tag_retag", PROBE.tag_id(dtag))
+    if ev is None or PROBE.held is None:
+        PROBE.end(ev, flops, nbytes, nclients)
+        return
     wtag, wfl, wnb, _ = PROBE.held
     PROBE.held = None
-    kind = "conv_bwd_dual:" if duals > duals0 else "conv_bwd_seq:"
-    dtag = kind + wtag.split(":", 1)[1]
     if wtag in PROBE.exec_ratio:
         PROBE.exec_ratio[dtag] = PROBE.exec_ratio[wtag]
     PROBE.end(ev, flops + wfl, nbytes + wnb, nclients, tag=dtag)
 
 
-def conv_pair_reset():
-    """Disarm and drop a held WGRAD launch unissued (fh_conv_pair(-1)): a step's error path."""
-    call("fh_conv_pair", -1)
+def timing_enable(tags, reserve=65536):
+    """Time every launch of these launch shapes from now on (fh_timing_enable; [] = off)."""
+    ids = (ctypes.c_int32 * max(1, len(tags)))(*[PROBE.tag_id(t) for t in tags])
+    call("fh_timing_enable", ids, len(tags), int(reserve) if tags else 0)
+
+
+def timing_collect(tag):
+    """(launches, total ms, dropped groups) timed for a launch shape since timing_enable."""
+    n, ms, dr = ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
+    call("fh_timing_collect", PROBE.tag_id(tag), ctypes.byref(n), ctypes.byref(ms),
+         ctypes.byref(dr))
+    return n.value, ms.value, dr.value
 
 
 def _ws_for(fn_name, device, *args):
@@ -426,7 +471,8 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
              _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
              int(accumulate), ptr(ws), nb, stream_handle())
     _probe_dgrad_end(ev, duals0, _conv_flops(nclients, batch, cin, ah, aw, cout, k, stride, pad),
-                     _conv_bytes(nclients, batch, cin, ah, aw, cout, k, stride, pad), nclients)
+                     _conv_bytes(nclients, batch, cin, ah, aw, cout, k, stride, pad), nclients,
+                     tag)
     return dx
 
 

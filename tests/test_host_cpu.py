@@ -254,3 +254,20 @@ def test_conv_pair_status_without_gpu():
     assert held.value == 0 and duals.value == 0
     with pytest.raises(_lib.FedHipError):
         _lib.call("fh_conv_pair_status", None, None)
+
+
+def test_launch_group_tags_without_gpu():
+    """fh_tag_* / fh_timing_* (bench.py's timed-round roofline): host bookkeeping only when no
+    program records and no tag is enabled."""
+    import ctypes
+    with pytest.raises(_lib.FedHipError, match="tag"):
+        _lib.call("fh_tag_begin", 0)
+    with pytest.raises(_lib.FedHipError, match="retag"):
+        _lib.call("fh_tag_retag", 3)           # no open group
+    _lib.call("fh_tag_begin", 3)
+    _lib.call("fh_tag_retag", 4)
+    _lib.call("fh_tag_end")
+    _lib.call("fh_timing_enable", None, 0, 0)  # off, no events created
+    n, ms, dr = ctypes.c_int64(7), ctypes.c_double(7.0), ctypes.c_int64(7)
+    _lib.call("fh_timing_collect", 4, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(dr))
+    assert (n.value, ms.value, dr.value) == (0, 0.0, 0)

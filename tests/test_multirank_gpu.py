@@ -194,3 +194,26 @@ def test_rankround_exact_mode_bitwise():
         assert np.array_equal(r0["gbufs"].view(np.uint32), bseq.astype(np.float32).view(np.uint32))
         if rnd + 1 < ROUNDS:  # the next round starts from the exact global model
             assert np.array_equal(res[0][rnd + 1]["start"], r0["glob"])
+
+
+def test_bench_strong_scaling_rehearsal():
+    """bench.py --strong (r05): the config's fixed client set (K2: 32 clients) LPT-sharded over
+    2 ranks on cuda:0 over gloo, one all-reduce per round; the line says "strong" and counts
+    the same 32 clients as the one-GPU run."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = 29870 + os.getpid() % 100
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--steps", "1", "--warmup", "1", "--config", "K2", "--dist-backend", "gloo",
+           "--one-device", "--no-cpu-baseline", "--rounds-target", "0", "--strong",
+           "--no-instances", "--detail-out", ""]
+    r = subprocess.run(cmd, cwd=repo, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["scaling"] == "strong"
+    assert out["config"]["clients"] == 32
+    import bench
+    assert out["config"]["images_per_round"] == sum(bench.build_clients(bench.CONFIGS["K2"], 1)[1])
