@@ -195,7 +195,7 @@ def timed_passes(run_client, sizes, seconds, passes=3):
     """BASELINE.md §2 / SURVEY.md §8d: one warm-up client (untimed: first-touch allocations,
     oneDNN primitive creation), then the same client sample timed `passes` times; the
     baseline is the median pass.  The sample is the clients median shard size first, as many
-    as the warm-up client's rate says fit in ~`seconds` per pass.  run_client(i, n) trains
+    as the warm-up client's second (warm) run says fit in ~`seconds` per pass.  run_client(i, n) trains
     client i of `sizes` and returns its client-images and its result row; run_client.prepare(i)
     generates client i's data (untimed) and run_client.finish(rows, ns) runs once per pass
     (FedAvg)."""
@@ -203,8 +203,9 @@ def timed_passes(run_client, sizes, seconds, passes=3):
     order = [i for i in sorted(range(len(sizes)), key=lambda i: (abs(sizes[i] - med), sizes[i]))
              if sizes[i] > 0]
     run_client.prepare(order[0])
+    run_client(order[0])  # cold: its rate would undersize the sample
     t0 = time.perf_counter()
-    imgs0, _ = run_client(order[0])
+    imgs0, _ = run_client(order[0])  # warm: sizes the sample
     rate = imgs0 / max(time.perf_counter() - t0, 1e-6)
     sample, budget = [], 0.0
     for i in order:

@@ -342,6 +342,14 @@ def _probe_dgrad_end(ev, duals0, flops, nbytes, nclients, tag):
     PROBE.end(ev, flops + wfl, nbytes + wnb, nclients, tag=dtag)
 
 
+def conv_pair_reset():
+    """Disarm and drop a held WGRAD launch unissued (fh_conv_pair(-1)): a step's error path.
+    Also closes an open launch group."""
+    PROBE.held = None
+    PROBE.close()
+    call("fh_conv_pair", -1)
+
+
 def timing_enable(tags, reserve=65536):
     """Time every launch of these launch shapes from now on (fh_timing_enable; [] = off)."""
     ids = (ctypes.c_int32 * max(1, len(tags)))(*[PROBE.tag_id(t) for t in tags])

@@ -271,3 +271,23 @@ def test_launch_group_tags_without_gpu():
     n, ms, dr = ctypes.c_int64(7), ctypes.c_double(7.0), ctypes.c_int64(7)
     _lib.call("fh_timing_collect", 4, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(dr))
     assert (n.value, ms.value, dr.value) == (0, 0.0, 0)
+
+
+def test_every_ops_attribute_used_exists():
+    """Every `ops.<name>` the product modules reference is defined in fedhip/ops.py (an
+    AttributeError there would only show on the GPU box)."""
+    import ast
+    import glob
+    from fedhip import ops
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "federated-learning-for-privacy-preserving-image-classification_amd")
+    files = glob.glob(os.path.join(pkg, "fedhip", "*.py")) + \
+        glob.glob(os.path.join(pkg, "src", "**", "*.py"), recursive=True) + \
+        [os.path.join(os.path.dirname(pkg), "bench.py")]
+    missing = set()
+    for f in files:
+        for node in ast.walk(ast.parse(open(f).read())):
+            if (isinstance(node, ast.Attribute) and isinstance(node.value, ast.Name)
+                    and node.value.id in ("ops", "_ops") and not hasattr(ops, node.attr)):
+                missing.add((os.path.basename(f), node.attr))
+    assert not missing, sorted(missing)
