@@ -515,23 +515,38 @@ def roofline_of(tag, n, t, f, b, peak, hbm=False, workload=None):
                 frac=round(ach / peak, 4), traffic=measured_traffic(tag, f / n, workload))
 
 
-def timed_roofline(tag, inst_row, timed, steps, peak, ridge, workload, hbm=False):
+def launch_stamps_for(tag, dev):
+    """ops.LaunchStamps for a dual-role conv backward shape "conv_bwd_dual:c{cin}x{h}x{w}->
+    {cout}k3s1" (the kernel's plane: h scaled by sqrt(executed / algorithmic), e.g. SimpleCNN's
+    14x14 map on 16x16 planes), else None (other shapes: instrumented-round timing only)."""
+    m = re.match(r"conv_bwd_dual:c(\d+)x(\d+)x\d+->(\d+)k3s1$", tag)
+    if not m:
+        return None
+    cin, h, cout = int(m.group(1)), int(m.group(2)), int(m.group(3))
+    w = int(round(h * math.sqrt(ops.PROBE.exec_ratio.get(tag, 1.0))))
+    return ops.LaunchStamps(dev, w, cin, cout)
+
+
+def timed_roofline(tag, inst_row, timed, steps, peak, workload):
     """The roofline object of a launch shape from its launches in the TIMED rounds:
-    `timed` = (launches, total ms, dropped) of fh_timing_collect; the algorithmic FLOPs /
-    bytes per launch from the instrumented round's row (launches, ms, flops, bytes)."""
+    `timed` = (per-launch durations in ms, dropped records) from ops.LaunchStamps; the
+    algorithmic FLOPs / bytes per launch from the instrumented round's row (launches, ms,
+    flops, bytes)."""
     if not timed or not timed[0]:
         return None
-    n_t, ms_t, dropped = timed
+    durs, dropped = timed
+    n_t, ms_t = len(durs), float(sum(durs))
     n_i, _, f_i, b_i = inst_row
     fpl, bpl = f_i / n_i, b_i / n_i
-    r = roofline_of(tag, n_t, ms_t, fpl * n_t, bpl * n_t, peak, hbm=hbm, workload=workload)
-    r["measured"] = ("HIP events on the lane stream around every launch of this shape in the "
-                     "timed rounds (lanes concurrent, step programs as timed); algorithmic work "
-                     "per launch from the instrumented round")
+    r = roofline_of(tag, n_t, ms_t, fpl * n_t, bpl * n_t, peak, workload=workload)
+    r["measured"] = ("every launch of this shape in the timed rounds (lanes concurrent, step "
+                     "programs as timed), begin-to-end from the kernel's own 100 MHz wall-clock "
+                     "stamps per workgroup (ops.LaunchStamps); algorithmic work per launch from "
+                     "the instrumented round")
     r["launches_per_round"] = round(n_t / max(steps, 1), 2)
     r["instrumented_launches_per_round"] = n_i
     if dropped:
-        r["untimed_launches"] = dropped
+        r["dropped_records"] = dropped
     return r
 
 
@@ -598,11 +613,6 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     gen = torch.Generator().manual_seed(7)
     if os.environ.get("FH_DUMP_MAPS"):
         dump_maps_periodically(os.environ["FH_DUMP_MAPS"])
-    # launch-group tags on from the first capture: each step program knows which of its
-    # kernels form which launch shape; every lane replays its steps as a program
-    ops.PROBE.tagging = True
-    for ln in rr.trainer.lanes:
-        ln.launch_mode = "program"
     for w in range(warmup):
         rr.run(data, lab, offs, args.opt, args.lr, seed=w, generator=gen)
     torch.cuda.synchronize()
@@ -611,11 +621,10 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     # linear launch — every client count, ragged and tail steps included.  Launches are the
     # timed rounds' launches: each layer's WGRAD + DGRAD pair is the one dual-role grid
     # (conv_bwd_dual:<shape>, timed against both roles' FLOPs).  It picks the roofline launch
-    # shapes, which the timed rounds then time on their own streams.
-    inst = buckets = rows = None
+    # shape, whose launches the timed rounds then time from the kernel's own wall-clock stamps.
+    inst = buckets = rows = stamps = None
     peak = FP32_MFMA_PEAK_TFLOPS
     ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
-    timed_tags = []
     if not args.no_instances:
         ops.PROBE.reset()
         ops.PROBE.tag, ops.PROBE.enabled = "*", True
@@ -624,11 +633,9 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         inst = ops.PROBE.by_tag()
         buckets = ops.PROBE.by_tag_bucket()
         rows = summarize_instances(inst, buckets, peak)[0]
-        timed_tags = [rows[0][0]]
-        hb = [tg for tg, vv in rows if vv[2] <= ridge * vv[3]]
-        if hb and hb[0] not in timed_tags:
-            timed_tags.append(hb[0])
-        ops.timing_enable(timed_tags, reserve=max(4096, 2 * steps * max(v[0] for v in inst.values())))
+        stamps = launch_stamps_for(rows[0][0], dev)
+        if stamps is not None:
+            stamps.start()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -641,9 +648,11 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    timed = {t: ops.timing_collect(t) for t in timed_tags}
-    ops.timing_enable([])
-    ops.PROBE.tagging = False
+    timed = None
+    if stamps is not None:
+        stamps.stop()
+        timed = stamps.durations_ms()
+        del stamps
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -653,26 +662,24 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     value = total_images * steps / elapsed
     fl = TRAIN_FLOPS[flops_key(cfg)]
     roof = roof_hbm = instances = by_bucket = conv_all = None
-    roof_iso = roof_hbm_iso = None
+    roof_iso = None
     if inst:
         rows, instances, by_bucket, conv_all = summarize_instances(inst, buckets, peak)
         # the roofline kernel: the launch shape with the largest share of the instrumented
-        # round's conv/linear time; roofline_hbm: the largest HBM-bound shape.  Their
-        # numbers: every launch of the shape in the TIMED rounds, HIP events on its lane's
-        # stream (lanes concurrent, as timed), algorithmic FLOPs / bytes per launch from the
-        # instrumented round (the same launches: same clients, shard sizes and plan shape).
-        # The *_isolated objects: the instrumented round's own timing (lanes serialised).
+        # round's conv/linear time.  Its numbers: every launch of the shape in the TIMED rounds
+        # (lanes concurrent, step programs, as timed), begin-to-end from the kernel's own
+        # wall-clock stamps; algorithmic FLOPs / bytes per launch from the instrumented round
+        # (the same launches: same clients, shard sizes and plan shape).  roofline_isolated:
+        # the instrumented round's HIP-event timing of the same shape (lanes serialised).
+        # roofline_hbm: the largest HBM-bound shape, instrumented-round timing.
         by = dict(rows)
-        tag = timed_tags[0]
-        v = by[tag]
+        tag, v = rows[0]
         roof_iso = roofline_of(tag, *v, peak, hbm=v[2] <= ridge * v[3], workload=key)
-        roof = timed_roofline(tag, v, timed.get(tag), steps, peak, ridge, key) or roof_iso
-        hb = [tg for tg in timed_tags[1:]] or ([tag] if v[2] <= ridge * v[3] else [])
+        roof = timed_roofline(tag, v, timed, steps, peak, key) or roof_iso
+        hb = [tg for tg, vv in rows if vv[2] <= ridge * vv[3]]
         if hb:
-            roof_hbm_iso = roofline_of(hb[0], *by[hb[0]], peak, hbm=True)
-            roof_hbm = timed_roofline(hb[0], by[hb[0]], timed.get(hb[0]), steps, peak, ridge,
-                                      None, hbm=True) or roof_hbm_iso
-        for r in [roof, roof_hbm, roof_iso, roof_hbm_iso] + instances:
+            roof_hbm = roofline_of(hb[0], *by[hb[0]], peak, hbm=True)
+        for r in [roof, roof_hbm, roof_iso] + instances:
             if r and ops.PROBE.exec_ratio.get(r.get("kernel", r.get("launch"))):
                 # the kernel runs this layer's map inside zero-ringed planes: FLOPs above are
                 # the algorithmic ones, the kernel executes this factor more
@@ -707,7 +714,6 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         "roofline": roof,
         "roofline_hbm": roof_hbm,
         "roofline_isolated": roof_iso,
-        "roofline_hbm_isolated": roof_hbm_iso,
         "conv_linear_all_launches": conv_all,
         "instances": instances,
         "instances_by_clients": by_bucket,

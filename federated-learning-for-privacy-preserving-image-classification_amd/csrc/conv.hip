@@ -1798,6 +1798,28 @@ extern "C" int fh_conv_pair(int32_t mode) {
     return flush_pending_wgrad();
 }
 
+extern "C" int fh_launch_ts_set(void* rec, void* count, uint32_t cap, int32_t w, int32_t cin,
+                                int32_t cout) {
+    FH_REQUIRE(!rec || (count && cap > 0 && ((uintptr_t)rec % 16) == 0 && w > 0 && cin > 0 &&
+                        cout > 0 && cin < 4096 && cout < 4096 && w < 256),
+               "launch_ts_set: bad arguments");
+    LaunchTs t{(uint32_t*)rec, (uint32_t*)count, rec ? cap : 0u,
+               rec ? dual_shape_key(w, cin, cout) : 0u};
+    const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_launch_ts), &t, sizeof(t));
+    FH_REQUIRE(e == hipSuccess, "launch_ts_set: %s", hipGetErrorString(e));
+    return FH_OK;
+}
+
+extern "C" int fh_wall_clock_khz(int32_t* khz) {
+    FH_REQUIRE(khz, "wall_clock_khz: null pointer");
+    int dev = 0, v = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev);
+    FH_REQUIRE(e == hipSuccess, "wall_clock_khz: %s", hipGetErrorString(e));
+    *khz = v;
+    return FH_OK;
+}
+
 extern "C" int fh_conv_pair_status(int32_t* held, int64_t* dual_launches) {
     FH_REQUIRE(held && dual_launches, "conv_pair_status: null pointer");
     *held = g_pend.on ? 1 : 0;

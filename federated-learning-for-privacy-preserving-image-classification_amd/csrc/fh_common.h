@@ -76,11 +76,6 @@ struct Recorder;                            // program.hip
 extern thread_local Recorder* g_recorder;   // non-null while recording a step program
 void record_kernel(Recorder* r, const void* func, dim3 grid, dim3 block, size_t shmem,
                    KernelArgs* args /* ownership passes */);
-// launch-group timing (program.hip, fh_tag_begin / fh_timing_enable): non-zero while the
-// calling thread is inside a tagged call whose tag is being timed; the hook records the
-// group's start event ahead of its first eager launch
-extern thread_local int g_tag_timed;
-void tag_before_launch(hipStream_t st);
 
 inline bool launch_geometry_ok(dim3 grid, dim3 block) {
     return grid.x && grid.y && grid.z && block.x && block.y && block.z &&
@@ -92,7 +87,6 @@ inline hipError_t launch_kernel(void (*k)(P...), dim3 grid, dim3 block, size_t s
                                 hipStream_t st, A&&... a) {
     static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
     if (!launch_geometry_ok(grid, block)) return hipErrorInvalidConfiguration;
-    if (g_tag_timed) tag_before_launch(st);
     if (g_recorder) {
         auto* owned = new KernelArgsT<std::decay_t<P>...>(static_cast<std::decay_t<P>>(a)...);
         const hipError_t e = hipLaunchKernel((const void*)k, grid, block, owned->params, shmem, st);

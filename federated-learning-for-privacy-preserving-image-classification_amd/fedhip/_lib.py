@@ -151,11 +151,8 @@ SIGNATURES = {
     "fh_get_fill_fraction": (F32, []),
     "fh_conv_pair": (I32, [I32]),
     "fh_conv_pair_status": (I32, [P, P]),
-    "fh_tag_begin": (I32, [I32]),
-    "fh_tag_retag": (I32, [I32]),
-    "fh_tag_end": (I32, []),
-    "fh_timing_enable": (I32, [P, I32, I32]),
-    "fh_timing_collect": (I32, [I32, P, P, P]),
+    "fh_launch_ts_set": (I32, [P, P, ctypes.c_uint32, I32, I32, I32]),
+    "fh_wall_clock_khz": (I32, [P]),
     "fh_stream_create": (I32, [I32, P, I32, P]),
     "fh_stream_destroy": (I32, [P]),
     "fh_record_begin": (I32, [P]),

@@ -84,30 +84,7 @@ class LaunchProbe:
     # the launch itself, not the host's issue time (the spin is outside the window)
     lead_cycles = 120_000
 
-    # r05 launch-group tags: with `tagging` on, every probed call is bracketed by
-    # fh_tag_begin / fh_tag_end, so a recorded step program knows which of its kernels form
-    # which launch shape, and bench.py times one shape over the TIMED rounds with HIP events
-    # on the launch stream (fh_timing_enable / fh_timing_collect, csrc/program.hip)
-    tagging = False
-    _ids: dict = {}
-    _open = False
-
-    def tag_id(self, tag):
-        i = self._ids.get(tag)
-        if i is None:
-            i = self._ids[tag] = len(self._ids) + 1
-        return i
-
-    def close(self):
-        """End the open launch group (fh_tag_end), if any."""
-        if self._open:
-            self._open = False
-            call("fh_tag_end")
-
     def begin(self, tag):
-        if self.tagging:
-            call("fh_tag_begin", self.tag_id(tag))
-            self._open = True
         if not self.enabled:
             return None
         self.seen[tag] = self.seen.get(tag, 0) + 1
@@ -123,7 +100,6 @@ class LaunchProbe:
         """flops / nbytes: the launch's algorithmic work — every operand read
         and every result written once; clients: its active-client count (bench.py buckets);
         tag: record under this launch shape instead of begin()'s."""
-        self.close()
         if h is None:
             return
         e2 = torch.cuda.Event(enable_timing=True)
@@ -303,7 +279,6 @@ def _probe_wgrad_end(ev, tag, flops, nbytes, nclients):
     whose window then times both (_probe_dgrad_end)."""
     if ev is not None and _pair_status()[0]:
         PROBE.held = (tag, flops, nbytes, nclients)
-        PROBE.close()
         return
     PROBE.end(ev, flops, nbytes, nclients)
 
@@ -311,7 +286,7 @@ def _probe_wgrad_end(ev, tag, flops, nbytes, nclients):
 def _probe_dgrad_begin(tag):
     """PROBE.begin for a DGRAD call, plus the dual-launch count when a WGRAD is held for it."""
     ev = PROBE.begin(tag)
-    if (ev is None or PROBE.held is None) and not PROBE.tagging:
+    if ev is None or PROBE.held is None:
         return ev, None
     held, duals = _pair_status()
     return ev, (duals if held else None)
@@ -320,8 +295,7 @@ def _probe_dgrad_begin(tag):
 def _probe_dgrad_end(ev, duals0, flops, nbytes, nclients, tag):
     """PROBE.end for a DGRAD call.  With a WGRAD held before it, the call issued the dual-role
     launch (recorded as conv_bwd_dual:<shape>, FLOPs / bytes = both roles') or the held WGRAD
-    on its own ahead of the DGRAD (conv_bwd_seq:<shape>, both launches); tagging renames the
-    launch group the same way."""
+    on its own ahead of the DGRAD (conv_bwd_seq:<shape>, both launches)."""
     if duals0 is None:
         PROBE.end(ev, flops, nbytes, nclients)
         return
@@ -330,11 +304,6 @@ def _probe_dgrad_end(ev, duals0, flops, nbytes, nclients, tag):
         PROBE.end(ev, flops, nbytes, nclients)
         return
     dtag = ("conv_bwd_dual:" if duals > duals0 else "conv_bwd_seq:") + tag.split(":", 1)[1]
-    if PROBE.tagging:
-        call("fh_tag_retag", PROBE.tag_id(dtag))
-    if ev is None or PROBE.held is None:
-        PROBE.end(ev, flops, nbytes, nclients)
-        return
     wtag, wfl, wnb, _ = PROBE.held
     PROBE.held = None
     if wtag in PROBE.exec_ratio:
@@ -343,25 +312,54 @@ def _probe_dgrad_end(ev, duals0, flops, nbytes, nclients, tag):
 
 
 def conv_pair_reset():
-    """Disarm and drop a held WGRAD launch unissued (fh_conv_pair(-1)): a step's error path.
-    Also closes an open launch group."""
+    """Disarm and drop a held WGRAD launch unissued (fh_conv_pair(-1)): a step's error path."""
     PROBE.held = None
-    PROBE.close()
     call("fh_conv_pair", -1)
 
 
-def timing_enable(tags, reserve=65536):
-    """Time every launch of these launch shapes from now on (fh_timing_enable; [] = off)."""
-    ids = (ctypes.c_int32 * max(1, len(tags)))(*[PROBE.tag_id(t) for t in tags])
-    call("fh_timing_enable", ids, len(tags), int(reserve) if tags else 0)
+class LaunchStamps:
+    """Per-launch durations of one dual-role conv backward shape over a stretch of rounds
+    (fh_launch_ts_set): the kernel's workgroups append {dispatch, shape, first tick, last
+    tick}; a launch is the records of one dispatch packet, its duration max(last) - min(first)
+    on the 100 MHz wall clock — a kernel trace's begin-to-end, without events in the stream."""
 
+    def __init__(self, device, w, cin, cout, cap=1 << 23):
+        self.rec = torch.zeros(cap, 4, dtype=torch.int32, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.cap, self.shape = cap, (w, cin, cout)
+        khz = ctypes.c_int32()
+        call("fh_wall_clock_khz", ctypes.byref(khz))
+        self.khz = khz.value
 
-def timing_collect(tag):
-    """(launches, total ms, dropped groups) timed for a launch shape since timing_enable."""
-    n, ms, dr = ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
-    call("fh_timing_collect", PROBE.tag_id(tag), ctypes.byref(n), ctypes.byref(ms),
-         ctypes.byref(dr))
-    return n.value, ms.value, dr.value
+    def start(self):
+        self.count.zero_()
+        call("fh_launch_ts_set", ptr(self.rec), ptr(self.count), self.cap, *self.shape)
+
+    def stop(self):
+        call("fh_launch_ts_set", None, None, 0, 0, 0, 0)
+
+    def durations_ms(self):
+        """(durations in ms of every recorded launch, records dropped past cap)."""
+        import numpy as np
+        n = int(self.count.item())
+        r = self.rec[:min(n, self.cap)].cpu().numpy().view(np.uint32).astype(np.int64)
+        if not len(r):
+            return [], max(0, n - self.cap)
+        base = r[0, 2]
+        t0 = (r[:, 2] - base) % (1 << 32)  # the 32-bit clock may wrap once inside the window
+        t1 = (r[:, 3] - base) % (1 << 32)
+        order = np.lexsort((t0, r[:, 0]))
+        key, t0, t1 = r[order, 0], t0[order], t1[order]
+        gap = 20 * self.khz // 1000  # 20 us: one packet slot is reused only after a queue wrap
+        out, i = [], 0
+        while i < len(key):
+            j, lo, hi = i + 1, t0[i], t1[i]
+            while j < len(key) and key[j] == key[i] and t0[j] <= hi + gap:
+                hi = max(hi, t1[j])
+                j += 1
+            out.append((hi - lo) / self.khz)
+            i = j
+        return out, max(0, n - self.cap)
 
 
 def _ws_for(fn_name, device, *args):

@@ -701,19 +701,16 @@ int fh_program_matches_graph(void* program, void* graph, int32_t* match_out);
 int fh_program_launch(void* program, void* stream);
 int fh_program_destroy(void* program);
 
-/* Launch-group timing (bench.py's roofline over the timed rounds; replaces the reference's
- * wall-clock timers around train_local_model, training.py:86,140).  The caller brackets one
- * library call (a launch shape: its kernel + split-K reduction) with fh_tag_begin(tag) /
- * fh_tag_end() on the calling thread; fh_tag_retag renames the open group.  While a step
- * program is recorded the group's first / last kernels are marked; a program replay, or an
- * eager call, then records HIP events around every group whose tag fh_timing_enable turned
- * on (n = 0: off; `reserve` event pairs are created up front, a group past them is counted
- * as dropped).  fh_timing_collect waits for the events and sums the durations of one tag. */
-int fh_tag_begin(int32_t tag);
-int fh_tag_retag(int32_t tag);
-int fh_tag_end(void);
-int fh_timing_enable(const int32_t* tags, int32_t n, int32_t reserve);
-int fh_timing_collect(int32_t tag, int64_t* launches, double* total_ms, int64_t* dropped);
+/* Launch timestamps of the dual-role conv backward (bench.py's roofline over the TIMED
+ * rounds; replaces the reference's wall-clock timers around train_local_model,
+ * training.py:86,140).  While rec is non-null, every dconv_wgrad_dual_kernel launch of the
+ * layer shape (map w x w, cin -> cout) appends one record per workgroup to rec [cap][4]
+ * uint32: its dispatch packet key, the shape key, and the workgroup's first / last wall-clock
+ * tick (100 MHz counter, low 32 bits; fh_wall_clock_khz); *count (uint32, caller-zeroed) is
+ * the next free record.  A launch's duration is max(last) - min(first) over its records —
+ * the kernel trace's begin-to-end.  rec = null turns it off.  Host calls, outside a capture. */
+int fh_launch_ts_set(void* rec, void* count, uint32_t cap, int32_t w, int32_t cin, int32_t cout);
+int fh_wall_clock_khz(int32_t* khz);
 /* dst[0:nbytes) = src[0:nbytes) by a kernel (16-B aligned, nbytes % 16 == 0): the per-step
  * input row copy of a lane in program mode. */
 int fh_copy_bytes(const void* src, void* dst, int64_t nbytes, void* stream);

@@ -256,21 +256,29 @@ def test_conv_pair_status_without_gpu():
         _lib.call("fh_conv_pair_status", None, None)
 
 
-def test_launch_group_tags_without_gpu():
-    """fh_tag_* / fh_timing_* (bench.py's timed-round roofline): host bookkeeping only when no
-    program records and no tag is enabled."""
-    import ctypes
-    with pytest.raises(_lib.FedHipError, match="tag"):
-        _lib.call("fh_tag_begin", 0)
-    with pytest.raises(_lib.FedHipError, match="retag"):
-        _lib.call("fh_tag_retag", 3)           # no open group
-    _lib.call("fh_tag_begin", 3)
-    _lib.call("fh_tag_retag", 4)
-    _lib.call("fh_tag_end")
-    _lib.call("fh_timing_enable", None, 0, 0)  # off, no events created
-    n, ms, dr = ctypes.c_int64(7), ctypes.c_double(7.0), ctypes.c_int64(7)
-    _lib.call("fh_timing_collect", 4, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(dr))
-    assert (n.value, ms.value, dr.value) == (0, 0.0, 0)
+def test_launch_stamps_grouping_without_gpu():
+    """ops.LaunchStamps (bench.py's timed-round roofline): workgroup records grouped per
+    dispatch packet — a packet slot reused after a queue wrap is a new launch — with the
+    duration max(last tick) - min(first tick), across a 32-bit clock wrap; fh_launch_ts_set
+    validates its arguments on the host."""
+    from fedhip import ops
+    with pytest.raises(_lib.FedHipError, match="bad arguments"):
+        _lib.call("fh_launch_ts_set", 16, None, 8, 32, 32, 32)
+    st = object.__new__(ops.LaunchStamps)
+    st.khz, st.cap = 100_000, 64  # 100 MHz: 100 ticks per us
+    base = (1 << 32) - 1500       # the clock wraps inside the window
+    recs = [  # (dispatch key, shape, t0, t1)
+        (7, 1, base + 0, base + 900), (7, 1, base + 100, base + 1200),   # launch A: 12 us
+        (9, 1, base + 300, base + 800),                                     # launch B: 5 us
+        (7, 1, base + 900_000, base + 905_000),                           # A's slot reused: 50 us
+    ]
+    arr = np.zeros((64, 4), dtype=np.uint32)
+    for i, r in enumerate(recs):
+        arr[i] = [v % (1 << 32) for v in r]
+    st.rec = torch.from_numpy(arr.view(np.int32))
+    st.count = torch.tensor([len(recs)], dtype=torch.int32)
+    d, dropped = st.durations_ms()
+    assert dropped == 0 and sorted(round(x * 1e3, 3) for x in d) == [5.0, 12.0, 50.0]
 
 
 def test_every_ops_attribute_used_exists():
