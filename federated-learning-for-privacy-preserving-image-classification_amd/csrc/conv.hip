@@ -787,6 +787,13 @@ struct U8Src {
     int64_t xo_cs;
 };
 
+// r05: a workgroup takes one group of kC1PoolCg channels (blockIdx.y) of one client
+// (blockIdx.z), so the weights and bias are workgroup-uniform: scalar loads, the FMAs take them
+// as SGPR operands (r02-r04 staged all COUT x 9 in LDS and read them back per channel), and a
+// one-client launch runs COUT / 8 times as many workgroups.  Each thread still computes one
+// pooled pixel's window with the same fmaf order per channel; with U8Src only the first
+// channel group writes x and the labels (every group reads the bytes).
+constexpr int kC1PoolCg = 8;
 template <int COUT>
 __global__ void __launch_bounds__(256)
 conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ w,
@@ -794,12 +801,8 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
                         float* __restrict__ y, int64_t y_cs, uint8_t* __restrict__ idx,
                         int64_t i_cs, const int32_t* __restrict__ counts, int batch, int H,
                         int W, int yh, int yw, const U8Src src) {
-    __shared__ float ws[COUT * 9], bs[COUT];
-    const int z = blockIdx.y;
+    const int z = blockIdx.z, cg = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
-    for (int i = threadIdx.x; i < COUT * 9; i += 256) ws[i] = w[z * w_cs + i];
-    for (int i = threadIdx.x; i < COUT; i += 256) bs[i] = bias ? bias[z * b_cs + i] : 0.f;
-    __syncthreads();
     const int OH = H / 2, OW = W / 2, OHW = OH * OW;
     const int n = blockIdx.x * 256 + threadIdx.x;
     if (n >= cnt * OHW) return;
@@ -810,6 +813,7 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
         const int64_t s = src.gidx[z * src.g_cs + img];
         const uint8_t* si = src.data + s * H * W;
         float* xo = src.xo + z * src.xo_cs + (int64_t)img * H * W;
+        const bool wr = cg == 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -819,11 +823,11 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
                 if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
                     const float u = __fdiv_rn((float)si[yy * W + xx], 255.f);
                     v = __fdiv_rn(u - src.mean, src.stdv);
-                    if (i >= 1 && i <= 2 && j >= 1 && j <= 2) xo[yy * W + xx] = v;  // own window
+                    if (wr && i >= 1 && i <= 2 && j >= 1 && j <= 2) xo[yy * W + xx] = v;  // own window
                 }
                 t[i][j] = v;
             }
-        if (q == 0) src.ylab[z * src.yl_cs + img] = src.labels[s];
+        if (wr && q == 0) src.ylab[z * src.yl_cs + img] = src.labels[s];
     } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -835,18 +839,22 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
                               : 0.f;
             }
     }
-    float* yo = y + z * y_cs + (int64_t)img * COUT * yh * yw + oh * yw + ow;
-    uint8_t* io = idx + z * i_cs + (int64_t)img * COUT * OHW + q;
-#pragma unroll 2
-    for (int co = 0; co < COUT; ++co) {
+    const int c0 = cg * kC1PoolCg;
+    const float* wz = w + z * w_cs + c0 * 9;  // workgroup-uniform: scalar loads
+    const float* bz = bias ? bias + z * b_cs + c0 : nullptr;
+    float* yo = y + z * y_cs + ((int64_t)img * COUT + c0) * yh * yw + oh * yw + ow;
+    uint8_t* io = idx + z * i_cs + ((int64_t)img * COUT + c0) * OHW + q;
+#pragma unroll
+    for (int c = 0; c < kC1PoolCg; ++c) {
         float v[4];
+        const float bc = bz ? bz[c] : 0.f;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {  // window slot s = (dy, dx) = (s >> 1, s & 1)
             float a = 0.f;
 #pragma unroll
             for (int k = 0; k < 9; ++k)
-                a = fmaf(ws[co * 9 + k], t[(s >> 1) + k / 3][(s & 1) + k % 3], a);
-            a = a + bs[co];
+                a = fmaf(wz[c * 9 + k], t[(s >> 1) + k / 3][(s & 1) + k % 3], a);
+            a = a + bc;
             v[s] = fmaxf(a, 0.f);
         }
         float m = v[0];
@@ -854,8 +862,8 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
         if (v[1] > m) { m = v[1]; am = 1; }
         if (v[2] > m) { m = v[2]; am = 2; }
         if (v[3] > m) { m = v[3]; am = 3; }
-        yo[(int64_t)co * yh * yw] = m;
-        io[(int64_t)co * OHW] = (uint8_t)am;
+        yo[(int64_t)c * yh * yw] = m;
+        io[(int64_t)c * OHW] = (uint8_t)am;
     }
 }
 
@@ -2162,7 +2170,8 @@ extern "C" int fh_conv2d_c1_pool_fwd(const float* x, int64_t x_cs, const float* 
     FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_fwd: cout %d (32 or 64)", cout);
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && w && y && idx, "conv2d_c1_pool_fwd: null pointer");
-    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256), (unsigned)nclients);
+    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256),
+              (unsigned)(cout / kC1PoolCg), (unsigned)nclients);
     hipStream_t st = as_stream(stream);
     if (cout == 32)
         FH_LAUNCH(conv_c1_pool_fwd_kernel<32>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
@@ -2194,7 +2203,8 @@ extern "C" int fh_conv2d_c1_pool_fwd_u8(const uint8_t* data, const int64_t* labe
     FH_REQUIRE(data && labels && gidx && x && y_lab && w && y && idx,
                "conv2d_c1_pool_fwd_u8: null pointer");
     const U8Src src{data, labels, gidx, g_cs, y_lab, yl_cs, mean, stdv, x, x_cs};
-    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256), (unsigned)nclients);
+    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256),
+              (unsigned)(cout / kC1PoolCg), (unsigned)nclients);
     hipStream_t st = as_stream(stream);
     if (cout == 32)
         FH_LAUNCH(conv_c1_pool_fwd_kernel<32>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,

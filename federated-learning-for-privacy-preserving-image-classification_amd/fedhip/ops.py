@@ -345,8 +345,11 @@ class LaunchStamps:
         r = self.rec[:min(n, self.cap)].cpu().numpy().view(np.uint32).astype(np.int64)
         if not len(r):
             return [], max(0, n - self.cap)
-        base = r[0, 2]
-        t0 = (r[:, 2] - base) % (1 << 32)  # the 32-bit clock may wrap once inside the window
+        # ticks relative to a point 2^30 ticks (~10 s) before the first record's start: the
+        # 32-bit clock may wrap inside the window, and records are in completion order (an
+        # earlier record can have started later than a later one)
+        base = r[0, 2] - (1 << 30)
+        t0 = (r[:, 2] - base) % (1 << 32)
         t1 = (r[:, 3] - base) % (1 << 32)
         order = np.lexsort((t0, r[:, 0]))
         key, t0, t1 = r[order, 0], t0[order], t1[order]

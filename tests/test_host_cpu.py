@@ -267,8 +267,8 @@ def test_launch_stamps_grouping_without_gpu():
     st = object.__new__(ops.LaunchStamps)
     st.khz, st.cap = 100_000, 64  # 100 MHz: 100 ticks per us
     base = (1 << 32) - 1500       # the clock wraps inside the window
-    recs = [  # (dispatch key, shape, t0, t1)
-        (7, 1, base + 0, base + 900), (7, 1, base + 100, base + 1200),   # launch A: 12 us
+    recs = [  # (dispatch key, shape, t0, t1), in completion order
+        (7, 1, base + 100, base + 1200), (7, 1, base + 0, base + 900),   # launch A: 12 us
         (9, 1, base + 300, base + 800),                                     # launch B: 5 us
         (7, 1, base + 900_000, base + 905_000),                           # A's slot reused: 50 us
     ]
