@@ -787,14 +787,16 @@ struct U8Src {
     int64_t xo_cs;
 };
 
-// r05: a workgroup takes one group of kC1PoolCg channels (blockIdx.y) of one client
-// (blockIdx.z), so the weights and bias are workgroup-uniform: scalar loads, the FMAs take them
-// as SGPR operands (r02-r04 staged all COUT x 9 in LDS and read them back per channel), and a
-// one-client launch runs COUT / 8 times as many workgroups.  Each thread still computes one
-// pooled pixel's window with the same fmaf order per channel; with U8Src only the first
+// r05: a workgroup takes one group of CG channels (blockIdx.y) of one client (blockIdx.z), so
+// the weights and bias are workgroup-uniform: scalar loads, the FMAs take them as SGPR operands
+// (r02-r04 staged all COUT x 9 in LDS and read them back per channel).  CG = 8 on narrow
+// launches (a one-client launch runs COUT / 8 times the workgroups: K2's one-client conv1
+// 14.9 -> 11.4 us), CG = COUT from kC1PoolWide clients on (the patch is loaded once per pixel:
+// the 8-channel groups re-read it and were 3 % slower at 9-32 clients).  Each thread computes
+// one pooled pixel's window with the same fmaf order per channel; with U8Src only the first
 // channel group writes x and the labels (every group reads the bytes).
-constexpr int kC1PoolCg = 8;
-template <int COUT>
+constexpr int kC1PoolWide = 8;
+template <int COUT, int CG>
 __global__ void __launch_bounds__(256)
 conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ w,
                         int64_t w_cs, const float* __restrict__ bias, int64_t b_cs,
@@ -839,13 +841,13 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
                               : 0.f;
             }
     }
-    const int c0 = cg * kC1PoolCg;
+    const int c0 = cg * CG;
     const float* wz = w + z * w_cs + c0 * 9;  // workgroup-uniform: scalar loads
     const float* bz = bias ? bias + z * b_cs + c0 : nullptr;
     float* yo = y + z * y_cs + ((int64_t)img * COUT + c0) * yh * yw + oh * yw + ow;
     uint8_t* io = idx + z * i_cs + ((int64_t)img * COUT + c0) * OHW + q;
-#pragma unroll
-    for (int c = 0; c < kC1PoolCg; ++c) {
+#pragma unroll(CG == COUT ? 2 : CG)
+    for (int c = 0; c < CG; ++c) {
         float v[4];
         const float bc = bz ? bz[c] : 0.f;
 #pragma unroll
@@ -2156,6 +2158,30 @@ extern "C" int fh_conv2d_dgrad_s2_shortcut(const float* dy, int64_t dy_cs, const
     return run_dconv_dgrad_s2(d, oh, nclients, workspace, ws_bytes, as_stream(stream));
 }
 
+namespace fh {
+static int conv_c1_pool_launch(const float* x, int64_t x_cs, const float* w, int64_t w_cs,
+                               const float* bias, int64_t b_cs, float* y, int64_t y_cs,
+                               uint8_t* idx, int64_t i_cs, const int32_t* counts, int nclients,
+                               int batch, int h, int w_, int cout, int yh, int yw, const U8Src& src,
+                               hipStream_t st) {
+    const bool wide = nclients >= kC1PoolWide;
+    const int cg = wide ? cout : 8;
+    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256), (unsigned)(cout / cg),
+              (unsigned)nclients);
+#define FH_C1P(CO, CG)                                                                           \
+    FH_LAUNCH((conv_c1_pool_fwd_kernel<CO, CG>), grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,    \
+              b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, src)
+    if (cout == 32) {
+        if (wide) FH_C1P(32, 32); else FH_C1P(32, 8);
+    } else {
+        if (wide) FH_C1P(64, 64); else FH_C1P(64, 8);
+    }
+#undef FH_C1P
+    FH_LAUNCH_CHECK("conv2d_c1_pool_fwd");
+    return FH_OK;
+}
+}  // namespace fh
+
 // SimpleCNN conv1 -> ReLU -> 2x2 max-pool in one launch (conv_c1_pool_fwd_kernel): y = the
 // pooled output in planes yh x yw (the H/2 x W/2 map in the top-left corner; yh = H/2, yw = W/2
 // for dense planes), idx the dense uint8 argmax [img][cout][H/2][W/2].  cin = 1, 3x3 / s1 /
@@ -2170,17 +2196,8 @@ extern "C" int fh_conv2d_c1_pool_fwd(const float* x, int64_t x_cs, const float* 
     FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_fwd: cout %d (32 or 64)", cout);
     if (nclients == 0) return FH_OK;
     FH_REQUIRE(x && w && y && idx, "conv2d_c1_pool_fwd: null pointer");
-    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256),
-              (unsigned)(cout / kC1PoolCg), (unsigned)nclients);
-    hipStream_t st = as_stream(stream);
-    if (cout == 32)
-        FH_LAUNCH(conv_c1_pool_fwd_kernel<32>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
-                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, U8Src{});
-    else
-        FH_LAUNCH(conv_c1_pool_fwd_kernel<64>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
-                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, U8Src{});
-    FH_LAUNCH_CHECK("conv2d_c1_pool_fwd");
-    return FH_OK;
+    return conv_c1_pool_launch(x, x_cs, w, w_cs, bias, b_cs, y, y_cs, idx, i_cs, counts, nclients,
+                               batch, h, w_, cout, yh, yw, U8Src{}, as_stream(stream));
 }
 
 // fh_conv2d_c1_pool_fwd with the step's batch gather folded in (U8Src): x [z][batch][h][w] is
@@ -2203,17 +2220,8 @@ extern "C" int fh_conv2d_c1_pool_fwd_u8(const uint8_t* data, const int64_t* labe
     FH_REQUIRE(data && labels && gidx && x && y_lab && w && y && idx,
                "conv2d_c1_pool_fwd_u8: null pointer");
     const U8Src src{data, labels, gidx, g_cs, y_lab, yl_cs, mean, stdv, x, x_cs};
-    dim3 grid((unsigned)ceil_div((int64_t)batch * (h / 2) * (w_ / 2), 256),
-              (unsigned)(cout / kC1PoolCg), (unsigned)nclients);
-    hipStream_t st = as_stream(stream);
-    if (cout == 32)
-        FH_LAUNCH(conv_c1_pool_fwd_kernel<32>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
-                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, src);
-    else
-        FH_LAUNCH(conv_c1_pool_fwd_kernel<64>, grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
-                  b_cs, y, y_cs, idx, i_cs, counts, batch, h, w_, yh, yw, src);
-    FH_LAUNCH_CHECK("conv2d_c1_pool_fwd_u8");
-    return FH_OK;
+    return conv_c1_pool_launch(x, x_cs, w, w_cs, bias, b_cs, y, y_cs, idx, i_cs, counts, nclients,
+                               batch, h, w_, cout, yh, yw, src, as_stream(stream));
 }
 
 // Its backward's weight gradient: fh_maxpool2_bwd(dpool, idx, xin = the ReLU output) +

@@ -45,6 +45,8 @@ if [[ $ST == *p* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline --rounds-target 0 --detail-out $O/prof_detail.json > $O/prof_bench.json 2> $O/prof_bench.err
   python3 $R/tools/trace_summary.py $O/prof > $O/trace_summary.txt 2>&1 || true
   head -5 $O/trace_summary.txt
+  python3 $R/tools/roofline_check.py $O/prof $O/prof_detail.json > $O/roofline_check.json 2>&1 || true
+  cat $O/roofline_check.json
   cd $R
 fi
 if [[ $ST == *q* ]]; then  # the same kernel trace with WGRAD / DGRAD as separate launches
