@@ -1481,6 +1481,7 @@ static int dconv_launch_w(const DPlan& p, dim3 grid, const DConvArgs& a, hipStre
 struct PendingWgrad {
     bool on = false;
     int w = 0, mode = 1;
+    bool pdy = false;  // its dY is the armed pooled gradient (g_pdy), not yet materialised
     dim3 grid;
     DWArgs d{};
     hipStream_t st = nullptr;
@@ -1489,8 +1490,35 @@ thread_local int g_pair_mode = 0;
 thread_local PendingWgrad g_pend;
 thread_local int64_t g_dual_launches = 0;  // fh_conv_pair_status (instrumentation)
 
+// Pooled output gradient of the next WGRAD + DGRAD pair (fh_conv_pooled_dy, r05): when the pair
+// becomes one dual-role launch on 16x16 planes, both roles route dY from the pooled gradient on
+// load (PooledDy) and the dY tensor is never written; on any other path the pair's dY buffer is
+// first filled by fh_maxpool2_bwd_ymask (the unfused step's own launch), once.
+struct PdyArm {
+    bool on = false, done = false;
+    PooledDy p{};
+};
+thread_local PdyArm g_pdy;
+
+static int pdy_materialize(float* dy, int64_t dy_cs, const int32_t* counts, int nclients,
+                           int batch, int C, int plane, hipStream_t st) {
+    if (!g_pdy.on || g_pdy.done) return FH_OK;
+    g_pdy.done = true;
+    const PooledDy& q = g_pdy.p;
+    return fh_maxpool2_bwd_ymask(q.g, q.g_cs, q.idx, q.i_cs, q.yp, q.y_cs, dy, dy_cs, counts,
+                                 nclients, batch, C, 2 * q.ph, 2 * q.ph, q.ph, q.ph, plane, plane,
+                                 st);
+}
+
 static int flush_pending_wgrad() {
     if (!g_pend.on) return FH_OK;
+    if (g_pend.pdy) {  // issued on its own: its dY must exist first
+        g_pend.pdy = false;
+        const int rc = pdy_materialize(const_cast<float*>(g_pend.d.dy), g_pend.d.dy_cs,
+                                       g_pend.d.counts, (int)g_pend.grid.z, g_pend.d.batch,
+                                       g_pend.d.M, g_pend.w, g_pend.st);
+        if (rc) return rc;
+    }
     g_pend.on = false;
     const PendingWgrad& q = g_pend;
     if (q.w == 32) FH_LAUNCH((dwgrad_q_kernel<32, 128, false>), q.grid, dim3(256), 0, q.st, q.d);
@@ -1500,7 +1528,7 @@ static int flush_pending_wgrad() {
     return FH_OK;
 }
 
-template <int W, bool BNB>
+template <int W, bool BNB, bool PDY = false>
 static int launch_dual(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_t st) {
     (void)p;
     const PendingWgrad& q = g_pend;
@@ -1508,8 +1536,8 @@ static int launch_dual(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_
     const int64_t nd = (int64_t)grid.x * grid.y * grid.z;
     FH_REQUIRE(nw + nd < (1ll << 31), "dual conv backward: grid %lld + %lld", (long long)nw,
                (long long)nd);
-    FH_LAUNCH((dconv_wgrad_dual_kernel<W, BNB>), dim3((unsigned)(nw + nd)), dim3(256), 0, st,
-              q.d, (int)q.grid.x, (int)q.grid.y, (int)nw, a, (int)grid.x, (int)grid.y,
+    FH_LAUNCH((dconv_wgrad_dual_kernel<W, BNB, PDY>), dim3((unsigned)(nw + nd)), dim3(256), 0,
+              st, q.d, (int)q.grid.x, (int)q.grid.y, (int)nw, a, (int)grid.x, (int)grid.y,
               (int)nd, q.mode == 1 ? 1 : 0);
     ++g_dual_launches;
     return FH_OK;
@@ -1546,18 +1574,37 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
         if (g_pend.on) {
             if (g_pend.st == st && g_pend.w == w && p.bm == 32 && p.ck == 8 && a.wvec) {
                 const bool bnb = a.bn_part && p.splits == 1;
-                rc = w == 32 ? (bnb ? launch_dual<32, true>(p, grid, a, st)
-                                    : launch_dual<32, false>(p, grid, a, st))
-                   : w == 16 ? (bnb ? launch_dual<16, true>(p, grid, a, st)
-                                    : launch_dual<16, false>(p, grid, a, st))
-                             : (bnb ? launch_dual<8, true>(p, grid, a, st)
-                                    : launch_dual<8, false>(p, grid, a, st));
+                if (g_pend.pdy && w == 16 && !bnb && !a.accumulate) {
+                    // the pooled gradient routed on load by both roles: dY is never written
+                    a.pdy = g_pdy.p;
+                    g_pdy.done = true;
+                    rc = launch_dual<16, false, true>(p, grid, a, st);
+                } else {
+                    if (g_pend.pdy) {
+                        g_pend.pdy = false;
+                        rc = pdy_materialize(const_cast<float*>(a.in), a.in_cs, a.counts, nclients,
+                                             a.batch, a.Cr, w, st);
+                        if (rc) return rc;
+                    }
+                    rc = w == 32 ? (bnb ? launch_dual<32, true>(p, grid, a, st)
+                                        : launch_dual<32, false>(p, grid, a, st))
+                       : w == 16 ? (bnb ? launch_dual<16, true>(p, grid, a, st)
+                                        : launch_dual<16, false>(p, grid, a, st))
+                                 : (bnb ? launch_dual<8, true>(p, grid, a, st)
+                                        : launch_dual<8, false>(p, grid, a, st));
+                }
                 g_pend.on = false;
+                g_pend.pdy = false;
                 if (rc) return rc;
                 dual = true;
             } else if (const int fr = flush_pending_wgrad()) {
                 return fr;
             }
+        }
+        if (!dual && g_pdy.on && !g_pdy.done) {  // this DGRAD reads the pair's dY: fill it
+            rc = pdy_materialize(const_cast<float*>(a.in), a.in_cs, a.counts, nclients, a.batch,
+                                 a.Cr, w, st);
+            if (rc) return rc;
         }
     }
     if (dual) {
@@ -1798,6 +1845,8 @@ extern "C" int fh_conv_pair(int32_t mode) {
     if (mode < 0) {  // error paths: drop a held launch unissued
         g_pair_mode = 0;
         g_pend.on = false;
+        g_pend.pdy = false;
+        g_pdy = PdyArm{};
         return FH_OK;
     }
     if (mode > 0) {
@@ -1805,7 +1854,18 @@ extern "C" int fh_conv_pair(int32_t mode) {
         return FH_OK;
     }
     g_pair_mode = 0;
-    return flush_pending_wgrad();
+    const int rc = flush_pending_wgrad();
+    g_pdy = PdyArm{};
+    return rc;
+}
+
+extern "C" int fh_conv_pooled_dy(const float* dpool, int64_t dp_cs, const uint8_t* pidx,
+                                 int64_t pi_cs, const float* ypool, int64_t yp_cs, int32_t ph) {
+    FH_REQUIRE(dpool && pidx && ypool && ph > 0, "conv_pooled_dy: bad arguments");
+    g_pdy.on = true;
+    g_pdy.done = false;
+    g_pdy.p = PooledDy{dpool, pidx, ypool, dp_cs, pi_cs, yp_cs, ph};
+    return FH_OK;
 }
 
 extern "C" int fh_launch_ts_set(void* rec, void* count, uint32_t cap, int32_t w, int32_t cin,
@@ -2364,6 +2424,21 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
     a.M = cout; a.N = cin * kh * kw; a.K = batch * oh * ow;
     const bool aligned = ((uintptr_t)x % 16 == 0) && ((uintptr_t)dy % 16 == 0) && x_cs % 4 == 0 &&
                          dy_cs % 4 == 0;
+    // an armed pooled dY (fh_conv_pooled_dy) travels with a held 16x16 launch into the dual-role
+    // grid; any other path reads dy, which is filled first
+    bool pdy_hold = false;
+    if (g_pdy.on && !g_pdy.done) {
+        if (pair && !in_scale && aligned && w_ == 16 &&
+            dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad)) {
+            const DWPlan pq = plan_dwq(cout, cin, batch, w_, nclients);
+            pdy_hold = pq.sr * w_ != 64 && (pq.splits == 1 || defer_splits);
+        }
+        if (!pdy_hold) {
+            rc = pdy_materialize(const_cast<float*>(dy), dy_cs, counts, nclients, batch, cout, w_,
+                                 as_stream(stream));
+            if (rc) return rc;
+        }
+    }
     if (in_scale && !(aligned && dwgrad_supported(cin, cout, h, w_, kh, kw, stride, pad))) {
         set_error("conv2d_wgrad_bnrelu: needs the direct 3x3 wgrad (16-B aligned, channels %% 32)");
         return FH_E_UNSUPPORTED;
@@ -2480,6 +2555,8 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
             g_pend.d = d;
             g_pend.st = st;
             g_pend.on = true;
+            g_pend.pdy = pdy_hold;
+            if (pdy_hold) g_pend.d.pdy = g_pdy.p;
         } else {
             if (w_ == 32) FH_LAUNCH((dwgrad_q_kernel<32, 128, false>), grid, dim3(256), 0, st, d);
             else if (w_ == 16) FH_LAUNCH((dwgrad_q_kernel<16, 128, false>), grid, dim3(256), 0, st, d);

@@ -24,6 +24,38 @@
 
 namespace fh {
 
+// Pooled output gradient (r05, SimpleCNN conv2's backward; fh_conv_pooled_dy): the layer's
+// output gradient is not materialised.  Pixel (y, x) of a plane takes the following 2x2
+// max-pool's gradient g[y/2][x/2] (dense pooled planes ph x ph) when (y, x) is its window's
+// argmax idx and the pooled ReLU output yp there is > 0, else 0 — fh_maxpool2_bwd_ymask's values
+// bit for bit, with rows / columns past the 2ph x 2ph map zero (the plane's zero ring).
+struct PooledDy {
+    const float* g;      // [z][img][C][ph][ph]
+    const uint8_t* idx;  // same layout
+    const float* yp;     // same layout
+    int64_t g_cs, i_cs, y_cs;
+    int ph;
+};
+// raw loads of a quad (y, x0 .. x0 + 3), x0 % 4 == 0: two pooled gradients, two pooled outputs,
+// two argmax bytes | the row parity (routed in pdy_route, after the loads have landed)
+__device__ __forceinline__ void pdy_load(const PooledDy& q, int z, int64_t plane, int y, int x0,
+                                         bool ok, float2& g, float2& yp, int& code) {
+    const int py = y >> 1, px = x0 >> 1;
+    const bool r_ok = ok && py < q.ph;
+    const bool c0 = r_ok && px < q.ph, c1 = r_ok && px + 1 < q.ph;
+    const int64_t e = (plane * q.ph + py) * q.ph + px;
+    g = make_float2(c0 ? q.g[z * q.g_cs + e] : 0.f, c1 ? q.g[z * q.g_cs + e + 1] : 0.f);
+    yp = make_float2(c0 ? q.yp[z * q.y_cs + e] : 0.f, c1 ? q.yp[z * q.y_cs + e + 1] : 0.f);
+    code = (c0 ? (int)q.idx[z * q.i_cs + e] : 0) | ((c1 ? (int)q.idx[z * q.i_cs + e + 1] : 0) << 8) |
+           ((y & 1) << 17);
+}
+__device__ __forceinline__ float4 pdy_route(float2 g, float2 yp, int code) {
+    const int r = code >> 16, i0 = code & 0xff, i1 = (code >> 8) & 0xff;
+    const float g0 = yp.x > 0.f ? g.x : 0.f, g1 = yp.y > 0.f ? g.y : 0.f;
+    return make_float4(i0 == r ? g0 : 0.f, i0 == (r | 1) ? g0 : 0.f, i1 == r ? g1 : 0.f,
+                       i1 == (r | 1) ? g1 : 0.f);
+}
+
 struct DConvArgs {
     const float* in;   // X (FWD) or dY (DGRAD): [client][img][Cr][H][W]
     const float* wt;   // [client] W[cout][cin][3][3]
@@ -79,6 +111,8 @@ struct DConvArgs {
     uint8_t* pool_idx;
     int64_t py_cs, pix_cs;
     int pool_hw;
+    // DGRAD, the PDY instances: dY routed from a 2x2 max-pool's gradient (in is not read)
+    PooledDy pdy;
 };
 
 // Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
@@ -143,10 +177,12 @@ constexpr int dconv_lds_floats() {
 
 // the workgroup body; smem holds dconv_lds_floats() floats (dconv_kernel's own array, or
 // the array a dual-role launch shares with a WGRAD body: dconv_wgrad_dual_kernel)
-template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC, int S = 1, bool BNB = false>
+template <int OP, int W, int BM, int WAVES_M, int CK, bool WVEC, int S = 1, bool BNB = false,
+          bool PDY = false>
 __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int bx, int by,
                                            int bz) {
     using G = DGeom<W>;
+    static_assert(!PDY || (OP == OP_DGRAD && S == 1 && W % 4 == 0), "pooled dY: DGRAD");
     static_assert(S == 1 || (S == 2 && OP == OP_FWD), "stride 2: forward only");
     static_assert(!BNB || S == 1, "statistics epilogue: stride 1");
     constexpr int WI = S * W, HI = S * G::H;               // input map
@@ -216,6 +252,8 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
 
     float4 rp[NPT], ra[NAV];
     float bsc[NPT], bsh[NPT];  // BN affine of each staged row (in_scale set)
+    float2 pg[PDY ? NPT : 1], pp[PDY ? NPT : 1];  // PDY: raw pooled loads, routed in store()
+    int pc[PDY ? NPT : 1];
     auto load = [&](int c0) {
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
@@ -224,6 +262,10 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
             const int seg = pr / PRS, rr = pr % PRS;
             const int img = img0 + seg, y = S * y0 + rr - 1;
             const bool ok = q < NPR && img < cnt && (unsigned)y < (unsigned)HI && c0 + cl < cend;
+            if constexpr (PDY) {
+                pdy_load(a.pdy, z, (int64_t)img * a.Cr + c0 + cl, y, px, ok, pg[i], pp[i], pc[i]);
+                continue;
+            }
             rp[i] = ok ? *reinterpret_cast<const float4*>(
                              inz + ((int64_t)(img * a.Cr + c0 + cl) * HI + y) * WI + px)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -279,6 +321,7 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
         for (int i = 0; i < NPT; ++i) {
             const int q = prt + i * RPI;
             if (q < NPR) {
+                if constexpr (PDY) rp[i] = pdy_route(pg[i], pp[i], pc[i]);
                 if (OP == OP_FWD && a.in_scale != nullptr) rp[i] = bn_relu4(rp[i], bsc[i], bsh[i]);
                 float* d = &Ps[buf][(q / PR) * CSTR + (q % PR) * PW + 1 + px];
                 d[0] = rp[i].x;
@@ -1055,6 +1098,8 @@ struct DWArgs {
     int64_t dw_cs;
     float* db;
     int64_t db_cs;
+    // dwgrad_q (the dual-role launch's WGRAD role), PDY: dY routed from a 2x2 max-pool's gradient
+    PooledDy pdy;
 };
 
 // Two workgroups per CU when the double-buffered staging fits twice in the 160 KB LDS:
@@ -1317,7 +1362,7 @@ constexpr int dwq_lds_floats(int W, int SPX, bool DB) {
     return st > 32 * 289 + 128 ? st : 32 * 289 + 128;
 }
 
-template <int W, int SPX, bool DB>
+template <int W, int SPX, bool DB, bool PDY = false>
 __device__ __forceinline__ void dwgrad_q_body(const DWArgs& a, float* smem, int bx, int by,
                                               int bz) {
     constexpr int H = W, HW = H * W;
@@ -1361,15 +1406,23 @@ __device__ __forceinline__ void dwgrad_q_body(const DWArgs& a, float* smem, int 
     const int dq = tid % DQ, dco = tid / DQ;  // dY: pixel quad, first channel row
     float4 rd[NDY], rp[NPT];
     float bsc[NPT], bsh[NPT];
+    float2 pg[PDY ? NDY : 1], pp[PDY ? NDY : 1];  // PDY: raw pooled loads, routed in store()
+    int pc[PDY ? NDY : 1];
     auto load = [&](int st) {
         const int gp = st * SPX + 4 * dq;
         const int img = gp / HW, pix = gp % HW;
         const bool ok = img < cnt;
         const float* src = dyz + ((int64_t)(img * a.M + co0 + dco) * HW + pix);
 #pragma unroll
-        for (int i = 0; i < NDY; ++i)
+        for (int i = 0; i < NDY; ++i) {
+            if constexpr (PDY) {
+                pdy_load(a.pdy, z, (int64_t)img * a.M + co0 + dco + i * CPP, pix / W, pix % W, ok,
+                         pg[i], pp[i], pc[i]);
+                continue;
+            }
             rd[i] = ok ? *reinterpret_cast<const float4*>(src + (int64_t)i * CPP * HW)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         const int img0 = (st * SPX) / HW, y0 = ((st * SPX) % HW) / W;
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
@@ -1391,6 +1444,7 @@ __device__ __forceinline__ void dwgrad_q_body(const DWArgs& a, float* smem, int 
         float* P = D + DSZ;
 #pragma unroll
         for (int i = 0; i < NDY; ++i) {
+            if constexpr (PDY) rd[i] = pdy_route(pg[i], pp[i], pc[i]);
             float2* d = reinterpret_cast<float2*>(D + (dco + i * CPP) * DP + 4 * dq);
             d[0] = make_float2(rd[i].x, rd[i].y);
             d[1] = make_float2(rd[i].z, rd[i].w);
@@ -1452,7 +1506,14 @@ __device__ __forceinline__ void dwgrad_q_body(const DWArgs& a, float* smem, int 
                 __syncthreads();
                 b ^= 1;
             } else {
-                rows(0, 0, SR);
+                if constexpr (PDY && SR <= H) {
+                    // rows past the pooled map's 2 ph rows carry a zero gradient: skipping them
+                    // adds nothing the MFMA chain would not have added as exact zeros
+                    const int y0 = ((st * SPX) % HW) / W;
+                    rows(0, 0, max(0, min(SR, 2 * a.pdy.ph - y0)));
+                } else {
+                    rows(0, 0, SR);
+                }
                 if (more) {
                     __syncthreads();  // every wave is done reading this stage
                     store(0);
@@ -1522,7 +1583,7 @@ __host__ __device__ constexpr uint32_t dual_shape_key(int w, int cin, int cout) 
 // of the WGRAD grid (wx, wy, z) first (wfirst) or after the nd of the DGRAD grid (dx, dy, z),
 // each x-fastest as in its own launch.  The layer's backward is then one dependent step instead of
 // two, and the two grids fill each other's tails.
-template <int W, bool BNB>
+template <int W, bool BNB, bool PDY = false>
 __global__ void __launch_bounds__(256, 3)
     dconv_wgrad_dual_kernel(const DWArgs wa, int wx, int wy, int nw, const DConvArgs da, int dx,
                             int dy, int nd, int wfirst) {
@@ -1538,11 +1599,11 @@ __global__ void __launch_bounds__(256, 3)
     if (isw) {
         const int q = wfirst ? b : b - nd;
         const int bz = q / (wx * wy), r = q - bz * wx * wy;
-        dwgrad_q_body<W, 128, false>(wa, smem, r % wx, r / wx, bz);
+        dwgrad_q_body<W, 128, false, PDY>(wa, smem, r % wx, r / wx, bz);
     } else {
         const int q = wfirst ? b - nw : b;
         const int bz = q / (dx * dy), r = q - bz * dx * dy;
-        dconv_body<OP_DGRAD, W, 32, 1, 8, true, 1, BNB>(da, smem, r % dx, r / dx, bz);
+        dconv_body<OP_DGRAD, W, 32, 1, 8, true, 1, BNB, PDY>(da, smem, r % dx, r / dx, bz);
     }
     if (stamp) {
         __syncthreads();

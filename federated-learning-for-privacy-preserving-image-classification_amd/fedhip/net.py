@@ -199,6 +199,10 @@ class PackedNet:
         # ... and each stride-1 ResNet block's conv1 pair (its DGRAD accumulates onto the
         # identity shortcut's gradient): K3 +0.5 %, K4 +0.8 % (x2, profiles/r04_dual/)
         self.dual_resnet_conv1 = True
+        # SimpleCNN: pool2's backward routed inside conv2's dual-role launch (fh_conv_pooled_dy:
+        # both roles read the pooled gradient, argmax and pooled ReLU output on load; the 16x16
+        # gradient da2 is never written and the maxpool2_bwd launch is gone)
+        self.pooled_dy_bwd = True
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -370,8 +374,14 @@ class PackedNet:
                 ops.linear_wgrad(A("p2", 64, 7, 7), dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), n,
                                  B, 3136, 128, counts=cnt)
                 ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
-            self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
+            pooled_dy = self.pooled_dy_bwd and self._pool2_fused and self.dual_bwd
+            if not pooled_dy:
+                self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
+        else:
+            pooled_dy = False
         ops.conv_pair(self.dual_bwd)  # conv2's WGRAD held for its DGRAD: one launch
+        if pooled_dy:  # pool2's backward routed inside that launch: da2 is never written
+            ops.conv_pooled_dy(dp2, i2, A("p2", 64, 7, 7))
         ops.conv2d_wgrad(p1, da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, hp, hp, 64,
                          3, 1, 1, counts=cnt, alg_hw=14)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,

@@ -267,6 +267,14 @@ def conv_pair(mode: int):
     call("fh_conv_pair", int(mode) if _PAIRING[0] else 0)
 
 
+def conv_pooled_dy(dpool, pidx, ypool):
+    """The next conv2d_wgrad + conv2d_dgrad pair's dY is maxpool2_bwd_ymask(dpool, pidx, ypool)
+    (fh_conv_pooled_dy; call after conv_pair(mode)): routed on load inside the dual-role launch,
+    else materialised into the pair's dY tensor by the library first."""
+    call("fh_conv_pooled_dy", ptr(dpool), _cs(dpool), ptr(pidx), _cs(pidx), ptr(ypool),
+         _cs(ypool), int(dpool.shape[-1]))
+
+
 def _pair_status():
     """(held, dual launches issued) of this thread (fh_conv_pair_status)."""
     held, duals = ctypes.c_int32(), ctypes.c_int64()

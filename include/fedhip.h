@@ -670,6 +670,15 @@ int fh_conv_pair(int32_t mode);
  * attributes a dual launch to both roles' work): *held = 1 while a WGRAD launch is held for
  * the next DGRAD, *dual_launches = dual-role grids this thread has issued so far. */
 int fh_conv_pair_status(int32_t* held, int64_t* dual_launches);
+/* The next WGRAD + DGRAD pair's output gradient is a 2x2 max-pool's backward (SimpleCNN conv2,
+ * models_pytorch.py:88-90, pool2 after relu(conv2)): dY(y, x) = dpool[y/2][x/2] where (y, x) is
+ * the window's argmax pidx and the pooled ReLU output ypool there is > 0, else 0
+ * (fh_maxpool2_bwd_ymask), pooled planes ph x ph, dense.  Call after fh_conv_pair(mode).  When
+ * the pair becomes one dual-role launch on 16x16 planes both roles route dY on load and the
+ * pair's dY tensor is never written; otherwise the library first fills it with
+ * fh_maxpool2_bwd_ymask.  fh_conv_pair(0 / -1) disarms. */
+int fh_conv_pooled_dy(const float* dpool, int64_t dp_cs, const uint8_t* pidx, int64_t pi_cs,
+                      const float* ypool, int64_t yp_cs, int32_t ph);
 
 /* Lane streams (fedhip/lanes.py; replaces the reference's one-thread-per-client
  * concurrency, federated_simulation.py:309-318).  cu_mask (nullable; mask_words 32-bit
