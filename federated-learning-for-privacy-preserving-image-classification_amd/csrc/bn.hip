@@ -288,6 +288,7 @@ maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __re
     __syncthreads();
     const float s = s_aff[0], t = s_aff[1];
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
+    const uint64_t prow = drop_mode == 1 ? philox_row(seed_dev, z) : 0ull;  // once, not per store
 #pragma unroll
     for (int k = 0; k < kPoolEpt; ++k) {
         if (e[k] < 0) continue;
@@ -302,7 +303,7 @@ maxpool2_bnfin_kernel(const BNArgs a, float* __restrict__ scale_out, float* __re
         if (drop_mode) {
             uint8_t keep;
             if (drop_mode == 1) {
-                const uint4 rr = Philox::gen(seed, philox_row(seed_dev, z), (uint64_t)e[k]);
+                const uint4 rr = Philox::gen(seed, prow, (uint64_t)e[k]);
                 keep = u01(rr.x) <= keep_prob ? 1 : 0;
                 mask[z * m_cs + e[k]] = keep;
             } else {

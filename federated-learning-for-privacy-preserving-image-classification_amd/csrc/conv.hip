@@ -48,11 +48,26 @@ struct DropArgs {
     const uint64_t* seed_dev;
 };
 
-__device__ __forceinline__ float apply_dropout(const DropArgs& d, int z, int64_t e, float v) {
+// The Philox key of a client row (key = seed + *seed_dev, row = philox_row): read once per thread
+// ahead of an element loop.  r05: read per element, every uint8 keep-mask store (which may alias
+// anything) forced the compiler to reload the key words after it — three dependent global
+// round trips per element in the classifier forward's epilogue (fc2: 18 us for 8 workgroups).
+struct DropKey {
+    uint64_t seed, row;
+};
+__device__ __forceinline__ DropKey drop_key(const DropArgs& d, int z) {
+    DropKey k{0ull, 0ull};
+    if (d.mode == 1) {
+        k.seed = d.seed + (d.seed_dev ? *d.seed_dev : 0ull);
+        k.row = philox_row(d.seed_dev, z);
+    }
+    return k;
+}
+__device__ __forceinline__ float apply_dropout(const DropArgs& d, const DropKey& k, int z,
+                                               int64_t e, float v) {
     uint8_t keep;
     if (d.mode == 1) {
-        const uint64_t seed = d.seed + (d.seed_dev ? *d.seed_dev : 0ull);
-        const uint4 r = Philox::gen(seed, philox_row(d.seed_dev, z), (uint64_t)e);
+        const uint4 r = Philox::gen(k.seed, k.row, (uint64_t)e);
         keep = u01(r.x) <= d.keep ? 1 : 0;
         d.mask[z * d.m_cs + e] = keep;
     } else {
@@ -396,6 +411,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
                 bv_r[i][r] = (bz && m < M) ? bz[m] : 0.f;
             }
     }
+    const DropKey dkey = drop_key(a.drop, z);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
         const int n = n0 + wn * WN + j * 32 + col;
@@ -428,7 +444,8 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvArgs a) {
                             if (has_bias) v = v + bv_r[i][r];
                             if (a.relu) v = fmaxf(v, 0.f);
                             if (a.drop.mode)
-                                v = apply_dropout(a.drop, z, ((int64_t)img * a.cout + m) * ohw + p, v);
+                                v = apply_dropout(a.drop, dkey, z,
+                                                  ((int64_t)img * a.cout + m) * ohw + p, v);
                             op[(int64_t)m * ohw] = v;
                         }
                     }
@@ -626,7 +643,7 @@ splitk_epilogue_kernel(const float* __restrict__ part, int splits, int M, int Nf
         if (bias) s = s + bias[z * b_cs + m];
         if (relu) s = fmaxf(s, 0.f);
         const int img = n / sp, pix = n - img * sp;
-        if (drop.mode) s = apply_dropout(drop, z, ((int64_t)img * M + m) * sp + pix, s);
+        if (drop.mode) s = apply_dropout(drop, drop_key(drop, z), z, ((int64_t)img * M + m) * sp + pix, s);
         float* o = out + z * out_cs + ((int64_t)img * M + m) * sp + pix;
         if (accumulate) s = *o + s;
         if (bb.x) {  // ReLU mask of the BN in front; (x - mean) * g for its statistics
@@ -3000,6 +3017,7 @@ linear_fwd_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float*
     if (!active || o >= M) return;
     if (gx == 1) {
         const float bv = bias ? bias[z * b_cs + o] : 0.f;
+        const DropKey dk = drop_key(drop, z);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int img = (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -3008,7 +3026,7 @@ linear_fwd_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const float*
                 if (bias) v = v + bv;
                 if (relu) v = fmaxf(v, 0.f);
                 const int64_t e = (int64_t)img * M + o;
-                if (drop.mode) v = apply_dropout(drop, z, e, v);
+                if (drop.mode) v = apply_dropout(drop, dk, z, e, v);
                 Y[z * y_cs + e] = v;
             }
         }
@@ -3046,7 +3064,7 @@ linear_fwd_epilogue_kernel(const float* __restrict__ part, int splits, int M,
     }
     if (bias) v = v + bias[z * b_cs + e % M];
     if (relu) v = fmaxf(v, 0.f);
-    if (drop.mode) v = apply_dropout(drop, z, e, v);
+    if (drop.mode) v = apply_dropout(drop, drop_key(drop, z), z, e, v);
     Y[z * y_cs + e] = v;
 }
 

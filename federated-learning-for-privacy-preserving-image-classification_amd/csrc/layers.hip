@@ -35,6 +35,7 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
     // ring for the direct-conv kernels); idx / mask stay dense [img][C][H/2][W/2]
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
     const int z = blockIdx.y;
+    const uint64_t prow = drop_mode == 1 ? philox_row(seed_dev, z) : 0ull;  // once, not per store
     const int cnt = counts ? counts[z] : batch;
     const int OH = H / 2, OW = W / 2;
     // 32-bit unsigned index arithmetic (a client's batch is < 2^31 elements; the 64-bit
@@ -67,7 +68,7 @@ maxpool2_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict
         if (drop_mode) {
             uint8_t keep;
             if (drop_mode == 1) {
-                const uint4 r = Philox::gen(seed, philox_row(seed_dev, z), (uint64_t)e);
+                const uint4 r = Philox::gen(seed, prow, (uint64_t)e);
                 keep = u01(r.x) <= keep_prob ? 1 : 0;
                 mask[z * m_cs + e] = keep;
             } else {
@@ -125,13 +126,14 @@ dropout_fwd_kernel(const float* __restrict__ x, int64_t x_cs, float* __restrict_
                    uint64_t seed_salt, const uint64_t* __restrict__ seed_dev) {
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
     const int z = blockIdx.y;
+    const uint64_t prow = drop_mode == 1 ? philox_row(seed_dev, z) : 0ull;  // once, not per store
     const int cnt = counts ? counts[z] : batch;
     const int64_t total = cnt * per_img;
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * blockDim.x) {
         uint8_t keep;
         if (drop_mode == 1) {
-            const uint4 r = Philox::gen(seed, philox_row(seed_dev, z), (uint64_t)e);
+            const uint4 r = Philox::gen(seed, prow, (uint64_t)e);
             keep = u01(r.x) <= keep_prob ? 1 : 0;
             mask[z * m_cs + e] = keep;
         } else {
@@ -772,6 +774,7 @@ gather_u8_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ l
     const uint32_t plane = (uint32_t)(H * W), per = plane * (uint32_t)C;
     const uint32_t total = (uint32_t)cnt * per;  // 32-bit index arithmetic (< 2^31 per client)
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
+    const uint64_t prow = philox_row(seed_dev, z);  // once, not per store
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += gridDim.x * blockDim.x) {
         const uint32_t b = e / per;
@@ -785,7 +788,7 @@ gather_u8_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ l
                 const uchar4 a = aug_in[z * aug_cs + b];
                 ci = a.x; cj = a.y; fl = a.z;
             } else {
-                const uint4 rr = Philox::gen(seed, philox_row(seed_dev, z), (uint64_t)b);
+                const uint4 rr = Philox::gen(seed, prow, (uint64_t)b);
                 const uint32_t span = 2u * (uint32_t)pad + 1u;
                 ci = pad > 0 ? (int)(((uint64_t)rr.x * span) >> 32) : 0;
                 cj = pad > 0 ? (int)(((uint64_t)rr.y * span) >> 32) : 0;
