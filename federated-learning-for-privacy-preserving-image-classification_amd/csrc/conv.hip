@@ -2781,6 +2781,21 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
         __syncthreads();
     }
     if (wid != 0) return;
+    // the epilogue's operands (keep-mask, ReLU reference, pool argmax) loaded for every element
+    // first: interleaved with the dX stores (which may alias them) each element cost one
+    // dependent round trip — r05: fc2's backward took ~21 us at every client count
+    uint32_t kp[KT][16];  // keep | relu-ok << 1 | argmax << 2
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int img = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t e = (int64_t)(img < cnt ? img : 0) * K + k0 + 32 * t + r32;
+            const uint32_t keep = ep.mask ? (ep.mask[z * ep.m_cs + e] ? 1u : 0u) : 1u;
+            const uint32_t rok = ep.relu_ref ? (ep.relu_ref[z * ep.r_cs + e] > 0.f ? 2u : 0u) : 2u;
+            const uint32_t am = ep.pidx ? ((uint32_t)ep.pidx[z * ep.pi_cs + e] << 2) : 0u;
+            kp[t][r] = keep | rok | am;
+        }
 #pragma unroll
     for (int t = 0; t < KT; ++t)
 #pragma unroll
@@ -2789,12 +2804,12 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
             if (img >= cnt) continue;
             float v = acc[t][r];
             const int64_t e = (int64_t)img * K + k0 + 32 * t + r32;
-            if (ep.mask) v = ep.mask[z * ep.m_cs + e] ? v * ep.scale : 0.f;
-            if (ep.relu_ref && !(ep.relu_ref[z * ep.r_cs + e] > 0.f)) v = 0.f;
+            if (ep.mask) v = (kp[t][r] & 1u) ? v * ep.scale : 0.f;
+            if (ep.relu_ref && !(kp[t][r] & 2u)) v = 0.f;
             if (ep.pidx) {
                 const int f = k0 + 32 * t + r32, c = f / ep.pohw, rem = f - c * ep.pohw;
                 const int oh = rem / ep.pow_, ow = rem - oh * ep.pow_;
-                const int a = ep.pidx[z * ep.pi_cs + e];
+                const int a = (int)(kp[t][r] >> 2);
                 float* d = dX + z * dx_cs +
                            ((int64_t)(img * (K / ep.pohw) + c) * ep.xh + 2 * oh) * ep.xw + 2 * ow;
                 d[0] = a == 0 ? v : 0.f;
