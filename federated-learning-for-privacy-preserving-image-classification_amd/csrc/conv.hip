@@ -3598,7 +3598,10 @@ dpsgd_norm_clip_kernel(const NormSrcs src, const int32_t* __restrict__ counts, i
         const float* xr = L.x + z * L.x_cs + (int64_t)i * L.in_f;
         const float* dr = L.dy + z * L.dy_cs + (int64_t)i * L.out_f;
         double sx = 0.0, sd = 0.0;
+        // unrolled loops keep each thread's order (the same sums) with several loads in flight
+#pragma unroll 4
         for (int k = threadIdx.x; k < L.in_f; k += 256) sx += (double)xr[k] * (double)xr[k];
+#pragma unroll 4
         for (int k = threadIdx.x; k < L.out_f; k += 256) sd += (double)dr[k] * (double)dr[k];
         sx = block_sum_256(sx, red);
         sd = block_sum_256(sd, red);
@@ -3607,6 +3610,7 @@ dpsgd_norm_clip_kernel(const NormSrcs src, const int32_t* __restrict__ counts, i
     for (int l = 0; l < src.nslab; ++l) {
         const float4* w4 = reinterpret_cast<const float4*>(src.sw[l] + row * src.per_w[l]);
         double sq = 0.0;
+#pragma unroll 4
         for (int q = threadIdx.x; q < src.per_w[l] / 4; q += 256) {
             const float4 v = w4[q];
             sq += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;

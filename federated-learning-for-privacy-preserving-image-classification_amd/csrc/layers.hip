@@ -738,12 +738,29 @@ gather_kernel(const float* __restrict__ data, const int64_t* __restrict__ labels
     const int z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
     const int64_t total = (int64_t)cnt * sample_elems;
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t b = e / sample_elems, off = e - b * sample_elems;
-        const int64_t s = idx[z * idx_cs + b];
-        x[z * x_cs + e] = data[s * sample_elems + off];
-        if (off == 0 && y) y[z * y_cs + b] = labels[s];
+    // four grid-stride elements per pass, loads ahead of stores (as gather_u8_kernel)
+    constexpr int U = 4;
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e0 < total; e0 += U * G) {
+        int64_t bq[U], oq[U], sq[U];
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t e = e0 + u * G;
+            bq[u] = e < total ? e / sample_elems : 0;
+            oq[u] = e - bq[u] * sample_elems;
+            sq[u] = e < total ? idx[z * idx_cs + bq[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = e0 + u * G < total ? data[sq[u] * sample_elems + oq[u]] : 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t e = e0 + u * G;
+            if (e >= total) break;
+            x[z * x_cs + e] = v[u];
+            if (oq[u] == 0 && y) y[z * y_cs + bq[u]] = labels[sq[u]];
+        }
     }
 }
 
@@ -775,36 +792,56 @@ gather_u8_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ l
     const uint32_t total = (uint32_t)cnt * per;  // 32-bit index arithmetic (< 2^31 per client)
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
     const uint64_t prow = philox_row(seed_dev, z);  // once, not per store
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
-         e += gridDim.x * blockDim.x) {
-        const uint32_t b = e / per;
-        const uint32_t r = e - b * per;
-        const int c = (int)(r / plane);
-        const uint32_t p = r - (uint32_t)c * plane;
-        const int yy = (int)(p / (uint32_t)W), xx = (int)(p - (uint32_t)yy * (uint32_t)W);
-        int ci = pad, cj = pad, fl = 0;
-        if (pad > 0 || flip) {
-            if (aug_in) {
-                const uchar4 a = aug_in[z * aug_cs + b];
-                ci = a.x; cj = a.y; fl = a.z;
-            } else {
-                const uint4 rr = Philox::gen(seed, prow, (uint64_t)b);
-                const uint32_t span = 2u * (uint32_t)pad + 1u;
-                ci = pad > 0 ? (int)(((uint64_t)rr.x * span) >> 32) : 0;
-                cj = pad > 0 ? (int)(((uint64_t)rr.y * span) >> 32) : 0;
-                fl = flip ? (int)(rr.z >> 31) : 0;
-                if (aug_out && r == 0) aug_out[z * aug_cs + b] = make_uchar4(ci, cj, fl, 0);
+    // four grid-stride elements per pass, every load issued before the first store (r05: one
+    // element per pass left two dependent round trips — sample index, then byte — per element)
+    constexpr int U = 4;
+    const uint32_t G = gridDim.x * blockDim.x;
+    for (uint32_t e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += U * G) {
+        uint32_t bq[U], rq[U];
+        int cq[U], sy[U], sx[U];
+        int64_t sq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t e = e0 + u * G;
+            const uint32_t b = e < total ? e / per : 0u;
+            const uint32_t r = e - b * per;
+            const int c = (int)(r / plane);
+            const uint32_t p = r - (uint32_t)c * plane;
+            const int yy = (int)(p / (uint32_t)W), xx = (int)(p - (uint32_t)yy * (uint32_t)W);
+            int ci = pad, cj = pad, fl = 0;
+            if (e < total && (pad > 0 || flip)) {
+                if (aug_in) {
+                    const uchar4 a = aug_in[z * aug_cs + b];
+                    ci = a.x; cj = a.y; fl = a.z;
+                } else {
+                    const uint4 rr = Philox::gen(seed, prow, (uint64_t)b);
+                    const uint32_t span = 2u * (uint32_t)pad + 1u;
+                    ci = pad > 0 ? (int)(((uint64_t)rr.x * span) >> 32) : 0;
+                    cj = pad > 0 ? (int)(((uint64_t)rr.y * span) >> 32) : 0;
+                    fl = flip ? (int)(rr.z >> 31) : 0;
+                    if (aug_out && r == 0) aug_out[z * aug_cs + b] = make_uchar4(ci, cj, fl, 0);
+                }
             }
+            const int sx0 = fl ? (W - 1 - xx) : xx;  // flip acts on the cropped image
+            bq[u] = b; rq[u] = r; cq[u] = c;
+            sy[u] = yy + ci - pad;
+            sx[u] = sx0 + cj - pad;
+            sq[u] = e < total ? idx[z * idx_cs + b] : 0;
         }
-        const int sx0 = fl ? (W - 1 - xx) : xx;  // flip acts on the cropped image
-        const int sy = yy + ci - pad, sx = sx0 + cj - pad;
-        const int64_t s = idx[z * idx_cs + b];
-        float u = 0.f;
-        if (sy >= 0 && sy < H && sx >= 0 && sx < W)
-            u = (float)data[((s * H + sy) * W + sx) * C + c];
-        const float v = __fdiv_rn(u, 255.f);
-        x[z * x_cs + e] = __fdiv_rn(v - np.mean[c], np.stdv[c]);
-        if (r == 0 && y) y[z * y_cs + b] = labels[s];
+        float uq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = e0 + u * G < total && sy[u] >= 0 && sy[u] < H && sx[u] >= 0 && sx[u] < W;
+            uq[u] = in ? (float)data[((sq[u] * H + sy[u]) * W + sx[u]) * C + cq[u]] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t e = e0 + u * G;
+            if (e >= total) break;
+            const float v = __fdiv_rn(uq[u], 255.f);
+            x[z * x_cs + e] = __fdiv_rn(v - np.mean[cq[u]], np.stdv[cq[u]]);
+            if (rq[u] == 0 && y) y[z * y_cs + bq[u]] = labels[sq[u]];
+        }
     }
 }
 

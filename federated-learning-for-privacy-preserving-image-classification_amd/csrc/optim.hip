@@ -244,13 +244,25 @@ opt_slabs_kernel(float4* __restrict__ p, float4* __restrict__ g, float4* __restr
         const float4* src = R.slab + (int64_t)z * R.splits * R.len4 + e;
         const float* cz = d.coef + (int64_t)z * d.batch;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int i = 0; i < cnt; ++i) {  // fh_persample_slab_wsum's order and operations
-            const float c = cz[i];
-            const float4 v = src[(int64_t)i * R.len4];
-            acc.x = acc.x + c * v.x;
-            acc.y = acc.y + c * v.y;
-            acc.z = acc.z + c * v.z;
-            acc.w = acc.w + c * v.w;
+        // fh_persample_slab_wsum's order and operations, eight images' loads in flight (r05:
+        // one image at a time left one dependent round trip per image)
+        for (int i0 = 0; i0 < cnt; i0 += 8) {
+            float c[8];
+            float4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const bool ok = i0 + j < cnt;
+                c[j] = ok ? cz[i0 + j] : 0.f;
+                v[j] = ok ? src[(int64_t)(i0 + j) * R.len4] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (i0 + j < cnt) {
+                    acc.x = acc.x + c[j] * v[j].x;
+                    acc.y = acc.y + c[j] * v[j].y;
+                    acc.z = acc.z + c[j] * v[j].z;
+                    acc.w = acc.w + c[j] * v[j].w;
+                }
         }
         dp_noise4(acc, d, key, row, (int64_t)R.off4 + e, s);
         g[base + e] = acc;
