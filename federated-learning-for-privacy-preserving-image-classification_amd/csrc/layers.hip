@@ -353,8 +353,20 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         if (mask && dx) {
             const uint8_t* mz = mask + z * m_cs;
             if (((uintptr_t)mz & 3) == 0) {  // cnt * F % 16 == 0
-                for (int e = tid; e < cnt * F / 4; e += 256)
-                    reinterpret_cast<uint32_t*>(Ms)[e] = reinterpret_cast<const uint32_t*>(mz)[e];
+                // every word loaded before the first LDS store (r05: the loop waited for each
+                // load in turn — eight dependent global round trips per thread at F = 256)
+                constexpr int NM = 32 * FMAX / 4 / 256;
+                uint32_t mw[NM];
+#pragma unroll
+                for (int i = 0; i < NM; ++i) {
+                    const int e = tid + 256 * i;
+                    mw[i] = e < cnt * F / 4 ? reinterpret_cast<const uint32_t*>(mz)[e] : 0u;
+                }
+#pragma unroll
+                for (int i = 0; i < NM; ++i) {
+                    const int e = tid + 256 * i;
+                    if (e < cnt * F / 4) reinterpret_cast<uint32_t*>(Ms)[e] = mw[i];
+                }
             } else {
                 for (int e = tid; e < cnt * F; e += 256) Ms[e] = mz[e];
             }
