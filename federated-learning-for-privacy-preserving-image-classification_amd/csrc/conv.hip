@@ -3524,6 +3524,29 @@ extern "C" int fh_conv2d_wgrad_persample(const float* x, int64_t x_cs, const flo
     d.bias_part = (float*)((char*)slab + wslab_bias_off(nclients, batch, cout * N));
     hipStream_t st = as_stream(stream);
     const dim3 grid((unsigned)batch, (unsigned)((cout / 32) * (cin / 32)), (unsigned)nclients);
+    // fh_conv_pair armed (r05, DP-SGD's conv2): the slabs need no reduction launch, so the launch
+    // is held for the layer's DGRAD like a training step's deferred WGRAD (one dual-role grid),
+    // with an armed pooled dY (fh_conv_pooled_dy) travelling along
+    const int pair = g_pair_mode;
+    g_pair_mode = 0;
+    const bool hold = pair && w_ != 8;
+    if (g_pdy.on && !g_pdy.done && !(hold && w_ == 16)) {
+        const int rc = pdy_materialize(const_cast<float*>(dy), dy_cs, counts, nclients, batch, cout,
+                                       w_, st);
+        if (rc) return rc;
+    }
+    if (hold) {
+        if (const int fr = flush_pending_wgrad()) return fr;
+        g_pend.w = w_;
+        g_pend.mode = pair;
+        g_pend.grid = grid;
+        g_pend.d = d;
+        g_pend.st = st;
+        g_pend.on = true;
+        g_pend.pdy = g_pdy.on && !g_pdy.done && w_ == 16;
+        if (g_pend.pdy) g_pend.d.pdy = g_pdy.p;
+        return FH_OK;
+    }
     if (w_ == 32) FH_LAUNCH((dwgrad_q_kernel<32, 128, false>), grid, dim3(256), 0, st, d);
     else if (w_ == 16) FH_LAUNCH((dwgrad_q_kernel<16, 128, false>), grid, dim3(256), 0, st, d);
     else FH_LAUNCH((dwgrad_q_kernel<8, 64, true>), grid, dim3(256), 0, st, d);

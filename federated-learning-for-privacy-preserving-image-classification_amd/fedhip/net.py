@@ -449,10 +449,18 @@ class PackedNet:
         dp2 = A("dp2", 64, 7, 7)
         ops.linear_dgrad(dh1, W(P_, "fc1.weight"), dp2, n, B, 3136, 128, counts=cnt)
         i2 = A("i2", 64, 7, 7, dtype=torch.uint8)
-        self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
+        # r05: conv2's per-image WGRAD slabs and its DGRAD as one dual-role launch (the slabs need
+        # no reduction launch), with pool2's backward routed inside it (fh_conv_pooled_dy)
+        pooled_dy = self.pooled_dy_bwd and self._pool2_fused and self.dual_bwd
+        if not pooled_dy:
+            self._pool2_bwd(dp2, i2, a2, da2, n, cnt)
+        ops.conv_pair(self.dual_bwd)
+        if pooled_dy:
+            ops.conv_pooled_dy(dp2, i2, p2)
         ops.conv2d_wgrad_persample(p1, da2, s2, n, B, 32, hp, hp, 64, counts=cnt, alg_hw=14)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt, alg_hw=14)
+        ops.conv_pair(0)
         # conv1's per-image slabs from pool1's gradient (the pooled ReLU output p1 > 0 is the
         # mask at each window's argmax, whether or not conv1's output was written)
         ops.conv2d_c1_pool_wgrad_persample(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8),

@@ -896,9 +896,10 @@ def conv2d_wgrad_persample(x, dy, slab, nclients, batch, cin, h, wd, cout, count
     ev = PROBE.begin(tag)
     call("fh_conv2d_wgrad_persample", ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(slab.buf), nb,
          _counts(counts), nclients, batch, cin, h, wd, cout, stream_handle())
-    PROBE.end(ev, _conv_flops(nclients, batch, cin, ah, aw, cout, 3, 1, 1),
-              _conv_bytes(nclients, batch, cin, ah, aw, cout, 3, 1, 1) +
-              4.0 * nclients * batch * cout * (cin * 9 + 1), nclients)
+    # armed by conv_pair, the launch may be held for the DGRAD (one dual-role grid)
+    _probe_wgrad_end(ev, tag, _conv_flops(nclients, batch, cin, ah, aw, cout, 3, 1, 1),
+                     _conv_bytes(nclients, batch, cin, ah, aw, cout, 3, 1, 1) +
+                     4.0 * nclients * batch * cout * (cin * 9 + 1), nclients)
 
 
 def conv2d_c1_pool_wgrad_persample(x, dpool, idx, y, slab, nclients, batch, h, wd, cout,
