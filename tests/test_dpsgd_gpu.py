@@ -310,3 +310,24 @@ def test_dpsgd_norm_clip_matches_per_layer_path():
         torch.testing.assert_close(coef_a[z, :n], coef_b[z, :n], rtol=2e-7, atol=0)
         assert torch.all(coef_a[z, n:] == 0)
     assert (coef_a < 1).any() and (coef_a == 1).any()  # both branches of the clip exercised
+
+
+@pytest.mark.parametrize("seed_cfg", [None, 9])
+def test_dpsgd_dual_pooled_bit_identical(seed_cfg):
+    """conv2's per-image WGRAD slabs held for its DGRAD (one dual-role launch) with pool2's
+    backward routed inside (r05) == the two-launch path with the separate maxpool2_bwd launch,
+    bit for bit (params, optimizer state), ragged clients, noise on (fixed noise key)."""
+    sizes = [32, 32, 17, 5]
+    counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
+    cfg = dict(max_grad_norm=0.5, noise_multiplier=0.7, seed=seed_cfg if seed_cfg else 3)
+    out = []
+    for dual, pooled in ((2, True), (0, False), (0, True)):
+        eng, _, _ = _engine(sizes, DPSGDConfig(**cfg))
+        eng.net.dual_bwd, eng.net.pooled_dy_bwd = dual, pooled
+        for _ in range(3):
+            eng.step(3, counts)
+        torch.cuda.synchronize()
+        out.append(eng)
+    for e in out[1:]:
+        assert torch.equal(out[0].params, e.params)
+        assert torch.equal(out[0].state1, e.state1)
