@@ -833,20 +833,40 @@ conv_c1_pool_fwd_kernel(const float* __restrict__ x, int64_t x_cs, const float* 
         const uint8_t* si = src.data + s * H * W;
         float* xo = src.xo + z * src.xo_cs + (int64_t)img * H * W;
         const bool wr = cg == 0;
+        // every byte (and the label) loaded before the first x store (r05: xo may alias the
+        // bytes for the compiler, so each later load waited for the stores before it — a
+        // dependent global round trip per window row)
+        uint32_t b[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int yy = 2 * oh + i - 1, xx = 2 * ow + j - 1;
+                b[i][j] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                              ? (uint32_t)si[yy * W + xx] : 0x100u;  // 0x100: padding
+            }
+        const int64_t lab = wr && q == 0 ? src.labels[s] : 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
                 float v = 0.f;
-                if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
-                    const float u = __fdiv_rn((float)si[yy * W + xx], 255.f);
+                if (b[i][j] < 0x100u) {
+                    const float u = __fdiv_rn((float)b[i][j], 255.f);
                     v = __fdiv_rn(u - src.mean, src.stdv);
-                    if (wr && i >= 1 && i <= 2 && j >= 1 && j <= 2) xo[yy * W + xx] = v;  // own window
                 }
                 t[i][j] = v;
             }
-        if (wr && q == 0) src.ylab[z * src.yl_cs + img] = src.labels[s];
+        if (wr) {
+#pragma unroll
+            for (int i = 1; i <= 2; ++i)
+#pragma unroll
+                for (int j = 1; j <= 2; ++j) {  // own window: always inside the image
+                    const int yy = 2 * oh + i - 1, xx = 2 * ow + j - 1;
+                    xo[yy * W + xx] = t[i][j];
+                }
+            if (q == 0) src.ylab[z * src.yl_cs + img] = lab;
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1009,8 +1029,12 @@ conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float
     constexpr int DP = 4 * MAXW + 2;  // dY pitch per channel (4 rows), = 2 (mod 4)
     constexpr int PW = MAXW + 4;      // patch row pitch: image column c at 2 + c
     constexpr int NDQ = COUT * MAXW / 256;  // dY float4s per thread (upper bound)
-    __shared__ float Ds[COUT * DP];
-    __shared__ float Ps[6 * PW];
+    // r05: two 4-row stages per LDS round (one load round trip and two barriers per pair: the
+    // one-stage rounds waited a full memory latency for 14 MFMAs each); the pixel order of the
+    // MFMA chain is unchanged, so the sums are the same bits
+    constexpr int NS = 2;
+    __shared__ float Ds[NS][COUT * DP];
+    __shared__ float Ps[NS][6 * PW];
     __shared__ float red[4][COUT * 10];
     const int split = blockIdx.x, z = blockIdx.y;
     const int cnt = counts ? counts[z] : batch;
@@ -1021,67 +1045,78 @@ conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const float* xz = x + z * x_cs;
     const float* dyz = dy + z * dy_cs;
-    if (tid < 6) {  // zero halo columns -1 and W (never overwritten)
-        Ps[tid * PW + 1] = 0.f;
-        Ps[tid * PW + W + 2] = 0.f;
+    if (tid < 6 * NS) {  // zero halo columns -1 and W (never overwritten)
+        Ps[tid / 6][(tid % 6) * PW + 1] = 0.f;
+        Ps[tid / 6][(tid % 6) * PW + W + 2] = 0.f;
     }
     const int nd4 = COUT * 4 * Q;
-    float4 rd[NDQ], rx = make_float4(0.f, 0.f, 0.f, 0.f);
-    float2 pg[POOLED ? NDQ : 1], py[POOLED ? NDQ : 1];  // POOLED: raw loads, routed in store()
-    int pc[POOLED ? NDQ : 1];                            // argmax bytes | code row << 16
-    auto load = [&](int st) {
-        const int img = (4 * st) / H, y0 = (4 * st) % H;
+    float4 rd[NS][NDQ], rx[NS];
+    float2 pg[NS][POOLED ? NDQ : 1], py[NS][POOLED ? NDQ : 1];  // POOLED: raw loads, routed
+    int pc[NS][POOLED ? NDQ : 1];                    // in store(); argmax bytes | code row << 16
+    auto load = [&](int st0) {
 #pragma unroll
-        for (int i = 0; i < NDQ; ++i) {
-            const int q = tid + 256 * i;
-            const int co = q / (4 * Q), rem = q % (4 * Q), rr = rem / Q, qq = rem % Q;
-            if constexpr (POOLED) {
-                const int yy = y0 + rr, OHW = (H / 2) * (W / 2);
-                const int64_t pl = (int64_t)img * COUT + co;
-                const int64_t go = pl * gh * gw + (yy >> 1) * gw + 2 * qq;
-                const int64_t io = pl * OHW + (yy >> 1) * (W / 2) + 2 * qq;
-                const bool ok = q < nd4;
-                pg[i] = ok ? make_float2(dyz[go], dyz[go + 1]) : make_float2(0.f, 0.f);
-                py[i] = ok ? make_float2(yp[z * yp_cs + go], yp[z * yp_cs + go + 1])
-                           : make_float2(0.f, 0.f);
-                pc[i] = ok ? (pidx[z * pi_cs + io] | (pidx[z * pi_cs + io + 1] << 8) |
-                              ((yy & 1) << 17))
-                           : 0;
-            } else {
-                rd[i] = q < nd4 ? *reinterpret_cast<const float4*>(
-                                      dyz + ((int64_t)(img * COUT + co) * HW + (y0 + rr) * W + 4 * qq))
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int u = 0; u < NS; ++u) {
+            const int st = st0 + u;
+            const bool live = st < send;
+            const int img = (4 * st) / H, y0 = (4 * st) % H;
+#pragma unroll
+            for (int i = 0; i < NDQ; ++i) {
+                const int q = tid + 256 * i;
+                const int co = q / (4 * Q), rem = q % (4 * Q), rr = rem / Q, qq = rem % Q;
+                const bool ok = live && q < nd4;
+                if constexpr (POOLED) {
+                    const int yy = y0 + rr, OHW = (H / 2) * (W / 2);
+                    const int64_t pl = (int64_t)img * COUT + co;
+                    const int64_t go = pl * gh * gw + (yy >> 1) * gw + 2 * qq;
+                    const int64_t io = pl * OHW + (yy >> 1) * (W / 2) + 2 * qq;
+                    pg[u][i] = ok ? make_float2(dyz[go], dyz[go + 1]) : make_float2(0.f, 0.f);
+                    py[u][i] = ok ? make_float2(yp[z * yp_cs + go], yp[z * yp_cs + go + 1])
+                                  : make_float2(0.f, 0.f);
+                    pc[u][i] = ok ? (pidx[z * pi_cs + io] | (pidx[z * pi_cs + io + 1] << 8) |
+                                     ((yy & 1) << 17))
+                                  : 0;
+                } else {
+                    rd[u][i] = ok ? *reinterpret_cast<const float4*>(
+                                        dyz + ((int64_t)(img * COUT + co) * HW + (y0 + rr) * W +
+                                               4 * qq))
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
             }
-        }
-        if (tid < 6 * Q) {
-            const int pr = tid / Q, qq = tid % Q, y = y0 + pr - 1;
-            rx = (unsigned)y < (unsigned)H
-                     ? *reinterpret_cast<const float4*>(xz + (int64_t)img * HW + y * W + 4 * qq)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+            rx[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (tid < 6 * Q) {
+                const int pr = tid / Q, qq = tid % Q, y = y0 + pr - 1;
+                if (live && (unsigned)y < (unsigned)H)
+                    rx[u] = *reinterpret_cast<const float4*>(xz + (int64_t)img * HW + y * W + 4 * qq);
+            }
         }
     };
     auto store = [&]() {
 #pragma unroll
-        for (int i = 0; i < NDQ; ++i) {
-            const int q = tid + 256 * i;
-            if constexpr (POOLED) {  // maxpool2_bwd_kernel's routing: (code == a) ? g : 0
-                const int r = pc[i] >> 16, i0 = pc[i] & 0xff, i1 = (pc[i] >> 8) & 0xff;
-                const float g0 = py[i].x > 0.f ? pg[i].x : 0.f, g1 = py[i].y > 0.f ? pg[i].y : 0.f;
-                rd[i] = make_float4(i0 == r ? g0 : 0.f, i0 == (r | 1) ? g0 : 0.f,
-                                    i1 == r ? g1 : 0.f, i1 == (r | 1) ? g1 : 0.f);
+        for (int u = 0; u < NS; ++u) {
+#pragma unroll
+            for (int i = 0; i < NDQ; ++i) {
+                const int q = tid + 256 * i;
+                if constexpr (POOLED) {  // maxpool2_bwd_kernel's routing: (code == a) ? g : 0
+                    const int c = pc[u][i];
+                    const int r = c >> 16, i0 = c & 0xff, i1 = (c >> 8) & 0xff;
+                    const float g0 = py[u][i].x > 0.f ? pg[u][i].x : 0.f;
+                    const float g1 = py[u][i].y > 0.f ? pg[u][i].y : 0.f;
+                    rd[u][i] = make_float4(i0 == r ? g0 : 0.f, i0 == (r | 1) ? g0 : 0.f,
+                                           i1 == r ? g1 : 0.f, i1 == (r | 1) ? g1 : 0.f);
+                }
+                if (q < nd4) {
+                    const int co = q / (4 * Q), rem = q % (4 * Q), rr = rem / Q, qq = rem % Q;
+                    float2* d = reinterpret_cast<float2*>(&Ds[u][co * DP + rr * W + 4 * qq]);
+                    d[0] = make_float2(rd[u][i].x, rd[u][i].y);
+                    d[1] = make_float2(rd[u][i].z, rd[u][i].w);
+                }
             }
-            if (q < nd4) {
-                const int co = q / (4 * Q), rem = q % (4 * Q), rr = rem / Q, qq = rem % Q;
-                float2* d = reinterpret_cast<float2*>(Ds + co * DP + rr * W + 4 * qq);
-                d[0] = make_float2(rd[i].x, rd[i].y);
-                d[1] = make_float2(rd[i].z, rd[i].w);
+            if (tid < 6 * Q) {
+                const int pr = tid / Q, qq = tid % Q;
+                float2* d = reinterpret_cast<float2*>(&Ps[u][pr * PW + 2 + 4 * qq]);
+                d[0] = make_float2(rx[u].x, rx[u].y);
+                d[1] = make_float2(rx[u].z, rx[u].w);
             }
-        }
-        if (tid < 6 * Q) {
-            const int pr = tid / Q, qq = tid % Q;
-            float2* d = reinterpret_cast<float2*>(Ps + pr * PW + 2 + 4 * qq);
-            d[0] = make_float2(rx.x, rx.y);
-            d[1] = make_float2(rx.z, rx.w);
         }
     };
     // lane roles: m / n = lane & 15 (channel of the A operand / tap of the B operand),
@@ -1096,17 +1131,22 @@ conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float
         load(sbeg);
         store();
         __syncthreads();
-        for (int st = sbeg; st < send; ++st) {
-            const bool more = st + 1 < send;
-            if (more) load(st + 1);
-            const float* Pr = Ps + wid * PW + kk + toff;
-            const float* Dr = Ds + mn * DP + wid * W + kk;
-            for (int g = 0; g < Q; ++g) {
-                const float b = mn < 9 ? Pr[4 * g] : tconst;
+        for (int st = sbeg; st < send; st += NS) {
+            const bool more = st + NS < send;
+            if (more) load(st + NS);
 #pragma unroll
-                for (int q = 0; q < NQ; ++q)
-                    acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(Dr[q * 16 * DP + 4 * g], b, acc[q],
-                                                                  0, 0, 0);
+            for (int u = 0; u < NS; ++u) {
+                if (st + u < send) {  // block-uniform
+                    const float* Pr = &Ps[u][wid * PW + kk + toff];
+                    const float* Dr = &Ds[u][mn * DP + wid * W + kk];
+                    for (int g = 0; g < Q; ++g) {
+                        const float b = mn < 9 ? Pr[4 * g] : tconst;
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q)
+                            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(Dr[q * 16 * DP + 4 * g], b,
+                                                                          acc[q], 0, 0, 0);
+                    }
+                }
             }
             if (more) {
                 __syncthreads();

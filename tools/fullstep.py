@@ -39,8 +39,9 @@ def breakdown(d, top=40):
         print(f"{t / 1e3 / n:8.1f} us/step {100 * t / busy:5.1f}% {c / n:5.1f}x {t / c / 1e3:7.1f} us  {k}")
 
 
-def run(model_name="cifar10_cnn", clients=32, steps=12):
+def run(model_name="cifar10_cnn", clients=32, steps=12, u8=False, fill=None):
     import torch
+    from fedhip import ops
     from fedhip.engine import PackedTrainer
     from src.shared import models_pytorch as hm
     dev = torch.device("cuda")
@@ -49,11 +50,21 @@ def run(model_name="cifar10_cnn", clients=32, steps=12):
     model = hm.ModelFactory.create_model(model_name).to(dev)
     eng = PackedTrainer(model, capacity=clients, batch=32, device=dev)
     eng.launch_mode = "program"
+    if fill:
+        ops.set_fill_fraction(fill)
+    if u8:  # raw uint8 images with the MNIST / CIFAR transform on the chip, as the bench
+        eng.transform = ops.DataTransform.mnist() if model_name == "simple_cnn" else \
+            ops.DataTransform.cifar10()
     for k in range(clients):
         eng.load_module_state(k, model)
     per = 32 * steps
     g = torch.Generator().manual_seed(1)
-    data = torch.randn(clients * per, *shape, generator=g).to(dev)
+    if u8:
+        data = torch.randint(0, 256, (clients * per, *shape[1:], shape[0]) if shape[0] == 3
+                             else (clients * per, *shape[1:]), generator=g,
+                             dtype=torch.uint8).to(dev)
+    else:
+        data = torch.randn(clients * per, *shape, generator=g).to(dev)
     labels = torch.randint(0, 10, (clients * per,), generator=g).to(dev)
     offs = [k * per for k in range(clients)]
     gen = torch.Generator().manual_seed(2)
@@ -70,7 +81,19 @@ def run(model_name="cifar10_cnn", clients=32, steps=12):
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--breakdown":
         breakdown(sys.argv[2])
-    else:
+    else:  # [--u8] [--lib PATH] [--fill F] model clients steps
         a = sys.argv[1:]
+        u8 = "--u8" in a
+        a = [x for x in a if x != "--u8"]
+        fill = None
+        if "--lib" in a:
+            i = a.index("--lib")
+            from fedhip import _lib
+            _lib.load.__defaults__ = (a[i + 1],)
+            del a[i:i + 2]
+        if "--fill" in a:
+            i = a.index("--fill")
+            fill = float(a[i + 1])
+            del a[i:i + 2]
         run(a[0] if a else "cifar10_cnn", int(a[1]) if len(a) > 1 else 32,
-            int(a[2]) if len(a) > 2 else 12)
+            int(a[2]) if len(a) > 2 else 12, u8=u8, fill=fill)

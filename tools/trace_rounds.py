@@ -20,8 +20,8 @@ def main(d, rounds, families=("fh::dconv_kernel",)):
     f = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    first_spin = next(i for i, r in enumerate(rows) if "sleep" in r["Kernel_Name"]
-                      or short(r["Kernel_Name"]).startswith("at::cuda::"))
+    first_spin = next((i for i, r in enumerate(rows) if "sleep" in r["Kernel_Name"]
+                       or short(r["Kernel_Name"]).startswith("at::cuda::")), len(rows))
     win = rows[:first_spin]
     tot = collections.defaultdict(float)
     cnt = collections.Counter()
