@@ -2786,20 +2786,37 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
     for (int t = 0; t < KT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 2
-    for (int mb = mbeg; mb < mbeg + mw; mb += 8) {
-        const float4 a = yok ? *reinterpret_cast<const float4*>(yrow + mb + 4 * h) : zero;
-        float b[4][KT];
+    // software-pipelined: the next 8-m block's loads are issued before this block's MFMAs, and
+    // no load sits under a branch (yrow / wcol are always in bounds; rows past the count are
+    // zeroed by a select) — r05: the conditional dY load put each block's loads in a basic
+    // block of their own, one dependent round trip per block
+    auto ld = [&](int mb, float4& a, float (&b)[4][KT]) {
+        a = *reinterpret_cast<const float4*>(yrow + mb + 4 * h);
+        if (!yok) a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int t = 0; t < KT; ++t) b[q][t] = wcol[(int64_t)(mb + 4 * h + q) * K + 32 * t];
+    };
+    float4 a0, a1;
+    float b0[4][KT], b1[4][KT];
+    if (mw > 0) ld(mbeg, a0, b0);
+    for (int mb = mbeg; mb < mbeg + mw; mb += 16) {
+        const bool more1 = mb + 8 < mbeg + mw;
+        if (more1) ld(mb + 8, a1, b1);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int t = 0; t < KT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a, q), b[q][t], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a0, q), b0[q][t], acc[t], 0, 0, 0);
+        if (!more1) break;
+        const bool more2 = mb + 16 < mbeg + mw;
+        if (more2) ld(mb + 16, a0, b0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a1, q), b1[q][t], acc[t], 0, 0, 0);
     }
     // waves 1..3 hand their partials to wave 0 one at a time through one wave's worth of
     // LDS (16 KB at KT = 4, so LDS does not cap the workgroups per CU); wave 0 adds them in
@@ -2824,18 +2841,32 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
     // the epilogue's operands (keep-mask, ReLU reference, pool argmax) loaded for every element
     // first: interleaved with the dX stores (which may alias them) each element cost one
     // dependent round trip — r05: fc2's backward took ~21 us at every client count
+    // r05: per 32-feature tile, the three operand streams are loaded unconditionally (a null
+    // operand reads this client's dX rows instead and is discarded by a uniform select), then
+    // combined — one round trip per tile (the combined form had put each load and its use in a
+    // branch of its own: a dependent round trip per element and operand, 48 per tile)
+    const uint8_t* dxb = reinterpret_cast<const uint8_t*>(dX + z * dx_cs);
+    const uint8_t* mkp = ep.mask ? ep.mask + z * ep.m_cs : dxb;
+    const float* rrp = ep.relu_ref ? ep.relu_ref + z * ep.r_cs : dX + z * dx_cs;
+    const uint8_t* pap = ep.pidx ? ep.pidx + z * ep.pi_cs : dxb;
     uint32_t kp[KT][16];  // keep | relu-ok << 1 | argmax << 2
 #pragma unroll
-    for (int t = 0; t < KT; ++t)
+    for (int t = 0; t < KT; ++t) {
+        uint32_t mk[16], pa[16];
+        float rr[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int img = (r & 3) + 8 * (r >> 2) + 4 * h;
             const int64_t e = (int64_t)(img < cnt ? img : 0) * K + k0 + 32 * t + r32;
-            const uint32_t keep = ep.mask ? (ep.mask[z * ep.m_cs + e] ? 1u : 0u) : 1u;
-            const uint32_t rok = ep.relu_ref ? (ep.relu_ref[z * ep.r_cs + e] > 0.f ? 2u : 0u) : 2u;
-            const uint32_t am = ep.pidx ? ((uint32_t)ep.pidx[z * ep.pi_cs + e] << 2) : 0u;
-            kp[t][r] = keep | rok | am;
+            mk[r] = mkp[e];
+            rr[r] = rrp[e];
+            pa[r] = pap[e];
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            kp[t][r] = (ep.mask ? (mk[r] ? 1u : 0u) : 1u) |
+                       (ep.relu_ref ? (rr[r] > 0.f ? 2u : 0u) : 2u) | (ep.pidx ? pa[r] << 2 : 0u);
+    }
 #pragma unroll
     for (int t = 0; t < KT; ++t)
 #pragma unroll
@@ -2898,15 +2929,27 @@ __device__ __forceinline__ void linear_wgrad_skinny_body(
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     // row scales: lane l holds row l's (one coalesced load), image b's comes by a lane shuffle
     const float rs_l = (rowscale && r32 < cnt) ? rowscale[(int64_t)z * batch + r32] : 1.f;
+    // every image's operands loaded first, from in-bounds addresses (rows past the count and
+    // columns past M read row 0 / column m0 and are zeroed by a select): r05 — the conditional
+    // loads had put each image pair's loads and MFMA in a basic block of their own, 16
+    // dependent round trips per tile
+    const float* yzc = dY + z * dy_cs + (mok ? m0 + r32 : 0);
+    float av[16], bv[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+        const int b = 2 * p + h, bc = b < cnt ? b : 0;
+        av[p] = yzc[(int64_t)bc * M];
+        bv[p] = xz[(int64_t)bc * K];
+    }
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
         const int b = 2 * p + h;
         const bool ok = b < cnt;
-        float av = ok && mok ? yz[(int64_t)b * M] : 0.f;
+        float a = ok && mok ? av[p] : 0.f;
         const float rsb = __shfl(rs_l, b, 64);
-        if (rowscale && ok) av = rsb * av;
-        const float bv = ok ? xz[(int64_t)b * K] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        if (rowscale && ok) a = rsb * a;
+        const float bb = ok ? bv[p] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc, 0, 0, 0);
     }
     float* wz = dW + z * dw_cs + k0 + r32;
 #pragma unroll

@@ -335,49 +335,44 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     const float* wz = w + z * w_cs;
     const int FP = F + 1;
     const int S = gridDim.x;
-    // block 0, thread 0: the running accumulators it updates at the end, loaded now
+    // block 0, thread 0: the running accumulators it updates at the end (SMALLK: loaded after
+    // the operands' loads are issued)
     bool rs0 = false;
     double al0 = 0.0;
     int64_t ac0 = 0, as0 = 0;
-    if (part == 0 && tid == 0) {
-        rs0 = reset && reset[z];
-        if (acc_loss) al0 = acc_loss[z];
-        if (acc_correct) ac0 = acc_correct[z];
-        if (acc_seen) as0 = acc_seen[z];
-    }
+    auto load_acc = [&]() {
+        if (part == 0 && tid == 0) {
+            rs0 = reset && reset[z];
+            if (acc_loss) al0 = acc_loss[z];
+            if (acc_correct) ac0 = acc_correct[z];
+            if (acc_seen) as0 = acc_seen[z];
+        }
+    };
     const int dx_per = (cnt * F + S - 1) / S, dx_e0 = part * dx_per;
     const int dx_e1 = min(cnt * F, dx_e0 + dx_per);
     if constexpr (SMALLK) {
-        if (tid < cnt) Ts[tid] = targets[z * t_cs + tid];
-        if (tid < K) Bs[tid] = bias ? bias[z * b_cs + tid] : 0.f;
-        if (mask && dx) {
-            const uint8_t* mz = mask + z * m_cs;
-            if (((uintptr_t)mz & 3) == 0) {  // cnt * F % 16 == 0
-                // every word loaded before the first LDS store (r05: the loop waited for each
-                // load in turn — eight dependent global round trips per thread at F = 256)
-                constexpr int NM = 32 * FMAX / 4 / 256;
-                uint32_t mw[NM];
+        // every global load of the prologue is issued before the first LDS store: the targets,
+        // the bias, the keep-mask words, x and W, then the accumulators (r05: each section's
+        // store waited for its own loads before the next section's loads were issued — four
+        // dependent global round trips; r03 / r04 had removed those inside the sections)
+        const int64_t tv = tid < cnt ? targets[z * t_cs + tid] : 0;
+        const float bv = (tid < K && bias) ? bias[z * b_cs + tid] : 0.f;
+        const uint8_t* mz = mask + z * m_cs;
+        const bool mwords = mask && dx && ((uintptr_t)mz & 3) == 0;  // cnt * F % 16 == 0
+        constexpr int NM = 32 * FMAX / 4 / 256;
+        uint32_t mw[NM];
+        if (mwords) {
 #pragma unroll
-                for (int i = 0; i < NM; ++i) {
-                    const int e = tid + 256 * i;
-                    mw[i] = e < cnt * F / 4 ? reinterpret_cast<const uint32_t*>(mz)[e] : 0u;
-                }
-#pragma unroll
-                for (int i = 0; i < NM; ++i) {
-                    const int e = tid + 256 * i;
-                    if (e < cnt * F / 4) reinterpret_cast<uint32_t*>(Ms)[e] = mw[i];
-                }
-            } else {
-                for (int e = tid; e < cnt * F; e += 256) Ms[e] = mz[e];
+            for (int i = 0; i < NM; ++i) {
+                const int e = tid + 256 * i;
+                mw[i] = e < cnt * F / 4 ? reinterpret_cast<const uint32_t*>(mz)[e] : 0u;
             }
         }
-        // float4 loads, all issued before the LDS stores (r03: the element loop waited for
-        // each load in turn — ~20 dependent global round trips per launch)
         const bool v4 = (F & 3) == 0 && ((uintptr_t)xz & 15) == 0 && ((uintptr_t)wz & 15) == 0;
+        constexpr int NX = 32 * FMAX / 4 / 256, NW = KMAX * FMAX / 4 / 256;
+        const int F4 = F / 4;
+        float4 xv[NX], wv[NW];
         if (v4) {
-            constexpr int NX = 32 * FMAX / 4 / 256, NW = KMAX * FMAX / 4 / 256;
-            const int F4 = F / 4;
-            float4 xv[NX], wv[NW];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
                 const int e4 = tid + 256 * i;
@@ -390,6 +385,20 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
                 wv[i] = e4 < K * F4 ? *reinterpret_cast<const float4*>(wz + 4 * e4)
                                     : make_float4(0.f, 0.f, 0.f, 0.f);
             }
+        }
+        load_acc();
+        if (tid < cnt) Ts[tid] = tv;
+        if (tid < K) Bs[tid] = bv;
+        if (mwords) {
+#pragma unroll
+            for (int i = 0; i < NM; ++i) {
+                const int e = tid + 256 * i;
+                if (e < cnt * F / 4) reinterpret_cast<uint32_t*>(Ms)[e] = mw[i];
+            }
+        } else if (mask && dx) {
+            for (int e = tid; e < cnt * F; e += 256) Ms[e] = mz[e];
+        }
+        if (v4) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
                 const int e4 = tid + 256 * i;
@@ -419,6 +428,8 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
             }
         }
         __syncthreads();
+    } else {
+        load_acc();
     }
     auto X = [&](int b, int f) -> float { return SMALLK ? Xs[b * FP + f] : xz[(int64_t)b * F + f]; };
     auto Wt = [&](int k, int f) -> float { return SMALLK ? Ws[k * FP + f] : wz[(int64_t)k * F + f]; };
