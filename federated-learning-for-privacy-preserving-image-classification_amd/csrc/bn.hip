@@ -356,12 +356,18 @@ __device__ __forceinline__ float4 upstream4(const BNArgs& a, int z, int64_t o) {
     a.fd_w.divmod((uint32_t)(o - plane * a.HW), y, x);
     const int64_t e = plane * (a.HW >> 2) + (int64_t)(y >> 1) * (a.W >> 1) + (x >> 1);
     const int r = (y & 1) << 1;
+    // every load unconditional (a null keep-mask reads the argmax bytes) and each keep byte
+    // folded into its argmax code, which every result uses: r05 — under `if (pmask)` each mask
+    // byte's load and use sat in a branch of their own, a dependent round trip per byte
+    const uint8_t* pk = a.pmask ? a.pmask + z * a.pm_cs : a.pidx + z * a.pi_cs;
     float g0 = a.dpool[z * a.dp_cs + e], g1 = a.dpool[z * a.dp_cs + e + 1];
-    if (a.pmask) {
-        g0 = a.pmask[z * a.pm_cs + e] ? g0 * a.pscale : 0.f;
-        g1 = a.pmask[z * a.pm_cs + e + 1] ? g1 * a.pscale : 0.f;
-    }
-    const int i0 = a.pidx[z * a.pi_cs + e], i1 = a.pidx[z * a.pi_cs + e + 1];
+    const int c0 = a.pidx[z * a.pi_cs + e] | (pk[e] ? 4 : 0);
+    const int c1 = a.pidx[z * a.pi_cs + e + 1] | (pk[e + 1] ? 4 : 0);
+    const bool dm = a.pmask != nullptr;
+    const float h0 = dm ? g0 * a.pscale : g0, h1 = dm ? g1 * a.pscale : g1;
+    g0 = (!dm || (c0 & 4)) ? h0 : 0.f;
+    g1 = (!dm || (c1 & 4)) ? h1 : 0.f;
+    const int i0 = c0 & 3, i1 = c1 & 3;
     return make_float4(i0 == r ? g0 : 0.f, i0 == (r | 1) ? g0 : 0.f, i1 == r ? g1 : 0.f,
                        i1 == (r | 1) ? g1 : 0.f);
 }

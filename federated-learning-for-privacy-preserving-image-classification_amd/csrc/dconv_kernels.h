@@ -465,19 +465,31 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
                 float xv[FM][16];  // all loads of the column first: `out` may alias `bnx`
                 int cd[FM][16];    // pooled: argmax (bits 0-1) | kept (bit 2)
                 if (pooled) {
+                    // argmax and keep-mask bytes of the column loaded from in-bounds addresses
+                    // (dead elements read element 0; a null keep-mask reads the argmax bytes)
+                    // and combined after: r05 — the keep-mask test had put each element's load
+                    // and use in a branch of its own, one dependent round trip per element
                     const int64_t e0 = (int64_t)img * M * G::HW + p;
+                    const uint8_t* pi = a.pidx + z * a.pi_cs;
+                    const uint8_t* pk = a.pmask ? a.pmask + z * a.pm_cs : pi;
+                    uint32_t ib[FM][16], kb[FM][16];
 #pragma unroll
                     for (int i = 0; i < FM; ++i)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
-                            int code = 0;
-                            if (live && m < M) {
-                                const int64_t e = e0 + (int64_t)m * G::HW;
-                                code = a.pidx[z * a.pi_cs + e];
-                                code |= (!a.pmask || a.pmask[z * a.pm_cs + e]) ? 4 : 0;
-                            }
-                            cd[i][r] = code;
+                            const int64_t e = (live && m < M) ? e0 + (int64_t)m * G::HW : 0;
+                            ib[i][r] = pi[e];
+                            kb[i][r] = pk[e];
+                        }
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                            cd[i][r] = (live && m < M)
+                                           ? (int)ib[i][r] | ((!a.pmask || kb[i][r]) ? 4 : 0)
+                                           : 0;
                         }
                     const int py = p / G::H, px = p % G::H;
                     const float* xz = a.bnx + z * a.bnx_cs + (int64_t)img * M * 4 * G::HW +

@@ -816,26 +816,38 @@ gather_u8_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ l
     const uint64_t seed = seed_salt + (seed_dev ? *seed_dev : 0ull);
     const uint64_t prow = philox_row(seed_dev, z);  // once, not per store
     // four grid-stride elements per pass, every load issued before the first store (r05: one
-    // element per pass left two dependent round trips — sample index, then byte — per element)
+    // element per pass left two dependent round trips — sample index, then byte — per element).
+    // Loads come in two waves (sample index and recorded augmentation, then the image byte and
+    // the label), each from in-bounds addresses with the result selected after, so no load sits
+    // under a branch with its use (r05: the byte load behind `in ?` and the recorded offsets
+    // behind `if (aug_in)` had been one dependent round trip per element each)
     constexpr int U = 4;
     const uint32_t G = gridDim.x * blockDim.x;
+    const bool aug = pad > 0 || flip;
     for (uint32_t e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += U * G) {
         uint32_t bq[U], rq[U];
         int cq[U], sy[U], sx[U];
         int64_t sq[U];
+        uchar4 aq[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t e = e0 + u * G;
             const uint32_t b = e < total ? e / per : 0u;
-            const uint32_t r = e - b * per;
+            bq[u] = b;
+            rq[u] = e - b * per;
+            sq[u] = idx[z * idx_cs + b];
+            aq[u] = aug_in ? aug_in[z * aug_cs + b] : make_uchar4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t e = e0 + u * G, b = bq[u], r = rq[u];
             const int c = (int)(r / plane);
             const uint32_t p = r - (uint32_t)c * plane;
             const int yy = (int)(p / (uint32_t)W), xx = (int)(p - (uint32_t)yy * (uint32_t)W);
             int ci = pad, cj = pad, fl = 0;
-            if (e < total && (pad > 0 || flip)) {
+            if (e < total && aug) {
                 if (aug_in) {
-                    const uchar4 a = aug_in[z * aug_cs + b];
-                    ci = a.x; cj = a.y; fl = a.z;
+                    ci = aq[u].x; cj = aq[u].y; fl = aq[u].z;
                 } else {
                     const uint4 rr = Philox::gen(seed, prow, (uint64_t)b);
                     const uint32_t span = 2u * (uint32_t)pad + 1u;
@@ -846,24 +858,27 @@ gather_u8_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ l
                 }
             }
             const int sx0 = fl ? (W - 1 - xx) : xx;  // flip acts on the cropped image
-            bq[u] = b; rq[u] = r; cq[u] = c;
+            cq[u] = c;
             sy[u] = yy + ci - pad;
             sx[u] = sx0 + cj - pad;
-            sq[u] = e < total ? idx[z * idx_cs + b] : 0;
         }
-        float uq[U];
+        uint32_t ub[U];
+        int64_t lq[U];
+        bool inq[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const bool in = e0 + u * G < total && sy[u] >= 0 && sy[u] < H && sx[u] >= 0 && sx[u] < W;
-            uq[u] = in ? (float)data[((sq[u] * H + sy[u]) * W + sx[u]) * C + cq[u]] : 0.f;
+            inq[u] = e0 + u * G < total && sy[u] >= 0 && sy[u] < H && sx[u] >= 0 && sx[u] < W;
+            const int64_t off = inq[u] ? ((sq[u] * H + sy[u]) * W + sx[u]) * C + cq[u] : 0;
+            ub[u] = data[off];
+            lq[u] = labels[sq[u]];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t e = e0 + u * G;
             if (e >= total) break;
-            const float v = __fdiv_rn(uq[u], 255.f);
+            const float v = __fdiv_rn(inq[u] ? (float)ub[u] : 0.f, 255.f);
             x[z * x_cs + e] = __fdiv_rn(v - np.mean[cq[u]], np.stdv[cq[u]]);
-            if (rq[u] == 0 && y) y[z * y_cs + bq[u]] = labels[sq[u]];
+            if (rq[u] == 0 && y) y[z * y_cs + bq[u]] = lq[u];
         }
     }
 }

@@ -179,15 +179,31 @@ __device__ __forceinline__ void dp_noise4(float4& g, const OptDp& d, uint64_t ke
     if (j + 3 < d.n_noise) g.w = g.w + s * r[3];
 }
 
+// The update of one float4 in two phases: opt_load4 issues its loads (p and the state, from
+// in-bounds addresses — a missing momentum buffer reads p — so no load sits under a branch),
+// opt_apply4 computes and stores.  The plain ranges load all their float4s first (r05: with
+// the momentum load under `if (use_buf)` each float4's loads and update were one dependent
+// round trip).
+struct OptIn {
+    float4 p, m, v;
+};
 template <bool ADAM>
-__device__ __forceinline__ void opt_update4(float4* p, float4* s1, float4* s2, int64_t i,
-                                            float4 gv, const OptScal& o, float bc2_sqrt,
-                                            float neg_step) {
-    const float4 pv = p[i];
+__device__ __forceinline__ void opt_load4(const float4* p, const float4* s1, const float4* s2,
+                                          int64_t i, OptIn& in) {
+    in.p = p[i];
+    in.m = (s1 ? s1 : p)[i];
+    if constexpr (ADAM) in.v = s2[i];
+}
+
+template <bool ADAM>
+__device__ __forceinline__ void opt_apply4(float4* p, float4* s1, float4* s2, int64_t i,
+                                           const OptIn& in, float4 gv, const OptScal& o,
+                                           float bc2_sqrt, float neg_step) {
+    const float4 pv = in.p;
     float4 out;
     if constexpr (!ADAM) {
         const bool use_buf = o.mom != 0.f;
-        const float4 bv = (use_buf && !o.first) ? s1[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 bv = (use_buf && !o.first) ? in.m : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 b;
         out.x = sgd_elem(pv.x, gv.x, bv.x, o.neg_lr, o.mom, o.wd, o.first, b.x);
         out.y = sgd_elem(pv.y, gv.y, bv.y, o.neg_lr, o.mom, o.wd, o.first, b.y);
@@ -195,7 +211,7 @@ __device__ __forceinline__ void opt_update4(float4* p, float4* s1, float4* s2, i
         out.w = sgd_elem(pv.w, gv.w, bv.w, o.neg_lr, o.mom, o.wd, o.first, b.w);
         if (use_buf) s1[i] = b;
     } else {
-        float4 mv = s1[i], vv = s2[i];
+        float4 mv = in.m, vv = in.v;
 #define FH_ADAM_LANE(c) out.c = adam_elem(pv.c, gv.c, mv.c, vv.c, o.wd, o.decay_mul, o.decoupled, \
                                           o.one_m_b1, o.b2, o.one_m_b2, bc2_sqrt, o.eps, neg_step)
         FH_ADAM_LANE(x); FH_ADAM_LANE(y); FH_ADAM_LANE(z); FH_ADAM_LANE(w);
@@ -226,21 +242,32 @@ opt_slabs_kernel(float4* __restrict__ p, float4* __restrict__ g, float4* __restr
         const uint64_t key = d.seed + (d.seed_dev ? *d.seed_dev : 0ull);
         const uint64_t row = philox_row(d.seed_dev, z);
         if (R.slab == nullptr) {
+            constexpr int U = kOptPlainPer / 256;
             const int i0 = (bx - R.blk0) * kOptPlainPer + t;
+            OptIn in[U];
+            float4 gq[U];
 #pragma unroll
-            for (int u = 0; u < kOptPlainPer / 256; ++u) {
+            for (int u = 0; u < U; ++u) {  // every float4's loads first (as the plain path below)
+                const int i = i0 + 256 * u < R.len4 ? i0 + 256 * u : 0;
+                gq[u] = g[base + i];
+                opt_load4<ADAM>(p, s1, s2, base + i, in[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
                 const int i = i0 + 256 * u;
                 if (i < R.len4) {
-                    float4 gv = g[base + i];
+                    float4 gv = gq[u];
                     dp_noise4(gv, d, key, row, (int64_t)R.off4 + i, s);
                     g[base + i] = gv;
-                    opt_update4<ADAM>(p, s1, s2, base + i, gv, o, bc2_sqrt, neg_step);
+                    opt_apply4<ADAM>(p, s1, s2, base + i, in[u], gv, o, bc2_sqrt, neg_step);
                 }
             }
             return;
         }
         const int e = (bx - R.blk0) * 256 + t;
         if (e >= R.len4) return;
+        OptIn in;  // the parameter / state loads in flight with the slab sums
+        opt_load4<ADAM>(p, s1, s2, base + e, in);
         const float4* src = R.slab + (int64_t)z * R.splits * R.len4 + e;
         const float* cz = d.coef + (int64_t)z * d.batch;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -266,15 +293,24 @@ opt_slabs_kernel(float4* __restrict__ p, float4* __restrict__ g, float4* __restr
         }
         dp_noise4(acc, d, key, row, (int64_t)R.off4 + e, s);
         g[base + e] = acc;
-        opt_update4<ADAM>(p, s1, s2, base + e, acc, o, bc2_sqrt, neg_step);
+        opt_apply4<ADAM>(p, s1, s2, base + e, in, acc, o, bc2_sqrt, neg_step);
         return;
     }
     if (R.slab == nullptr) {
+        constexpr int U = kOptPlainPer / 256;
         const int i0 = (bx - R.blk0) * kOptPlainPer + t;
+        OptIn in[U];
+        float4 gq[U];
 #pragma unroll
-        for (int u = 0; u < kOptPlainPer / 256; ++u) {
+        for (int u = 0; u < U; ++u) {  // every float4's loads first (past the range: its start)
+            const int i = i0 + 256 * u < R.len4 ? i0 + 256 * u : 0;
+            gq[u] = g[base + i];
+            opt_load4<ADAM>(p, s1, s2, base + i, in[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
             const int i = i0 + 256 * u;
-            if (i < R.len4) opt_update4<ADAM>(p, s1, s2, base + i, g[base + i], o, bc2_sqrt, neg_step);
+            if (i < R.len4) opt_apply4<ADAM>(p, s1, s2, base + i, in[u], gq[u], o, bc2_sqrt, neg_step);
         }
         return;
     }
@@ -282,6 +318,8 @@ opt_slabs_kernel(float4* __restrict__ p, float4* __restrict__ g, float4* __restr
     const int e = (bx - R.blk0) * C + t % C;
     const int piece = t / C, splits = R.splits;
     const int s0 = (int)((int64_t)splits * piece / G), s1e = (int)((int64_t)splits * (piece + 1) / G);
+    OptIn in;  // the updating thread's parameter / state loads in flight with the slab sums
+    if (piece == 0) opt_load4<ADAM>(p, s1, s2, base + (e < R.len4 ? e : 0), in);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (e < R.len4) {
         const float4* src = R.slab + (int64_t)z * splits * R.len4 + e;
@@ -314,7 +352,7 @@ opt_slabs_kernel(float4* __restrict__ p, float4* __restrict__ g, float4* __restr
     }
     if (e >= R.len4) return;
     g[base + e] = acc;
-    opt_update4<ADAM>(p, s1, s2, base + e, acc, o, bc2_sqrt, neg_step);
+    opt_apply4<ADAM>(p, s1, s2, base + e, in, acc, o, bc2_sqrt, neg_step);
 }
 
 // conv.hip splitk_sum's thread-group count for a split count (kept identical: same bits)
