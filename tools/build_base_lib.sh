@@ -9,10 +9,11 @@ T=$(mktemp -d)
 git -C $R archive $REV $PKG/csrc include | tar -x -C $T
 shift || true
 for f in "$@"; do cp $R/$f $T/$f; done
-mkdir -p $R/ab_lib/base
+OUT=${OUT:-base}
+mkdir -p $R/ab_lib/$OUT
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -munsafe-fp-atomics -I$T/include -Wno-unused-result"
 for s in $T/$PKG/csrc/*.hip; do /opt/rocm/bin/hipcc $F -c $s -o ${s%.hip}.o & done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $T/$PKG/csrc/*.o -o $R/ab_lib/base/libfedhip.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $T/$PKG/csrc/*.o -o $R/ab_lib/$OUT/libfedhip.so
 rm -rf $T
-echo "built ab_lib/base/libfedhip.so from $REV"
+echo "built ab_lib/$OUT/libfedhip.so from $REV"
