@@ -2960,12 +2960,18 @@ __device__ __forceinline__ void linear_wgrad_skinny_body(
     if (db && kblock == 0 && wid == 0 && h == 0 && mok) {
         // every image's term loaded first, then added in image order (the loop's loads had
         // waited for each other: 32 dependent round trips in the kernel's tail — r04)
-        float t[32];
+        // (r05: from in-bounds addresses, selects after — the conditional loads had sat in
+        // branches with their uses under a row scale)
+        const float* rsz = rowscale ? rowscale + (int64_t)z * batch : yz;
+        float t[32], sc[32];
 #pragma unroll
-        for (int b = 0; b < 32; ++b)
-            t[b] = b < cnt ? (rowscale ? rowscale[(int64_t)z * batch + b] * yz[(int64_t)b * M]
-                                       : yz[(int64_t)b * M])
-                           : 0.f;
+        for (int b = 0; b < 32; ++b) {
+            const int bc = b < cnt ? b : 0;
+            t[b] = yz[(int64_t)bc * M];
+            sc[b] = rsz[rowscale ? bc : 0];
+        }
+#pragma unroll
+        for (int b = 0; b < 32; ++b) t[b] = b < cnt ? (rowscale ? sc[b] * t[b] : t[b]) : 0.f;
         float v = 0.f;
 #pragma unroll
         for (int b = 0; b < 32; ++b)

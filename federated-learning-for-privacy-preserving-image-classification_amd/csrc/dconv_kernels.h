@@ -44,10 +44,15 @@ __device__ __forceinline__ void pdy_load(const PooledDy& q, int z, int64_t plane
     const bool r_ok = ok && py < q.ph;
     const bool c0 = r_ok && px < q.ph, c1 = r_ok && px + 1 < q.ph;
     const int64_t e = (plane * q.ph + py) * q.ph + px;
-    g = make_float2(c0 ? q.g[z * q.g_cs + e] : 0.f, c1 ? q.g[z * q.g_cs + e + 1] : 0.f);
-    yp = make_float2(c0 ? q.yp[z * q.y_cs + e] : 0.f, c1 ? q.yp[z * q.y_cs + e + 1] : 0.f);
-    code = (c0 ? (int)q.idx[z * q.i_cs + e] : 0) | ((c1 ? (int)q.idx[z * q.i_cs + e + 1] : 0) << 8) |
-           ((y & 1) << 17);
+    // in-bounds addresses (element 0 of the client for a dead operand), selects after: r05 —
+    // each conditional argmax byte had sat in a branch with its use, one round trip per byte
+    const int64_t e0 = c0 ? e : 0, e1 = c1 ? e + 1 : 0;
+    const float g0 = q.g[z * q.g_cs + e0], g1 = q.g[z * q.g_cs + e1];
+    const float y0 = q.yp[z * q.y_cs + e0], y1 = q.yp[z * q.y_cs + e1];
+    const int i0 = q.idx[z * q.i_cs + e0], i1 = q.idx[z * q.i_cs + e1];
+    g = make_float2(c0 ? g0 : 0.f, c1 ? g1 : 0.f);
+    yp = make_float2(c0 ? y0 : 0.f, c1 ? y1 : 0.f);
+    code = (c0 ? i0 : 0) | ((c1 ? i1 : 0) << 8) | ((y & 1) << 17);
 }
 __device__ __forceinline__ float4 pdy_route(float2 g, float2 yp, int code) {
     const int r = code >> 16, i0 = code & 0xff, i1 = (code >> 8) & 0xff;
@@ -610,8 +615,19 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
         } else {
             float* op = a.out + z * a.out_cs + (int64_t)img * M * G::HW + p;
             const bool has_bias = a.bias != nullptr;
+            // DGRAD accumulating onto dX (a ResNet block's conv1 onto the shortcut gradient):
+            // each 16-row group's old values loaded first (r05: read under the branch, each
+            // element's read-modify-write was one dependent round trip)
 #pragma unroll
-            for (int i = 0; i < FM; ++i)
+            for (int i = 0; i < FM; ++i) {
+                float old[16];
+                if (OP == OP_DGRAD && a.accumulate) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+                        old[r] = op[(int64_t)(m < M ? m : 0) * G::HW];
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int ml = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
@@ -625,11 +641,12 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
                             if (stats || pooled) red[ml * kStatPitch + n - n0] = v;
                             if (pooled) continue;  // only the pooled map leaves the tile
                         } else if (a.accumulate) {
-                            v = *q + v;
+                            v = old[r] + v;
                         }
                         *q = v;
                     }
                 }
+            }
         }
     }
     if constexpr (OP == OP_FWD && POOL_LDS && G::HW <= 256) {
