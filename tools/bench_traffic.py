@@ -14,7 +14,10 @@ share a template (KT conv3 / conv4 at 16x16, conv5 / conv6 at 8x8), by their ord
 a step (the forward issues the shallower layer first, the backward the deeper one).  Average bytes per launch = the same
 averaging as roofline.achieved (all launches of the shape).
 
-usage: python tools/bench_traffic.py <fetch_dir> <write_dir> <out.json>"""
+K2 (SimpleCNN, r05): one 16x16-plane layer (conv2 on its zero-ringed 14x14 map): its forward and
+its dual-role backward (pooled dY routed on load), named on the 14x14 map as bench.py does.
+
+usage: python tools/bench_traffic.py <fetch_dir> <write_dir> <out.json> [KT|K2]"""
 import collections
 import csv
 import glob
@@ -65,7 +68,14 @@ KT = {("wgrad", 32, 0): "conv_wgrad:c32x32x32->32k3s1",
       ("dual", 8, 0): "conv_bwd_dual:c128x8x8->128k3s1", ("dual", 8, 1): "conv_bwd_dual:c64x8x8->128k3s1"}
 
 
-def main(fd, wd, out):
+K2 = {("fwd", 16, 0): "conv_fwd:c32x14x14->64k3s1",
+      ("dual", 16, 0): "conv_bwd_dual:c32x14x14->64k3s1",
+      ("dgrad", 16, 0): "conv_dgrad:c32x14x14->64k3s1",
+      ("wgrad", 16, 0): "conv_wgrad:c32x14x14->64k3s1"}
+
+
+def main(fd, wd, out, workload="KT"):
+    table_of = K2 if workload == "K2" else KT
     F, Wr = dispatches(fd, "FETCH_SIZE"), dispatches(wd, "WRITE_SIZE")
     res = collections.defaultdict(list)
     for src, ctr, scale in ((F, "fetch", 2 * 1024), (Wr, "write", 1024)):
@@ -80,9 +90,9 @@ def main(fd, wd, out):
                     continue
                 # occurrence of this template within the step: wgrad kernels of one width come
                 # in layer order (deeper first); forward / dgrad 32-wide kernels are unique
-                occ = seen[sh] % (2 if sh[1] in (16, 8) else 1)
+                occ = seen[sh] % (2 if sh[1] in (16, 8) and workload != "K2" else 1)
                 seen[sh] += 1
-                tag = KT.get((sh[0], sh[1], occ))
+                tag = table_of.get((sh[0], sh[1], occ))
                 if tag is None:
                     continue
                 b = src[k]["v"] * scale
@@ -99,11 +109,11 @@ def main(fd, wd, out):
         table[t] = {"launches": len(f), "fetch_bytes_per_launch": sum(f) / len(f),
                     "write_bytes_per_launch": sum(w) / len(w),
                     "bytes_per_launch": sum(f) / len(f) + sum(w) / len(w)}
-    json.dump({"method": __doc__.split("\n\n")[0], "workload": "KT", "shapes": table},
+    json.dump({"method": __doc__.split("\n\n")[0], "workload": workload, "shapes": table},
               open(out, "w"), indent=1)
     for t, v in table.items():
         print(f"{t:36s} {v['launches']:5d} launches  {v['bytes_per_launch'] / 1e6:8.2f} MB/launch")
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

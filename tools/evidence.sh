@@ -10,6 +10,7 @@
 #   m  separate rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of the KT bench -> the
 #      per-launch-shape HBM traffic of the timed launches as they run, dual-role WGRAD + DGRAD
 #      grids included (tools/bench_traffic.py)
+#   n  the same two passes of the K2 config (its conv2 forward and dual-role backward)
 # default stages "tsb".  Every GPU step has its own time limit and the chain stops at the
 # first failure (set -e).
 set -e
@@ -62,5 +63,14 @@ if [[ $ST == *m* ]]; then
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --no-cpu-baseline --rounds-target 0 --steps 1 --warmup 1 --no-instances --no-k2 --detail-out '' > $O/pmc_write.json 2> $O/pmc_write.log
   python3 $R/tools/bench_traffic.py $O/pmc_fetch $O/pmc_write $O/bench_traffic.json > $O/bench_traffic.log 2>&1 || true
   tail -5 $O/bench_traffic.log
+  cd $R
+fi
+if [[ $ST == *n* ]]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_k2_fetch -o run -- python3 $R/bench.py --config K2 --no-cpu-baseline --rounds-target 0 --steps 1 --warmup 1 --no-instances --detail-out '' > $O/pmc_k2_fetch.json 2> $O/pmc_k2_fetch.log
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_k2_write -o run -- python3 $R/bench.py --config K2 --no-cpu-baseline --rounds-target 0 --steps 1 --warmup 1 --no-instances --detail-out '' > $O/pmc_k2_write.json 2> $O/pmc_k2_write.log
+  mkdir -p $O/k2
+  python3 $R/tools/bench_traffic.py $O/pmc_k2_fetch $O/pmc_k2_write $O/k2/bench_traffic.json K2 > $O/bench_traffic_k2.log 2>&1 || true
+  tail -5 $O/bench_traffic_k2.log
   cd $R
 fi
