@@ -1546,6 +1546,7 @@ struct PendingWgrad {
 thread_local int g_pair_mode = 0;
 thread_local PendingWgrad g_pend;
 thread_local int64_t g_dual_launches = 0;  // fh_conv_pair_status (instrumentation)
+constexpr bool kDualForceBm32 = true;
 
 // Pooled output gradient of the next WGRAD + DGRAD pair (fh_conv_pooled_dy, r05): when the pair
 // becomes one dual-role launch on 16x16 planes, both roles route dY from the pooled gradient on
@@ -1607,6 +1608,13 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     const bool aligned = ((uintptr_t)a.wt % 16 == 0) && a.w_cs % 4 == 0;
     if (!(aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0)) && p.bm != 32) {
         p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients, /*force_bm32=*/true, S == 2);  // scalar
+    }
+    if constexpr (OP == OP_DGRAD && S == 1) {
+        // r05: a held WGRAD of this map width pairs only with a BM = 32 DGRAD — plan that
+        // instead of BM = 64 so the layer's backward stays one dual-role launch on wide grids
+        // (KT conv4 and the ResNet 64-channel layers at >= 16 clients ran as two launches)
+        if (kDualForceBm32 && g_pend.on && g_pend.st == st && g_pend.w == w && p.bm != 32)
+            p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients, /*force_bm32=*/true, false);
     }
     if (p.splits > 1 && (!ws || ws_bytes < dconv_ws_bytes(p, nclients, a.M, a.batch, sp))) {
         p.splits = 1;
