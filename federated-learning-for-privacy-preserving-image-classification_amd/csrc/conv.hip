@@ -1017,7 +1017,7 @@ conv_c1_wgrad_kernel(const float* __restrict__ x, int64_t x_cs, const float* __r
 // there is > 0, else 0 — per staged quad two pooled values, two argmax bytes, two yp values.
 // The same fp32 values reach the same MFMA chain, so the result equals the unfused pair
 // (maxpool2_bwd_ymask + this kernel on its output) bit for bit.
-template <int COUT, bool POOLED>
+template <int COUT, bool POOLED, int NS = 2>
 __global__ void __launch_bounds__(256)
 conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ dy,
                           int64_t dy_cs, float* __restrict__ part, float* __restrict__ bpart,
@@ -1029,10 +1029,11 @@ conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float
     constexpr int DP = 4 * MAXW + 2;  // dY pitch per channel (4 rows), = 2 (mod 4)
     constexpr int PW = MAXW + 4;      // patch row pitch: image column c at 2 + c
     constexpr int NDQ = COUT * MAXW / 256;  // dY float4s per thread (upper bound)
-    // r05: two 4-row stages per LDS round (one load round trip and two barriers per pair: the
-    // one-stage rounds waited a full memory latency for 14 MFMAs each); the pixel order of the
-    // MFMA chain is unchanged, so the sums are the same bits
-    constexpr int NS = 2;
+    // r05: NS 4-row stages per LDS round (one load round trip and two barriers per NS stages:
+    // the one-stage rounds waited a full memory latency for 14 MFMAs each); the pixel order of
+    // the MFMA chain is unchanged, so the sums are the same bits.  NS = 2 (40 KB of LDS, four
+    // workgroups per CU); NS = 4 for the per-image DP-SGD slabs on narrow grids (75 KB: seven
+    // stages = one image in two rounds)
     __shared__ float Ds[NS][COUT * DP];
     __shared__ float Ps[NS][6 * PW];
     __shared__ float red[4][COUT * 10];
@@ -3520,6 +3521,7 @@ extern "C" int fh_conv2d_persample_sqnorm(const float* x, int64_t x_cs, const fl
 // dY and no implicit-GEMM norm tiles.  SimpleCNN: conv2 on the padded 16x16 planes
 // (dwgrad_q_kernel, two 128-pixel stages = one image per split), conv1 from pool1's gradient
 // (conv_c1_wgrad_mfma_kernel<POOLED>, seven 4-row stages = one 28x28 image per split).
+constexpr int kC1PersampleNs4Max = 512;  // image workgroups: ~two per CU
 static size_t persample_slab_bytes(int nclients, int batch, int per_w, int per_b) {
     return (size_t)wslab_bias_off(nclients, batch, per_w) +
            (size_t)nclients * batch * per_b * sizeof(float);
@@ -3673,7 +3675,12 @@ extern "C" int fh_conv2d_c1_pool_wgrad_persample(const float* x, int64_t x_cs, c
     const int sps = h / 4;  // one image per split
     const dim3 grid((unsigned)batch, (unsigned)nclients);
     hipStream_t st = as_stream(stream);
-    if (cout == 32)
+    // narrow grids (fewer image workgroups than ~two per CU): four stages per LDS round
+    const bool wide4 = (int64_t)batch * nclients <= kC1PersampleNs4Max;
+    if (cout == 32 && wide4)
+        FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true, 4>), grid, dim3(256), 0, st, x, x_cs, dpool,
+                  dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, gw);
+    else if (cout == 32)
         FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
                   dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, gw);
     else

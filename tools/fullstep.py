@@ -39,16 +39,17 @@ def breakdown(d, top=40):
         print(f"{t / 1e3 / n:8.1f} us/step {100 * t / busy:5.1f}% {c / n:5.1f}x {t / c / 1e3:7.1f} us  {k}")
 
 
-def run(model_name="cifar10_cnn", clients=32, steps=12, u8=False, fill=None):
+def run(model_name="cifar10_cnn", clients=32, steps=12, u8=False, fill=None, dpsgd=False):
     import torch
     from fedhip import ops
-    from fedhip.engine import PackedTrainer
+    from fedhip.engine import DPSGDConfig, PackedTrainer
     from src.shared import models_pytorch as hm
     dev = torch.device("cuda")
     shape = (1, 28, 28) if model_name == "simple_cnn" else (3, 32, 32)
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model(model_name).to(dev)
-    eng = PackedTrainer(model, capacity=clients, batch=32, device=dev)
+    eng = PackedTrainer(model, capacity=clients, batch=32, device=dev,
+                        dpsgd=DPSGDConfig(max_grad_norm=1.0, noise_multiplier=1.0) if dpsgd else None)
     eng.launch_mode = "program"
     if fill:
         ops.set_fill_fraction(fill)
@@ -81,10 +82,11 @@ def run(model_name="cifar10_cnn", clients=32, steps=12, u8=False, fill=None):
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--breakdown":
         breakdown(sys.argv[2])
-    else:  # [--u8] [--lib PATH] [--fill F] model clients steps
+    else:  # [--u8] [--dpsgd] [--lib PATH] [--fill F] model clients steps
         a = sys.argv[1:]
         u8 = "--u8" in a
-        a = [x for x in a if x != "--u8"]
+        dp = "--dpsgd" in a
+        a = [x for x in a if x not in ("--u8", "--dpsgd")]
         fill = None
         if "--lib" in a:
             i = a.index("--lib")
@@ -96,4 +98,4 @@ if __name__ == "__main__":
             fill = float(a[i + 1])
             del a[i:i + 2]
         run(a[0] if a else "cifar10_cnn", int(a[1]) if len(a) > 1 else 32,
-            int(a[2]) if len(a) > 2 else 12, u8=u8, fill=fill)
+            int(a[2]) if len(a) > 2 else 12, u8=u8, fill=fill, dpsgd=dp)
