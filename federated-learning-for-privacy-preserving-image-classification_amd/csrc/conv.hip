@@ -3007,6 +3007,43 @@ linear_wgrad_skinny_kernel(const float* __restrict__ X, int64_t x_cs, const floa
                              rest / gy, kb, rest % gy, rowscale);
 }
 
+// Several linear layers' weight gradients in one launch (r05, DP-SGD's pass 2: fc2's and
+// fc1's clipped sums on the same row scales were two dependent launches): the grid is the
+// layers' skinny-WGRAD grids one after another, each block running linear_wgrad_skinny_body
+// for its layer with that layer's own XCD-aware order — the same tiles, the same bits.
+struct LinWgLayer {
+    const float* x;
+    int64_t x_cs;
+    const float* dy;
+    int64_t dy_cs;
+    float* dw;
+    int64_t dw_cs;
+    float* db;
+    int64_t db_cs;
+    int K, M, gx, gy, nblk;  // in_f, out_f, grid x / y, blocks (gx * gy * clients)
+};
+constexpr int kMaxLinWg = 4;
+struct LinWgSet {
+    LinWgLayer l[kMaxLinWg];
+    int n;
+};
+
+__global__ void __launch_bounds__(256)
+linear_wgrad_skinny_multi_kernel(const LinWgSet set, const int32_t* __restrict__ counts, int batch,
+                                 const float* __restrict__ rowscale) {
+    int b = blockIdx.x, li = 0;
+    while (li + 1 < set.n && b >= set.l[li].nblk) {
+        b -= set.l[li].nblk;
+        ++li;
+    }
+    const LinWgLayer& L = set.l[li];
+    const int N = L.nblk;
+    if ((N & 7) == 0) b = (b & 7) * (N >> 3) + (b >> 3);  // as linear_wgrad_skinny_kernel
+    const int kb = b % L.gx, rest = b / L.gx;
+    linear_wgrad_skinny_body(L.x, L.x_cs, L.dy, L.dy_cs, L.dw, L.dw_cs, L.db, L.db_cs, counts,
+                             batch, L.K, L.M, rest / L.gy, kb, rest % L.gy, rowscale);
+}
+
 // A whole linear backward in one launch: workgroups [0, nw) of each client are the skinny
 // WGRAD tiles (in_f/128 x ceil(out_f/32)), the rest the skinny DGRAD tiles with the Dropout /
 // ReLU backward of the layer's input fused into the epilogue — three launches (wgrad, dgrad,
@@ -3417,6 +3454,41 @@ extern "C" int fh_linear_wgrad_rowscale(const float* x, int64_t x_cs, const floa
               dim3(256), 0, as_stream(stream), x, x_cs, dy, dy_cs, dw, dw_cs, db, db_cs, counts,
               batch, in_f, out_f, rowscale);
     FH_LAUNCH_CHECK("linear_wgrad_rowscale");
+    return FH_OK;
+}
+
+extern "C" int fh_linear_wgrad_rowscale_multi(const fh_linear_wgrad_src* layers, int32_t nlayers,
+                                              const float* rowscale, const int32_t* counts,
+                                              int32_t nclients, int32_t batch, void* stream) {
+    FH_REQUIRE(nlayers >= 1 && nlayers <= kMaxLinWg && layers,
+               "linear_wgrad_rowscale_multi: 1..%d layers (got %d)", kMaxLinWg, nlayers);
+    FH_REQUIRE(nclients >= 0 && batch > 0 && batch <= 32,
+               "linear_wgrad_rowscale_multi: batch <= 32 (got %d)", batch);
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(rowscale, "linear_wgrad_rowscale_multi: null row scales");
+    LinWgSet set{};
+    set.n = nlayers;
+    int64_t total = 0;
+    for (int i = 0; i < nlayers; ++i) {
+        const fh_linear_wgrad_src& q = layers[i];
+        FH_REQUIRE(q.x && q.dy && q.dw && q.in_f > 0 && q.in_f % 32 == 0 && q.out_f > 0,
+                   "linear_wgrad_rowscale_multi: layer %d (in_f %d, out_f %d)", i, q.in_f,
+                   q.out_f);
+        LinWgLayer& L = set.l[i];
+        L.x = q.x; L.x_cs = q.x_cs; L.dy = q.dy; L.dy_cs = q.dy_cs;
+        L.dw = q.dw; L.dw_cs = q.dw_cs; L.db = q.db; L.db_cs = q.db_cs;
+        L.K = q.in_f; L.M = q.out_f;
+        L.gx = (int)ceil_div(q.in_f, 128);
+        L.gy = (int)ceil_div(q.out_f, 32);
+        const int64_t nb = (int64_t)L.gx * L.gy * nclients;
+        FH_REQUIRE(nb < (1ll << 30), "linear_wgrad_rowscale_multi: grid");
+        L.nblk = (int)nb;
+        total += nb;
+    }
+    FH_REQUIRE(total < (1ll << 31), "linear_wgrad_rowscale_multi: grid");
+    FH_LAUNCH(linear_wgrad_skinny_multi_kernel, dim3((unsigned)total), dim3(256), 0,
+              as_stream(stream), set, counts, batch, rowscale);
+    FH_LAUNCH_CHECK("linear_wgrad_rowscale_multi");
     return FH_OK;
 }
 

@@ -131,6 +131,7 @@ SIGNATURES = {
     "fh_conv2d_c1_pool_wgrad_persample": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P, I32,
                                                 I32, I32, I32, I32, I32, I32, P]),
     "fh_persample_slab_sqnorm": (I32, [P, I32, I32, P, I32, I32, P, P]),
+    "fh_linear_wgrad_rowscale_multi": (I32, [P, I32, P, P, I32, I32, P]),
     "fh_linear_wgrad_rowscale": (I32, [P, I64, P, I64, P, P, I64, P, I64, P, I32, I32, I32, I32,
                                        P]),
     "fh_dpsgd_norm_clip": (I32, [P, I32, P, I32, P, I32, I32, F64, P, P, P]),

@@ -203,6 +203,9 @@ class PackedNet:
         # both roles read the pooled gradient, argmax and pooled ReLU output on load; the 16x16
         # gradient da2 is never written and the maxpool2_bwd launch is gone)
         self.pooled_dy_bwd = True
+        # DP-SGD pass 2: fc1's and fc2's row-scaled weight gradients as one launch
+        # (fh_linear_wgrad_rowscale_multi, r05)
+        self.lin_wgrad_multi = True
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -468,11 +471,18 @@ class PackedNet:
         # every image's norm over all four layers and its clip coefficient: one launch
         ops.dpsgd_norm_clip([(self._fc_in, self.dlogits, 128, K), (p2, dh1, 3136, 128)],
                             [s2, s1], coef, n, B, max_norm, sqnorm=sqnorm, counts=cnt)
-        # pass 2: the linear layers' clipped sums (dY rows scaled by c_i as they are loaded)
-        ops.linear_wgrad_rowscale(self._fc_in, self.dlogits, coef, W(G, "fc2.weight"),
-                                  W(G, "fc2.bias"), n, B, 128, K, counts=cnt)
-        ops.linear_wgrad_rowscale(p2, dh1, coef, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B, 3136,
-                                  128, counts=cnt)
+        # pass 2: the linear layers' clipped sums (dY rows scaled by c_i as they are loaded),
+        # fc1's and fc2's in one launch (r05)
+        if self.lin_wgrad_multi:
+            ops.linear_wgrad_rowscale_multi(
+                [(p2, dh1, W(G, "fc1.weight"), W(G, "fc1.bias"), 3136, 128),
+                 (self._fc_in, self.dlogits, W(G, "fc2.weight"), W(G, "fc2.bias"), 128, K)],
+                coef, n, B, counts=cnt)
+        else:
+            ops.linear_wgrad_rowscale(self._fc_in, self.dlogits, coef, W(G, "fc2.weight"),
+                                      W(G, "fc2.bias"), n, B, 128, K, counts=cnt)
+            ops.linear_wgrad_rowscale(p2, dh1, coef, W(G, "fc1.weight"), W(G, "fc1.bias"), n, B,
+                                      3136, 128, counts=cnt)
         return s1.ranges(G, W(G, "conv1.weight"), W(G, "conv1.bias")) + \
             s2.ranges(G, W(G, "conv2.weight"), W(G, "conv2.bias"))
 

@@ -940,6 +940,28 @@ def linear_wgrad_rowscale(x, dy, rowscale, dw, db, nclients, batch, in_f, out_f,
               _linear_bytes(nclients, batch, in_f, out_f), nclients)
 
 
+class FhLinearWgradSrc(ctypes.Structure):
+    """include/fedhip.h fh_linear_wgrad_src."""
+    _fields_ = [("x", ctypes.c_void_p), ("x_cs", ctypes.c_int64), ("dy", ctypes.c_void_p),
+                ("dy_cs", ctypes.c_int64), ("dw", ctypes.c_void_p), ("dw_cs", ctypes.c_int64),
+                ("db", ctypes.c_void_p), ("db_cs", ctypes.c_int64), ("in_f", ctypes.c_int32),
+                ("out_f", ctypes.c_int32)]
+
+
+def linear_wgrad_rowscale_multi(layers, rowscale, nclients, batch, counts=None):
+    """Several layers' linear_wgrad_rowscale in one launch (fh_linear_wgrad_rowscale_multi):
+    layers = [(x, dy, dw, db, in_f, out_f)], the same row scales / counts / batch."""
+    evs = [PROBE.begin(f"linear_wgrad:{l[4]}->{l[5]}") for l in layers[:1]]
+    arr = (FhLinearWgradSrc * len(layers))()
+    for i, (x, dy, dw, db, in_f, out_f) in enumerate(layers):
+        arr[i] = FhLinearWgradSrc(ptr(x), _cs(x), ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db),
+                                  _cs(db), in_f, out_f)
+    call("fh_linear_wgrad_rowscale_multi", arr, len(layers), ptr(rowscale), _counts(counts),
+         nclients, batch, stream_handle())
+    PROBE.end(evs[0], sum(2.0 * nclients * batch * l[4] * l[5] for l in layers),
+              sum(_linear_bytes(nclients, batch, l[4], l[5]) for l in layers), nclients)
+
+
 class FhLinearNormSrc(ctypes.Structure):
     """include/fedhip.h fh_linear_norm_src."""
     _fields_ = [("x", ctypes.c_void_p), ("x_cs", ctypes.c_int64), ("dy", ctypes.c_void_p),

@@ -173,6 +173,23 @@ int fh_linear_wgrad_rowscale(const float* x, int64_t x_cs, const float* dy, int6
                              const float* rowscale, float* dw, int64_t dw_cs, float* db,
                              int64_t db_cs, const int32_t* counts, int32_t nclients,
                              int32_t batch, int32_t in_f, int32_t out_f, void* stream);
+/* Up to four linear layers' fh_linear_wgrad_rowscale in ONE launch (the same row scales,
+ * counts and batch; each layer's tiles, order and bits as its own call): DP-SGD's pass 2 runs
+ * fc2's and fc1's clipped sums as one launch (r05).  batch <= 32, in_f % 32 == 0 per layer. */
+typedef struct fh_linear_wgrad_src {
+    const float* x;
+    int64_t x_cs;
+    const float* dy;
+    int64_t dy_cs;
+    float* dw;
+    int64_t dw_cs;
+    float* db;      /* nullable */
+    int64_t db_cs;
+    int32_t in_f, out_f;
+} fh_linear_wgrad_src;
+int fh_linear_wgrad_rowscale_multi(const fh_linear_wgrad_src* layers, int32_t nlayers,
+                                   const float* rowscale, const int32_t* counts,
+                                   int32_t nclients, int32_t batch, void* stream);
 int fh_dpsgd_step_slabs(float* param, float* grad, float* state1, float* state2,
                         int64_t row_stride, int64_t row_len, int32_t nclients,
                         const fh_grad_slab* slabs, int32_t nslabs, const float* coef,

@@ -331,3 +331,42 @@ def test_dpsgd_dual_pooled_bit_identical(seed_cfg):
     for e in out[1:]:
         assert torch.equal(out[0].params, e.params)
         assert torch.equal(out[0].state1, e.state1)
+
+
+def test_linear_wgrad_rowscale_multi_bit_identical():
+    """fh_linear_wgrad_rowscale_multi (r05) == one fh_linear_wgrad_rowscale per layer, bit for
+    bit (ragged counts, with and without bias), and DP-SGD steps with it == without it."""
+    from fedhip import ops
+    g = torch.Generator().manual_seed(21)
+    C, B = 3, 32
+    cd = torch.tensor([32, 17, 1], dtype=torch.int32, device=DEV)
+    coef = torch.rand(C, B, generator=g).to(DEV)
+    shapes = [(3136, 128, True), (128, 10, True), (256, 64, False)]
+    ins = [(torch.randn(C, B, fi, generator=g).to(DEV), torch.randn(C, B, fo, generator=g).to(DEV))
+           for fi, fo, _ in shapes]
+    outs = []
+    for multi in (True, False):
+        dws = [torch.zeros(C, fo, fi, device=DEV) for fi, fo, _ in shapes]
+        dbs = [torch.zeros(C, fo, device=DEV) if bias else None for fi, fo, bias in shapes]
+        if multi:
+            ops.linear_wgrad_rowscale_multi(
+                [(x, dy, dw, db, fi, fo) for (x, dy), dw, db, (fi, fo, _) in
+                 zip(ins, dws, dbs, shapes)], coef, C, B, counts=cd)
+        else:
+            for (x, dy), dw, db, (fi, fo, _) in zip(ins, dws, dbs, shapes):
+                ops.linear_wgrad_rowscale(x, dy, coef, dw, db, C, B, fi, fo, counts=cd)
+        torch.cuda.synchronize()
+        outs.append((dws, dbs))
+    for a, b in zip(outs[0][0] + outs[0][1], outs[1][0] + outs[1][1]):
+        assert (a is None and b is None) or torch.equal(a, b)
+    sizes = [32, 32, 17, 5]
+    counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
+    engs = []
+    for multi in (True, False):
+        eng, _, _ = _engine(sizes, DPSGDConfig(max_grad_norm=0.5, noise_multiplier=0.7, seed=4))
+        eng.net.lin_wgrad_multi = multi
+        for _ in range(2):
+            eng.step(2, counts)
+        torch.cuda.synchronize()
+        engs.append(eng)
+    assert torch.equal(engs[0].params, engs[1].params)
