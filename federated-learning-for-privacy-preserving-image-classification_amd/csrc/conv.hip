@@ -1017,13 +1017,97 @@ conv_c1_wgrad_kernel(const float* __restrict__ x, int64_t x_cs, const float* __r
 // there is > 0, else 0 — per staged quad two pooled values, two argmax bytes, two yp values.
 // The same fp32 values reach the same MFMA chain, so the result equals the unfused pair
 // (maxpool2_bwd_ymask + this kernel on its output) bit for bit.
-template <int COUT, bool POOLED, int NS = 2>
+constexpr int kNormSrcMax = 4;
+struct NormSrcs {
+    fh_linear_norm_src lin[kNormSrcMax];
+    int nlin;
+    const float* sw[kNormSrcMax];  // slab weights [z][i][per_w]
+    const float* sb[kNormSrcMax];  // slab bias [z][i][per_b] (nullable)
+    int per_w[kNormSrcMax], per_b[kNormSrcMax];
+    int nslab;
+};
+
+// Image i of client z: its squared gradient norm over every layer — linear layers by the rank-1
+// identity ||dy_i||^2 (||x_i||^2 + bias), conv layers as the sum of squares of the image's slab
+// rows — in fp64, then its clip coefficient (clip_coef_kernel's arithmetic).  The body of
+// dpsgd_norm_clip_kernel (one workgroup per (image, client)) and, r05, the tail of the per-image
+// conv1 slab launch (conv_c1_wgrad_mfma_kernel<..., NORM>), which runs the same code on the same
+// grid after its own slab row is written: the same sums, one launch less per DP-SGD step.
+__device__ __forceinline__ void dpsgd_norm_clip_body(const NormSrcs& src, int cnt, int batch,
+                                                     double max_norm, double* __restrict__ sqnorm,
+                                                     float* __restrict__ coef, int i, int z,
+                                                     double* red) {
+    const int64_t row = (int64_t)z * batch + i;
+    if (i >= cnt) {  // block-uniform
+        if (threadIdx.x == 0) {
+            coef[row] = 0.f;
+            if (sqnorm) sqnorm[row] = 0.0;
+        }
+        return;
+    }
+    double total = 0.0;
+    for (int l = 0; l < src.nlin; ++l) {
+        const fh_linear_norm_src& L = src.lin[l];
+        const float* xr = L.x + z * L.x_cs + (int64_t)i * L.in_f;
+        const float* dr = L.dy + z * L.dy_cs + (int64_t)i * L.out_f;
+        double sx = 0.0, sd = 0.0;
+        // unrolled loops keep each thread's order (the same sums) with several loads in flight
+#pragma unroll 4
+        for (int k = threadIdx.x; k < L.in_f; k += 256) sx += (double)xr[k] * (double)xr[k];
+#pragma unroll 4
+        for (int k = threadIdx.x; k < L.out_f; k += 256) sd += (double)dr[k] * (double)dr[k];
+        sx = block_sum_256(sx, red);
+        sd = block_sum_256(sd, red);
+        total += sd * (sx + (L.with_bias ? 1.0 : 0.0));
+    }
+    for (int l = 0; l < src.nslab; ++l) {
+        const float4* w4 = reinterpret_cast<const float4*>(src.sw[l] + row * src.per_w[l]);
+        double sq = 0.0;
+#pragma unroll 4
+        for (int q = threadIdx.x; q < src.per_w[l] / 4; q += 256) {
+            const float4 v = w4[q];
+            sq += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+        }
+        if (src.sb[l])
+            for (int q = threadIdx.x; q < src.per_b[l]; q += 256) {
+                const double v = src.sb[l][row * src.per_b[l] + q];
+                sq += v * v;
+            }
+        total += block_sum_256(sq, red);
+    }
+    if (threadIdx.x == 0) {
+        if (sqnorm) sqnorm[row] = total;
+        // ||g_i|| = B * ||g_i / B||  (the stored gradients are of the batch-mean loss)
+        const double norm = (double)cnt * sqrt(total);
+        coef[row] = norm > max_norm ? (float)(max_norm / norm) : 1.0f;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+dpsgd_norm_clip_kernel(const NormSrcs src, const int32_t* __restrict__ counts, int batch,
+                       double max_norm, double* __restrict__ sqnorm, float* __restrict__ coef) {
+    __shared__ double red[4];
+    const int i = blockIdx.x, z = blockIdx.y;
+    const int cnt = counts ? counts[z] : batch;
+    dpsgd_norm_clip_body(src, cnt, batch, max_norm, sqnorm, coef, i, z, red);
+}
+
+// the norm / clip tail of the per-image conv1 slab launch (NORM instances)
+struct NormTail {
+    NormSrcs src;
+    double max_norm;
+    double* sqnorm;
+    float* coef;
+};
+
+template <int COUT, bool POOLED, int NS = 2, bool NORM = false>
 __global__ void __launch_bounds__(256)
 conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ dy,
                           int64_t dy_cs, float* __restrict__ part, float* __restrict__ bpart,
                           const int32_t* __restrict__ counts, int batch, int H, int W,
                           int nsplits, int sps, const uint8_t* __restrict__ pidx, int64_t pi_cs,
-                          const float* __restrict__ yp, int64_t yp_cs, int gh, int gw) {
+                          const float* __restrict__ yp, int64_t yp_cs, int gh, int gw,
+                          const NormTail tail) {
     constexpr int NQ = COUT / 16;     // 16-channel groups
     constexpr int MAXW = 32;
     constexpr int DP = 4 * MAXW + 2;  // dY pitch per channel (4 rows), = 2 (mod 4)
@@ -1170,6 +1254,16 @@ conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float
         const int co = e / 10, k = e % 10;
         if (k < 9) part[slab * COUT * 9 + co * 9 + k] = v;
         else if (bpart) bpart[slab * COUT + co] = v;
+    }
+    if constexpr (NORM) {
+        // one split = one image (the per-image launch): its slab row is written above; after
+        // a workgroup-scope release / barrier every thread reads it back with the other layers'
+        // sources (written by earlier launches) for the image's norm and clip coefficient
+        __shared__ double nred[4];
+        __threadfence_block();
+        __syncthreads();
+        dpsgd_norm_clip_body(tail.src, cnt, nsplits, tail.max_norm, tail.sqnorm, tail.coef,
+                             split, z, nred);
     }
 }
 
@@ -2383,11 +2477,11 @@ static int c1_pool_wgrad_impl(const float* x, int64_t x_cs, const float* dpool, 
         if (cout == 32)
             FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
                       dp_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps, idx, i_cs, y,
-                      y_cs, gh, gw);
+                      y_cs, gh, gw, NormTail{});
         else
             FH_LAUNCH((conv_c1_wgrad_mfma_kernel<64, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
                       dp_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps, idx, i_cs, y,
-                      y_cs, gh, gw);
+                      y_cs, gh, gw, NormTail{});
         FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad mfma");
         if (defer_splits) {  // the optimizer step sums the chunks (fh_sgd_step_slabs)
             *defer_splits = p.splits;
@@ -2523,11 +2617,13 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
         if (cout == 32)
             FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, false>), grid, dim3(256), 0, st, x, x_cs, dy,
                       dy_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps,
-                      (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0);
+                      (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0,
+                      NormTail{});
         else
             FH_LAUNCH((conv_c1_wgrad_mfma_kernel<64, false>), grid, dim3(256), 0, st, x, x_cs, dy,
                       dy_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps,
-                      (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0);
+                      (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0,
+                      NormTail{});
         FH_LAUNCH_CHECK("conv2d_wgrad c1 mfma");
         if (defer_splits) {
             *defer_splits = p.splits;
@@ -3725,13 +3821,11 @@ extern "C" int fh_conv2d_wgrad_persample(const float* x, int64_t x_cs, const flo
     return FH_OK;
 }
 
-extern "C" int fh_conv2d_c1_pool_wgrad_persample(const float* x, int64_t x_cs, const float* dpool,
-                                                 int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
-                                                 const float* y, int64_t y_cs, void* slab,
-                                                 size_t slab_bytes, const int32_t* counts,
-                                                 int32_t nclients, int32_t batch, int32_t h,
-                                                 int32_t w_, int32_t cout, int32_t gh, int32_t gw,
-                                                 void* stream) {
+static int c1_persample_impl(const float* x, int64_t x_cs, const float* dpool, int64_t dp_cs,
+                             const uint8_t* idx, int64_t i_cs, const float* y, int64_t y_cs,
+                             void* slab, size_t slab_bytes, const int32_t* counts,
+                             int32_t nclients, int32_t batch, int32_t h, int32_t w_, int32_t cout,
+                             int32_t gh, int32_t gw, const NormTail* tail, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && h % 4 == 0 && w_ % 4 == 0 && w_ <= 32 &&
                gh >= h / 2 && gw >= w_ / 2, "conv2d_c1_pool_wgrad_persample: bad shape");
     FH_REQUIRE(cout == 32 || cout == 64, "conv2d_c1_pool_wgrad_persample: cout %d (32 or 64)", cout);
@@ -3749,98 +3843,41 @@ extern "C" int fh_conv2d_c1_pool_wgrad_persample(const float* x, int64_t x_cs, c
     hipStream_t st = as_stream(stream);
     // narrow grids (fewer image workgroups than ~two per CU): four stages per LDS round
     const bool wide4 = (int64_t)batch * nclients <= kC1PersampleNs4Max;
-    if (cout == 32 && wide4)
-        FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true, 4>), grid, dim3(256), 0, st, x, x_cs, dpool,
-                  dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, gw);
-    else if (cout == 32)
-        FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
-                  dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, gw);
-    else
-        FH_LAUNCH((conv_c1_wgrad_mfma_kernel<64, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
-                  dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, gw);
+    const NormTail t = tail ? *tail : NormTail{};
+#define FH_C1PS(CO, NS, NORM)                                                                    \
+    FH_LAUNCH((conv_c1_wgrad_mfma_kernel<CO, true, NS, NORM>), grid, dim3(256), 0, st, x, x_cs,  \
+              dpool, dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, \
+              gw, t)
+    if (tail) {
+        FH_REQUIRE(cout == 32, "conv2d_c1_pool_wgrad_persample_clip: cout 32 (got %d)", cout);
+        if (wide4) FH_C1PS(32, 4, true); else FH_C1PS(32, 2, true);
+    } else if (cout == 32) {
+        if (wide4) FH_C1PS(32, 4, false); else FH_C1PS(32, 2, false);
+    } else {
+        FH_C1PS(64, 2, false);
+    }
+#undef FH_C1PS
     FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad_persample");
     return FH_OK;
 }
 
-namespace fh {
-constexpr int kNormSrcMax = 4;
-struct NormSrcs {
-    fh_linear_norm_src lin[kNormSrcMax];
-    int nlin;
-    const float* sw[kNormSrcMax];  // slab weights [z][i][per_w]
-    const float* sb[kNormSrcMax];  // slab bias [z][i][per_b] (nullable)
-    int per_w[kNormSrcMax], per_b[kNormSrcMax];
-    int nslab;
-};
-
-// One workgroup per (image, client): the image's squared gradient norm over every layer —
-// linear layers by the rank-1 identity ||dy_i||^2 (||x_i||^2 + bias), conv layers as the sum
-// of squares of the image's slab rows — in fp64, then its clip coefficient (clip_coef_kernel's
-// arithmetic).  Replaces the zero fill, the per-layer norm launches and the coefficient launch.
-__global__ void __launch_bounds__(256)
-dpsgd_norm_clip_kernel(const NormSrcs src, const int32_t* __restrict__ counts, int batch,
-                       double max_norm, double* __restrict__ sqnorm, float* __restrict__ coef) {
-    __shared__ double red[4];
-    const int i = blockIdx.x, z = blockIdx.y;
-    const int cnt = counts ? counts[z] : batch;
-    const int64_t row = (int64_t)z * batch + i;
-    if (i >= cnt) {  // block-uniform
-        if (threadIdx.x == 0) {
-            coef[row] = 0.f;
-            if (sqnorm) sqnorm[row] = 0.0;
-        }
-        return;
-    }
-    double total = 0.0;
-    for (int l = 0; l < src.nlin; ++l) {
-        const fh_linear_norm_src& L = src.lin[l];
-        const float* xr = L.x + z * L.x_cs + (int64_t)i * L.in_f;
-        const float* dr = L.dy + z * L.dy_cs + (int64_t)i * L.out_f;
-        double sx = 0.0, sd = 0.0;
-        // unrolled loops keep each thread's order (the same sums) with several loads in flight
-#pragma unroll 4
-        for (int k = threadIdx.x; k < L.in_f; k += 256) sx += (double)xr[k] * (double)xr[k];
-#pragma unroll 4
-        for (int k = threadIdx.x; k < L.out_f; k += 256) sd += (double)dr[k] * (double)dr[k];
-        sx = block_sum_256(sx, red);
-        sd = block_sum_256(sd, red);
-        total += sd * (sx + (L.with_bias ? 1.0 : 0.0));
-    }
-    for (int l = 0; l < src.nslab; ++l) {
-        const float4* w4 = reinterpret_cast<const float4*>(src.sw[l] + row * src.per_w[l]);
-        double sq = 0.0;
-#pragma unroll 4
-        for (int q = threadIdx.x; q < src.per_w[l] / 4; q += 256) {
-            const float4 v = w4[q];
-            sq += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
-        }
-        if (src.sb[l])
-            for (int q = threadIdx.x; q < src.per_b[l]; q += 256) {
-                const double v = src.sb[l][row * src.per_b[l] + q];
-                sq += v * v;
-            }
-        total += block_sum_256(sq, red);
-    }
-    if (threadIdx.x == 0) {
-        if (sqnorm) sqnorm[row] = total;
-        // ||g_i|| = B * ||g_i / B||  (the stored gradients are of the batch-mean loss)
-        const double norm = (double)cnt * sqrt(total);
-        coef[row] = norm > max_norm ? (float)(max_norm / norm) : 1.0f;
-    }
+extern "C" int fh_conv2d_c1_pool_wgrad_persample(const float* x, int64_t x_cs, const float* dpool,
+                                                 int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
+                                                 const float* y, int64_t y_cs, void* slab,
+                                                 size_t slab_bytes, const int32_t* counts,
+                                                 int32_t nclients, int32_t batch, int32_t h,
+                                                 int32_t w_, int32_t cout, int32_t gh, int32_t gw,
+                                                 void* stream) {
+    return c1_persample_impl(x, x_cs, dpool, dp_cs, idx, i_cs, y, y_cs, slab, slab_bytes, counts,
+                             nclients, batch, h, w_, cout, gh, gw, nullptr, stream);
 }
-}  // namespace fh
 
-extern "C" int fh_dpsgd_norm_clip(const fh_linear_norm_src* lin, int32_t nlin,
-                                  const fh_slab_norm_src* slabs, int32_t nslab,
-                                  const int32_t* counts, int32_t nclients, int32_t batch,
-                                  double max_norm, double* sqnorm, float* coef, void* stream) {
-    FH_REQUIRE(nclients >= 0 && batch > 0 && nlin >= 0 && nlin <= kNormSrcMax && nslab >= 0 &&
-                   nslab <= kNormSrcMax, "dpsgd_norm_clip: bad shape (%d linear, %d slab sources)",
-               nlin, nslab);
-    FH_REQUIRE(max_norm > 0.0, "dpsgd_norm_clip: max_norm must be > 0");
-    if (nclients == 0) return FH_OK;
-    FH_REQUIRE(coef && (nlin == 0 || lin) && (nslab == 0 || slabs), "dpsgd_norm_clip: null pointer");
-    NormSrcs s{};
+static int norm_srcs(const fh_linear_norm_src* lin, int32_t nlin, const fh_slab_norm_src* slabs,
+                     int32_t nslab, int32_t nclients, int32_t batch, NormSrcs& s) {
+    FH_REQUIRE(nlin >= 0 && nlin <= kNormSrcMax && nslab >= 0 && nslab <= kNormSrcMax,
+               "dpsgd_norm_clip: bad shape (%d linear, %d slab sources)", nlin, nslab);
+    FH_REQUIRE((nlin == 0 || lin) && (nslab == 0 || slabs), "dpsgd_norm_clip: null pointer");
+    s = NormSrcs{};
     s.nlin = nlin;
     for (int l = 0; l < nlin; ++l) {
         FH_REQUIRE(lin[l].x && lin[l].dy && lin[l].in_f > 0 && lin[l].out_f > 0,
@@ -3859,10 +3896,51 @@ extern "C" int fh_dpsgd_norm_clip(const fh_linear_norm_src* lin, int32_t nlin,
         s.per_w[l] = slabs[l].per_w;
         s.per_b[l] = slabs[l].per_b;
     }
+    return FH_OK;
+}
+
+extern "C" int fh_dpsgd_norm_clip(const fh_linear_norm_src* lin, int32_t nlin,
+                                  const fh_slab_norm_src* slabs, int32_t nslab,
+                                  const int32_t* counts, int32_t nclients, int32_t batch,
+                                  double max_norm, double* sqnorm, float* coef, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0, "dpsgd_norm_clip: bad shape");
+    FH_REQUIRE(max_norm > 0.0, "dpsgd_norm_clip: max_norm must be > 0");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(coef, "dpsgd_norm_clip: null pointer");
+    NormSrcs s;
+    if (const int rc = norm_srcs(lin, nlin, slabs, nslab, nclients, batch, s)) return rc;
     FH_LAUNCH(dpsgd_norm_clip_kernel, dim3((unsigned)batch, (unsigned)nclients), dim3(256), 0,
               as_stream(stream), s, counts, batch, max_norm, sqnorm, coef);
     FH_LAUNCH_CHECK("dpsgd_norm_clip");
     return FH_OK;
+}
+
+// fh_conv2d_c1_pool_wgrad_persample + fh_dpsgd_norm_clip in ONE launch (r05): the per-image
+// conv1 slab workgroup (one per image and client, the norm launch's grid) finishes with the
+// image's norm over the given sources — which must include this launch's own slab — and its
+// clip coefficient, the same code and sums as fh_dpsgd_norm_clip.  cout 32.
+extern "C" int fh_conv2d_c1_pool_wgrad_persample_clip(
+        const float* x, int64_t x_cs, const float* dpool, int64_t dp_cs, const uint8_t* idx,
+        int64_t i_cs, const float* y, int64_t y_cs, void* slab, size_t slab_bytes,
+        const int32_t* counts, int32_t nclients, int32_t batch, int32_t h, int32_t w_,
+        int32_t cout, int32_t gh, int32_t gw, const fh_linear_norm_src* lin, int32_t nlin,
+        const fh_slab_norm_src* slabs, int32_t nslab, double max_norm, double* sqnorm,
+        float* coef, void* stream) {
+    FH_REQUIRE(nclients >= 0 && batch > 0, "conv2d_c1_pool_wgrad_persample_clip: bad shape");
+    FH_REQUIRE(max_norm > 0.0, "conv2d_c1_pool_wgrad_persample_clip: max_norm must be > 0");
+    if (nclients == 0) return FH_OK;
+    FH_REQUIRE(coef, "conv2d_c1_pool_wgrad_persample_clip: null pointer");
+    bool own = false;
+    for (int l = 0; l < nslab && slabs; ++l) own = own || slabs[l].slab == slab;
+    FH_REQUIRE(own, "conv2d_c1_pool_wgrad_persample_clip: the slab sources must include this "
+                    "launch's own slab");
+    NormTail t{};
+    if (const int rc = norm_srcs(lin, nlin, slabs, nslab, nclients, batch, t.src)) return rc;
+    t.max_norm = max_norm;
+    t.sqnorm = sqnorm;
+    t.coef = coef;
+    return c1_persample_impl(x, x_cs, dpool, dp_cs, idx, i_cs, y, y_cs, slab, slab_bytes, counts,
+                             nclients, batch, h, w_, cout, gh, gw, &t, stream);
 }
 
 extern "C" int fh_persample_slab_sqnorm(const void* slab, int32_t per_w, int32_t per_b,

@@ -135,6 +135,9 @@ SIGNATURES = {
     "fh_linear_wgrad_rowscale": (I32, [P, I64, P, I64, P, P, I64, P, I64, P, I32, I32, I32, I32,
                                        P]),
     "fh_dpsgd_norm_clip": (I32, [P, I32, P, I32, P, I32, I32, F64, P, P, P]),
+    "fh_conv2d_c1_pool_wgrad_persample_clip": (I32, [P, I64, P, I64, P, I64, P, I64, P, SZ, P,
+                                                     I32, I32, I32, I32, I32, I32, I32, P, I32,
+                                                     P, I32, F64, P, P, P]),
     "fh_dpsgd_step_slabs": (I32, [P, P, P, P, I64, I64, I32, P, I32, P, P, I32, I64, F32, U64, P,
                                   I32, F64, F64, F64, F64, F64, F64, I32, I32, F64, F64, P, P]),
     "fh_persample_slab_wsum": (I32, [P, I32, I32, P, P, I32, I32, P, I64, P, I64, P]),

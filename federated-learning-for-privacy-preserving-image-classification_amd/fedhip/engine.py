@@ -301,6 +301,8 @@ class PackedTrainer:
     # ------------------------------------------------------------ one packed step
     def step(self, n, counts, reset=None):
         """fwd + CE + bwd + optimizer for slots [0, n) on the batch in net.x / net.y."""
+        if not 0 <= n <= self.capacity:  # every buffer holds `capacity` slots: never launch past
+            raise FedHipError(f"step: {n} active slots on a trainer of {self.capacity}")
         self.opt_step += 1
         self._step_launches(n, counts, reset, first=(self.opt_step == 1))
         self._after_step(n)

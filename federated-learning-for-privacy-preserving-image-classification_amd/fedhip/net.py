@@ -206,6 +206,9 @@ class PackedNet:
         # DP-SGD pass 2: fc1's and fc2's row-scaled weight gradients as one launch
         # (fh_linear_wgrad_rowscale_multi, r05)
         self.lin_wgrad_multi = True
+        # ... and conv1's per-image slabs with every image's norm / clip coefficient as one
+        # launch (fh_conv2d_c1_pool_wgrad_persample_clip, r05)
+        self.c1_norm_fused = True
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -465,12 +468,18 @@ class PackedNet:
                          counts=cnt, alg_hw=14)
         ops.conv_pair(0)
         # conv1's per-image slabs from pool1's gradient (the pooled ReLU output p1 > 0 is the
-        # mask at each window's argmax, whether or not conv1's output was written)
-        ops.conv2d_c1_pool_wgrad_persample(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8),
-                                           p1, s1, n, B, 28, 28, 32, counts=cnt)
-        # every image's norm over all four layers and its clip coefficient: one launch
-        ops.dpsgd_norm_clip([(self._fc_in, self.dlogits, 128, K), (p2, dh1, 3136, 128)],
-                            [s2, s1], coef, n, B, max_norm, sqnorm=sqnorm, counts=cnt)
+        # mask at each window's argmax, whether or not conv1's output was written), and every
+        # image's norm over all four layers with its clip coefficient — r05: in the same launch
+        i1 = A("i1", 32, 14, 14, dtype=torch.uint8)
+        lin = [(self._fc_in, self.dlogits, 128, K), (p2, dh1, 3136, 128)]
+        if self.c1_norm_fused:
+            ops.conv2d_c1_pool_wgrad_persample_clip(self.x, dp1, i1, p1, s1, n, B, 28, 28, 32, lin,
+                                                    [s2, s1], coef, max_norm, sqnorm=sqnorm,
+                                                    counts=cnt)
+        else:
+            ops.conv2d_c1_pool_wgrad_persample(self.x, dp1, i1, p1, s1, n, B, 28, 28, 32,
+                                               counts=cnt)
+            ops.dpsgd_norm_clip(lin, [s2, s1], coef, n, B, max_norm, sqnorm=sqnorm, counts=cnt)
         # pass 2: the linear layers' clipped sums (dY rows scaled by c_i as they are loaded),
         # fc1's and fc2's in one launch (r05)
         if self.lin_wgrad_multi:

@@ -917,6 +917,23 @@ def conv2d_c1_pool_wgrad_persample(x, dpool, idx, y, slab, nclients, batch, h, w
               4.0 * nclients * batch * (h * wd + cout * 10) + 9.0 * pooled, nclients)
 
 
+def conv2d_c1_pool_wgrad_persample_clip(x, dpool, idx, y, slab, nclients, batch, h, wd, cout,
+                                        linear, slabs, coef, max_norm, sqnorm=None, counts=None):
+    """conv2d_c1_pool_wgrad_persample + dpsgd_norm_clip in one launch
+    (fh_conv2d_c1_pool_wgrad_persample_clip): `slabs` must include `slab` itself."""
+    nb = slab.ensure(nclients, batch, 1, cout)
+    gh, gw = dpool.shape[-2], dpool.shape[-1]
+    la, sa = _norm_sources(linear, slabs)
+    ev = PROBE.begin(_conv_tag("pswgrad", 1, h, wd, cout, 3, 1) + "+pool")
+    call("fh_conv2d_c1_pool_wgrad_persample_clip", ptr(x), _cs(x), ptr(dpool), _cs(dpool),
+         ptr(idx), _cs(idx), ptr(y), _cs(y), ptr(slab.buf), nb, _counts(counts), nclients, batch,
+         h, wd, cout, gh, gw, la, len(linear), sa, len(slabs), float(max_norm), ptr(sqnorm),
+         ptr(coef), stream_handle())
+    pooled = nclients * batch * cout * (h // 2) * (wd // 2)
+    PROBE.end(ev, _conv_flops(nclients, batch, 1, h, wd, cout, 3, 1, 1),
+              4.0 * nclients * batch * (h * wd + cout * 10) + 9.0 * pooled, nclients)
+
+
 def slab_sqnorm(slab, sqnorm, counts=None):
     """sqnorm[z][i] += ||slab row (z, i)||^2 (weights + bias, fp64)."""
     call("fh_persample_slab_sqnorm", ptr(slab.buf), slab.per_w, slab.per_b, _counts(counts),
@@ -974,10 +991,7 @@ class FhSlabNormSrc(ctypes.Structure):
     _fields_ = [("slab", ctypes.c_void_p), ("per_w", ctypes.c_int32), ("per_b", ctypes.c_int32)]
 
 
-def dpsgd_norm_clip(linear, slabs, coef, nclients, batch, max_norm, sqnorm=None, counts=None):
-    """fh_dpsgd_norm_clip: every image's squared gradient norm over the linear sources
-    [(x, dy, in_f, out_f)] (rank-1 identity, with bias) and the PersampleSlab sources, and its
-    clip coefficient, in one launch."""
+def _norm_sources(linear, slabs):
     la = (FhLinearNormSrc * max(1, len(linear)))()
     for i, (x, dy, fi, fo) in enumerate(linear):
         la[i].x, la[i].x_cs, la[i].dy, la[i].dy_cs = ptr(x), _cs(x), ptr(dy), _cs(dy)
@@ -985,6 +999,14 @@ def dpsgd_norm_clip(linear, slabs, coef, nclients, batch, max_norm, sqnorm=None,
     sa = (FhSlabNormSrc * max(1, len(slabs)))()
     for i, s in enumerate(slabs):
         sa[i].slab, sa[i].per_w, sa[i].per_b = s.buf.data_ptr(), s.per_w, s.per_b
+    return la, sa
+
+
+def dpsgd_norm_clip(linear, slabs, coef, nclients, batch, max_norm, sqnorm=None, counts=None):
+    """fh_dpsgd_norm_clip: every image's squared gradient norm over the linear sources
+    [(x, dy, in_f, out_f)] (rank-1 identity, with bias) and the PersampleSlab sources, and its
+    clip coefficient, in one launch."""
+    la, sa = _norm_sources(linear, slabs)
     ev = PROBE.begin("dpsgd_norm_clip")
     call("fh_dpsgd_norm_clip", la, len(linear), sa, len(slabs), _counts(counts), nclients, batch,
          float(max_norm), ptr(sqnorm), ptr(coef), stream_handle())

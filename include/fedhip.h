@@ -166,6 +166,16 @@ typedef struct {
 int fh_dpsgd_norm_clip(const fh_linear_norm_src* lin, int32_t nlin, const fh_slab_norm_src* slabs,
                        int32_t nslab, const int32_t* counts, int32_t nclients, int32_t batch,
                        double max_norm, double* sqnorm, float* coef, void* stream);
+/* fh_conv2d_c1_pool_wgrad_persample + fh_dpsgd_norm_clip in ONE launch (r05): each per-image
+ * conv1 slab workgroup ends with the image's norm over the sources (which must include this
+ * launch's own slab) and its clip coefficient — fh_dpsgd_norm_clip's code and sums.  cout 32. */
+int fh_conv2d_c1_pool_wgrad_persample_clip(
+    const float* x, int64_t x_cs, const float* dpool, int64_t dp_cs, const uint8_t* idx,
+    int64_t i_cs, const float* y, int64_t y_cs, void* slab, size_t slab_bytes,
+    const int32_t* counts, int32_t nclients, int32_t batch, int32_t h, int32_t w, int32_t cout,
+    int32_t gh, int32_t gw, const fh_linear_norm_src* lin, int32_t nlin,
+    const fh_slab_norm_src* slabs, int32_t nslab, double max_norm, double* sqnorm, float* coef,
+    void* stream);
 /* fh_linear_wgrad on row-scaled dY: dy row b of client z multiplied by rowscale[z][b] as it is
  * loaded (the products fh_scale_rows would store: same bits as scale_rows + linear_wgrad);
  * DP-SGD's clipped linear-layer sums.  batch <= 32, in_f % 32 == 0. */

@@ -370,3 +370,21 @@ def test_linear_wgrad_rowscale_multi_bit_identical():
         torch.cuda.synchronize()
         engs.append(eng)
     assert torch.equal(engs[0].params, engs[1].params)
+
+
+@pytest.mark.parametrize("sizes", [[32, 32, 17, 5], [9]])
+def test_c1_slabs_with_norm_clip_bit_identical(sizes):
+    """fh_conv2d_c1_pool_wgrad_persample_clip (r05: the norm / clip launch folded into the
+    per-image conv1 slab launch) == the two launches: the same coefficients, squared norms and
+    DP-SGD steps, bit for bit (ragged counts, narrow and wide grids)."""
+    counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
+    engs = []
+    for fused in (True, False):
+        eng, _, _ = _engine(sizes, DPSGDConfig(max_grad_norm=0.3, noise_multiplier=0.6, seed=8))
+        eng.net.c1_norm_fused = fused
+        for _ in range(2):
+            eng.step(len(sizes), counts)
+        torch.cuda.synchronize()
+        engs.append(eng)
+    assert torch.equal(engs[0].params, engs[1].params)
+    assert torch.equal(engs[0].state1, engs[1].state1)

@@ -299,3 +299,12 @@ def test_every_ops_attribute_used_exists():
                     and node.value.id in ("ops", "_ops") and not hasattr(ops, node.attr)):
                 missing.add((os.path.basename(f), node.attr))
     assert not missing, sorted(missing)
+
+
+def test_step_refuses_more_slots_than_capacity():
+    """PackedTrainer.step raises before launching when n exceeds the trainer's slots (r05: a
+    test stepping 2 slots of a 1-slot trainer launched past every buffer)."""
+    import inspect
+    from fedhip import engine
+    src = inspect.getsource(engine.PackedTrainer.step)
+    assert "self.capacity" in src and "raise FedHipError" in src
