@@ -391,7 +391,20 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
         b_lane[j] = h * CSTR + (seg * PRS + S * lr) * PW + S * c;
     }
 
-    if (cbeg < cend) {
+    // r05: live map rows.  SimpleCNN's conv2 runs its 14x14 map on zero-ringed 16x16 planes;
+    // the pooled forward (pool_y set) and the pooled-dY DGRAD read / write only the map's rows,
+    // so the output block of rows 14-15 (the last 32-pixel block of a one-image W = 16 tile) is
+    // never read: the wave owning it skips that block's operand reads and MFMAs (its
+    // accumulator stays zero; every live block's MFMA chain is unchanged, the same bits).
+    int live_h = G::H;
+    if constexpr (W == 16 && S == 1 && G::NI == 1) {
+        if (OP == OP_FWD && a.pool_y != nullptr) live_h = a.pool_hw;
+        if constexpr (PDY) live_h = 2 * a.pdy.ph;
+    }
+    const bool skip_last = W == 16 && (wn * WN + (FN - 1) * 32) / W >= live_h;  // wave-uniform
+
+    auto kloop = [&](auto nl_c) {
+        constexpr int NL = decltype(nl_c)::value;  // live 32-pixel blocks of this wave
         load(cbeg);
         store(0, cbeg);
         __syncthreads();
@@ -415,7 +428,7 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
                     for (int i = 0; i < FM; ++i)
                         av[slot][i] = Ab[(kw * CK + 2 * cp) * BMP + i * 32];
 #pragma unroll
-                    for (int jj = 0; jj < FN; ++jj)
+                    for (int jj = 0; jj < NL; ++jj)
                         bv[slot][jj] = Pb[b_lane[jj] + 2 * cp * CSTR + kw];
                 };
                 fetch(0, 0);
@@ -425,20 +438,28 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
 #pragma unroll
                     for (int i = 0; i < FM; ++i)
 #pragma unroll
-                        for (int jj = 0; jj < FN; ++jj)
+                        for (int jj = 0; jj < NL; ++jj)
                             acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(
                                 av[j & 1][i], bv[j & 1][jj], acc[i][jj], 0, 0, 0);
                     // schedule: the next item's operand reads (DS read group), then this item's
                     // MFMAs — one group per item, so each wait covers only the reads issued an
                     // item earlier (r04: the compiler had paired items and waited on fresh reads;
                     // per launch 1-4 %, the 8x8 FWD at 23 clients 16 %, profiles/r04_h/)
-                    if (j + 1 < NI) __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, FM * FN, 0);
+                    if (j + 1 < NI) __builtin_amdgcn_sched_group_barrier(0x100, FM + NL, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, FM * NL, 0);
                 }
             }
             if (more) store(buf ^ 1, c0 + CK);
             __syncthreads();
             buf ^= 1;
+        }
+    };
+    if (cbeg < cend) {
+        if constexpr (W == 16 && FN > 1) {
+            if (skip_last) kloop(std::integral_constant<int, FN - 1>{});
+            else kloop(std::integral_constant<int, FN>{});
+        } else {
+            kloop(std::integral_constant<int, FN>{});
         }
     }
 
