@@ -1092,6 +1092,17 @@ dpsgd_norm_clip_kernel(const NormSrcs src, const int32_t* __restrict__ counts, i
     dpsgd_norm_clip_body(src, cnt, batch, max_norm, sqnorm, coef, i, z, red);
 }
 
+// a split DGRAD's partial slab read in place of its reduced output (fh_conv_defer_dgrad, r05):
+// element (img, c, y, x) of the dX planes (256-pixel planes) is
+// sum_s p[((z * splits + s) * M + c) * Nfull + img * 256 + y * 16 + x], summed as
+// splitk_epilogue_kernel sums it (0 + p0 + p1 + ... in split order): the same bits
+struct DgradParts {
+    const float* p;  // nullptr: off
+    int splits, M;
+    int64_t Nfull;
+};
+constexpr int kDgradPartsMax = 4;  // kDconvMaxSplits
+
 // the norm / clip tail of the per-image conv1 slab launch (NORM instances)
 struct NormTail {
     NormSrcs src;
@@ -1100,14 +1111,14 @@ struct NormTail {
     float* coef;
 };
 
-template <int COUT, bool POOLED, int NS = 2, bool NORM = false>
+template <int COUT, bool POOLED, int NS = 2, bool NORM = false, int NP = 0>
 __global__ void __launch_bounds__(256)
 conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ dy,
                           int64_t dy_cs, float* __restrict__ part, float* __restrict__ bpart,
                           const int32_t* __restrict__ counts, int batch, int H, int W,
                           int nsplits, int sps, const uint8_t* __restrict__ pidx, int64_t pi_cs,
                           const float* __restrict__ yp, int64_t yp_cs, int gh, int gw,
-                          const NormTail tail) {
+                          const NormTail tail, const DgradParts dp) {
     constexpr int NQ = COUT / 16;     // 16-channel groups
     constexpr int MAXW = 32;
     constexpr int DP = 4 * MAXW + 2;  // dY pitch per channel (4 rows), = 2 (mod 4)
@@ -1136,6 +1147,7 @@ conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float
     }
     const int nd4 = COUT * 4 * Q;
     float4 rd[NS][NDQ], rx[NS];
+    float2 pq[NS][POOLED ? NDQ : 1][NP > 0 ? NP : 1];  // NP: deferred DGRAD partials (dp.p)
     float2 pg[NS][POOLED ? NDQ : 1], py[NS][POOLED ? NDQ : 1];  // POOLED: raw loads, routed
     int pc[NS][POOLED ? NDQ : 1];                    // in store(); argmax bytes | code row << 16
     auto load = [&](int st0) {
@@ -1154,11 +1166,22 @@ conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float
                     const int64_t pl = (int64_t)img * COUT + co;
                     const int64_t go = pl * gh * gw + (yy >> 1) * gw + 2 * qq;
                     const int64_t io = pl * OHW + (yy >> 1) * (W / 2) + 2 * qq;
-                    pg[u][i] = ok ? make_float2(dyz[go], dyz[go + 1]) : make_float2(0.f, 0.f);
+                    if (NP > 0 && dp.p) {  // the partials of the deferred DGRAD reduction
+                        const int64_t po = ((int64_t)z * dp.splits * dp.M + co) * dp.Nfull +
+                                           (int64_t)img * (gh * gw) + (yy >> 1) * gw + 2 * qq;
+                        const int64_t ss = (int64_t)dp.M * dp.Nfull;
+#pragma unroll
+                        for (int sp = 0; sp < NP; ++sp) {
+                            const int64_t o = ok && sp < dp.splits ? po + sp * ss : 0;
+                            pq[u][i][sp] = make_float2(dp.p[o], dp.p[o + 1]);
+                        }
+                    }
+                    pg[u][i] = make_float2(0.f, 0.f);
+                    if (!(NP > 0 && dp.p) && ok) pg[u][i] = make_float2(dyz[go], dyz[go + 1]);
                     py[u][i] = ok ? make_float2(yp[z * yp_cs + go], yp[z * yp_cs + go + 1])
                                   : make_float2(0.f, 0.f);
                     pc[u][i] = ok ? (pidx[z * pi_cs + io] | (pidx[z * pi_cs + io + 1] << 8) |
-                                     ((yy & 1) << 17))
+                                     ((yy & 1) << 17) | (1 << 24))  // bit 24: a live quad
                                   : 0;
                 } else {
                     rd[u][i] = ok ? *reinterpret_cast<const float4*>(
@@ -1182,8 +1205,18 @@ conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float
             for (int i = 0; i < NDQ; ++i) {
                 const int q = tid + 256 * i;
                 if constexpr (POOLED) {  // maxpool2_bwd_kernel's routing: (code == a) ? g : 0
+                    if (NP > 0 && dp.p) {  // splitk_epilogue_kernel's sum: 0 + p0 + p1 + ...
+                        float2 g = make_float2(0.f, 0.f);
+#pragma unroll
+                        for (int sp = 0; sp < NP; ++sp)
+                            if (sp < dp.splits) {
+                                g.x += pq[u][i][sp].x;
+                                g.y += pq[u][i][sp].y;
+                            }
+                        pg[u][i] = (pc[u][i] >> 24) & 1 ? g : make_float2(0.f, 0.f);
+                    }
                     const int c = pc[u][i];
-                    const int r = c >> 16, i0 = c & 0xff, i1 = (c >> 8) & 0xff;
+                    const int r = (c >> 16) & 0xff, i0 = c & 0xff, i1 = (c >> 8) & 0xff;
                     const float g0 = py[u][i].x > 0.f ? pg[u][i].x : 0.f;
                     const float g1 = py[u][i].y > 0.f ? pg[u][i].y : 0.f;
                     rd[u][i] = make_float4(i0 == r ? g0 : 0.f, i0 == (r | 1) ? g0 : 0.f,
@@ -1653,6 +1686,49 @@ struct PdyArm {
 };
 thread_local PdyArm g_pdy;
 
+// Deferred DGRAD reduction (fh_conv_defer_dgrad, r05): the next split direct DGRAD on 16x16
+// planes with a plain sum epilogue leaves its partial slab unreduced; the conv1 weight gradient
+// that reads its output (c1 pooled WGRAD, per-image slabs) sums the partials as it stages them,
+// with the epilogue's order — one launch less per narrow step.  Anything else materialises it
+// (the epilogue launch it skipped) first.
+struct DgradDefer {
+    bool armed = false, pending = false;
+    const float* part = nullptr;
+    int splits = 0, M = 0, nclients = 0, batch = 0;
+    int64_t Nfull = 0, out_cs = 0;
+    float* out = nullptr;
+    const int32_t* counts = nullptr;
+    hipStream_t st = nullptr;
+};
+thread_local DgradDefer g_ddef;
+
+static int ddef_materialize() {
+    if (!g_ddef.pending) return FH_OK;
+    g_ddef.pending = false;
+    const DgradDefer& d = g_ddef;
+    dim3 eg((unsigned)ceil_div(d.Nfull, 256), (unsigned)d.M, (unsigned)d.nclients);
+    FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, d.st, d.part, d.splits, d.M, (int)d.Nfull,
+              d.out, d.out_cs, (const float*)nullptr, (int64_t)0, 0, 0, d.counts, d.batch, 256,
+              (double*)nullptr, 0, DropArgs{}, BnBwdEpi{}, PoolEpi{});
+    FH_LAUNCH_CHECK("deferred dgrad reduction");
+    return FH_OK;
+}
+
+// the partials for a consumer reading `dpool` (planes of 256 pixels) on stream st, else {}
+// after materialising whatever is pending
+static int ddef_take(const float* dpool, int64_t dp_cs, int gh, int gw, hipStream_t st,
+                     DgradParts& dp) {
+    dp = DgradParts{};
+    if (!g_ddef.pending) return FH_OK;
+    if (g_ddef.out == dpool && g_ddef.out_cs == dp_cs && g_ddef.st == st && gh * gw == 256 &&
+        g_ddef.splits <= kDgradPartsMax) {
+        dp = DgradParts{g_ddef.part, g_ddef.splits, g_ddef.M, g_ddef.Nfull};
+        g_ddef.pending = false;
+        return FH_OK;
+    }
+    return ddef_materialize();
+}
+
 static int pdy_materialize(float* dy, int64_t dy_cs, const int32_t* counts, int nclients,
                            int batch, int C, int plane, hipStream_t st) {
     if (!g_pdy.on || g_pdy.done) return FH_OK;
@@ -1785,6 +1861,27 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     }
     if (rc) return rc;
     FH_LAUNCH_CHECK(name);
+    if constexpr (OP == OP_DGRAD && S == 1) {
+        if (g_ddef.armed) {
+            g_ddef.armed = false;  // the next DGRAD only
+            if (p.splits > 1 && w == 16 && !a.accumulate && a.bnx == nullptr &&
+                a.pidx == nullptr && p.splits <= kDgradPartsMax) {
+                if (const int rc = ddef_materialize()) return rc;
+                g_ddef.pending = true;
+                g_ddef.part = (const float*)ws;
+                g_ddef.splits = p.splits;
+                g_ddef.M = a.M;
+                g_ddef.Nfull = a.Nfull;
+                g_ddef.out = out;
+                g_ddef.out_cs = a.out_cs;
+                g_ddef.counts = a.counts;
+                g_ddef.nclients = nclients;
+                g_ddef.batch = a.batch;
+                g_ddef.st = st;
+                return FH_OK;
+            }
+        }
+    }
     if (p.splits > 1) {
         dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
@@ -2017,6 +2114,17 @@ extern "C" int fh_conv_pair(int32_t mode) {
     const int rc = flush_pending_wgrad();
     g_pdy = PdyArm{};
     return rc;
+}
+
+// fh_conv_defer_dgrad(1): the calling thread's next split direct DGRAD on 16x16 planes with a
+// plain sum epilogue leaves its partials unreduced for the conv1 weight gradient that reads its
+// output (fh_conv2d_c1_pool_wgrad[_deferred], fh_conv2d_c1_pool_wgrad_persample[_clip]), which
+// sums them as it stages them — the epilogue's order, the same bits (r05).  A consumer of any
+// other tensor, or fh_conv_defer_dgrad(0), launches the skipped reduction first.
+extern "C" int fh_conv_defer_dgrad(int32_t on) {
+    g_ddef.armed = on != 0;
+    if (!on) return ddef_materialize();
+    return FH_OK;
 }
 
 extern "C" int fh_conv_pooled_dy(const float* dpool, int64_t dp_cs, const uint8_t* pidx,
@@ -2472,16 +2580,32 @@ static int c1_pool_wgrad_impl(const float* x, int64_t x_cs, const float* dpool, 
     const size_t wbytes = ((size_t)nclients * p.splits * cout * 9 * sizeof(float) + 255) / 256 * 256;
     float* bpart = db ? (float*)((char*)workspace + wbytes) : nullptr;
     hipStream_t st = as_stream(stream);
+    // a deferred DGRAD reduction of dpool (fh_conv_defer_dgrad): summed while staging, unless
+    // this launch's own partial output would overlap the slab being read
+    DgradParts dpa{};
+    if (const int rc = ddef_take(dpool, dp_cs, gh, gw, st, dpa)) return rc;
+    if (dpa.p && (!mfma || cout != 32 ||
+                  ((const char*)dpa.p < (const char*)workspace + need &&
+                   (const char*)workspace <
+                       (const char*)(dpa.p + (int64_t)nclients * dpa.splits * dpa.M * dpa.Nfull)))) {
+        g_ddef.pending = true;  // give it back and reduce it the usual way
+        if (const int rc = ddef_materialize()) return rc;
+        dpa = DgradParts{};
+    }
     if (mfma) {  // conv_c1_wgrad_mfma_kernel<POOLED>: the routed gradient on the matrix cores
         const dim3 grid((unsigned)p.splits, (unsigned)nclients);
-        if (cout == 32)
+        if (cout == 32 && dpa.p)
+            FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true, 2, false, kDgradPartsMax>), grid,
+                      dim3(256), 0, st, x, x_cs, dpool, dp_cs, part, bpart, counts, batch, h, w_,
+                      p.splits, p.sps, idx, i_cs, y, y_cs, gh, gw, NormTail{}, dpa);
+        else if (cout == 32)
             FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
                       dp_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps, idx, i_cs, y,
-                      y_cs, gh, gw, NormTail{});
+                      y_cs, gh, gw, NormTail{}, DgradParts{});
         else
             FH_LAUNCH((conv_c1_wgrad_mfma_kernel<64, true>), grid, dim3(256), 0, st, x, x_cs, dpool,
                       dp_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps, idx, i_cs, y,
-                      y_cs, gh, gw, NormTail{});
+                      y_cs, gh, gw, NormTail{}, DgradParts{});
         FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad mfma");
         if (defer_splits) {  // the optimizer step sums the chunks (fh_sgd_step_slabs)
             *defer_splits = p.splits;
@@ -2618,12 +2742,12 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
             FH_LAUNCH((conv_c1_wgrad_mfma_kernel<32, false>), grid, dim3(256), 0, st, x, x_cs, dy,
                       dy_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps,
                       (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0,
-                      NormTail{});
+                      NormTail{}, DgradParts{});
         else
             FH_LAUNCH((conv_c1_wgrad_mfma_kernel<64, false>), grid, dim3(256), 0, st, x, x_cs, dy,
                       dy_cs, part, bpart, counts, batch, h, w_, p.splits, p.sps,
                       (const uint8_t*)nullptr, (int64_t)0, (const float*)nullptr, (int64_t)0, 0, 0,
-                      NormTail{});
+                      NormTail{}, DgradParts{});
         FH_LAUNCH_CHECK("conv2d_wgrad c1 mfma");
         if (defer_splits) {
             *defer_splits = p.splits;
@@ -3844,17 +3968,28 @@ static int c1_persample_impl(const float* x, int64_t x_cs, const float* dpool, i
     // narrow grids (fewer image workgroups than ~two per CU): four stages per LDS round
     const bool wide4 = (int64_t)batch * nclients <= kC1PersampleNs4Max;
     const NormTail t = tail ? *tail : NormTail{};
-#define FH_C1PS(CO, NS, NORM)                                                                    \
-    FH_LAUNCH((conv_c1_wgrad_mfma_kernel<CO, true, NS, NORM>), grid, dim3(256), 0, st, x, x_cs,  \
-              dpool, dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y, y_cs, gh, \
-              gw, t)
+    DgradParts dpa{};  // a deferred DGRAD reduction of dpool: summed while staging (cout 32)
+    if (const int rc = ddef_take(dpool, dp_cs, gh, gw, st, dpa)) return rc;
+    if (dpa.p && cout != 32) {
+        g_ddef.pending = true;
+        if (const int rc = ddef_materialize()) return rc;
+        dpa = DgradParts{};
+    }
+#define FH_C1PS(CO, NS, NORM, NP)                                                                \
+    FH_LAUNCH((conv_c1_wgrad_mfma_kernel<CO, true, NS, NORM, NP>), grid, dim3(256), 0, st, x,   \
+              x_cs, dpool, dp_cs, part, bpart, counts, batch, h, w_, batch, sps, idx, i_cs, y,   \
+              y_cs, gh, gw, t, dpa)
     if (tail) {
         FH_REQUIRE(cout == 32, "conv2d_c1_pool_wgrad_persample_clip: cout 32 (got %d)", cout);
-        if (wide4) FH_C1PS(32, 4, true); else FH_C1PS(32, 2, true);
+        if (dpa.p) FH_C1PS(32, 2, true, kDgradPartsMax);
+        else if (wide4) FH_C1PS(32, 4, true, 0);
+        else FH_C1PS(32, 2, true, 0);
     } else if (cout == 32) {
-        if (wide4) FH_C1PS(32, 4, false); else FH_C1PS(32, 2, false);
+        if (dpa.p) FH_C1PS(32, 2, false, kDgradPartsMax);
+        else if (wide4) FH_C1PS(32, 4, false, 0);
+        else FH_C1PS(32, 2, false, 0);
     } else {
-        FH_C1PS(64, 2, false);
+        FH_C1PS(64, 2, false, 0);
     }
 #undef FH_C1PS
     FH_LAUNCH_CHECK("conv2d_c1_pool_wgrad_persample");

@@ -209,6 +209,9 @@ class PackedNet:
         # ... and conv1's per-image slabs with every image's norm / clip coefficient as one
         # launch (fh_conv2d_c1_pool_wgrad_persample_clip, r05)
         self.c1_norm_fused = True
+        # SimpleCNN: a split conv2 DGRAD (narrow lanes) leaves its partials for conv1's weight
+        # gradient to sum as it stages them (fh_conv_defer_dgrad, r05): one launch less
+        self.defer_dgrad = True
 
     # -------------------------------------------------------------- helpers
     def W(self, rows, name):
@@ -390,6 +393,9 @@ class PackedNet:
             ops.conv_pooled_dy(dp2, i2, A("p2", 64, 7, 7))
         ops.conv2d_wgrad(p1, da2, W(G, "conv2.weight"), W(G, "conv2.bias"), n, B, 32, hp, hp, 64,
                          3, 1, 1, counts=cnt, alg_hw=14)
+        defer = self.fuse_pool1_bwd and self.defer_dgrad and hp == 16
+        if defer:  # a split DGRAD's reduction summed by conv1's WGRAD as it stages dp1 (r05)
+            ops.conv_defer_dgrad(True)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt, alg_hw=14)
         ops.conv_pair(0)
@@ -397,6 +403,8 @@ class PackedNet:
             ops.conv2d_c1_pool_wgrad(self.x, dp1, A("i1", 32, 14, 14, dtype=torch.uint8), p1,
                                      W(G, "conv1.weight"), W(G, "conv1.bias"), n, B, 28, 28, 32,
                                      counts=cnt)
+            if defer:
+                ops.conv_defer_dgrad(False)
             return
         da1 = A("da1", 32, 28, 28)
         if self._pool1_fused:  # a1 not written: the ReLU mask at the argmax is p1 > 0
@@ -464,6 +472,8 @@ class PackedNet:
         if pooled_dy:
             ops.conv_pooled_dy(dp2, i2, p2)
         ops.conv2d_wgrad_persample(p1, da2, s2, n, B, 32, hp, hp, 64, counts=cnt, alg_hw=14)
+        if self.defer_dgrad:  # the split DGRAD's reduction summed by conv1's slab launch (r05)
+            ops.conv_defer_dgrad(True)
         ops.conv2d_dgrad(da2, W(P_, "conv2.weight"), dp1, n, B, 32, hp, hp, 64, 3, 1, 1,
                          counts=cnt, alg_hw=14)
         ops.conv_pair(0)
@@ -480,6 +490,8 @@ class PackedNet:
             ops.conv2d_c1_pool_wgrad_persample(self.x, dp1, i1, p1, s1, n, B, 28, 28, 32,
                                                counts=cnt)
             ops.dpsgd_norm_clip(lin, [s2, s1], coef, n, B, max_norm, sqnorm=sqnorm, counts=cnt)
+        if self.defer_dgrad:
+            ops.conv_defer_dgrad(False)
         # pass 2: the linear layers' clipped sums (dY rows scaled by c_i as they are loaded),
         # fc1's and fc2's in one launch (r05)
         if self.lin_wgrad_multi:

@@ -275,6 +275,13 @@ def conv_pooled_dy(dpool, pidx, ypool):
          _cs(ypool), int(dpool.shape[-1]))
 
 
+def conv_defer_dgrad(on):
+    """fh_conv_defer_dgrad: on — the next split 16x16 direct DGRAD leaves its partials for the
+    conv1 weight gradient reading its output to sum while staging; off — reduce anything
+    still pending (the skipped epilogue launch)."""
+    call("fh_conv_defer_dgrad", int(bool(on)))
+
+
 def _pair_status():
     """(held, dual launches issued) of this thread (fh_conv_pair_status)."""
     held, duals = ctypes.c_int32(), ctypes.c_int64()

@@ -697,6 +697,12 @@ int fh_conv_pair(int32_t mode);
  * attributes a dual launch to both roles' work): *held = 1 while a WGRAD launch is held for
  * the next DGRAD, *dual_launches = dual-role grids this thread has issued so far. */
 int fh_conv_pair_status(int32_t* held, int64_t* dual_launches);
+/* r05: fh_conv_defer_dgrad(1) arms the calling thread's next split direct DGRAD on 16x16
+ * planes with a plain sum epilogue to leave its partials unreduced; the conv1 weight gradient
+ * that reads its output (fh_conv2d_c1_pool_wgrad[_deferred], fh_conv2d_c1_pool_wgrad_persample
+ * [_clip]) sums them while staging (the epilogue's order: the same bits).  Any other consumer
+ * path, or fh_conv_defer_dgrad(0), launches the skipped reduction first. */
+int fh_conv_defer_dgrad(int32_t on);
 /* The next WGRAD + DGRAD pair's output gradient is a 2x2 max-pool's backward (SimpleCNN conv2,
  * models_pytorch.py:88-90, pool2 after relu(conv2)): dY(y, x) = dpool[y/2][x/2] where (y, x) is
  * the window's argmax pidx and the pooled ReLU output ypool there is > 0, else 0

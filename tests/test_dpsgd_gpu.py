@@ -388,3 +388,20 @@ def test_c1_slabs_with_norm_clip_bit_identical(sizes):
         engs.append(eng)
     assert torch.equal(engs[0].params, engs[1].params)
     assert torch.equal(engs[0].state1, engs[1].state1)
+
+
+@pytest.mark.parametrize("sizes", [[32, 17, 5], [23]])
+def test_dpsgd_deferred_dgrad_reduction_bit_identical(sizes):
+    """r05 fh_conv_defer_dgrad in DP-SGD: conv1's per-image slab launch (with the norm / clip
+    tail) sums conv2's split DGRAD partials while staging — the same steps, bit for bit."""
+    counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
+    engs = []
+    for defer in (True, False):
+        eng, _, _ = _engine(sizes, DPSGDConfig(max_grad_norm=0.4, noise_multiplier=0.5, seed=2))
+        eng.net.defer_dgrad = defer
+        for _ in range(2):
+            eng.step(len(sizes), counts)
+        torch.cuda.synchronize()
+        engs.append(eng)
+    assert torch.equal(engs[0].params, engs[1].params)
+    assert torch.equal(engs[0].state1, engs[1].state1)

@@ -17,13 +17,14 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _round(pooled, opt, sizes, rounds=2, dual=2):
+def _round(pooled, opt, sizes, rounds=2, dual=2, defer=True):
     torch.manual_seed(0)
     model = hm.ModelFactory.create_model("simple_cnn", dropout_rate=0.25).to(DEV)
     S = len(sizes)
     eng = PackedTrainer(model, capacity=S, batch=32, device=DEV)
     eng.net.pooled_dy_bwd = pooled
     eng.net.dual_bwd = dual
+    eng.net.defer_dgrad = defer
     for k in range(S):
         eng.load_module_state(k, model)
     g = torch.Generator().manual_seed(5)
@@ -108,3 +109,18 @@ def test_pooled_dy_op_level():
         # outside a training step's GradSlabs scope a WGRAD that splits over pixels has its own
         # reduction launch, so it is not held for the pair: the library filled dY first
         assert not dual and torch.equal(dy1, outs[0][3]), nc
+
+
+@pytest.mark.parametrize("opt,sizes", [("sgd", [70, 33, 9]), ("adam", [40]),
+                                       ("sgd", [130, 64, 64, 50, 9])])
+def test_deferred_dgrad_reduction_bit_identical(opt, sizes):
+    """r05 fh_conv_defer_dgrad: conv2's split DGRAD (narrow grids) leaves its partials and
+    conv1's weight gradient sums them while staging dp1 — the same rounds as with the split-K
+    epilogue launch, bit for bit."""
+    a, ma = _round(True, opt, sizes, defer=True)
+    b, mb = _round(True, opt, sizes, defer=False)
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.state1, b.state1)
+    for ra, rb in zip(ma, mb):
+        for x, y in zip(ra, rb):
+            assert (x.loss, x.accuracy) == (y.loss, y.accuracy)
