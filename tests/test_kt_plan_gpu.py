@@ -1,0 +1,175 @@
+"""The full KT plan against the CPU oracle: bench.py's headline workload through
+fedhip.round.RankRound exactly as the timed rounds build it, checked per client.
+
+KT = CIFAR10CNN (dropout 0.5, the reference default), 32 Dirichlet(0.5) clients over 50,000
+labels from the reference partitioner (data_loader.py:139-177) + 90 % train split = 45,015
+train images, one local epoch, SGD lr 0.01.  The lane planner cuts the 32 slots [0, 1, 9, 32]
+(one 131-step client; 8 clients; 23 clients), so one round launches every instance the timed
+rounds launch: the 1-client lane, the 8-client lane, the 23-client BM=64 grids and every
+ragged / tail width as clients finish.  The small-size tests reach the same templates; this
+one runs the exact launch set.
+
+  * eager round (test hooks on every lane): four clients — the 1-client lane's, the last of
+    the 8-client lane and the first and last of the 23-client lane — against their own
+    oracle LocalTrainer runs on the same batches (fp32 reference + fp64 twin replaying the
+    HIP run's dropout masks, max-pool argmax and ReLU decisions; tolerance of
+    tests/test_train_gpu.py), loss included; accuracy against the fp64 twin's count;
+  * the timed path (no hooks: first step eager, then captured step programs, lanes
+    concurrent): two more rounds from the same global model and the same plan, every one of
+    the 32 trained rows bit-identical to the eager round's;
+  * FedAvg of the eager round's rows bit-exact against oracle/fedavg_ref.py.
+
+Data: N(0, 1) fp32 images (the u8 gather + transform of the bench is covered by
+test_pipeline_gpu.py; transforms stay unpinned).
+"""
+import math
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from fedhip.partition import partition, train_split_sizes
+from fedhip.round import RankRound
+from oracle import fedavg_ref, train_ref
+from src.shared import models_pytorch as hm
+from test_train_gpu import check_loss, check_params
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+B, LR = 32, 0.01
+
+
+def kt_sizes():
+    """bench.build_clients(CONFIGS["KT"], world=1): the same draw, restated."""
+    labels = np.random.default_rng(0).integers(0, 10, size=50000)
+    random.seed(0)
+    np.random.seed(0)
+    parts = partition(labels, 32, "non_iid", 0.5)
+    return train_split_sizes([len(parts.get(c, [])) for c in range(32)], 0.1)
+
+
+def _decisions(eng, j):
+    """Slot j's discrete decisions after a step: (max-pool argmax as torch flat indices,
+    ReLU masks, dropout keep-masks), each a list in forward order."""
+    pools = []
+    for buf, H, W in eng.net.pool_index_buffers():
+        a = buf[j].long().cpu()
+        OH, OW = a.shape[-2:]
+        oh = torch.arange(OH).view(1, 1, OH, 1)
+        ow = torch.arange(OW).view(1, 1, 1, OW)
+        pools.append((2 * oh + a // 2) * W + (2 * ow + a % 2))
+    relus = [b[j].cpu() > 0 for b in eng.net.relu_output_buffers()]
+    drops = [b[j].cpu().clone() for b in eng.net.mask_buffers()]
+    return pools, relus, drops
+
+
+def _split(row, layout):
+    return [row[o:o + int(np.prod(s))].reshape(s) for o, s in zip(layout.offsets, layout.shapes)]
+
+
+@pytest.mark.timeout(900)
+def test_kt_full_plan_matches_oracle():
+    sizes = kt_sizes()
+    assert sum(sizes) == 45015 and max(sizes) == 4171
+    C = len(sizes)
+    torch.manual_seed(0)
+    model = hm.ModelFactory.create_model("cifar10_cnn")
+    assert model.dropout_rate > 0
+    gsd = {k: v.clone() for k, v in model.state_dict().items()}
+    init = {k: p.detach().clone() for k, p in model.named_parameters()}
+    rr = RankRound(model.to(DEV), sizes, list(range(C)), epochs=1, device=DEV,
+                   shuffle_seed=123)
+    tr = rr.trainer
+    cut = list(tr.cut)
+    assert cut == [0, 1, 9, 32], cut  # the planner's KT cut (bench_detail.json "lanes")
+    L, S, P = tr.layout, len(rr.slots), rr.P
+    g = torch.Generator().manual_seed(77)
+    datas = {k: (torch.randn(n, 3, 32, 32, generator=g),
+                 torch.randint(0, 10, (n,), generator=g)) for k, n in enumerate(sizes)}
+    data = torch.cat([datas[k][0] for k in rr.slots]).to(DEV)
+    labels = torch.cat([datas[k][1] for k in rr.slots]).to(DEV)
+    offs = np.cumsum([0] + [sizes[k] for k in rr.slots][:-1]).tolist()
+    G0 = rr.global_flat.clone()
+
+    check = [0, 8, 9, 31]  # slots: lane 0; last of lane 1; first and last of lane 2
+    lane_of = {s: next(i for i in range(len(cut) - 1) if cut[i] <= s < cut[i + 1])
+               for s in check}
+    snaps = {s: [] for s in check}
+
+    def hook(li):
+        mine = [s for s in check if lane_of[s] == li]
+
+        def on_step(e, n):
+            for s in mine:
+                j = s - cut[li]
+                if j < n:  # slot j took a step: its decisions of this step
+                    snaps[s].append(_decisions(e, j))
+        return on_step
+
+    for li, ln in enumerate(tr.lanes):
+        ln.on_step = hook(li)
+    trained = {}
+    rr.on_trained = lambda params, s: trained.__setitem__("rows", params[:s, :P].clone())
+    metrics = rr.run(data, labels, offs, "sgd", LR, seed=0)
+    torch.cuda.synchronize()
+    plans = rr.last_plan
+    R = trained["rows"].cpu().numpy()
+    G1 = rr.global_flat.cpu().numpy().copy()
+    assert [m.samples_processed for m in metrics] == [sizes[k] for k in rr.slots]
+
+    # ---- the timed path (hooks off: step programs, lanes concurrent) reproduces every row
+    for ln in tr.lanes:
+        ln.on_step = None
+    for rep in range(2):
+        rr.set_global(G0)
+        rr.run(data, labels, offs, "sgd", LR, seed=0)
+        torch.cuda.synchronize()
+        Rt = trained["rows"].cpu().numpy()
+        assert rr.last_plan[0]["G"] == plans[0]["G"]
+        bad = [i for i in range(S) if not np.array_equal(Rt[i].view(np.uint32),
+                                                         R[i].view(np.uint32))]
+        assert not bad, f"replay {rep}: rows of slots {bad} differ from the eager round"
+
+    # ---- the checked clients against their own oracle LocalTrainer on the same batches
+    for s in check:
+        li = lane_of[s]
+        j, k, plan = s - cut[li], rr.slots[s], plans[li]
+        n = sizes[k]
+        st = math.ceil(n / B)
+        assert len(snaps[s]) == st
+        ref = train_ref.make_model("cifar10_cnn", None)
+        ref.load_state_dict(gsd)
+        ref64 = train_ref.make_model("cifar10_cnn", None).double()
+        ref64.load_state_dict({a: (v.double() if v.is_floating_point() else v)
+                               for a, v in gsd.items()})
+        optr, opt64 = train_ref.make_optimizer(ref, "sgd", LR), \
+            train_ref.make_optimizer(ref64, "sgd", LR)
+        running, r64, correct, c64s, seen = 0.0, 0.0, 0, 0, 0
+        for gs in range(st):
+            idx = plan["index"][gs, j, :plan["counts"][gs, j]]
+            m = idx.numel()
+            xb, yb = datas[k][0][idx], datas[k][1][idx]
+            pools, relus, drops = snaps[s][gs]
+            mk = [d[:m] for d in drops]
+            li32, cc, _, _ = train_ref.train_step(ref, optr, xb, yb, masks=mk)
+            l64, c64, _, _ = train_ref.train_step(ref64, opt64, xb.double(), yb, masks=mk,
+                                                pools=[p[:m] for p in pools],
+                                                relus=[r[:m] for r in relus])
+            running, r64, seen = running + li32, r64 + l64, seen + m
+            correct, c64s = correct + cc, c64s + c64
+        mt = metrics[s]
+        check_loss(mt.loss, running / st, r64 / st)
+        # accuracy against the fp64 twin (the HIP run's decisions): over 131 steps the fp32
+        # CPU run takes its own ReLU / pool decisions and its argmax drifts (untrained model,
+        # random labels: 10 logits within ~1e-6 of each other); a near-tie may still resolve
+        # either way, so 0.1 % of the samples (+1) may differ
+        assert abs(mt.accuracy * seen - c64s) <= 1 + 1e-3 * seen, (mt.accuracy * seen, c64s,
+                                                                 correct)
+        got = {nm: torch.from_numpy(t) for nm, t in zip(L.names, _split(R[s], L))}
+        check_params(got, ref, ref64, init, st, LR, "sgd")
+
+    # ---- FedAvg of the eager round's rows (weights n_k / sum(n))
+    w = fedavg_ref.calculate_sample_weights(sizes)
+    glob = fedavg_ref.weighted_average([R[rr.slot_of[k]] for k in range(C)], w)
+    assert np.array_equal(G1.view(np.uint32), glob.view(np.uint32))
