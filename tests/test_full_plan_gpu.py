@@ -1,5 +1,6 @@
-"""The full KT plan against the CPU oracle: bench.py's headline workload through
-fedhip.round.RankRound exactly as the timed rounds build it, checked per client.
+"""The full KT and K2 plans against the CPU oracle: bench.py's headline workload and
+BASELINE.json's 1-GPU config through fedhip.round.RankRound exactly as the timed rounds build
+them, checked per client.
 
 KT = CIFAR10CNN (dropout 0.5, the reference default), 32 Dirichlet(0.5) clients over 50,000
 labels from the reference partitioner (data_loader.py:139-177) + 90 % train split = 45,015
@@ -19,6 +20,11 @@ one runs the exact launch set.
     the 32 trained rows bit-identical to the eager round's;
   * FedAvg of the eager round's rows bit-exact against oracle/fedavg_ref.py.
 
+K2 = SimpleCNN (dropout 0.25), 32 Dirichlet(0.5) clients over 60,000 MNIST labels, update-level
+DP eps=1.0 (noise injected: the GPU's clip + noise on the GPU-trained rows against
+oracle/privacy_ref.apply_update_dp, as tests/test_configs_gpu.py), lanes as the planner cuts.
+Checked clients: the first and last slot of every lane.
+
 Data: N(0, 1) fp32 images (the u8 gather + transform of the bench is covered by
 test_pipeline_gpu.py; transforms stay unpinned).
 """
@@ -31,7 +37,8 @@ import torch
 
 from fedhip.partition import partition, train_split_sizes
 from fedhip.round import RankRound
-from oracle import fedavg_ref, train_ref
+from fedhip.round import DPConfig
+from oracle import fedavg_ref, privacy_ref, train_ref
 from src.shared import models_pytorch as hm
 from test_train_gpu import check_loss, check_params
 
@@ -40,13 +47,21 @@ DEV = torch.device("cuda")
 B, LR = 32, 0.01
 
 
-def kt_sizes():
-    """bench.build_clients(CONFIGS["KT"], world=1): the same draw, restated."""
-    labels = np.random.default_rng(0).integers(0, 10, size=50000)
+def bench_sizes(samples):
+    """bench.build_clients(CONFIGS[KT|K2], world=1): the same draw, restated."""
+    labels = np.random.default_rng(0).integers(0, 10, size=samples)
     random.seed(0)
     np.random.seed(0)
     parts = partition(labels, 32, "non_iid", 0.5)
     return train_split_sizes([len(parts.get(c, [])) for c in range(32)], 0.1)
+
+
+CASES = {
+    "KT": dict(model="cifar10_cnn", shape=(3, 32, 32), samples=50000, dp=None,
+               total=45015, cut=[0, 1, 9, 32]),
+    "K2": dict(model="simple_cnn", shape=(1, 28, 28), samples=60000, dp=1.0,
+               total=None, cut=None),
+}
 
 
 def _decisions(eng, j):
@@ -69,30 +84,35 @@ def _split(row, layout):
 
 
 @pytest.mark.timeout(900)
-def test_kt_full_plan_matches_oracle():
-    sizes = kt_sizes()
-    assert sum(sizes) == 45015 and max(sizes) == 4171
-    C = len(sizes)
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_full_plan_matches_oracle(case):
+    c = CASES[case]
+    sizes = bench_sizes(c["samples"])
+    if c["total"]:
+        assert sum(sizes) == c["total"]
+    C, name = len(sizes), c["model"]
     torch.manual_seed(0)
-    model = hm.ModelFactory.create_model("cifar10_cnn")
+    model = hm.ModelFactory.create_model(name)
     assert model.dropout_rate > 0
     gsd = {k: v.clone() for k, v in model.state_dict().items()}
     init = {k: p.detach().clone() for k, p in model.named_parameters()}
     rr = RankRound(model.to(DEV), sizes, list(range(C)), epochs=1, device=DEV,
-                   shuffle_seed=123)
+                   shuffle_seed=123, dp_seed=9, dp=DPConfig(epsilon=c["dp"]) if c["dp"] else None)
     tr = rr.trainer
     cut = list(tr.cut)
-    assert cut == [0, 1, 9, 32], cut  # the planner's KT cut (bench_detail.json "lanes")
+    if c["cut"]:
+        assert cut == c["cut"], cut  # the planner's KT cut (bench_detail.json "lanes")
+    assert len(cut) == 4, cut  # three concurrent lanes
     L, S, P = tr.layout, len(rr.slots), rr.P
     g = torch.Generator().manual_seed(77)
-    datas = {k: (torch.randn(n, 3, 32, 32, generator=g),
+    datas = {k: (torch.randn(n, *c["shape"], generator=g),
                  torch.randint(0, 10, (n,), generator=g)) for k, n in enumerate(sizes)}
     data = torch.cat([datas[k][0] for k in rr.slots]).to(DEV)
     labels = torch.cat([datas[k][1] for k in rr.slots]).to(DEV)
     offs = np.cumsum([0] + [sizes[k] for k in rr.slots][:-1]).tolist()
     G0 = rr.global_flat.clone()
 
-    check = [0, 8, 9, 31]  # slots: lane 0; last of lane 1; first and last of lane 2
+    check = sorted({x for a, b in zip(cut, cut[1:]) for x in (a, b - 1)})  # lanes' ends
     lane_of = {s: next(i for i in range(len(cut) - 1) if cut[i] <= s < cut[i + 1])
                for s in check}
     snaps = {s: [] for s in check}
@@ -109,6 +129,10 @@ def test_kt_full_plan_matches_oracle():
 
     for li, ln in enumerate(tr.lanes):
         ln.on_step = hook(li)
+    noise = None
+    if c["dp"]:
+        noise = 1e-3 * torch.randn(S, P, generator=torch.Generator().manual_seed(5))
+        rr.dp_noise = noise.to(DEV)
     trained = {}
     rr.on_trained = lambda params, s: trained.__setitem__("rows", params[:s, :P].clone())
     metrics = rr.run(data, labels, offs, "sgd", LR, seed=0)
@@ -116,6 +140,7 @@ def test_kt_full_plan_matches_oracle():
     plans = rr.last_plan
     R = trained["rows"].cpu().numpy()
     G1 = rr.global_flat.cpu().numpy().copy()
+    final = tr.params[:S, :P].cpu().numpy()
     assert [m.samples_processed for m in metrics] == [sizes[k] for k in rr.slots]
 
     # ---- the timed path (hooks off: step programs, lanes concurrent) reproduces every row
@@ -138,9 +163,9 @@ def test_kt_full_plan_matches_oracle():
         n = sizes[k]
         st = math.ceil(n / B)
         assert len(snaps[s]) == st
-        ref = train_ref.make_model("cifar10_cnn", None)
+        ref = train_ref.make_model(name, None)
         ref.load_state_dict(gsd)
-        ref64 = train_ref.make_model("cifar10_cnn", None).double()
+        ref64 = train_ref.make_model(name, None).double()
         ref64.load_state_dict({a: (v.double() if v.is_floating_point() else v)
                                for a, v in gsd.items()})
         optr, opt64 = train_ref.make_optimizer(ref, "sgd", LR), \
@@ -169,7 +194,17 @@ def test_kt_full_plan_matches_oracle():
         got = {nm: torch.from_numpy(t) for nm, t in zip(L.names, _split(R[s], L))}
         check_params(got, ref, ref64, init, st, LR, "sgd")
 
-    # ---- FedAvg of the eager round's rows (weights n_k / sum(n))
+    # ---- update DP on the GPU-trained rows, exactly as the oracle states it
+    if c["dp"]:
+        gparts = _split(G0.cpu().numpy(), L)
+        for i in range(S):
+            out, _, _, _ = privacy_ref.apply_update_dp(_split(R[i], L), gparts, 1.0, c["dp"],
+                                                       1e-5, _split(noise[i].numpy(), L))
+            e = np.concatenate([o.reshape(-1) for o in out])
+            d = np.abs(final[i].astype(np.float64) - e)
+            assert d.max() <= 4 * np.finfo(np.float32).eps * max(1.0, np.abs(e).max()), i
+
+    # ---- FedAvg of the eager round's final rows (weights n_k / sum(n))
     w = fedavg_ref.calculate_sample_weights(sizes)
-    glob = fedavg_ref.weighted_average([R[rr.slot_of[k]] for k in range(C)], w)
+    glob = fedavg_ref.weighted_average([final[rr.slot_of[k]] for k in range(C)], w)
     assert np.array_equal(G1.view(np.uint32), glob.view(np.uint32))
