@@ -208,3 +208,89 @@ def test_full_plan_matches_oracle(case):
     w = fedavg_ref.calculate_sample_weights(sizes)
     glob = fedavg_ref.weighted_average([final[rr.slot_of[k]] for k in range(C)], w)
     assert np.array_equal(G1.view(np.uint32), glob.view(np.uint32))
+
+
+@pytest.mark.timeout(900)
+def test_k2_dpsgd_full_plan_matches_oracle():
+    """bench.py --config K2-dpsgd's plan (32 clients over 60,000, slots by descending shard,
+    the planner's three lanes, per-sample clipping C=1) as the timed rounds build it, noise
+    off and dropout off (oracle/dpsgd_ref.py replays neither; the noise is pinned by
+    tests/test_dpsgd_gpu.py): the first and last slot of every lane against
+    dpsgd_ref.dpsgd_step on the same batches (fp32 + fp64 twin, both replaying the HIP run's
+    pool / ReLU decisions; tolerance of tests/test_dpsgd_gpu.py), and the timed path (step
+    programs, lanes concurrent) bit-identical to the eager round on every row."""
+    from fedhip.engine import DPSGDConfig
+    from fedhip.lanes import LanedTrainer
+    from oracle import dpsgd_ref
+    train = bench_sizes(60000)
+    sizes = sorted(train, reverse=True)
+    torch.manual_seed(0)
+    model = hm.ModelFactory.create_model("simple_cnn", dropout_rate=0.0).to(DEV)
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    eng = LanedTrainer(model, [math.ceil(n / B) for n in sizes], batch=B, device=DEV,
+                       dpsgd=DPSGDConfig(max_grad_norm=1.0, noise_multiplier=0.0))
+    cut, P, S = list(eng.cut), eng.layout.P, len(sizes)
+    assert len(cut) == 4, cut
+    g = torch.Generator().manual_seed(1000)
+    xs = [torch.randn(n, 1, 28, 28, generator=g) for n in sizes]
+    ys = [torch.randint(0, 10, (n,), generator=g) for n in sizes]
+    data, lab = torch.cat(xs).to(DEV), torch.cat(ys).to(DEV)
+    offs = np.cumsum([0] + sizes[:-1]).tolist()
+    plans = eng.make_plan(sizes, 1, generator=torch.Generator().manual_seed(7))
+
+    check = sorted({x for a, b in zip(cut, cut[1:]) for x in (a, b - 1)})
+    lane_of = {s: next(i for i in range(3) if cut[i] <= s < cut[i + 1]) for s in check}
+    snaps = {s: [] for s in check}
+
+    def hook(li):
+        mine = [s for s in check if lane_of[s] == li]
+
+        def on_step(e, n):
+            for s in mine:
+                if s - cut[li] < n:
+                    snaps[s].append(_decisions(e, s - cut[li])[:2])
+        return on_step
+
+    def round_rows(hooks):
+        for k in range(S):
+            eng.load_module_state(k, model)
+        for li, ln in enumerate(eng.lanes):
+            ln.on_step = hook(li) if hooks else None
+        eng.run_round(data, lab, offs, plans, "sgd", LR)
+        torch.cuda.synchronize()
+        return eng.params[:S, :P].cpu().numpy().copy()
+
+    R = round_rows(True)
+    for rep in range(2):
+        Rt = round_rows(False)
+        bad = [i for i in range(S) if not np.array_equal(Rt[i].view(np.uint32),
+                                                         R[i].view(np.uint32))]
+        assert not bad, f"replay {rep}: rows of slots {bad} differ from the eager round"
+
+    for s in check:
+        li = lane_of[s]
+        j, plan = s - cut[li], plans[li]
+        st = math.ceil(sizes[s] / B)
+        assert len(snaps[s]) == st
+        ref32 = train_ref.make_model("simple_cnn", None, dropout_rate=0.0)
+        ref32.load_state_dict(sd)
+        ref64 = train_ref.make_model("simple_cnn", None, dropout_rate=0.0).double()
+        ref64.load_state_dict({a: b.double() for a, b in sd.items()})
+        p0 = train_ref.param_vector(ref64).clone()
+        opt32 = train_ref.make_optimizer(ref32, "sgd", LR)
+        opt64 = train_ref.make_optimizer(ref64, "sgd", LR)
+        for gs in range(st):
+            idx = plan["index"][gs, j, :plan["counts"][gs, j]]
+            m = idx.numel()
+            pools, relus = snaps[s][gs]
+            pools, relus = [p[:m] for p in pools], [r[:m] for r in relus]
+            dpsgd_ref.dpsgd_step(ref32, opt32, xs[s][idx], ys[s][idx], 1.0, pools=pools,
+                                 relus=relus)
+            dpsgd_ref.dpsgd_step(ref64, opt64, xs[s][idx].double(), ys[s][idx], 1.0,
+                                 pools=pools, relus=relus)
+        p32 = train_ref.param_vector(ref32).double()
+        p64 = train_ref.param_vector(ref64)
+        pg = torch.from_numpy(R[s]).double()
+        e_hip, e_cpu = (pg - p64).norm().item(), (p32 - p64).norm().item()
+        assert e_hip <= 4 * e_cpu + 1e-4 * (p64 - p0).norm().item() + 1e-7 * p64.norm().item(), \
+            (s, st, e_hip, e_cpu)
