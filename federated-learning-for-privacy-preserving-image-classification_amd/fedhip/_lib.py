@@ -185,6 +185,30 @@ SIGNATURES = {
 _lib = None
 
 
+def check_build_record(path: str = LIB_PATH, record_path: str | None = None):
+    """The in-tree library must match its build record (build_native.py): same source digest
+    as the sources beside it, same library bytes.  Raises FedHipError otherwise."""
+    import hashlib
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_fh_build_native", os.path.join(_PKG_ROOT, "build_native.py"))
+    bn = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bn)
+    rec = bn.read_record(record_path)
+    if rec is None:
+        raise FedHipError(f"{path} has no build record ({record_path or bn.RECORD}); rebuild "
+                          "it with "
+                          "`python build_native.py`")
+    if rec.get("sources_sha256") != bn.source_digest():
+        raise FedHipError(f"{path} was built from other sources than the tree's (stale "
+                          "library); rebuild it with `python build_native.py`")
+    with open(path, "rb") as fh:
+        if hashlib.sha256(fh.read()).hexdigest() != rec.get("lib_sha256"):
+            raise FedHipError(f"{path} is not the library its build record describes; "
+                              "rebuild it with `python build_native.py`")
+    return rec
+
+
 def load(path: str = LIB_PATH):
     """Load libfedhip.so and bind every declared symbol (raises if absent)."""
     global _lib
@@ -194,6 +218,8 @@ def load(path: str = LIB_PATH):
         raise FedHipError(
             f"libfedhip.so not found at {path}; build it with "
             "`python build_native.py` (HIP/gfx950) — there is no CPU fallback")
+    if os.path.abspath(path) == os.path.abspath(LIB_PATH):
+        check_build_record(path)
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -41,6 +41,21 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(syms), "ctypes table and header disagree"
 
 
+def test_library_matches_its_build_record(tmp_path):
+    """The in-tree library carries a build record (build_native.py) whose source digest is
+    the tree's; a library whose record names other sources, or other bytes, is refused."""
+    rec = _lib.check_build_record()
+    assert rec["arch"] == "gfx950" and "-ffp-contract=off" in rec["cflags"]
+    assert not any(REPO in f for f in rec["cflags"])  # nothing tied to the checkout's path
+    for bad, msg in ((dict(rec, sources_sha256="0" * 64), "other sources"),
+                     (dict(rec, lib_sha256="0" * 64), "not the library")):
+        (tmp_path / "rec.json").write_text(json.dumps(bad))
+        with pytest.raises(_lib.FedHipError, match=msg):
+            _lib.check_build_record(_lib.LIB_PATH, str(tmp_path / "rec.json"))
+    with pytest.raises(_lib.FedHipError, match="no build record"):
+        _lib.check_build_record(_lib.LIB_PATH, str(tmp_path / "absent.json"))
+
+
 def test_error_path_without_gpu():
     """Argument validation runs on the host: a bad call fails with a message, no launch."""
     with pytest.raises(_lib.FedHipError, match="bad shape"):
