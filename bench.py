@@ -191,14 +191,16 @@ def _cpu_threads():
     return host, (max(1, int(min(lim))) if lim else torch.get_num_threads())
 
 
-def timed_passes(run_client, sizes, seconds, passes=3):
+def timed_passes(run_client, sizes, seconds, passes=3, fixed_images=None):
     """BASELINE.md §2 / SURVEY.md §8d: one warm-up client (untimed: first-touch allocations,
     oneDNN primitive creation), then the same client sample timed `passes` times; the
     baseline is the median pass.  The sample is the clients median shard size first, as many
     as the warm-up client's second (warm) run says fit in ~`seconds` per pass.  run_client(i, n) trains
     client i of `sizes` and returns its client-images and its result row; run_client.prepare(i)
     generates client i's data (untimed) and run_client.finish(rows, ns) runs once per pass
-    (FedAvg)."""
+    (FedAvg).  fixed_images: the sample is the median-first clients up to that many images
+    whatever the warm rate (the same sample on every box: r06, K2-dpsgd's baseline drifted 57 %
+    between boxes with a rate-sized sample)."""
     med = float(np.median(sizes))
     order = [i for i in sorted(range(len(sizes)), key=lambda i: (abs(sizes[i] - med), sizes[i]))
              if sizes[i] > 0]
@@ -211,7 +213,10 @@ def timed_passes(run_client, sizes, seconds, passes=3):
     for i in order:
         sample.append(i)
         budget += sizes[i] * run_client.epochs / rate
-        if budget >= seconds:
+        if fixed_images is not None:
+            if sum(sizes[k] for k in sample) >= fixed_images:
+                break
+        elif budget >= seconds:
             break
     for i in sample:  # data generated before the timed passes, reused by every pass
         run_client.prepare(i)
@@ -633,7 +638,7 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
         inst = ops.PROBE.by_tag()
         buckets = ops.PROBE.by_tag_bucket()
         rows = summarize_instances(inst, buckets, peak)[0]
-        stamps = launch_stamps_for(rows[0][0], dev)
+        stamps = None if args.no_stamps else launch_stamps_for(rows[0][0], dev)
         if stamps is not None:
             stamps.start()
     torch.cuda.synchronize()
@@ -869,7 +874,8 @@ def predict_strong(key, args, dev, worlds, steps, warmup):
                       "time)", "steps": steps, "warmup": warmup, "worlds": res}
 
 
-def cpu_baseline_dpsgd(sizes, lr=0.01, seconds=5.0, max_norm=1.0, eps=1.0, delta=1e-5):
+def cpu_baseline_dpsgd(sizes, lr=0.01, seconds=5.0, max_norm=1.0, eps=1.0, delta=1e-5,
+                       fixed_images=3000):
     """The K2-dpsgd round on the host cores: oracle/dpsgd_ref.py (explicit per-sample
     gradients, per-sample clip to C, N(0, (sigma C)^2) noise with the reference's
     Gaussian-mechanism sigma, privacy.py:209) over whole client shards of N(0,1) MNIST-shaped
@@ -904,7 +910,8 @@ def cpu_baseline_dpsgd(sizes, lr=0.01, seconds=5.0, max_norm=1.0, eps=1.0, delta
 
     run_client.epochs, run_client.prepare = 1, prepare
     run_client.finish = lambda rows, ns: None
-    value, rates, nclients, imgs, secs = timed_passes(run_client, sizes, seconds)
+    value, rates, nclients, imgs, secs = timed_passes(run_client, sizes, seconds,
+                                                      fixed_images=fixed_images)
     torch.set_num_threads(prev)
     return {"value": value, "unit": "client-images/s", "cores": threads, "kind": "port",
             "host": host, "passes": [round(r, 1) for r in rates],
@@ -972,27 +979,42 @@ def compact(out):
                                               "executed_over_algorithmic") else {})) or None,
                       "roofline_hbm": _roof_short(k2.get("roofline_hbm")),
                       "cpu_baseline": _cpu_short(k2.get("cpu_baseline"))}
+    dp = out.get("k2_dpsgd")
+    if dp:
+        r, c = dp.get("roofline") or {}, dp.get("cpu_baseline") or {}
+        line["k2_dpsgd"] = {"value": dp["value"], "unit": dp["unit"],
+                            "ms_per_step": dp["ms_per_step"], "steps": dp["steps"],
+                            "workload": "K2 with per-sample DP-SGD (clip C=1, eps=1)",
+                            "round_frac": dp["round_frac"],
+                            "roofline": {k: r[k] for k in ("kernel", "bound", "achieved", "frac",
+                                                           "avg_launch_ms") if k in r} or None,
+                            "cpu_baseline": {k: c[k] for k in ("value", "cores", "kind")
+                                             if k in c} or None}
     line["env"] = out.get("env", {})
     line["detail"] = out.get("detail_file")
     s = json.dumps(line)
     if len(s) > MAX_LINE_BYTES:  # never let the headline overflow the driver's tail
-        for k in ("data", "roofline_hbm", "detail"):
+        for k in ("roofline_hbm", "detail", "data"):
             line.pop(k, None)
-            if "k2" in line:
-                line["k2"].pop(k, None)
+            for blk in ("k2", "k2_dpsgd"):
+                if blk in line:
+                    line[blk].pop(k, None)
             if len(json.dumps(line)) <= MAX_LINE_BYTES:
                 break
     # still too long: shorten the free-text fields, longest first, then drop the k2 block
     texts = [(line.get("config") or {}, "workload"), (line.get("cpu_baseline") or {}, "sample"),
              (line.get("k2") or {}, "workload"), ((line.get("k2") or {}).get("cpu_baseline") or {},
-                                                   "sample")]
+                                                   "sample"),
+             (line.get("k2_dpsgd") or {}, "workload"),
+             ((line.get("k2_dpsgd") or {}).get("cpu_baseline") or {}, "sample")]
     for d, k in sorted(texts, key=lambda dk: -len(str(dk[0].get(dk[1], "")))):
         if len(json.dumps(line)) <= MAX_LINE_BYTES:
             break
         if isinstance(d.get(k), str) and len(d[k]) > 80:
             d[k] = d[k][:77] + "..."
-    if len(json.dumps(line)) > MAX_LINE_BYTES:
-        line.pop("k2", None)
+    for blk in ("k2_dpsgd", "k2"):
+        if len(json.dumps(line)) > MAX_LINE_BYTES:
+            line.pop(blk, None)
     if len(json.dumps(line)) > MAX_LINE_BYTES:
         line.pop("env", None)
     return line
@@ -1026,6 +1048,8 @@ def main():
                     help="skip the instrumented per-launch-shape round")
     ap.add_argument("--no-k2", action="store_true",
                     help="N=1 KT run: skip the K2 block (BASELINE.json's 1-GPU config)")
+    ap.add_argument("--no-dpsgd", action="store_true",
+                    help="N=1 KT run: skip the K2-dpsgd block (per-sample DP-SGD)")
     ap.add_argument("--rounds-target", type=float, default=0.91,
                     help="rounds-to-accuracy half of the metric (K1 MNIST proxy); 0 disables")
     ap.add_argument("--rounds-max", type=int, default=30)
@@ -1047,6 +1071,9 @@ def main():
                     help="N>1: all-gather + sequential FedAvg (bit-exact) instead of all-reduce")
     ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="JSON file for the full result (per-launch-shape tables); '' = none")
+    ap.add_argument("--no-stamps", action="store_true",
+                    help="A/B: timed rounds without the roofline shape's launch stamps (the "
+                         "roofline then falls back to the instrumented round's timing)")
     ap.add_argument("--separate-conv-bwd", action="store_true",
                     help="each layer's WGRAD and DGRAD as two launches (no dual-role launch): "
                          "the PMC traffic passes (tools/bench_traffic.py) attribute per kernel")
@@ -1076,11 +1103,21 @@ def main():
     out = run_config(args.config, args, world, rank, dev, args.steps, args.warmup, rtt=True)
     # BASELINE.json's only 1-GPU config (K2: SimpleCNN, 32 Dirichlet(0.5) clients, update DP
     # eps=1.0 timed) rides along the default N=1 line, measured the same way
+    k2 = dps = None
     if world == 1 and args.config == "KT" and not args.no_k2:
         k2 = run_config("K2", args, world, rank, dev, max(args.steps, 3), args.warmup)
-        if k2 is not None:
-            host_legs(k2, args, dev)
-            out["k2"] = k2
+        # r06: north_star's per-sample clipping (K2-dpsgd) rides along too, so the driver
+        # measures it: the same workload as `--config K2-dpsgd`
+        if not args.no_dpsgd:
+            dps = run_dpsgd(args, dev, max(args.steps, 3), args.warmup)
+    if k2 is not None:  # host-CPU legs after every timed GPU leg of the process
+        host_legs(k2, args, dev)
+        out["k2"] = k2
+    if dps is not None:
+        sizes = dps.pop("_sizes")
+        if not args.no_cpu_baseline:
+            dps["cpu_baseline"] = cpu_baseline_dpsgd(sizes, args.lr)
+        out["k2_dpsgd"] = dps
     if rank == 0:
         host_legs(out, args, dev)
         # every FH_* knob in the environment (diagnostics / A-B switches): none is set in a

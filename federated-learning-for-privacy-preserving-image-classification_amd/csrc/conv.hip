@@ -1114,11 +1114,14 @@ struct NormTail {
 template <int COUT, bool POOLED, int NS = 2, bool NORM = false, int NP = 0>
 __global__ void __launch_bounds__(256)
 conv_c1_wgrad_mfma_kernel(const float* __restrict__ x, int64_t x_cs, const float* __restrict__ dy,
-                          int64_t dy_cs, float* __restrict__ part, float* __restrict__ bpart,
+                          int64_t dy_cs, float* part, float* bpart,
                           const int32_t* __restrict__ counts, int batch, int H, int W,
                           int nsplits, int sps, const uint8_t* __restrict__ pidx, int64_t pi_cs,
                           const float* __restrict__ yp, int64_t yp_cs, int gh, int gw,
                           const NormTail tail, const DgradParts dp) {
+    // part / bpart carry no __restrict__: the NORM instance reads its own slab row back through
+    // tail.src after the workgroup barrier (they are only written in the epilogue, so the main
+    // loop's scheduling does not depend on it)
     constexpr int NQ = COUT / 16;     // 16-channel groups
     constexpr int MAXW = 32;
     constexpr int DP = 4 * MAXW + 2;  // dY pitch per channel (4 rows), = 2 (mod 4)
@@ -1701,6 +1704,9 @@ struct DgradDefer {
     hipStream_t st = nullptr;
 };
 thread_local DgradDefer g_ddef;
+// instrumentation (fh_conv_defer_status): DGRADs left unreduced, and partial slabs a consumer
+// summed while staging (the rest were materialised by the skipped epilogue launch)
+thread_local int64_t g_ddef_deferred = 0, g_ddef_taken = 0;
 
 static int ddef_materialize() {
     if (!g_ddef.pending) return FH_OK;
@@ -1724,6 +1730,7 @@ static int ddef_take(const float* dpool, int64_t dp_cs, int gh, int gw, hipStrea
         g_ddef.splits <= kDgradPartsMax) {
         dp = DgradParts{g_ddef.part, g_ddef.splits, g_ddef.M, g_ddef.Nfull};
         g_ddef.pending = false;
+        ++g_ddef_taken;
         return FH_OK;
     }
     return ddef_materialize();
@@ -1878,6 +1885,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
                 g_ddef.nclients = nclients;
                 g_ddef.batch = a.batch;
                 g_ddef.st = st;
+                ++g_ddef_deferred;
                 return FH_OK;
             }
         }
@@ -2104,6 +2112,9 @@ extern "C" int fh_conv_pair(int32_t mode) {
         g_pend.on = false;
         g_pend.pdy = false;
         g_pdy = PdyArm{};
+        // ... and a deferred DGRAD reduction armed or left pending by the failed step: its
+        // partials would otherwise be claimed (or never reduced) by an unrelated later launch
+        g_ddef = DgradDefer{};
         return FH_OK;
     }
     if (mode > 0) {
@@ -2124,6 +2135,13 @@ extern "C" int fh_conv_pair(int32_t mode) {
 extern "C" int fh_conv_defer_dgrad(int32_t on) {
     g_ddef.armed = on != 0;
     if (!on) return ddef_materialize();
+    return FH_OK;
+}
+
+extern "C" int fh_conv_defer_status(int64_t* deferred, int64_t* taken) {
+    FH_REQUIRE(deferred && taken, "conv_defer_status: null pointer");
+    *deferred = g_ddef_deferred;
+    *taken = g_ddef_taken;
     return FH_OK;
 }
 

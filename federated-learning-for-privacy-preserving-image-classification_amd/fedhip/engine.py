@@ -374,11 +374,14 @@ class PackedTrainer:
             # host-side seed, plus the slots' global client ids when set
             net.seed_dev = views["seed"]
             self._gather(st["data"], st["labels"], views, n, st["sample_elems"])
+            if ops.PROBE.enabled:  # the step's valid images (ragged last batches)
+                ops.PROBE.step_images = (int(plan["counts"][g, :n].sum()), self.batch)
             try:
                 self._step_launches(n, views["counts"], views["reset"], first=(g == 0),
                                     adam_dev=views["adam"])
             finally:
                 net._src = None
+                ops.PROBE.step_images = None
                 ops.conv_pair_reset()  # no-op unless the step raised between a pair's calls
             if arm and not ops.PROBE.all:
                 ops.PROBE.enabled = False

@@ -73,6 +73,10 @@ class LaunchProbe:
         # launch shapes whose kernels execute more than their algorithmic work (SimpleCNN's
         # 14x14 conv2 on padded 16x16 planes): tag -> executed / algorithmic FLOPs
         self.exec_ratio = {}
+        # (valid images, batch) of the step being issued (set by the engine in instrumented
+        # rounds): a launch's algorithmic work counts the step's real images, not the padded
+        # nclients x batch its grid covers (ragged last batches)
+        self.step_images = None
 
     @property
     def all(self):
@@ -102,12 +106,17 @@ class LaunchProbe:
         tag: record under this launch shape instead of begin()'s."""
         if h is None:
             return
+        if self.step_images is not None and clients:
+            imgs, batch = self.step_images
+            if 0 < imgs < clients * batch:
+                flops *= imgs / float(clients * batch)
         e2 = torch.cuda.Event(enable_timing=True)
         e2.record()
         self.records.append((tag or h[0], h[1], e2, flops, nbytes, clients))
 
     def reset(self):
         self.records, self.seen, self.held = [], {}, None
+        self.step_images = None
 
     def summary(self):
         torch.cuda.synchronize()
@@ -280,6 +289,14 @@ def conv_defer_dgrad(on):
     conv1 weight gradient reading its output to sum while staging; off — reduce anything
     still pending (the skipped epilogue launch)."""
     call("fh_conv_defer_dgrad", int(bool(on)))
+
+
+def defer_status():
+    """(DGRADs left unreduced, partial slabs summed by their consumer) on this thread
+    (fh_conv_defer_status): tests assert a deferral really happened."""
+    d, t = ctypes.c_int64(), ctypes.c_int64()
+    call("fh_conv_defer_status", ctypes.byref(d), ctypes.byref(t))
+    return d.value, t.value
 
 
 def _pair_status():

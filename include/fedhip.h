@@ -703,6 +703,9 @@ int fh_conv_pair_status(int32_t* held, int64_t* dual_launches);
  * [_clip]) sums them while staging (the epilogue's order: the same bits).  Any other consumer
  * path, or fh_conv_defer_dgrad(0), launches the skipped reduction first. */
 int fh_conv_defer_dgrad(int32_t on);
+/* r06 (instrumentation): DGRADs the calling thread left unreduced under fh_conv_defer_dgrad, and
+ * how many of those partial slabs a conv1 weight-gradient consumer summed while staging. */
+int fh_conv_defer_status(int64_t* deferred, int64_t* taken);
 /* The next WGRAD + DGRAD pair's output gradient is a 2x2 max-pool's backward (SimpleCNN conv2,
  * models_pytorch.py:88-90, pool2 after relu(conv2)): dY(y, x) = dpool[y/2][x/2] where (y, x) is
  * the window's argmax pidx and the pooled ReLU output ypool there is > 0, else 0

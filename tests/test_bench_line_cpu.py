@@ -97,3 +97,36 @@ def test_strong_client_set_is_fixed():
         assert len(sizes[0]) == cfg["clients"] * cfg.get("config_gpus", 1)
     weak = bench.build_clients(bench.CONFIGS["KT"], 2)[1]
     assert len(weak) == 64
+
+
+def test_compact_line_carries_k2_dpsgd():
+    """r06: the default line carries the K2-dpsgd block (north_star's per-sample clipping,
+    driver-measured) with its roofline and CPU baseline, and every contract key still fits
+    (the r05 final tree's full KT + K2 + K2-dpsgd results, profiles/r05_final/)."""
+    out = json.load(open(os.path.join(REPO, "profiles", "r05_final", "bench_detail.json")))
+    out["k2_dpsgd"] = json.load(open(os.path.join(REPO, "profiles", "r05_final",
+                                                  "detail_K2-dpsgd.json")))
+    out["detail_file"] = "gpurun_out/bench_detail.json"
+    line = bench.compact(out)
+    assert len(json.dumps(line)) <= bench.MAX_LINE_BYTES
+    for k in CONTRACT:
+        assert k in line, k
+    d = line["k2_dpsgd"]
+    assert d["value"] == out["k2_dpsgd"]["value"] and d["round_frac"] > 0
+    assert d["roofline"]["frac"] == out["k2_dpsgd"]["roofline"]["frac"]
+    assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1
+    assert "k2" in line
+
+
+def test_timed_passes_fixed_sample():
+    """fixed_images: the CPU baseline's client sample is the same whatever the warm rate."""
+    sizes = [100, 300, 200, 50, 400, 250]
+    seen = []
+
+    def run_client(i):
+        seen.append(i)
+        return sizes[i], None
+    run_client.epochs, run_client.prepare = 1, lambda i: None
+    run_client.finish = lambda rows, ns: None
+    _, _, n, imgs, _ = bench.timed_passes(run_client, sizes, 0.0, fixed_images=450)
+    assert n == 2 and imgs == 450  # median-first: 250 then 200

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 import torch
 
+from fedhip import ops
 from fedhip._lib import FedHipError
 from fedhip.engine import DPSGDConfig, PackedTrainer
 from oracle import dpsgd_ref, train_ref
@@ -396,12 +397,18 @@ def test_dpsgd_deferred_dgrad_reduction_bit_identical(sizes):
     tail) sums conv2's split DGRAD partials while staging — the same steps, bit for bit."""
     counts = torch.tensor(sizes, dtype=torch.int32, device=DEV)
     engs = []
+    taken = []
     for defer in (True, False):
         eng, _, _ = _engine(sizes, DPSGDConfig(max_grad_norm=0.4, noise_multiplier=0.5, seed=2))
         eng.net.defer_dgrad = defer
+        d0 = ops.defer_status()
         for _ in range(2):
             eng.step(len(sizes), counts)
         torch.cuda.synchronize()
+        d1 = ops.defer_status()
+        taken.append((d1[0] - d0[0], d1[1] - d0[1]))
         engs.append(eng)
+    # defer=True: both steps left conv2's DGRAD partials to conv1's slab launch (ADVICE r05)
+    assert taken[0][0] >= 2 and taken[0][1] >= 2 and taken[1] == (0, 0), taken
     assert torch.equal(engs[0].params, engs[1].params)
     assert torch.equal(engs[0].state1, engs[1].state1)

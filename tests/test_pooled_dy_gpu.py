@@ -117,8 +117,15 @@ def test_deferred_dgrad_reduction_bit_identical(opt, sizes):
     """r05 fh_conv_defer_dgrad: conv2's split DGRAD (narrow grids) leaves its partials and
     conv1's weight gradient sums them while staging dp1 — the same rounds as with the split-K
     epilogue launch, bit for bit."""
+    d0 = ops.defer_status()
     a, ma = _round(True, opt, sizes, defer=True)
+    d1 = ops.defer_status()
     b, mb = _round(True, opt, sizes, defer=False)
+    d2 = ops.defer_status()
+    # the deferral really happened (ADVICE r05): DGRADs were left unreduced and conv1's weight
+    # gradient summed their partials; the defer=False round deferred nothing
+    assert d1[0] > d0[0] and d1[1] > d0[1], (d0, d1)
+    assert d2 == d1, (d1, d2)
     assert torch.equal(a.params, b.params)
     assert torch.equal(a.state1, b.state1)
     for ra, rb in zip(ma, mb):

@@ -301,3 +301,26 @@ def test_simplecnn_padded_maps_match_dense(opt):
     for ra, rb in zip(ma, mb):
         for x, y in zip(ra, rb):
             assert abs(x.loss - y.loss) <= 1e-3 * max(1.0, abs(y.loss))
+
+
+def test_step_refuses_more_slots_than_capacity_gpu():
+    """PackedTrainer.step on a 1-slot trainer: n = 2 (one past every buffer) and n = -1 raise
+    FedHipError before any launch — nothing is written and the optimizer step count is kept
+    (the CPU test only read the guard's source)."""
+    from fedhip._lib import FedHipError
+    from fedhip.engine import PackedTrainer
+    torch.manual_seed(0)
+    model = hm.ModelFactory.create_model("simple_cnn").to(DEV)
+    eng = PackedTrainer(model, capacity=1, batch=32, device=DEV)
+    eng.load_module_state(0, model)
+    before = eng.params.clone()
+    counts = torch.full((2,), 32, dtype=torch.int32, device=DEV)
+    for n in (2, -1):
+        with pytest.raises(FedHipError):
+            eng.step(n, counts)
+    torch.cuda.synchronize()
+    assert eng.opt_step == 0
+    assert torch.equal(eng.params, before)
+    eng.step(1, counts[:1])  # the bound itself is allowed
+    torch.cuda.synchronize()
+    assert eng.opt_step == 1 and not torch.equal(eng.params, before)
