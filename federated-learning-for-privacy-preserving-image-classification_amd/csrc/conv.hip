@@ -2581,7 +2581,10 @@ static int c1_pool_wgrad_impl(const float* x, int64_t x_cs, const float* dpool, 
                               int32_t batch, int32_t h, int32_t w_, int32_t cout, int32_t gh,
                               int32_t gw, void* stream, int32_t* defer_splits,
                               int64_t* defer_boff) {
-    if (defer_splits) *defer_splits = 1;
+    // defer_splits: the partials left in the slab (>= 1; the optimizer sums them), 0 = dW / db
+    // written directly (r06: single-split slab paths reported 1, which read as "direct", and the
+    // layer's gradient never reached the optimizer)
+    if (defer_splits) *defer_splits = 0;
     if (defer_boff) *defer_boff = 0;
     FH_REQUIRE(nclients >= 0 && batch > 0 && h >= 2 && w_ >= 2 && !(h & 1) && !(w_ & 1) &&
                gh >= h / 2 && gw >= w_ / 2, "conv2d_c1_pool_wgrad: bad shape");
@@ -2712,7 +2715,9 @@ static int conv2d_wgrad_impl(const float* x, int64_t x_cs, const float* in_scale
     // workspace for the optimizer step to sum; the reduction launch is skipped
     const int pair = g_pair_mode;  // fh_conv_pair arms one call
     g_pair_mode = 0;
-    if (defer_splits) *defer_splits = 1;
+    // defer_splits: partials left in the slab (>= 1, also for a one-split plan whose kernel
+    // writes the slab: c1, small-cin, stride 2), 0 = dW / db written directly
+    if (defer_splits) *defer_splits = 0;
     if (defer_boff) *defer_boff = 0;
     int oh, ow;
     int rc = conv_common_check(nclients, batch, cin, h, w_, cout, kh, kw, stride, pad, oh, ow);

@@ -595,7 +595,7 @@ def conv2d_c1_pool_wgrad(x, dpool, idx, y, dw, db, nclients, batch, h, wd, cout,
              _cs(idx), ptr(y), _cs(y), ptr(dw), _cs(dw), ptr(db), _cs(db), base, nb,
              _counts(counts), nclients, batch, h, wd, cout, gh, gw, ctypes.byref(splits),
              ctypes.byref(boff), stream_handle())
-        if splits.value > 1:
+        if splits.value > 0:  # partials in the slab (0: dw / db written directly)
             d.ranges.append((off_w, cout * 9, base, splits.value))
             if db is not None:
                 d.ranges.append((off_b, cout, base + boff.value, splits.value))
@@ -714,7 +714,7 @@ def _wgrad_deferred(d, x, dy, dw, db, nclients, batch, cin, h, wd, cout, k, stri
          _cs(sc) if sc is not None else 0, ptr(dy), _cs(dy), ptr(dw), _cs(dw), ptr(db), _cs(db),
          base, nb, _counts(counts), nclients, batch, cin, h, wd, cout, k, k, stride, pad,
          ctypes.byref(splits), ctypes.byref(boff), stream_handle())
-    if splits.value > 1:
+    if splits.value > 0:  # partials in the slab (0: dw / db written directly)
         d.ranges.append((off_w, n_w, base, splits.value))
         if db is not None:
             d.ranges.append((off_b, cout, base + boff.value, splits.value))

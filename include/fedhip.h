@@ -541,10 +541,13 @@ int fh_conv2d_wgrad_bnrelu(const float* x, int64_t x_cs, const float* in_scale,
                            int32_t batch, int32_t cin, int32_t h, int32_t w_, int32_t cout,
                            int32_t kh, int32_t kw, int32_t stride, int32_t pad, void* stream);
 /* fh_conv2d_wgrad (in_scale / in_shift NULL) or fh_conv2d_wgrad_bnrelu without the final
- * reduction: when the plan splits the pixel reduction (*splits_out > 1) the partial sums stay
- * in `slab` (sized by fh_conv2d_wgrad_workspace) — weights [client][split][cout*cin*kh*kw] at
- * byte 0, bias [client][split][cout] at byte *bias_off_out — for an optimizer step to finish
- * (fh_sgd_step_slabs / fh_adam_step_slabs); *splits_out == 1: dw / db written directly. */
+ * reduction: when the kernel leaves partial sums (*splits_out >= 1 of them) they stay in `slab`
+ * (sized by fh_conv2d_wgrad_workspace) — weights [client][split][cout*cin*kh*kw] at byte 0,
+ * bias [client][split][cout] at byte *bias_off_out — for an optimizer step to finish
+ * (fh_sgd_step_slabs / fh_adam_step_slabs; a one-split slab is copied by it);
+ * *splits_out == 0: dw / db written directly.  (r06: one-split slab plans — single-channel,
+ * small-cin and stride-2 kernels — used to report 1, read as "written directly", so that
+ * layer's gradient was dropped; found by tests/test_full_plan_resnet_gpu.py, K5.) */
 int fh_conv2d_wgrad_deferred(const float* x, int64_t x_cs, const float* in_scale,
                              const float* in_shift, int64_t aff_cs, const float* dy,
                              int64_t dy_cs, float* dw, int64_t dw_cs, float* db, int64_t db_cs,
@@ -659,7 +662,8 @@ int fh_conv2d_c1_pool_wgrad(const float* x, int64_t x_cs, const float* dpool, in
                             int32_t batch, int32_t h, int32_t w_, int32_t cout, int32_t gh,
                             int32_t gw, void* stream);
 /* fh_conv2d_c1_pool_wgrad without the final reduction (as fh_conv2d_wgrad_deferred): the
- * per-chunk partials stay in `slab` for fh_sgd_step_slabs / fh_adam_step_slabs. */
+ * *splits_out >= 1 per-chunk partials stay in `slab` for fh_sgd_step_slabs /
+ * fh_adam_step_slabs. */
 int fh_conv2d_c1_pool_wgrad_deferred(const float* x, int64_t x_cs, const float* dpool,
                                      int64_t dp_cs, const uint8_t* idx, int64_t i_cs,
                                      const float* y, int64_t y_cs, float* dw, int64_t dw_cs,

@@ -73,6 +73,10 @@ def _layer_case(n, batch, cin, h, cout, k, stride, pad, affine, bias, opt, seed=
     (3, 32, 1, 28, 32, 3, 1, 1, False, True),      # MNIST conv1 (single-channel MFMA kernel)
     (2, 32, 64, 32, 128, 3, 2, 1, False, False),   # stride-2 direct WGRAD
     (2, 32, 64, 32, 128, 1, 2, 0, False, False),   # 1x1/s2 shortcut (implicit GEMM)
+    # r06: stride-2 direct WGRAD whose plan is ONE split (ResNet layer3.0.conv1 at 32 clients):
+    # the kernel still writes the slab, and the optimizer must copy it (it used to be reported
+    # as "written directly" and the layer's gradient was dropped — K5's full-plan test)
+    (32, 32, 128, 16, 256, 3, 2, 1, False, False),
 ])
 @pytest.mark.parametrize("opt", ["sgd", "adamw"])
 def test_deferred_layer_bit_identical(n, batch, cin, h, cout, k, stride, pad, affine, bias, opt):
@@ -82,6 +86,8 @@ def test_deferred_layer_bit_identical(n, batch, cin, h, cout, k, stride, pad, af
     assert torch.equal(p0, p1) and torch.equal(a0, a1) and torch.equal(b0, b1)
     if n == 1 and cin == 32:
         assert ranges and ranges[0][3] >= 16  # the G > 1 range-split path was exercised
+    if n == 32:
+        assert ranges and all(r[3] == 1 for r in ranges), ranges  # the one-split slab
 
 
 def test_slab_ranges_rejected_when_misaligned():
