@@ -40,7 +40,8 @@ PKG = os.path.join(REPO, "federated-learning-for-privacy-preserving-image-classi
 sys.path[:0] = [REPO, PKG]
 
 from fedhip import ops  # noqa: E402
-from fedhip.partition import lpt_assign, partition, train_split, train_split_sizes  # noqa: E402
+from fedhip.partition import (chain_assign, lpt_assign, partition, train_split,  # noqa: E402
+                              train_split_sizes)
 from fedhip.round import DPConfig, RankRound  # noqa: E402
 from src.shared import models_pytorch as hm  # noqa: E402
 
@@ -65,6 +66,10 @@ CONFIGS = {
                classes=100, clients=32, samples=6250, strategy="non_iid", alpha=0.1, epochs=1,
                dp=2.0, config_gpus=8),
 }
+# strong scaling (--strong / --predict-strong): partition.chain_assign's chain-latency weight =
+# a / b of the rank-time fit t_r = a * (longest client's steps) + b * (client-steps) over the
+# r05 / r06 predict-strong rank times (profiles/r06_strong/chain_fit.txt); K2 assumes KT's
+CHAIN_RATIO = {"KT": 5.5, "K1": 5.5, "K2": 5.5, "K3": 1.7, "K4": 0.94, "K5": 1.7}
 # train FLOPs / image = 6*MACs - 2*MACs(first layer)
 TRAIN_FLOPS = {"simple_cnn": 24_995_328, "cifar10_cnn": 237_124_608,
                "federated_resnet[1,1,1]": 1_164_721_152, "federated_resnet[2,2,2]": 2_523_675_648}
@@ -127,6 +132,15 @@ def make_rank_data(cfg, train_sizes, my_slots, device, seed, raw=True):
     labels = torch.randint(0, cfg["classes"], (total,), generator=g, device=device)
     offs = np.cumsum([0] + [train_sizes[k] for k in my_slots][:-1]).tolist()
     return data, labels, offs
+
+
+def assign_ranks(key, cfg, train, world, strong):
+    """Clients -> ranks.  Weak scaling: LPT by sample count (every GPU holds its slice).  Strong
+    scaling (a fixed client set): partition.chain_assign, which keeps the rank of a long
+    Dirichlet client's step chain light (r06; LPT when its modelled makespan is no better)."""
+    if strong:
+        return chain_assign(train, world, cfg["epochs"], 32, CHAIN_RATIO.get(key, 0.0))
+    return lpt_assign(train, world)
 
 
 def shard_report(train, assign, epochs, batch=32):
@@ -590,7 +604,7 @@ def run_config(key, args, world, rank, dev, steps, warmup, rtt=False, cpu=True):
     cfg = CONFIGS[key]
     labels, train = build_clients(cfg, world, strong=args.strong)
     C = len(train)
-    assign = lpt_assign(train, world)
+    assign = assign_ranks(key, cfg, train, world, args.strong)
     mine = assign[rank]
     torch.manual_seed(0)
     template = hm.ModelFactory.create_model(cfg["model"], **cfg["kw"]).to(dev)
@@ -836,7 +850,7 @@ def predict_strong(key, args, dev, worlds, steps, warmup):
                                  sparsity_ratio=cfg["compression"][1])
     res = {}
     for world in worlds:
-        assign = lpt_assign(train, world)
+        assign = assign_ranks(key, cfg, train, world, True)
         per = []
         for r in range(world):
             rr = RankRound(template, train, assign[r], epochs=cfg["epochs"], device=dev, dp=dp,

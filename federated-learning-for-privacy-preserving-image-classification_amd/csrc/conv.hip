@@ -3050,25 +3050,31 @@ __device__ __forceinline__ void linear_dgrad_skinny_body(
 #pragma unroll
             for (int t = 0; t < KT; ++t) b[q][t] = wcol[(int64_t)(mb + 4 * h + q) * K + 32 * t];
     };
-    float4 a0, a1;
-    float b0[4][KT], b1[4][KT];
-    if (mw > 0) ld(mbeg, a0, b0);
-    for (int mb = mbeg; mb < mbeg + mw; mb += 16) {
-        const bool more1 = mb + 8 < mbeg + mw;
-        if (more1) ld(mb + 8, a1, b1);
+    // r06: a ring of PD 8-m blocks in flight (was two): a block's 16 MFMAs (~0.4 us) hide a
+    // fraction of one memory round trip, so with one block of lookahead every block waited out
+    // most of a latency (KT fc1 at 8 clients, fill 0.5: 16 blocks per wave, 24.2 -> 22.4 us per
+    // launch; 23 clients 47.2 -> 43.9, tools/fcab.sh, profiles/r06_fc/).  Same MFMA order.
+    // (KT = 1, SimpleCNN fc1: 4 blocks per wave, +2-6 % per launch with PD = 4: kept at 2)
+    constexpr int PD = KT == 4 ? 4 : 2;
+    const int nb = mw / 8;
+    float4 a[PD];
+    float b[PD][4][KT];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+    for (int i = 0; i < PD; ++i)
+        if (i < nb) ld(mbeg + 8 * i, a[i], b[i]);
+    for (int j0 = 0; j0 < nb; j0 += PD) {
 #pragma unroll
-            for (int t = 0; t < KT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a0, q), b0[q][t], acc[t], 0, 0, 0);
-        if (!more1) break;
-        const bool more2 = mb + 16 < mbeg + mw;
-        if (more2) ld(mb + 16, a0, b0);
+        for (int i = 0; i < PD; ++i) {
+            if (j0 + i < nb) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+                for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int t = 0; t < KT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a1, q), b1[q][t], acc[t], 0, 0, 0);
+                    for (int t = 0; t < KT; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a[i], q), b[i][q][t],
+                                                                      acc[t], 0, 0, 0);
+                if (j0 + i + PD < nb) ld(mbeg + 8 * (j0 + i + PD), a[i], b[i]);
+            }
+        }
     }
     // waves 1..3 hand their partials to wave 0 one at a time through one wave's worth of
     // LDS (16 KB at KT = 4, so LDS does not cap the workgroups per CU); wave 0 adds them in
@@ -3467,6 +3473,9 @@ linear_fwd_epilogue_kernel(const float* __restrict__ part, int splits, int M,
 // output tile per workgroup)
 constexpr int kLfTarget = 512;
 constexpr int kLfMinKb = 4;
+// 32-k blocks of loads in flight per wave (r03: 2; r06 measured 4: within noise at C = 1 / 8,
+// +1-3 % per launch at 21-23 clients, tools/fcab.sh — kept at 2)
+constexpr int kLfDepth = 2;
 
 static bool linear_fwd_skinny_ok(int batch, int in_f, int out_f) {
     return kLinearSkinny && kLinearSkinny != 3 && batch > 0 && batch <= 32 && in_f > 0 &&
@@ -3498,7 +3507,7 @@ static int linear_fwd_skinny(const float* x, int64_t x_cs, const float* w, int64
         FH_REQUIRE(workspace && ws_bytes >= need, "linear_fwd: workspace %zu < %zu", ws_bytes, need);
         part = (float*)workspace;
     }
-    FH_LAUNCH((linear_fwd_skinny_kernel<2, 1>), grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
+    FH_LAUNCH((linear_fwd_skinny_kernel<kLfDepth, 1>), grid, dim3(256), 0, st, x, x_cs, w, w_cs, bias,
               b_cs, y, y_cs, part, counts, batch, in_f, out_f, kbps, relu, drop);
     if (splits > 1)
         FH_LAUNCH(linear_fwd_epilogue_kernel, dim3((unsigned)ceil_div(32 * out_f, 256), nclients),

@@ -95,6 +95,11 @@ class LanedTrainer:
             cut = list(cut)
             if cut[0] != 0 or cut[-1] != S or sorted(set(cut)) != cut:
                 raise ValueError(f"lane cut {cut} is not a cut of {S} slots")
+        elif lanes is None and os.environ.get("FH_LANE_CUT"):
+            # A/B diagnostic (recorded in a bench line's env field): "0,1,8,32"
+            cut = [int(v) for v in os.environ["FH_LANE_CUT"].split(",")]
+            if cut[0] != 0 or cut[-1] != S or sorted(set(cut)) != cut:
+                cut = plan_lanes(list(slot_steps))
         elif lanes is None:
             cut = plan_lanes(list(slot_steps))
         elif lanes <= 1:

@@ -102,3 +102,44 @@ def lpt_assign(sizes: Sequence[int], bins: int) -> List[List[int]]:
         out[b].append(i)
         load[b] += sizes[i]
     return out
+
+
+def _steps(n: int, epochs: int, batch: int) -> int:
+    return epochs * -(-n // batch)
+
+
+def rank_time_model(steps: Sequence[int], ratio: float) -> float:
+    """Modelled round time of one rank (in units of one client-step of packed work): its
+    clients' local epochs are dependent SGD chains, so the rank cannot finish before its
+    longest chain (ratio x that chain's steps: a chain step is latency-bound) nor before its
+    total client-steps are through (the packed / concurrent-lane throughput term)."""
+    return ratio * max(steps, default=0) + sum(steps)
+
+
+def chain_assign(sizes: Sequence[int], bins: int, epochs: int = 1, batch: int = 32,
+                 ratio: float = 0.0) -> List[List[int]]:
+    """Client -> rank assignment for a FIXED client set (strong scaling, r06).  Plain LPT
+    balances images, but a Dirichlet shard's local steps are a dependent chain: the rank holding
+    the longest client pays that chain's latency whatever else it holds (KT at 8 GPUs: the
+    131-step client plus two more, 61.4 ms, against 39-48 ms for the other ranks).  With
+    ratio > 0 clients go, in descending steps, to the rank whose modelled time
+    (rank_time_model) after adding them is least — the long chain's rank then takes little
+    else; the result is kept only if its modelled makespan beats LPT's.  ratio = per-step
+    chain latency / per-client-step packed cost, fitted per model on MI355X (bench.CONFIGS
+    `chain_ratio`, profiles/r06_strong/)."""
+    base = lpt_assign(sizes, bins)
+    if ratio <= 0 or bins <= 1:
+        return base
+    st = [_steps(n, epochs, batch) for n in sizes]
+    order = sorted(range(len(sizes)), key=lambda i: (-st[i], -sizes[i], i))
+    out: List[List[int]] = [[] for _ in range(bins)]
+    longest = [0] * bins
+    total = [0] * bins
+    for i in order:
+        b = min(range(bins), key=lambda j: (ratio * max(longest[j], st[i]) + total[j] + st[i],
+                                            total[j], j))
+        out[b].append(i)
+        longest[b] = max(longest[b], st[i])
+        total[b] += st[i]
+    span = lambda a: max(rank_time_model([st[k] for k in r], ratio) for r in a)
+    return out if span(out) < span(base) else base

@@ -130,3 +130,23 @@ def test_timed_passes_fixed_sample():
     run_client.finish = lambda rows, ns: None
     _, _, n, imgs, _ = bench.timed_passes(run_client, sizes, 0.0, fixed_images=450)
     assert n == 2 and imgs == 450  # median-first: 250 then 200
+
+
+def test_chain_assign_isolates_long_chain():
+    """r06 partition.chain_assign (strong scaling): every client on exactly one rank, the
+    modelled makespan never above LPT's, and on KT's fixed 32-client set at 8 ranks the rank
+    of the 131-step client holds nothing else (LPT gave it two more clients: 61.4 ms)."""
+    import math
+    from fedhip.partition import chain_assign, lpt_assign, rank_time_model
+    _, train = bench.build_clients(bench.CONFIGS["KT"], 1, strong=True)
+    steps = [math.ceil(n / 32) for n in train]
+    for world in (2, 4, 8):
+        a = chain_assign(train, world, 1, 32, bench.CHAIN_RATIO["KT"])
+        assert sorted(k for r in a for k in r) == list(range(len(train)))
+        span = lambda asg: max(rank_time_model([steps[k] for k in r], bench.CHAIN_RATIO["KT"])
+                               for r in asg)
+        assert span(a) <= span(lpt_assign(train, world))
+    a = chain_assign(train, 8, 1, 32, bench.CHAIN_RATIO["KT"])
+    long_rank = next(r for r in a if max(steps[k] for k in r) == max(steps))
+    assert len(long_rank) == 1
+    assert chain_assign(train, 8, 1, 32, 0.0) == lpt_assign(train, 8)  # ratio 0: plain LPT

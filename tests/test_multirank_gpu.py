@@ -197,7 +197,8 @@ def test_rankround_exact_mode_bitwise():
 
 
 def test_bench_strong_scaling_rehearsal():
-    """bench.py --strong (r05): the config's fixed client set (K2: 32 clients) LPT-sharded over
+    """bench.py --strong (r05): the config's fixed client set (K2: 32 clients) sharded (r06:
+    partition.chain_assign) over
     2 ranks on cuda:0 over gloo, one all-reduce per round; the line says "strong" and counts
     the same 32 clients as the one-GPU run."""
     import json

@@ -34,6 +34,8 @@ def timeit(fn, it=30):
 
 def main():
     dev = torch.device("cuda")
+    if os.environ.get("FH_BENCH_FILL"):  # a lane's split-K fill fraction (fedhip/lanes.py)
+        ops.set_fill_fraction(float(os.environ["FH_BENCH_FILL"]))
     B = 32
     for C in [int(v) for v in os.environ.get("FH_BENCH_CLIENTS", "32,23,8,1").split(",")]:
         tot = 0.0

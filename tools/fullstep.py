@@ -93,6 +93,10 @@ if __name__ == "__main__":
             from fedhip import _lib
             _lib.load.__defaults__ = (a[i + 1],)
             del a[i:i + 2]
+        if "--separate" in a:  # each layer's WGRAD and DGRAD as two launches
+            from fedhip import ops as _ops
+            _ops.set_conv_pairing(False)
+            a.remove("--separate")
         if "--fill" in a:
             i = a.index("--fill")
             fill = float(a[i + 1])
