@@ -1674,6 +1674,15 @@ struct PendingWgrad {
     DWArgs d{};
     hipStream_t st = nullptr;
 };
+// r06 in-launch split-K reduction: the calling thread's ticket counters (zeroed once by the
+// caller, left zero by every launch: each tile's last arriver resets its counter), one per
+// output tile of a split direct FWD / DGRAD launch (fh_set_split_tickets)
+struct SplitTickets {
+    uint32_t* p = nullptr;
+    int64_t n = 0;
+};
+thread_local SplitTickets g_tickets;
+thread_local int64_t g_inl_launches = 0;  // fh_conv_pair_status-style instrumentation
 thread_local int g_pair_mode = 0;
 thread_local PendingWgrad g_pend;
 thread_local int64_t g_dual_launches = 0;  // fh_conv_pair_status (instrumentation)
@@ -1801,22 +1810,42 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     a.splits = p.splits;
     a.cchunk = p.cchunk;
     a.Nfull = a.batch * sp;
+    dim3 grid((unsigned)ceil_div(a.Nfull, 256), (unsigned)ceil_div(a.M, p.bm),
+              (unsigned)(nclients * p.splits));
+    // r06: a split plan reduces in-launch (the tile's last arriver, dconv_body) when the
+    // thread has ticket counters for its tiles — except a DGRAD the deferred reduction will
+    // leave to conv1's weight gradient (fh_conv_defer_dgrad: its consumer reads the
+    // splitk_epilogue slab layout)
+    bool inl = p.splits > 1 && g_tickets.p != nullptr &&
+               (int64_t)grid.x * grid.y * nclients <= g_tickets.n;
+    if constexpr (OP == OP_DGRAD && S == 1) {
+        if (inl && g_ddef.armed && w == 16 && !a.accumulate && a.bnx == nullptr &&
+            a.pidx == nullptr && p.splits <= kDgradPartsMax)
+            inl = false;
+    }
     // split launches pool in the split reduction when each of its workgroups holds one whole
-    // image plane (sp = 256), else in a separate pass after it (the caller)
-    if (p.splits > 1 && sp != 256) a.pool_y = nullptr;
+    // image plane (sp = 256), else in a separate pass after it (the caller); an in-launch
+    // reduction pools in its last arriver's epilogue
+    if (p.splits > 1 && sp != 256 && !inl) a.pool_y = nullptr;
     if (pooled) *pooled = a.pool_y != nullptr;
     // float4 weight runs: 16-B aligned slices that never run past the tensor
     a.wvec = aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0);
     float* out = a.out;
-    dim3 grid((unsigned)ceil_div(a.Nfull, 256), (unsigned)ceil_div(a.M, p.bm),
-              (unsigned)(nclients * p.splits));
-    if (p.splits > 1) a.out = (float*)ws;
+    if (inl) {
+        a.slab = (float*)ws;
+        a.tickets = g_tickets.p;
+        a.gx = (int)grid.x;
+        a.gy = (int)grid.y;
+        ++g_inl_launches;
+    } else if (p.splits > 1) {
+        a.out = (float*)ws;
+    }
     int rc;
     bool dual = false;
     if constexpr (OP == OP_DGRAD && S == 1) {
         if (g_pend.on) {
             if (g_pend.st == st && g_pend.w == w && p.bm == 32 && p.ck == 8 && a.wvec) {
-                const bool bnb = a.bn_part && p.splits == 1;
+                const bool bnb = a.bn_part && (p.splits == 1 || inl);
                 if (g_pend.pdy && w == 16 && !bnb && !a.accumulate) {
                     // the pooled gradient routed on load by both roles: dY is never written
                     a.pdy = g_pdy.p;
@@ -1855,7 +1884,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     } else if constexpr (S == 2) {
         rc = w == 16 ? dconv_launch_w<OP, 16, 2>(p, grid, a, st)
                      : dconv_launch_w<OP, 8, 2>(p, grid, a, st);
-    } else if ((a.bn_part || (a.pool_y && p.bm != 32)) && p.splits == 1) {
+    } else if ((a.bn_part || (a.pool_y && p.bm != 32)) && (p.splits == 1 || inl)) {
         // the statistics-epilogue instances (and the pooled epilogue at BM = 64, whose tile
         // image needs their LDS; at BM = 32 the plain instance pools in the K loop's LDS)
         rc = w == 32 ? dconv_launch_w<OP, 32, 1, true>(p, grid, a, st)
@@ -1871,7 +1900,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
     if constexpr (OP == OP_DGRAD && S == 1) {
         if (g_ddef.armed) {
             g_ddef.armed = false;  // the next DGRAD only
-            if (p.splits > 1 && w == 16 && !a.accumulate && a.bnx == nullptr &&
+            if (!inl && p.splits > 1 && w == 16 && !a.accumulate && a.bnx == nullptr &&
                 a.pidx == nullptr && p.splits <= kDgradPartsMax) {
                 if (const int rc = ddef_materialize()) return rc;
                 g_ddef.pending = true;
@@ -1890,7 +1919,7 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
             }
         }
     }
-    if (p.splits > 1) {
+    if (p.splits > 1 && !inl) {
         dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
@@ -2135,6 +2164,23 @@ extern "C" int fh_conv_pair(int32_t mode) {
 extern "C" int fh_conv_defer_dgrad(int32_t on) {
     g_ddef.armed = on != 0;
     if (!on) return ddef_materialize();
+    return FH_OK;
+}
+
+// r06: ticket counters for the calling thread's in-launch split-K reductions (direct 3x3
+// stride-1 FWD / DGRAD with a split plan, incl. the dual-role DGRAD): n uint32 words the caller
+// zeroed once and keeps alive while any launch (or captured step) that used them may run; each
+// launch leaves them zero.  p = NULL: split plans launch splitk_epilogue_kernel as before.
+extern "C" int fh_set_split_tickets(void* p, int64_t n) {
+    FH_REQUIRE((p == nullptr) == (n == 0) && n >= 0 && ((uintptr_t)p % 4) == 0,
+               "set_split_tickets: bad buffer");
+    g_tickets = SplitTickets{(uint32_t*)p, n};
+    return FH_OK;
+}
+
+extern "C" int fh_split_tickets_status(int64_t* inl_launches) {
+    FH_REQUIRE(inl_launches, "split_tickets_status: null pointer");
+    *inl_launches = g_inl_launches;
     return FH_OK;
 }
 

@@ -118,6 +118,13 @@ struct DConvArgs {
     int pool_hw;
     // DGRAD, the PDY instances: dY routed from a 2x2 max-pool's gradient (in is not read)
     PooledDy pdy;
+    // r06, in-launch split-K reduction (tickets non-null, splits > 1): out is the final output;
+    // each split stores its partial tile write-through into slab [tile][split][thread][FM*FN*16]
+    // and takes a ticket; the tile's last arriver sums the partials in split order and runs the
+    // unsplit epilogue (no splitk_epilogue_kernel launch).  tile = (z * gy + by) * gx + bx.
+    float* slab;
+    uint32_t* tickets;
+    int gx, gy;
 };
 
 // Pitch of the [BM channels][256 pixels] fp32 image the statistics pass reduces: 264 = 8
@@ -225,11 +232,13 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
     const int n0 = t * 256;
     // block-uniform: BN statistics of the stored values (FWD) / BN backward statistics of
     // the stored gradient (DGRAD)
-    const bool stats = BNB && a.bn_part != nullptr && a.splits == 1;
+    // r06: an in-launch split reduction ends in the unsplit epilogue (the last arriver's tile)
+    const bool inl = a.splits > 1 && a.tickets != nullptr;
+    const bool stats = BNB && a.bn_part != nullptr && (a.splits == 1 || inl);
     // the pooled epilogue's [BM][kStatPitch] image fits in the K loop's LDS (the plain
     // instance: BM = 32) or in the statistics image (the BNB instance)
     constexpr bool POOL_LDS = BNB || LDS_MAIN >= BM * kStatPitch;
-    const bool pooled = POOL_LDS && OP == OP_FWD && a.pool_y != nullptr && a.splits == 1;
+    const bool pooled = POOL_LDS && OP == OP_FWD && a.pool_y != nullptr && (a.splits == 1 || inl);
     if (n0 >= cnt * G::HW) {  // a tile past this client's images: zero statistics
         if (stats && tid < BM && m0 + tid < a.M) {
             double* q = a.bn_part + (((int64_t)z * a.M + m0 + tid) * a.bn_tiles + t) * 2;
@@ -463,7 +472,85 @@ __device__ __forceinline__ void dconv_body(const DConvArgs& a, float* smem, int 
         }
     }
 
-    const int nsplit = a.splits;
+    if (inl) {
+        // r06 in-launch split-K reduction.  This split's partial tile leaves in register order
+        // (each thread its FM*FN*16 accumulators as float4 runs) through write-through (sc1)
+        // buffer stores, so no release fence is needed; every wave drains its stores, then one
+        // lane takes the tile's ticket (agent-scope atomic).  The split whose ticket completes the
+        // tile resets it (the next launch on this stream finds it zero), acquires, and sums the
+        // S partials in split order — ((0 + p0) + p1) + ..., splitk_epilogue_kernel's order —
+        // with sc1 loads; the others are done.  MI355X_MICROARCH.md, inter-workgroup visibility.
+        constexpr int NV = FM * FN * 16;
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const int64_t tile = ((int64_t)z * a.gy + by) * a.gx + bx;
+        const int64_t part_floats = (int64_t)256 * NV;  // = BM x 256 pixels
+        float* tbase = a.slab + tile * a.splits * part_floats;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            tbase, (short)0, (int)(a.splits * part_floats * 4), 0x00020000);
+        const int own = (split * 256 + tid) * NV * 4;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const u32x4 v = {__float_as_uint(acc[i][j][4 * q]),
+                                     __float_as_uint(acc[i][j][4 * q + 1]),
+                                     __float_as_uint(acc[i][j][4 * q + 2]),
+                                     __float_as_uint(acc[i][j][4 * q + 3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rs, own + ((i * FN + j) * 16 + 4 * q) * 4,
+                                                           0, 16);
+                }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        uint32_t* flag = reinterpret_cast<uint32_t*>(smem);  // the K loop is done with the LDS
+        if (tid == 0) {
+            const uint32_t old = __hip_atomic_fetch_add(a.tickets + tile, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = old == (uint32_t)(a.splits - 1);
+            if (last) {
+                __hip_atomic_store(a.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            flag[0] = last ? 1u : 0u;
+        }
+        __syncthreads();
+        const bool last = flag[0] != 0u;
+        __syncthreads();  // the flag is read before the epilogue reuses the LDS
+        if (!last) return;
+        // the NSP partials (<= kDconvMaxSplits = 4), every load issued before the sums; a split
+        // past NSP re-reads split NSP - 1 and is dropped by a select (no load under a branch)
+        // groups of GQ float4 runs (GQ x SMAX loads in flight, 16 registers per run)
+        constexpr int SMAX = 4, NQ = NV / 4, GQ = NQ < 4 ? NQ : 4;
+        const int NSP = a.splits;
+#pragma unroll
+        for (int g0 = 0; g0 < NQ; g0 += GQ) {
+            u32x4 v[GQ][SMAX];
+#pragma unroll
+            for (int g = 0; g < GQ; ++g)
+#pragma unroll
+                for (int sp = 0; sp < SMAX; ++sp) {
+                    const int ss = sp < NSP ? sp : NSP - 1;
+                    v[g][sp] = __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, (ss * 256 + tid) * NV * 4 + (g0 + g) * 16, 0, 16);
+                }
+#pragma unroll
+            for (int g = 0; g < GQ; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int sp = 0; sp < SMAX; ++sp) {
+                        const float t = sum + __uint_as_float(v[g][sp][e]);
+                        sum = sp < NSP ? t : sum;
+                    }
+                    const int k = g0 + g;  // run k = register run q of acc[i][j]
+                    acc[k / (4 * FN)][(k / 4) % FN][4 * (k % 4) + e] = sum;
+                }
+        }
+    }
+    const int nsplit = inl ? 1 : a.splits;
 
     // ---- epilogue: lanes = 32 consecutive pixels -> coalesced stores ----
     const int rbase = 4 * h;

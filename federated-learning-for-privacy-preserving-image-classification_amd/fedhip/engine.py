@@ -150,6 +150,10 @@ class PackedTrainer:
         # restores the separate reduction launches (tests compare the two bit for bit)
         self.defer_wgrad_reduce = True
         self._slabs = None
+        # r06: split direct convolutions reduce in-launch (their tile's last workgroup) with
+        # this trainer's ticket counters (ops.SplitTickets: zeroed here, left zero by every
+        # launch); None = the split-K epilogue launches (tests compare the two)
+        self.split_tickets = ops.SplitTickets(self.device) if ops.SPLIT_TICKETS[0] else None
         # Step graphs: every step after the first of a round is replayed from a HIP graph
         # captured once per (active slots, optimizer, lr, data); the per-step inputs (batch
         # indices, counts, epoch resets, dropout key, Adam bias corrections) are copied into
@@ -251,6 +255,10 @@ class PackedTrainer:
 
     def _step_launches(self, n, counts, reset, first, adam_dev=None):
         """The kernel sequence of one packed step (no host bookkeeping: graph-capturable)."""
+        with ops.tickets_scope(self.split_tickets):
+            self._step_launches_body(n, counts, reset, first, adam_dev)
+
+    def _step_launches_body(self, n, counts, reset, first, adam_dev=None):
         net = self.net
         ce = dict(loss_out=self.loss_out, acc_loss=self.acc_loss, acc_correct=self.acc_correct,
                   acc_seen=self.acc_seen, reset=reset)

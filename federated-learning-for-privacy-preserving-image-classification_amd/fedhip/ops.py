@@ -181,6 +181,71 @@ def _ws(device) -> Workspace:
 _WS_SIZE: dict = {}
 
 
+# ---- r06: in-launch split-K reduction (fh_set_split_tickets) ------------------------------
+# Off by default (FH_SPLIT_TICKETS=1 / tests turn it on): measured r06 against the split-K
+# epilogue launches it removes, interleaved x2 — KT 290.6k -> 273.2k, K2 1.77M -> 1.70M
+# client-images/s; a solo one-client KT step 0.392 -> 0.480 ms with 8 launches fewer
+# (profiles/r06_inlaunch/): each split tile's sc1 stores, their drain, the ticket atomic and the
+# last arriver's reads and epilogue add ~15 us to the tail of a launch that the 5 us epilogue
+# launch (+ ~1.5 us boundary) costs less than (MI355X_MICROARCH.md price list: splitk-seam)
+SPLIT_TICKETS = [os.environ.get("FH_SPLIT_TICKETS", "0") == "1"]
+_TK_ACTIVE = [None]     # the SplitTickets of the step being issued (PackedTrainer)
+_TK_SET = [None]        # the buffer registered with libfedhip on this thread
+_TK_DEFAULT: dict = {}  # (device, stream) -> SplitTickets for launches outside a trainer
+
+
+class SplitTickets:
+    """Ticket counters of one launch stream's in-launch split-K reductions: one uint32 per
+    output tile of a split direct FWD / DGRAD, zeroed once here; each launch's last-arriving
+    workgroup of a tile resets its counter, so every launch leaves them zero.  A trainer owns
+    one (its steps and their captured replays run in its stream's order)."""
+    N = 1 << 16
+
+    def __init__(self, device):
+        self.t = torch.zeros(self.N, dtype=torch.int32, device=device)
+
+
+class tickets_scope:
+    def __init__(self, tk):
+        self.tk = tk
+
+    def __enter__(self):
+        self.prev = _TK_ACTIVE[0]
+        _TK_ACTIVE[0] = self.tk
+        return self.tk
+
+    def __exit__(self, *exc):
+        _TK_ACTIVE[0] = self.prev
+        return False
+
+
+def _use_tickets(device):
+    """Register the ticket counters the next direct conv launch reduces with: the issuing
+    trainer's, else (eager calls outside a trainer) this stream's default buffer; none while a
+    graph is captured outside a trainer (those launches keep the epilogue launch)."""
+    tk = None
+    if SPLIT_TICKETS[0]:
+        tk = _TK_ACTIVE[0]
+        if tk is None and not torch.cuda.is_current_stream_capturing():
+            key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+            tk = _TK_DEFAULT.get(key)
+            if tk is None:
+                tk = _TK_DEFAULT[key] = SplitTickets(device)
+    if _TK_SET[0] is not tk:
+        if tk is None:
+            call("fh_set_split_tickets", None, 0)
+        else:
+            call("fh_set_split_tickets", ptr(tk.t), tk.t.numel())
+        _TK_SET[0] = tk
+
+
+def split_tickets_status():
+    """Launches of this thread that reduced their split-K in-launch (fh_split_tickets_status)."""
+    n = ctypes.c_int64()
+    call("fh_split_tickets_status", ctypes.byref(n))
+    return n.value
+
+
 def copy_bytes(src: torch.Tensor, dst: torch.Tensor):
     """dst <- src (same byte size, contiguous, 16-B multiple) by fh_copy_bytes on the
     current stream."""
@@ -440,6 +505,7 @@ def conv2d_fwd(x, w, bias, y, nclients, batch, cin, h, wd, cout, k, stride, pad,
     require_device(x, "x")
     ws, nb = _ws_for("fh_conv2d_fwd_workspace", x.device, nclients, batch, cin, h, wd, cout, k, k,
                      stride, pad)
+    _use_tickets(x.device)
     ev = PROBE.begin(_conv_tag("fwd", cin, h, wd, cout, k, stride))
     if bn_stats is not None:
         if relu or k != 3 or stride != 1 or pad != 1:
@@ -472,6 +538,7 @@ def conv2d_fwd_relu_pool(x, w, bias, y, py, pidx, nclients, batch, cin, h, cout,
     require_device(x, "x")
     ws, nb = _ws_for("fh_conv2d_fwd_workspace", x.device, nclients, batch, cin, h, h, cout, 3, 3,
                      1, 1)
+    _use_tickets(x.device)
     ah, _ = _alg_map(h, h, alg_hw, 3, 1, 1)
     tag = _conv_tag("fwd", cin, ah, ah, cout, 3, 1)
     _note_exec(tag, h, h, ah, ah)
@@ -494,6 +561,7 @@ def conv2d_dgrad(dy, w, dx, nclients, batch, cin, h, wd, cout, k, stride, pad, c
     is bn_bwd_pool_tiles."""
     ws, nb = _ws_for("fh_conv2d_dgrad_workspace", dy.device, nclients, batch, cin, h, wd, cout, k,
                      k, stride, pad)
+    _use_tickets(dy.device)
     ah, aw = _alg_map(h, wd, alg_hw, k, stride, pad)
     tag = _conv_tag("dgrad", cin, ah, aw, cout, k, stride)
     _note_exec(tag, h, wd, ah, aw)

@@ -710,6 +710,17 @@ int fh_conv_defer_dgrad(int32_t on);
 /* r06 (instrumentation): DGRADs the calling thread left unreduced under fh_conv_defer_dgrad, and
  * how many of those partial slabs a conv1 weight-gradient consumer summed while staging. */
 int fh_conv_defer_status(int64_t* deferred, int64_t* taken);
+/* r06: in-launch split-K reduction.  A direct 3x3 FWD / DGRAD (and the DGRAD role of the
+ * dual-role backward) whose plan splits the input-channel reduction stores each split's partial
+ * tile write-through and takes a ticket; the tile's last arriving workgroup sums the partials in
+ * split order and runs the unsplit epilogue (bias, ReLU, BN statistics, pool) — no
+ * splitk_epilogue launch.  `tickets` = n uint32 counters (one per output tile of a launch),
+ * zeroed ONCE by the caller, kept alive while launches or captured steps that used them may run,
+ * and left zero by every launch; per calling thread (one buffer per stream: concurrent launches
+ * must not share counters).  NULL / 0 = split-K epilogue launches as before. */
+int fh_set_split_tickets(void* tickets, int64_t n);
+/* launches of the calling thread that reduced their split-K in-launch (instrumentation) */
+int fh_split_tickets_status(int64_t* inl_launches);
 /* The next WGRAD + DGRAD pair's output gradient is a 2x2 max-pool's backward (SimpleCNN conv2,
  * models_pytorch.py:88-90, pool2 after relu(conv2)): dY(y, x) = dpool[y/2][x/2] where (y, x) is
  * the window's argmax pidx and the pooled ReLU output ypool there is > 0, else 0
