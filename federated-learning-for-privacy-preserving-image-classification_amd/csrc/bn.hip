@@ -16,6 +16,7 @@
 // Fused: the ReLU that follows BN (forward) and its mask (backward, g = dy*(y>0)),
 // and the ResNet residual add (forward) / residual-branch gradient (backward).
 #include "fh_common.h"
+#include "splitbn.h"
 
 namespace fh {
 
@@ -510,6 +511,391 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const BNArgs a) {
     });
 }
 
+// ---------------------------------------------------------------------------
+// r06: a split conv's reduction + the BatchNorm call after it as one launch (splitbn.h).
+// One 1024-thread workgroup per (channel, client): its four 256-thread groups take the
+// channel's 256-element tiles in turn — the slab summed in split order, the tile's statistics
+// pair formed as splitk_epilogue_kernel forms it (wave sums, then (w0 + w1) + (w2 + w3)) — and
+// wave 0 merges the tiles as merge() does.  Everything stored is bit-identical to the
+// epilogue launch + bn_finalize / maxpool2_bnfin / bn_bwd_apply pair it replaces.
+constexpr int kSbnTpt = 8;  // tiles per 256-thread group in flight per pass
+// Every global load of these kernels is unconditional (indices clamped into the tensor, the
+// value discarded by a select): a load under a branch is joined by a phi whose wait drains
+// the memory pipe — one dependent round trip per load (r06 first version: 4-8 per pass).
+
+struct SbnFwd {
+    SplitBnRec r;
+    BNArgs a;  // the finalize's parameters (gamma, beta, running / saved statistics, C, HW)
+    float* scale;
+    float* shift;
+    int64_t s_cs;
+    int ntile;
+    FastDiv fd_sp;
+    // 2x2 max-pool (+ dropout) of relu(y * scale + shift): maxpool2_bnfin_kernel's outputs
+    int pool;
+    float* y;
+    int64_t y_cs;
+    uint8_t* idx;
+    int64_t i_cs;
+    uint8_t* mask;
+    int64_t m_cs;
+    int H, W, drop_mode;
+    FastDiv fd_ohw, fd_ow;
+    float keep_prob, dscale;
+    uint64_t seed_salt;
+    const uint64_t* seed_dev;
+};
+
+struct SbnBwd {
+    SplitBnRec r;
+    BNArgs a;  // the apply's parameters (x, gamma, beta, saved statistics, dx, dgamma, dbeta)
+    int ntile;
+    FastDiv fd_sp, fd_pw;  // the DGRAD's plane (sp) and, pooled, its width
+};
+
+// Tile statistics without cross-lane trees per tile (r06 second version: 8 tiles x 2
+// xor-butterflies of ds_bpermute per thread dominated the 16x16 launches).  The epilogue's
+// tile pair is (w0 + w1) + (w2 + w3) over the tile's four 64-element chunks, each wN the
+// xor-butterfly wave_sum — whose value is the fixed tree x[i] += x[i + h], h = 32, 16, ..., 1.
+// The per-element values sit in LDS (v0; v1 or v0^2 for the second moment) and all 1024
+// threads build every chunk's tree level by level in T: the same sums in the same order.
+using SbnTree = double[2][kSbnMaxTiles * 4][16];
+
+template <bool SQ>
+__device__ __forceinline__ void sbn_tree(const float* v0, const float* v1, int nch, SbnTree& T) {
+    const int tid = threadIdx.x;
+    for (int it = tid; it < 2 * nch * 16; it += 1024) {  // levels h = 32 and 16 from LDS
+        const int st = it >= nch * 16, rem = it - st * nch * 16, ch = rem >> 4, i = rem & 15;
+        const int b = ch * 64 + i;
+        double x0, x1, x2, x3;
+        if (st == 0 || SQ) {
+            x0 = v0[b]; x1 = v0[b + 32]; x2 = v0[b + 16]; x3 = v0[b + 48];
+            if (st) { x0 = x0 * x0; x1 = x1 * x1; x2 = x2 * x2; x3 = x3 * x3; }
+        } else {
+            x0 = v1[b]; x1 = v1[b + 32]; x2 = v1[b + 16]; x3 = v1[b + 48];
+        }
+        T[st][ch][i] = (x0 + x1) + (x2 + x3);
+    }
+#pragma unroll
+    for (int h = 8; h >= 1; h >>= 1) {
+        __syncthreads();
+        for (int it = tid; it < 2 * nch * h; it += 1024) {
+            const int st = it >= nch * h, rem = it - st * nch * h, ch = rem / h, i = rem - ch * h;
+            T[st][ch][i] = T[st][ch][i] + T[st][ch][i + h];
+        }
+    }
+    __syncthreads();
+}
+
+// the tiles' statistics pairs -> (sum0, sum1) in wave 0 (merge()'s order)
+__device__ __forceinline__ void sbn_merge(const SbnTree& T, int ntile, double& s0, double& s1) {
+    s0 = 0.0;
+    s1 = 0.0;
+    for (int i = threadIdx.x & 63; i < ntile; i += 64) {
+        s0 += (T[0][4 * i][0] + T[0][4 * i + 1][0]) + (T[0][4 * i + 2][0] + T[0][4 * i + 3][0]);
+        s1 += (T[1][4 * i][0] + T[1][4 * i + 1][0]) + (T[1][4 * i + 2][0] + T[1][4 * i + 3][0]);
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+}
+
+// this thread's kSbnTpt slab values per split (clamped loads; splits <= 4)
+__device__ __forceinline__ void sbn_load_slab(const SplitBnRec& r, const float* pz, int64_t ss,
+                                              int t0, int grp, int lt, float (&v)[kSbnTpt][4]) {
+    const int nlast = (int)r.Nfull - 1, jl = r.splits - 1;
+#pragma unroll
+    for (int k = 0; k < kSbnTpt; ++k) {
+        const int nc = min((t0 + 4 * k + grp) * 256 + lt, nlast);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[k][j] = pz[min(j, jl) * ss + nc];
+    }
+}
+
+// splitk_epilogue_kernel's sum: 0 + p0 + p1 + ... in split order
+__device__ __forceinline__ float sbn_sum(const float (&v)[4], int splits) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (j < splits) s += v[j];
+    return s;
+}
+
+__global__ void __launch_bounds__(1024) split_bnfin_kernel(const SbnFwd f) {
+    __shared__ float ybuf[kSbnMaxElems];  // y, zero past the client's images
+    __shared__ SbnTree T;
+    __shared__ float s_aff[2];
+    const SplitBnRec& r = f.r;
+    const BNArgs& a = f.a;
+    const int c = blockIdx.x, z = blockIdx.y;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int nvalid = cnt * r.sp;
+    const int tid = threadIdx.x, grp = tid >> 8, lt = tid & 255, lane = tid & 63;
+    const float* pz = r.part + ((int64_t)z * r.splits * r.M + c) * r.Nfull;
+    const int64_t ss = (int64_t)r.M * r.Nfull;
+    const float bv = r.bias ? r.bias[z * r.b_cs + c] : 0.f;
+    float* oz = r.out + z * r.out_cs;
+    for (int t0 = 0; t0 < f.ntile; t0 += 4 * kSbnTpt) {
+        float v[kSbnTpt][4];
+        sbn_load_slab(r, pz, ss, t0, grp, lt, v);
+#pragma unroll
+        for (int k = 0; k < kSbnTpt; ++k) {
+            const int t = t0 + 4 * k + grp;
+            if (t >= f.ntile) break;  // uniform over the 256-thread group
+            const int n = t * 256 + lt;
+            const bool ok = n < nvalid;
+            float s = sbn_sum(v[k], r.splits);
+            if (r.bias) s = s + bv;
+            if (ok) {
+                uint32_t img, pix;
+                f.fd_sp.divmod((uint32_t)n, img, pix);
+                oz[((int64_t)img * r.M + c) * r.sp + pix] = s;
+            }
+            ybuf[n] = ok ? s : 0.f;
+        }
+    }
+    __syncthreads();
+    sbn_tree<true>(ybuf, nullptr, 4 * f.ntile, T);
+    if (tid < 64) {  // bn_finalize_kernel's operations
+        double sum, sq;
+        sbn_merge(T, f.ntile, sum, sq);
+        if (lane == 0) {
+            const int64_t n = (int64_t)cnt * a.HW;
+            const double mean = n > 0 ? sum / (double)n : 0.0;
+            double var = n > 0 ? sq / (double)n - mean * mean : 0.0;
+            if (var < 0.0) var = 0.0;
+            const double invstd = n > 0 ? 1.0 / sqrt(var + (double)a.eps) : 0.0;
+            const float meanf = (float)mean, invstdf = (float)invstd;
+            a.save_mean[z * a.C + c] = meanf;
+            a.save_invstd[z * a.C + c] = invstdf;
+            if (a.rmean && n > 0) {
+                const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+                float* rm = a.rmean + z * a.r_cs + c;
+                float* rv = a.rvar + z * a.r_cs + c;
+                *rm = (float)((double)a.momentum * mean + (1.0 - (double)a.momentum) * (double)*rm);
+                *rv = (float)((double)a.momentum * unb + (1.0 - (double)a.momentum) * (double)*rv);
+            }
+            const float alpha = invstdf * a.gamma[z * a.p_cs + c];
+            const float bconst = a.beta[z * a.p_cs + c] - meanf * alpha;
+            f.scale[z * f.s_cs + c] = alpha;
+            f.shift[z * f.s_cs + c] = bconst;
+            s_aff[0] = alpha;
+            s_aff[1] = bconst;
+        }
+    }
+    if (!f.pool) return;  // launch-uniform
+    __syncthreads();
+    // maxpool2_bnfin_kernel's pool of relu(y * alpha + beta') from the tile values in LDS
+    const float s = s_aff[0], t = s_aff[1];
+    const int ohw = (f.H / 2) * (f.W / 2);
+    const uint64_t seed = f.seed_salt + (f.seed_dev ? *f.seed_dev : 0ull);
+    const uint64_t prow = f.drop_mode == 1 ? philox_row(f.seed_dev, z) : 0ull;
+    for (int q = tid; q < cnt * ohw; q += 1024) {
+        uint32_t img, rr, oh, ow;
+        f.fd_ohw.divmod((uint32_t)q, img, rr);
+        f.fd_ow.divmod(rr, oh, ow);
+        const int64_t e = ((int64_t)img * a.C + c) * ohw + rr;
+        const float* pp = ybuf + img * a.HW + (2 * oh) * f.W + 2 * ow;
+        const float v0 = fmaxf(pp[0] * s + t, 0.f), v1 = fmaxf(pp[1] * s + t, 0.f);
+        const float v2 = fmaxf(pp[f.W] * s + t, 0.f), v3 = fmaxf(pp[f.W + 1] * s + t, 0.f);
+        float m = v0;
+        int am = 0;
+        if (v1 > m) { m = v1; am = 1; }
+        if (v2 > m) { m = v2; am = 2; }
+        if (v3 > m) { m = v3; am = 3; }
+        f.idx[z * f.i_cs + e] = (uint8_t)am;
+        if (f.drop_mode) {
+            uint8_t keep;
+            if (f.drop_mode == 1) {
+                const uint4 rn = Philox::gen(seed, prow, (uint64_t)e);
+                keep = u01(rn.x) <= f.keep_prob ? 1 : 0;
+                f.mask[z * f.m_cs + e] = keep;
+            } else {
+                keep = f.mask[z * f.m_cs + e];
+            }
+            m = keep ? m * f.dscale : 0.f;
+        }
+        f.y[z * f.y_cs + e] = m;
+    }
+}
+
+// Q: float4 quads per thread of the apply pass (cnt * HW <= Q * 4096), prefetched before the
+// statistics merge so their loads overlap it
+template <int Q, bool POOLED>
+__global__ void __launch_bounds__(1024) split_bnbwd_kernel(const SbnBwd b) {
+    __shared__ float gs[kSbnMaxElems];  // the masked gradient g (zero past the images)
+    __shared__ float ps[kSbnMaxElems];  // (x - mean) * g
+    __shared__ float gbuf[POOLED ? kSbnMaxElems : 1];    // pooled: the routed value gu
+    __shared__ uint8_t cbuf[POOLED ? kSbnMaxElems : 1];  // pooled: window argmax
+    __shared__ SbnTree T;
+    __shared__ double s_st[2];
+    const SplitBnRec& r = b.r;
+    const BNArgs& a = b.a;
+    const int c = blockIdx.x, z = blockIdx.y;
+    const int cnt = a.counts ? a.counts[z] : a.batch;
+    const int nvalid = cnt * r.sp;
+    const int tid = threadIdx.x, grp = tid >> 8, lt = tid & 255, lane = tid & 63;
+    constexpr bool pooled = POOLED;
+    const float* pz = r.part + ((int64_t)z * r.splits * r.M + c) * r.Nfull;
+    const int64_t ss = (int64_t)r.M * r.Nfull;
+    const float esc = r.bn_scale[z * r.bns_cs + c], esh = r.bn_shift[z * r.bns_cs + c];
+    const float emean = r.bn_mean[z * r.M + c];
+    const float* bx = r.bnx + z * r.bnx_cs;
+    // pooled: the keep-mask if any, else the argmax bytes again (a valid read, ignored)
+    const uint8_t* pk = !POOLED ? nullptr : r.pmask ? r.pmask + z * r.pm_cs : r.pidx + z * r.pi_cs;
+    const bool km = r.pmask != nullptr;
+    const int nlast = (int)r.Nfull - 1;
+    for (int t0 = 0; t0 < b.ntile; t0 += 4 * kSbnTpt) {
+        float v[kSbnTpt][4], xv[kSbnTpt];
+        int code[kSbnTpt];
+        bool keep[kSbnTpt];
+        sbn_load_slab(r, pz, ss, t0, grp, lt, v);
+#pragma unroll
+        for (int k = 0; k < kSbnTpt; ++k) {
+            const int nc = min((t0 + 4 * k + grp) * 256 + lt, nlast);
+            uint32_t img, pix;
+            b.fd_sp.divmod((uint32_t)nc, img, pix);
+            const int64_t e = ((int64_t)img * r.M + c) * r.sp + pix;
+            if constexpr (POOLED) {
+                code[k] = r.pidx[z * r.pi_cs + e];
+                keep[k] = (pk[e] != 0) | !km;
+                xv[k] = 0.f;
+            } else {
+                code[k] = 0;
+                keep[k] = true;
+                xv[k] = bx[e];
+            }
+        }
+        if constexpr (POOLED) {  // the BN input at each window's argmax (splitk_epilogue_kernel's read)
+#pragma unroll
+            for (int k = 0; k < kSbnTpt; ++k) {
+                const int nc = min((t0 + 4 * k + grp) * 256 + lt, nlast);
+                uint32_t img, pix, py, px;
+                b.fd_sp.divmod((uint32_t)nc, img, pix);
+                b.fd_pw.divmod(pix, py, px);
+                xv[k] = bx[((int64_t)img * r.M + c) * 4 * r.sp +
+                           (2 * py + (code[k] >> 1)) * (2 * r.pw) + 2 * px + (code[k] & 1)];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSbnTpt; ++k) {
+            const int t = t0 + 4 * k + grp;
+            if (t >= b.ntile) break;  // uniform over the 256-thread group
+            const int n = t * 256 + lt;
+            const bool ok = n < nvalid;
+            const float s = sbn_sum(v[k], r.splits);
+            float gu = s;
+            if (pooled && r.pmask) gu = keep[k] ? s * r.pscale : 0.f;
+            const float g = (xv[k] * esc + esh > 0.f) ? gu : 0.f;
+            const float d1f = (xv[k] - emean) * g;
+            gs[n] = ok ? g : 0.f;
+            ps[n] = ok ? d1f : 0.f;
+            if constexpr (POOLED) {
+                gbuf[n] = gu;
+                cbuf[n] = (uint8_t)code[k];
+            }
+        }
+    }
+    // the apply pass's x, in flight across the merge
+    const int ntot = cnt * a.HW;
+    const float* xz = a.x + z * a.x_cs;
+    const int64_t istride = (int64_t)a.C * a.HW, coff = (int64_t)c * a.HW;
+    float4 xq[Q];
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+        const int e = max(min(tid * 4 + i * 4096, ntot - 4), 0);
+        uint32_t img, p;
+        a.fd_hw.divmod((uint32_t)e, img, p);
+        xq[i] = ld4(xz + img * istride + coff + p);
+    }
+    __syncthreads();
+    sbn_tree<false>(gs, ps, 4 * b.ntile, T);
+    if (tid < 64) {
+        double sg, dot;
+        sbn_merge(T, b.ntile, sg, dot);
+        if (lane == 0) {
+            s_st[0] = sg;
+            s_st[1] = dot;
+        }
+    }
+    __syncthreads();
+    // bn_bwd_apply_kernel's operations over the channel's full-resolution elements
+    const double sg = s_st[0], dot = s_st[1];
+    const int64_t n = (int64_t)cnt * a.HW;
+    const float mean = a.save_mean[z * a.C + c], invstd = a.save_invstd[z * a.C + c];
+    if (tid == 0) {
+        if (a.dgamma) a.dgamma[z * a.g_cs + c] = (float)(dot * (double)invstd);
+        if (a.dbeta) a.dbeta[z * a.g_cs + c] = (float)sg;
+    }
+    if (!a.dx) return;
+    const float w = a.gamma[z * a.p_cs + c];
+    const float k = n > 0 ? (float)(dot * (double)invstd * (double)invstd / (double)n) : 0.f;
+    const float gm = n > 0 ? (float)(sg / (double)n) : 0.f;
+    float alpha = 0.f, bconst = 0.f;  // ReluMask mode 2 (pooled: recomputed from x)
+    if (pooled) {
+        alpha = invstd * a.gamma[z * a.p_cs + c];
+        bconst = a.beta[z * a.p_cs + c] - mean * alpha;
+    }
+    float* dxz = a.dx + z * a.dx_cs;
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+        const int e = tid * 4 + i * 4096;
+        if (e >= ntot) break;
+        uint32_t img, p;
+        a.fd_hw.divmod((uint32_t)e, img, p);
+        const int64_t o = img * istride + coff + p;
+        const float4 xv = xq[i];
+        float4 g;
+        if (pooled) {
+            uint32_t y, x;
+            a.fd_w.divmod(p, y, x);
+            const int pe = img * r.sp + (y >> 1) * r.pw + (x >> 1);
+            const int c0 = cbuf[pe], c1 = cbuf[pe + 1];
+            const float g0 = gbuf[pe], g1 = gbuf[pe + 1];
+            const int rr = (y & 1) << 1;
+            g = make_float4(c0 == rr ? g0 : 0.f, c0 == (rr | 1) ? g0 : 0.f, c1 == rr ? g1 : 0.f,
+                            c1 == (rr | 1) ? g1 : 0.f);
+            float4 m;
+            m.x = xv.x * alpha + bconst; m.y = xv.y * alpha + bconst;
+            m.z = xv.z * alpha + bconst; m.w = xv.w * alpha + bconst;
+            g.x = m.x > 0.f ? g.x : 0.f; g.y = m.y > 0.f ? g.y : 0.f;
+            g.z = m.z > 0.f ? g.z : 0.f; g.w = m.w > 0.f ? g.w : 0.f;
+        } else {
+            g = make_float4(gs[e], gs[e + 1], gs[e + 2], gs[e + 3]);
+        }
+        float4 rv;
+        rv.x = (((g.x - gm) - (xv.x - mean) * k) * invstd) * w;
+        rv.y = (((g.y - gm) - (xv.y - mean) * k) * invstd) * w;
+        rv.z = (((g.z - gm) - (xv.z - mean) * k) * invstd) * w;
+        rv.w = (((g.w - gm) - (xv.w - mean) * k) * invstd) * w;
+        st4(dxz + o, rv);
+    }
+}
+
+// the apply pass's quads per thread: 2 (<= 8192 elements per client-channel) or 8 (<= 32768)
+static int sbn_bwd_launch(SbnBwd& b, int C, int nclients, int batch, int HW, hipStream_t st) {
+    b.fd_sp = FastDiv((uint32_t)b.r.sp);
+    b.fd_pw = FastDiv((uint32_t)std::max(b.r.pw, 1));
+    const bool pooled = b.r.pidx != nullptr;
+    if ((int64_t)batch * HW <= 2 * 4096) {
+        if (pooled)
+            FH_LAUNCH((split_bnbwd_kernel<2, true>), dim3((unsigned)C, nclients), dim3(1024), 0, st, b);
+        else
+            FH_LAUNCH((split_bnbwd_kernel<2, false>), dim3((unsigned)C, nclients), dim3(1024), 0, st, b);
+    } else {
+        FH_REQUIRE(pooled && (int64_t)batch * HW <= 8 * 4096, "split bn backward: %d x %d", batch, HW);
+        FH_LAUNCH((split_bnbwd_kernel<8, true>), dim3((unsigned)C, nclients), dim3(1024), 0, st, b);
+    }
+    return FH_OK;
+}
+
+// fused launches issued (fh_conv_bn_defer_status)
+thread_local int64_t g_sbn_taken = 0;
+
+// a pending split record nobody here consumes: launch its epilogue first
+static int sbn_settle() { return sbn_rec().pending ? sbn_materialize() : FH_OK; }
+
+int64_t sbn_taken() { return g_sbn_taken; }
+
 static void bn_geometry(int nclients, int batch, int C, int HW, int& S, int& chunk) {
     const int64_t nmax = (int64_t)batch * HW;
     int64_t want = ceil_div(2048, (int64_t)C * std::max(nclients, 1));
@@ -553,6 +939,7 @@ extern "C" int fh_bn_fwd_train(const float* x, int64_t x_cs, float* y, int64_t y
                                int32_t relu, void* workspace, size_t ws_bytes, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_train: bad shape");
     if (nclients == 0) return FH_OK;
+    if (const int rc = sbn_settle()) return rc;
     FH_REQUIRE(x && y && gamma && beta && save_mean && save_invstd, "bn_fwd_train: null pointer");
     FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "bn_fwd_train: running stats");
     const size_t need = fh_bn_workspace(nclients, batch, C, HW);
@@ -581,6 +968,7 @@ extern "C" int fh_bn_fwd_stats(const float* x, int64_t x_cs, const float* gamma,
                                void* workspace, size_t ws_bytes, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_stats: bad shape");
     if (nclients == 0) return FH_OK;
+    if (const int rc = sbn_settle()) return rc;
     FH_REQUIRE(x && gamma && beta && save_mean && save_invstd && scale_out && shift_out,
                "bn_fwd_stats: null pointer");
     FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "bn_fwd_stats: running stats");
@@ -626,6 +1014,26 @@ extern "C" int fh_bn_finalize_tiles(const double* part, const float* gamma, cons
     a.save_invstd = save_invstd;
     a.p_cs = p_cs; a.r_cs = r_cs;
     a.eps = eps; a.momentum = momentum;
+    SplitBnRec& r = sbn_rec();
+    if (r.pending) {
+        if (r.op == 0 && r.bn_part == part && r.st == as_stream(stream) && r.M == C &&
+            r.sp == HW && r.nclients == nclients && r.batch == batch && r.counts == counts) {
+            // the split conv's reduction and this finalize: one launch (splitbn.h)
+            SbnFwd f{};
+            f.r = r;
+            f.a = a;
+            f.scale = scale_out; f.shift = shift_out; f.s_cs = s_cs;
+            f.ntile = a.SP;
+            f.fd_sp = FastDiv((uint32_t)HW);
+            r.pending = false;
+            FH_LAUNCH(split_bnfin_kernel, dim3((unsigned)C, nclients), dim3(1024), 0,
+                      as_stream(stream), f);
+            FH_LAUNCH_CHECK("bn_finalize_tiles (split conv reduction)");
+            ++g_sbn_taken;
+            return FH_OK;
+        }
+        if (const int rc = sbn_materialize()) return rc;
+    }
     FH_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(C, 4), nclients), dim3(256), 0,
               as_stream(stream), a, scale_out, shift_out, s_cs);
     FH_LAUNCH_CHECK("bn_finalize_tiles");
@@ -646,6 +1054,7 @@ extern "C" int fh_bn_apply_tiles(const double* part, const float* x, int64_t x_c
                                  float eps, float momentum, int32_t relu, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_apply_tiles: bad shape");
     if (nclients == 0) return FH_OK;
+    if (const int rc = sbn_settle()) return rc;
     FH_REQUIRE(part && x && y && gamma && beta && save_mean && save_invstd,
                "bn_apply_tiles: null pointer");
     FH_REQUIRE((running_mean == nullptr) == (running_var == nullptr),
@@ -693,6 +1102,32 @@ extern "C" int fh_maxpool2_fwd_bnfinalize(
     const int64_t per_ch = (int64_t)batch * (H / 2) * (W / 2);
     const int bpc = (int)std::max<int64_t>(1, ceil_div(per_ch, 256 * kPoolEpt));
     const float keep = 1.0f - p_drop;
+    SplitBnRec& r = sbn_rec();
+    if (r.pending) {
+        if (r.op == 0 && r.bn_part == part && r.st == as_stream(stream) && r.M == C &&
+            r.sp == H * W && r.out == x && r.out_cs == x_cs && r.nclients == nclients &&
+            r.batch == batch && r.counts == counts) {
+            SbnFwd f{};
+            f.r = r;
+            f.a = a;
+            f.scale = scale_out; f.shift = shift_out; f.s_cs = s_cs;
+            f.ntile = a.SP;
+            f.pool = 1;
+            f.y = y; f.y_cs = y_cs; f.idx = idx; f.i_cs = i_cs; f.mask = mask; f.m_cs = m_cs;
+            f.H = H; f.W = W; f.drop_mode = drop_mode; f.keep_prob = keep; f.dscale = 1.0f / keep;
+            f.seed_salt = seed; f.seed_dev = seed_dev;
+            f.fd_sp = FastDiv((uint32_t)(H * W));
+            f.fd_ohw = FastDiv((uint32_t)((H / 2) * (W / 2)));
+            f.fd_ow = FastDiv((uint32_t)(W / 2));
+            r.pending = false;
+            FH_LAUNCH(split_bnfin_kernel, dim3((unsigned)C, nclients), dim3(1024), 0,
+                      as_stream(stream), f);
+            FH_LAUNCH_CHECK("maxpool2_fwd_bnfinalize (split conv reduction)");
+            ++g_sbn_taken;
+            return FH_OK;
+        }
+        if (const int rc = sbn_materialize()) return rc;
+    }
     FH_LAUNCH(maxpool2_bnfin_kernel, dim3((unsigned)(C * bpc), nclients), dim3(256), 0,
               as_stream(stream), a, scale_out, shift_out, s_cs, x, x_cs, y, y_cs, idx, i_cs,
               mask, m_cs, H, W, drop_mode, keep, 1.0f / keep, seed, seed_dev, bpc);
@@ -708,6 +1143,7 @@ extern "C" int fh_bn_fwd_eval(const float* x, int64_t x_cs, float* y, int64_t y_
                               int32_t relu, void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_fwd_eval: bad shape");
     if (nclients == 0) return FH_OK;
+    if (const int rc = sbn_settle()) return rc;
     FH_REQUIRE(x && y && gamma && beta && running_mean && running_var, "bn_fwd_eval: null pointer");
     BNArgs a = bn_args(nclients, batch, C, HW, counts);
     a.x = x; a.y = y; a.res = res; a.gamma = gamma; a.beta = beta;
@@ -729,6 +1165,7 @@ extern "C" int fh_bn_bwd(const float* dy, int64_t dy_cs, const float* yout, int6
                          void* stream) {
     FH_REQUIRE(nclients >= 0 && batch > 0 && C > 0 && HW > 0, "bn_bwd: bad shape");
     if (nclients == 0) return FH_OK;
+    if (const int rc = sbn_settle()) return rc;
     FH_REQUIRE(dy && x && gamma && save_mean && save_invstd, "bn_bwd: null pointer");
     FH_REQUIRE(!relu || yout || beta, "bn_bwd: relu needs the forward output or beta");
     const size_t need = fh_bn_workspace(nclients, batch, C, HW);
@@ -765,6 +1202,7 @@ extern "C" int fh_bn_bwd_pool(const float* dpool, int64_t dp_cs, const uint8_t* 
                "bn_bwd_pool: bad shape");
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "bn_bwd_pool: p=%g", p_drop);
     if (nclients == 0) return FH_OK;
+    if (const int rc = sbn_settle()) return rc;
     FH_REQUIRE(dpool && pidx && x && gamma && save_mean && save_invstd, "bn_bwd_pool: null pointer");
     FH_REQUIRE(!relu || yout || beta, "bn_bwd_pool: relu needs the forward output or beta");
     const int HW = H * W;
@@ -811,6 +1249,26 @@ extern "C" int fh_bn_bwd_tiles(const double* part, const float* g, int64_t g_cs_
     a.dx = dx; a.dgamma = dgamma; a.dbeta = dbeta;
     a.dy_cs = g_cs_; a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs; a.g_cs = dg_cs;
     a.relu = 0;  // g is already masked
+    SplitBnRec& r = sbn_rec();
+    if (r.pending) {
+        if (r.op == 1 && !r.pidx && r.bn_part == part && r.st == as_stream(stream) && r.M == C &&
+            r.sp == HW && r.out == g && r.out_cs == g_cs_ && r.nclients == nclients &&
+            r.batch == batch && r.counts == counts && a.vec) {
+            // the split DGRAD's reduction + its BN-backward statistics and this apply: one
+            // launch; g itself is never stored (only this apply read it)
+            SbnBwd b{};
+            b.r = r;
+            b.a = a;
+            b.ntile = a.SP;
+            r.pending = false;
+            if (const int rc = sbn_bwd_launch(b, C, nclients, batch, HW, as_stream(stream)))
+                return rc;
+            FH_LAUNCH_CHECK("bn_bwd_tiles (split conv reduction)");
+            ++g_sbn_taken;
+            return FH_OK;
+        }
+        if (const int rc = sbn_materialize()) return rc;
+    }
     FH_LAUNCH(bn_bwd_apply_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
     FH_LAUNCH_CHECK("bn_bwd_tiles");
     return FH_OK;
@@ -846,6 +1304,26 @@ extern "C" int fh_bn_bwd_pool_tiles(const double* part, const float* dpool, int6
     a.x = x; a.gamma = gamma; a.beta = beta; a.save_mean = (float*)save_mean;
     a.save_invstd = (float*)save_invstd; a.dx = dx; a.dgamma = dgamma; a.dbeta = dbeta;
     a.x_cs = x_cs; a.p_cs = p_cs; a.dx_cs = dx_cs; a.g_cs = g_cs; a.relu = 1;
+    SplitBnRec& r = sbn_rec();
+    if (r.pending) {
+        if (r.op == 1 && r.pidx == pidx && r.pmask == pmask && r.pi_cs == pi_cs &&
+            r.pm_cs == pm_cs && r.pscale == a.pscale && r.bn_part == part &&
+            r.st == as_stream(stream) && r.M == C && 4 * r.sp == HW && 2 * r.pw == W &&
+            r.out == dpool && r.out_cs == dp_cs && r.nclients == nclients && r.batch == batch &&
+            r.counts == counts && a.vec) {
+            SbnBwd b{};
+            b.r = r;
+            b.a = a;
+            b.ntile = a.SP;
+            r.pending = false;
+            if (const int rc = sbn_bwd_launch(b, C, nclients, batch, HW, as_stream(stream)))
+                return rc;
+            FH_LAUNCH_CHECK("bn_bwd_pool_tiles (split conv reduction)");
+            ++g_sbn_taken;
+            return FH_OK;
+        }
+        if (const int rc = sbn_materialize()) return rc;
+    }
     FH_LAUNCH(bn_bwd_apply_kernel, dim3(a.S, C, nclients), dim3(256), 0, as_stream(stream), a);
     FH_LAUNCH_CHECK("bn_bwd_pool_tiles");
     return FH_OK;

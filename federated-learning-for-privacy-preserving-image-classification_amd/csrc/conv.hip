@@ -20,6 +20,7 @@
 // v_mfma_f32_32x32x2_f32 (exact fp32, 64 cyc/SIMD) is the MAC engine; each
 // wave owns an FM x FN grid of 32x32 accumulators.
 #include "fh_common.h"
+#include "splitbn.h"
 
 #include <cstdlib>
 
@@ -1717,6 +1718,32 @@ thread_local DgradDefer g_ddef;
 // summed while staging (the rest were materialised by the skipped epilogue launch)
 thread_local int64_t g_ddef_deferred = 0, g_ddef_taken = 0;
 
+// Split reduction left to the BatchNorm call after the conv (fh_conv_bn_defer, r06,
+// splitbn.h): armed by the host for the next fh_conv2d_{fwd,dgrad}_bnstats call, recorded by
+// run_dconv in place of its splitk_epilogue_kernel launch, consumed by the BN call (bn.hip);
+// anything else that finds it pending launches the skipped epilogue (sbn_materialize).
+thread_local SplitBnRec g_sbn;
+thread_local int g_sbn_armed = 0;  // fh_conv_bn_defer(max) -> the next _bnstats call
+thread_local int g_sbn_want = 0;   // ... inside that call
+thread_local int64_t g_sbn_deferred = 0;
+
+SplitBnRec& sbn_rec() { return g_sbn; }
+
+int sbn_materialize() {
+    if (!g_sbn.pending) return FH_OK;
+    g_sbn.pending = false;
+    const SplitBnRec& r = g_sbn;
+    dim3 eg((unsigned)ceil_div(r.Nfull, 256), (unsigned)r.M, (unsigned)r.nclients);
+    FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, r.st, r.part, r.splits, r.M, (int)r.Nfull,
+              r.out, r.out_cs, r.bias, r.b_cs, 0, 0, r.counts, r.batch, r.sp, r.bn_part,
+              r.bn_tiles, DropArgs{},
+              BnBwdEpi{r.bnx, r.bnx_cs, r.bn_scale, r.bn_shift, r.bns_cs, r.bn_mean, r.pidx,
+                       r.pmask, r.pi_cs, r.pm_cs, r.pscale, r.pw},
+              PoolEpi{});
+    FH_LAUNCH_CHECK("split conv reduction (deferred)");
+    return FH_OK;
+}
+
 static int ddef_materialize() {
     if (!g_ddef.pending) return FH_OK;
     g_ddef.pending = false;
@@ -1791,6 +1818,9 @@ static int launch_dual(const DPlan& p, dim3 grid, const DConvArgs& a, hipStream_
 template <int OP, int S = 1>
 static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes, int sp,
                      hipStream_t st, const char* name, bool* pooled = nullptr) {
+    const int sbn_want = g_sbn_want;
+    g_sbn_want = 0;
+    if (const int rc = sbn_materialize()) return rc;  // a pending split output may be read here
     DPlan p = plan_dconv(a.M, a.Cr, a.batch, sp, nclients, false, S == 2);
     const bool aligned = ((uintptr_t)a.wt % 16 == 0) && a.w_cs % 4 == 0;
     if (!(aligned && (OP == OP_FWD ? a.Cr % p.ck == 0 : a.M % p.bm == 0)) && p.bm != 32) {
@@ -1920,6 +1950,32 @@ static int run_dconv(DConvArgs a, int w, int nclients, void* ws, size_t ws_bytes
         }
     }
     if (p.splits > 1 && !inl) {
+        if (sbn_want && S == 1 && a.bn_part && !a.accumulate && !a.relu && !a.pool_y &&
+            p.splits <= 4 && (int64_t)a.batch * sp <= std::min(sbn_want, kSbnMaxElems) &&
+            a.bn_tiles == ceil_div(a.Nfull, 256) &&
+            (OP == OP_FWD ? a.bnx == nullptr : a.bnx != nullptr)) {
+            // the BN call after this conv sums the slab (splitbn.h, fh_conv_bn_defer)
+            SplitBnRec& r = g_sbn;
+            r = SplitBnRec{};
+            r.op = OP == OP_FWD ? 0 : 1;
+            r.part = (const float*)ws;
+            r.splits = p.splits; r.M = a.M; r.sp = sp; r.batch = a.batch; r.nclients = nclients;
+            r.Nfull = a.Nfull;
+            r.out = out; r.out_cs = a.out_cs;
+            r.bias = OP == OP_FWD ? a.bias : nullptr; r.b_cs = a.b_cs;
+            r.counts = a.counts;
+            r.bn_part = a.bn_part; r.bn_tiles = a.bn_tiles;
+            if (OP != OP_FWD) {
+                r.bnx = a.bnx; r.bnx_cs = a.bnx_cs; r.bn_scale = a.bn_scale;
+                r.bn_shift = a.bn_shift; r.bns_cs = a.bns_cs; r.bn_mean = a.bn_mean;
+                r.pidx = a.pidx; r.pmask = a.pmask; r.pi_cs = a.pi_cs; r.pm_cs = a.pm_cs;
+                r.pscale = a.pscale; r.pw = w;
+            }
+            r.st = st;
+            r.pending = true;
+            ++g_sbn_deferred;
+            return FH_OK;
+        }
         dim3 eg((unsigned)ceil_div(a.Nfull, 256), (unsigned)a.M, (unsigned)nclients);
         FH_LAUNCH(splitk_epilogue_kernel, eg, dim3(256), 0, st, (const float*)ws, p.splits,
                            a.M, a.Nfull, out, a.out_cs, OP == OP_FWD ? a.bias : nullptr, a.b_cs,
@@ -2144,6 +2200,8 @@ extern "C" int fh_conv_pair(int32_t mode) {
         // ... and a deferred DGRAD reduction armed or left pending by the failed step: its
         // partials would otherwise be claimed (or never reduced) by an unrelated later launch
         g_ddef = DgradDefer{};
+        g_sbn = SplitBnRec{};  // likewise a split reduction left for a BN call
+        g_sbn_armed = 0;
         return FH_OK;
     }
     if (mode > 0) {
@@ -2181,6 +2239,27 @@ extern "C" int fh_set_split_tickets(void* p, int64_t n) {
 extern "C" int fh_split_tickets_status(int64_t* inl_launches) {
     FH_REQUIRE(inl_launches, "split_tickets_status: null pointer");
     *inl_launches = g_inl_launches;
+    return FH_OK;
+}
+
+// fh_conv_bn_defer(1): the calling thread's next fh_conv2d_fwd_bnstats /
+// fh_conv2d_dgrad_bnstats call, when it plans a split direct launch, leaves its split reduction
+// to the BatchNorm call that consumes its statistics (fh_bn_finalize_tiles,
+// fh_maxpool2_fwd_bnfinalize, fh_bn_bwd_tiles, fh_bn_bwd_pool_tiles), which then sums the slab
+// and runs the BN pass as one launch — bit-identical outputs (splitbn.h).  A DGRAD's stored
+// gradient (dX) is then never written: only that BN call reads it.  Any other library call
+// that finds the reduction pending launches it first.  max_elems: the largest batch x plane
+// (elements per client and channel, <= 8192) the fusion takes; 0 disarms.
+extern "C" int fh_conv_bn_defer(int32_t max_elems) {
+    FH_REQUIRE(max_elems >= 0, "conv_bn_defer: %d", max_elems);
+    g_sbn_armed = max_elems;
+    return FH_OK;
+}
+
+extern "C" int fh_conv_bn_defer_status(int64_t* deferred, int64_t* taken) {
+    FH_REQUIRE(deferred && taken, "conv_bn_defer_status: null pointer");
+    *deferred = g_sbn_deferred;
+    *taken = sbn_taken();
     return FH_OK;
 }
 
@@ -2385,9 +2464,13 @@ extern "C" int fh_conv2d_fwd_bnstats(const float* x, int64_t x_cs, const float* 
     FH_REQUIRE(bn_part, "conv2d_fwd_bnstats: null statistics buffer");
     FH_REQUIRE(dconv_supported(h, w_, 3, 3, 1, 1), "conv2d_fwd_bnstats: needs a 3x3/s1/p1 conv "
                "on a square 8/16/32 map (got %dx%d)", h, w_);
-    return conv2d_fwd_impl(x, x_cs, in_scale, in_shift, aff_cs, w, w_cs, bias, b_cs, y, y_cs,
-                           counts, nclients, batch, cin, h, w_, cout, 3, 3, 1, 1, 0, workspace,
-                           ws_bytes, stream, bn_part);
+    g_sbn_want = g_sbn_armed;
+    g_sbn_armed = 0;
+    const int rc = conv2d_fwd_impl(x, x_cs, in_scale, in_shift, aff_cs, w, w_cs, bias, b_cs, y,
+                                   y_cs, counts, nclients, batch, cin, h, w_, cout, 3, 3, 1, 1, 0,
+                                   workspace, ws_bytes, stream, bn_part);
+    g_sbn_want = 0;
+    return rc;
 }
 
 extern "C" int fh_maxpool2_fwd_pitched(const float* x, int64_t x_cs, float* y, int64_t y_cs,
@@ -2512,8 +2595,12 @@ extern "C" int fh_conv2d_dgrad_bnstats(const float* dy, int64_t dy_cs, const flo
     FH_REQUIRE(p_drop >= 0.f && p_drop < 1.f, "conv2d_dgrad_bnstats: p=%g", p_drop);
     d.pidx = pidx; d.pmask = pidx ? pmask : nullptr; d.pi_cs = pi_cs; d.pm_cs = pm_cs;
     d.pscale = 1.0f / (1.0f - p_drop);
-    return run_dconv<OP_DGRAD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
-                               "conv2d_dgrad_bnstats");
+    g_sbn_want = g_sbn_armed;
+    g_sbn_armed = 0;
+    rc = run_dconv<OP_DGRAD>(d, w_, nclients, workspace, ws_bytes, h * w_, as_stream(stream),
+                             "conv2d_dgrad_bnstats");
+    g_sbn_want = 0;
+    return rc;
 }
 
 // The DGRAD of a ResNet down-sampling block's input in one launch (models_pytorch.py:176-194:

@@ -157,6 +157,8 @@ SIGNATURES = {
     "fh_conv_pair_status": (I32, [P, P]),
     "fh_conv_defer_dgrad": (I32, [I32]),
     "fh_conv_defer_status": (I32, [P, P]),
+    "fh_conv_bn_defer": (I32, [I32]),
+    "fh_conv_bn_defer_status": (I32, [P, P]),
     "fh_set_split_tickets": (I32, [P, I64]),
     "fh_split_tickets_status": (I32, [P]),
     "fh_conv_pooled_dy": (I32, [P, I64, P, I64, P, I64, I32]),

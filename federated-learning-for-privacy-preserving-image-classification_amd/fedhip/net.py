@@ -565,6 +565,7 @@ class PackedNet:
             part = None
             if fuse and self.bn_epilogue:
                 part = self._bn_part(bn, co, hw)
+                ops.conv_bn_defer()  # a split plan's reduction joins the BN finalize below
             ops.conv2d_fwd(xin, W(P_, f"{cv}.weight"), W(P_, f"{cv}.bias"), c, n, B, ci, hw, hw, co,
                            3, 1, 1, counts=cnt, in_affine=aff, bn_stats=part)
             pooled = i % 2 == 1
@@ -727,6 +728,7 @@ class PackedNet:
                           self._bn_save(pbn, ci)[0], bn_tiles,
                           A(f"i_{pcv}", ci, hw, hw, dtype=torch.uint8),
                           A(f"m_{pcv}", ci, hw, hw, dtype=torch.uint8) if dm else None, p)
+                    ops.conv_bn_defer()  # a split plan's reduction joins bn_bwd_pool_tiles
                 ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), dq, n, B, ci, hw, hw, co, 3, 1, 1,
                                  counts=cnt, bn_bwd=bb)
             else:
@@ -736,6 +738,7 @@ class PackedNet:
                     bn_tiles = self._bn_part(f"{pbn}.bwd", ci, hw)
                     bb = (A(f"c_{pcv}", ci, hw, hw), *self._bn_affine(pbn, ci),
                           self._bn_save(pbn, ci)[0], bn_tiles)
+                    ops.conv_bn_defer()  # ... joins bn_bwd_tiles
                 ops.conv2d_dgrad(dc, W(P_, f"{cv}.weight"), A(f"dr_{pcv}", ci, hw, hw), n, B, ci,
                                  hw, hw, co, 3, 1, 1, counts=cnt, bn_bwd=bb)
             ops.conv_pair(0)
@@ -766,6 +769,8 @@ class PackedNet:
             a = A(f"{pf}.a", co, ho, ho)
             bb, out = A(f"{pf}.b", co, ho, ho), A(f"{pf}.out", co, ho, ho)
             p1 = self._bn_part(f"{pf}.bn1", co, ho) if epi and s == 1 else None
+            if p1 is not None:
+                ops.conv_bn_defer()  # a split plan's reduction joins bn1's finalize
             ops.conv2d_fwd(xin, W(P_, f"{pf}.conv1.weight"), None, a, n, B, ci, hi, hi, co, 3, s, 1,
                            counts=cnt, bn_stats=p1)
             if fuse:
@@ -869,6 +874,7 @@ class PackedNet:
             if self._fused and self.bn_bwd_epilogue:
                 # conv2's dgrad masks by bn1's ReLU and leaves bn1's backward statistics
                 tiles = self._bn_part(f"{pf}.bn1.bwd", co, ho)
+                ops.conv_bn_defer()  # ... and bn1's backward apply
                 ops.conv2d_dgrad(db, W(P_, f"{pf}.conv2.weight"), dar, n, B, co, ho, ho, co, 3, 1,
                                  1, counts=cnt, bn_bwd=(a, *aff1, sm1, tiles))
                 ops.conv_pair(0)

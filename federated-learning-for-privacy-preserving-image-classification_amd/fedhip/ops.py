@@ -356,6 +356,37 @@ def conv_defer_dgrad(on):
     call("fh_conv_defer_dgrad", int(bool(on)))
 
 
+# ---- r06: a split conv's reduction inside the BatchNorm call after it (fh_conv_bn_defer) ----
+# The splitk_epilogue launch of a split direct conv with a statistics epilogue and the BN
+# finalize / pool-finalize / backward apply that reads it as one launch (bn.hip
+# split_bnfin_kernel / split_bnbwd_kernel), bit-identical (tests/test_split_bn_gpu.py).  Off by
+# default (FH_SPLIT_BN=1 turns it on): one 1024-thread workgroup per channel reduces the whole
+# map, a serial chain as long as the two wide launches it replaces — a solo one-client KT step
+# 42 -> 34 launches but 0.392 -> 0.391 ms, and KT -0.8 % (maps <= 2048 elements) / -1.1 % (all),
+# interleaved x2 (profiles/r06_splitbn/).
+SPLIT_BN = [os.environ.get("FH_SPLIT_BN", "0") == "1"]
+# the largest batch x plane (elements per client-channel) fused when on
+SPLIT_BN_MAX = [int(os.environ.get("FH_SPLIT_BN_MAX", "8192"))]
+
+
+def conv_bn_defer(max_elems=None):
+    """Arm fh_conv_bn_defer for this thread's next conv2d_fwd(bn_stats=...) /
+    conv2d_dgrad(bn_bwd=...): if it plans a split launch on a map of at most max_elems
+    (default SPLIT_BN_MAX) elements per client and channel, its reduction is left to the BN
+    call that consumes the statistics (which the caller must issue next).  A probed round that
+    keeps launches apart (PROBE tag other than "*") does not arm."""
+    if SPLIT_BN[0] and not (PROBE.enabled and not PROBE.all):
+        call("fh_conv_bn_defer", int(SPLIT_BN_MAX[0] if max_elems is None else max_elems))
+
+
+def bn_defer_status():
+    """(split reductions left to a BN call, fused launches issued) on this thread
+    (fh_conv_bn_defer_status)."""
+    d, t = ctypes.c_int64(), ctypes.c_int64()
+    call("fh_conv_bn_defer_status", ctypes.byref(d), ctypes.byref(t))
+    return d.value, t.value
+
+
 def defer_status():
     """(DGRADs left unreduced, partial slabs summed by their consumer) on this thread
     (fh_conv_defer_status): tests assert a deferral really happened."""

@@ -710,6 +710,23 @@ int fh_conv_defer_dgrad(int32_t on);
 /* r06 (instrumentation): DGRADs the calling thread left unreduced under fh_conv_defer_dgrad, and
  * how many of those partial slabs a conv1 weight-gradient consumer summed while staging. */
 int fh_conv_defer_status(int64_t* deferred, int64_t* taken);
+/* r06: fh_conv_bn_defer(max_elems) arms the calling thread's next fh_conv2d_fwd_bnstats /
+ * fh_conv2d_dgrad_bnstats call: when it plans a split direct launch (at most 4 splits, batch x
+ * plane <= min(max_elems, 8192)), its split reduction — the splitk_epilogue launch that writes
+ * the output and the statistics tiles — is left to the BatchNorm call that consumes those tiles, which the
+ * caller issues next: fh_bn_finalize_tiles or fh_maxpool2_fwd_bnfinalize after the FWD,
+ * fh_bn_bwd_tiles or fh_bn_bwd_pool_tiles after the DGRAD.  That call then runs the reduction
+ * and its own pass as ONE launch (one workgroup per channel and client), every stored value
+ * bit-identical to the two launches; the DGRAD's own output (the masked or pooled gradient,
+ * read by nothing but that BN call) is then not written.  Any other library call that finds
+ * the reduction pending launches it first; fh_conv_pair(-1) drops it.  max_elems 0 disarms.
+ * Measured no faster than the two launches on MI355X (fedhip.ops.SPLIT_BN: off by default).
+ * Replaces nothing in the reference: the pair is BatchNorm2d after Conv2d,
+ * src/shared/models_pytorch.py:133-150 (CIFAR10CNN), :189-194 (FederatedResNet block). */
+int fh_conv_bn_defer(int32_t max_elems);
+/* r06 (instrumentation): split reductions the calling thread left to a BN call, and fused
+ * launches the BN calls issued. */
+int fh_conv_bn_defer_status(int64_t* deferred, int64_t* taken);
 /* r06: in-launch split-K reduction.  A direct 3x3 FWD / DGRAD (and the DGRAD role of the
  * dual-role backward) whose plan splits the input-channel reduction stores each split's partial
  * tile write-through and takes a ticket; the tile's last arriving workgroup sums the partials in
