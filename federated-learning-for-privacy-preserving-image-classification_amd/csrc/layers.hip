@@ -443,10 +443,21 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         const bool arow = ia < cnt, bcol = mn < K;
         const float* xa = Xs + ia * FP + fh * Fh + kk;
         const float* wb = Ws + mn * FP + fh * Fh + kk;
+        // r06: every operand read up front (unconditional: the arrays hold FMAX-wide rows, so
+        // any F <= FMAX stays in bounds; past Fh the values are unused), then the MFMA chain in
+        // the same order — the read -> MFMA loop waited on each pair, ~2.5 us of the launch
+        constexpr int NQ = FMAX / 8;
+        float xr[NQ], wr[NQ];
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+            const float xv = xa[4 * u], wv2 = wb[4 * u];
+            xr[u] = arow ? xv : 0.f;
+            wr[u] = bcol ? wv2 : 0.f;
+        }
         hf32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int f = 0; f < Fh; f += 4)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(arow ? xa[f] : 0.f, bcol ? wb[f] : 0.f,
-                                                       acc, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < NQ; ++u)
+            if (4 * u < Fh) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[u], wr[u], acc, 0, 0, 0);
         float* lp = fh ? D : L;
 #pragma unroll
         for (int r = 0; r < 4; ++r) lp[(t * 16 + 4 * kk + r) * 16 + mn] = acc[r];
@@ -484,38 +495,62 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
     double lsum = 0.0;
     int corr = 0;
     if (K <= 16) {
+        // a group of 16 lanes per image, the group's two images (g, g + 16; batch <= 32) side
+        // by side so their shuffle chains overlap — each image's operations and order as before
         const int g = tid >> 4, l = tid & 15;
-        for (int img = g; img < cnt; img += 16) {
-            const float* row = L + img * K;
-            const int tgt = SMALLK ? (int)Ts[img] : (int)targets[z * t_cs + img];
-            const float v = l < K ? row[l] : -INFINITY;
-            float mx = v;
-            int amax = l < K ? l : K;
+        float v[2], mx[2], se[2];
+        int amax[2], tgt[2];
 #pragma unroll
-            for (int o = 8; o > 0; o >>= 1) {
-                const float om = __shfl_xor(mx, o, 16);
-                const int oa = __shfl_xor(amax, o, 16);
-                if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+        for (int u = 0; u < 2; ++u) {
+            const int img = g + 16 * u;  // < 32: L has 32 rows
+            tgt[u] = img < cnt ? (SMALLK ? (int)Ts[img] : (int)targets[z * t_cs + img]) : 0;
+            v[u] = l < K ? L[img * K + l] : -INFINITY;
+            mx[u] = v[u];
+            amax[u] = l < K ? l : K;
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float om = __shfl_xor(mx[u], o, 16);
+                const int oa = __shfl_xor(amax[u], o, 16);
+                if (om > mx[u] || (om == mx[u] && oa < amax[u])) { mx[u] = om; amax[u] = oa; }
             }
-            float se = l < K ? expf(v - mx) : 0.f;
 #pragma unroll
-            for (int o = 8; o > 0; o >>= 1) se += __shfl_xor(se, o, 16);
-            const float lse = logf(se);
+        for (int u = 0; u < 2; ++u) se[u] = l < K ? expf(v[u] - mx[u]) : 0.f;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) se[u] += __shfl_xor(se[u], o, 16);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int img = g + 16 * u;
+            if (img >= cnt) break;  // uniform over the group
+            const float lse = logf(se[u]);
             if (l == 0) {
-                li[img] = (double)(-((row[tgt] - mx) - lse));
-                ci[img] = amax == tgt;
+                li[img] = (double)(-((L[img * K + tgt[u]] - mx[u]) - lse));
+                ci[img] = amax[u] == tgt[u];
             }
             if (l < K) {
-                const float p = expf((v - mx) - lse);
-                D[img * K + l] = (p - (l == tgt ? 1.f : 0.f)) * inv_n;
+                const float p = expf((v[u] - mx[u]) - lse);
+                D[img * K + l] = (p - (l == tgt[u] ? 1.f : 0.f)) * inv_n;
             }
         }
         __syncthreads();
-        if (tid < 4) {
-            for (int img = tid; img < cnt; img += 4) {
-                lsum += li[img];
-                corr += ci[img];
+        if (tid < 4) {  // image order, the reads first
+            double lv[8];
+            int cv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                lv[j] = li[tid + 4 * j];
+                cv[j] = ci[tid + 4 * j];
             }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (tid + 4 * j < cnt) {
+                    lsum += lv[j];
+                    corr += cv[j];
+                }
             sl[tid] = lsum;
             sc[tid] = corr;
         }
@@ -569,9 +604,13 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         }
         if (SMALLK && db && wid == 0) {  // four image groups per class, then xor-combined
             const int k = lane & 15, g = lane >> 4;
-            float v = 0.f;
+            float v = 0.f, dv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dv[j] = D[(g + 4 * j) * K + k];  // < 32 x 16: in bounds
             if (k < K)
-                for (int b = g; b < cnt; b += 4) v += D[b * K + k];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (g + 4 * j < cnt) v += dv[j];
             v += __shfl_xor(v, 16, 64);
             v += __shfl_xor(v, 32, 64);
             if (lane < K) db[z * db_cs + lane] = v;
@@ -587,14 +626,19 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
         const int mn = lane & 15, kk = lane >> 4;
         for (int tt = part + S * wid; tt < F / 16; tt += 4 * S) {
             const int f0 = tt * 16;
-            hf32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            for (int b0 = 0; b0 < cnt; b0 += 4) {
-                const int b = b0 + kk;
+            float dr[8], xr2[8];  // operands read up front (in bounds: b < 32, mn < 16)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int b = 4 * q + kk;
                 const bool ok = b < cnt;
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ok && mn < K ? D[b * K + mn] : 0.f,
-                                                           ok ? Xs[b * FP + f0 + mn] : 0.f, acc,
-                                                           0, 0, 0);
+                const float dv = D[b * K + mn], xv = Xs[b * FP + f0 + mn];
+                dr[q] = ok && mn < K ? dv : 0.f;
+                xr2[q] = ok ? xv : 0.f;
             }
+            hf32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (4 * q < cnt) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dr[q], xr2[q], acc, 0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int k = 4 * kk + r;
@@ -622,13 +666,18 @@ linear_head_ce_kernel(const float* __restrict__ x, int64_t x_cs, const float* __
             const int t = tt & 1, f0 = (tt >> 1) * 16;
             if (t * 16 >= cnt) continue;  // wave-uniform
             const int ia = t * 16 + mn;
-            hf32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            for (int k0 = 0; k0 < K; k0 += 4) {
-                const int k = k0 + kk;
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                    k < K && ia < cnt ? D[ia * K + k] : 0.f, k < K ? Ws[k * FP + f0 + mn] : 0.f,
-                    acc, 0, 0, 0);
+            float dr[KMAX / 4], wr2[KMAX / 4];  // read up front (in bounds: ia < 32, k < 16)
+#pragma unroll
+            for (int q = 0; q < KMAX / 4; ++q) {
+                const int k = 4 * q + kk;
+                const float dv = D[ia * K + k], wv2 = Ws[k * FP + f0 + mn];
+                dr[q] = k < K && ia < cnt ? dv : 0.f;
+                wr2[q] = k < K ? wv2 : 0.f;
             }
+            hf32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < KMAX / 4; ++q)
+                if (4 * q < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dr[q], wr2[q], acc, 0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int img = t * 16 + 4 * kk + r, f = f0 + mn;

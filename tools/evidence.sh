@@ -24,7 +24,7 @@ summ() {  # one-line summary of a bench line
   python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; k=d.get('k2') or {}; print('$2', d['value'], d.get('round_frac'), r['kernel'], r['frac'], 'K2', k.get('value'), k.get('round_frac'), 'bytes', len(open('$1').read().strip().splitlines()[-1]))"
 }
 if [[ $ST == *t* ]]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
   tail -1 $O/gpu_tests.log
 fi
 if [[ $ST == *s* ]]; then
