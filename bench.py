@@ -1010,8 +1010,10 @@ def compact(out):
                             "round_frac": dp["round_frac"],
                             "roofline": {k: r[k] for k in ("kernel", "bound", "achieved", "frac",
                                                            "avg_launch_ms") if k in r} or None,
-                            "cpu_baseline": {k: c[k] for k in ("value", "cores", "kind")
-                                             if k in c} or None}
+                            "cpu_baseline": ({"value": round(c["value"], 1), "unit": c["unit"],
+                                              "cores": c["cores"], "kind": c["kind"],
+                                              "passes": c.get("passes")}
+                                             if "value" in c else None)}
     line["env"] = out.get("env", {})
     line["detail"] = out.get("detail_file")
     s = json.dumps(line)
