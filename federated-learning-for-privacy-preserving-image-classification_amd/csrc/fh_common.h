@@ -54,12 +54,15 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 struct KernelArgs {
     virtual ~KernelArgs() = default;
     void** params = nullptr;
+    const size_t* sizes = nullptr;  // bytes of each argument (program relocation, program.hip)
+    int nargs = 0;
 };
 
 template <typename... P>
 struct KernelArgsT final : KernelArgs {
     std::tuple<P...> vals;
     void* ptrs[sizeof...(P) > 0 ? sizeof...(P) : 1];
+    size_t szs[sizeof...(P) > 0 ? sizeof...(P) : 1];
     explicit KernelArgsT(P... p) : vals(p...) { bind(std::index_sequence_for<P...>{}); }
     KernelArgsT(const KernelArgsT&) = delete;
     KernelArgsT& operator=(const KernelArgsT&) = delete;
@@ -68,7 +71,10 @@ struct KernelArgsT final : KernelArgs {
     template <size_t... I>
     void bind(std::index_sequence<I...>) {
         ((ptrs[I] = (void*)&std::get<I>(vals)), ...);
+        ((szs[I] = sizeof(std::tuple_element_t<I, std::tuple<P...>>)), ...);
         params = ptrs;
+        sizes = szs;
+        nargs = (int)sizeof...(P);
     }
 };
 

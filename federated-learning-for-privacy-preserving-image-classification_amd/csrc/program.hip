@@ -18,6 +18,7 @@
 // contains anything the recorder cannot see (a memset, a copy, a kernel launched outside
 // libfedhip) makes the recording invalid and the caller replays the graph instead.
 #include <algorithm>
+#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -32,8 +33,16 @@ struct RecordedKernel {
     std::unique_ptr<KernelArgs> args;
 };
 
+// r06: argument words of the recorded launches that point into the step's per-step input
+// slot (fh_program_relocate); fh_program_launch_at rewrites them to another row first.
+struct Reloc {
+    uint64_t* word;
+    uint64_t off;
+};
+
 struct Recorder {
     std::vector<RecordedKernel> kernels;
+    std::vector<Reloc> relocs;
     Recorder* prev = nullptr;  // recorders nest per thread (never in practice)
 };
 
@@ -156,6 +165,62 @@ extern "C" int fh_program_launch(void* program, void* stream) {
         FH_HIPCHK(hipLaunchKernel(k.func, k.grid, k.block, k.args->params, k.shmem, st),
                   "fh_program_launch");
     return FH_OK;
+}
+
+// r06: relocation of the per-step input slot.  A step program's kernels read the step's
+// inputs (batch indices, counts, reset flags, Philox key block, Adam scalars) from one fixed
+// slot that a copy_bytes launch refills from the round's row g before every step — one more
+// ~4.5 us dependent launch per step on every lane.  fh_program_relocate finds every 8-byte
+// argument word (struct fields included) equal to one of the slot's view pointers `ptrs`; any
+// other word pointing into [base, base + len) fails the relocation (found = -1: the caller
+// keeps copying).  fh_program_launch_at rewrites those words to the same offsets in another
+// row (hipLaunchKernel copies the argument bytes at enqueue) and issues the program: the
+// kernels read row g itself and the copy launch disappears.
+extern "C" int fh_program_relocate(void* program, const uint64_t* ptrs, int32_t nptrs,
+                                   uint64_t base, int64_t len, int32_t* found) {
+    auto* r = (Recorder*)program;
+    if (!r || !found || (nptrs > 0 && !ptrs) || nptrs < 0 || len <= 0 || fh::g_recorder == r) {
+        fh::set_error("fh_program_relocate: bad arguments");
+        return FH_E_INVALID;
+    }
+    for (int j = 0; j < nptrs; ++j)
+        if (ptrs[j] < base || ptrs[j] >= base + (uint64_t)len) {
+            fh::set_error("fh_program_relocate: pointer %d outside the slot", j);
+            return FH_E_INVALID;
+        }
+    r->relocs.clear();
+    for (auto& k : r->kernels) {
+        const fh::KernelArgs* a = k.args.get();
+        for (int i = 0; i < a->nargs; ++i) {
+            char* p = (char*)a->params[i];
+            for (size_t o = 0; o + 8 <= a->sizes[i]; o += 8) {
+                if (((uintptr_t)(p + o)) % 8) continue;
+                uint64_t v;
+                memcpy(&v, p + o, 8);
+                if (v < base || v >= base + (uint64_t)len) continue;
+                bool known = false;
+                for (int j = 0; j < nptrs && !known; ++j) known = v == ptrs[j];
+                if (!known) {  // a pointer into the slot the caller did not declare
+                    r->relocs.clear();
+                    *found = -1;
+                    return FH_OK;
+                }
+                r->relocs.push_back(fh::Reloc{(uint64_t*)(p + o), v - base});
+            }
+        }
+    }
+    *found = (int32_t)r->relocs.size();
+    return FH_OK;
+}
+
+extern "C" int fh_program_launch_at(void* program, void* stream, uint64_t base) {
+    auto* r = (Recorder*)program;
+    if (!r || fh::g_recorder == r || r->relocs.empty() || !base) {
+        fh::set_error("fh_program_launch_at: no relocatable program");
+        return FH_E_INVALID;
+    }
+    for (const auto& rl : r->relocs) *rl.word = base + rl.off;
+    return fh_program_launch(program, stream);
 }
 
 // Per-step input row -> the fixed slot the step kernels read (a kernel: part of the

@@ -171,6 +171,8 @@ SIGNATURES = {
     "fh_graph_node_counts": (I32, [P, P, P]),
     "fh_program_matches_graph": (I32, [P, P, P]),
     "fh_program_launch": (I32, [P, P]),
+    "fh_program_relocate": (I32, [P, P, I32, U64, I64, P]),
+    "fh_program_launch_at": (I32, [P, P, U64]),
     "fh_program_destroy": (I32, [P]),
     "fh_copy_bytes": (I32, [P, P, I64, P]),
     "fh_gather_u8": (I32, [P, P, P, I64, P, I64, P, I64, P, I32, I32, I32, I32, I32, P, P, I32,

@@ -44,6 +44,9 @@ from .net import PackedNet
 # FH_LAUNCH=graph|program|eager overrides how steps after the first are issued
 # (diagnostics; "eager" = no capture at all, e.g. under rocprofv3 --pmc)
 _LAUNCH_ENV = os.environ.get("FH_LAUNCH", "")
+# r06: step programs read each step's input row in place (Program.relocate) instead of a
+# copy_bytes launch into the fixed slot; FH_RELOCATE=0 keeps the copy (A/B)
+RELOCATE = [os.environ.get("FH_RELOCATE", "1") != "0"]
 
 # Every trainer's captured steps are released at exit, programs before graphs and
 # after a device sync, while the HIP runtime is still up (destroying captured graphs
@@ -365,14 +368,19 @@ class PackedTrainer:
         n = plan["active"][g]
         if self.pre_step is not None:  # diagnostic hook
             self.pre_step(g, n, plan)
-        if (_LAUNCH_ENV or self.launch_mode) == "program":
+        program = (_LAUNCH_ENV or self.launch_mode) == "program"
+        full = n == self.capacity and (g == 0 or not self.probe_first_only)
+        replay = st["graphs"] and g > 0 and not (self.probe_full and full)
+        if replay and program:
+            pass  # _replay reads row g in place (a relocated program) or copies it first
+        elif program:
             ops.copy_bytes(st["rows"][g], st["cur"])
         else:
             st["cur"].copy_(st["rows"][g], non_blocking=True)
         self.opt_step += 1
-        full = n == self.capacity and (g == 0 or not self.probe_first_only)
-        if st["graphs"] and g > 0 and not (self.probe_full and full):
-            self._replay(n, st["data"], st["labels"], views, st["sample_elems"])
+        if replay:
+            self._replay(n, st["data"], st["labels"], views, st["sample_elems"],
+                         row=st["rows"][g] if program else None, cur=st["cur"])
         else:
             arm = self.probe_full and full and bool(st["full_batch"][g])
             if not ops.PROBE.all:  # "*": an instrumented round, every launch timed
@@ -464,12 +472,15 @@ class PackedTrainer:
             ops.gather_batch(data, labels, views["gidx"], net.x, net.y, sample_elems, n,
                              self.batch, counts=views["counts"])
 
-    def _replay(self, n, data, labels, views, sample_elems):
+    def _replay(self, n, data, labels, views, sample_elems, row=None, cur=None):
         """Replay the captured step for n active clients: as a HIP graph, or (launch_mode
         "program", concurrent lanes) as its recorded kernel list issued on this trainer's
         stream (csrc/program.hip; measured +1.3 % on KT with three lanes).  The program is
         recorded by libfedhip during the same capture; if it did not see every node of the
-        graph (a non-libfedhip op inside the step) the graph is replayed instead."""
+        graph (a non-libfedhip op inside the step) the graph is replayed instead.
+        row (program mode): this step's input row; the program's pointers into the per-step
+        slot are relocated onto it (r06, Program.relocate) — no copy launch — else it is
+        copied into the slot first."""
         key = (n, self.opt_type, self.lr, self.transform, data.data_ptr(), labels.data_ptr(),
                views["gidx"].data_ptr(), tuple(views["gidx"].shape))
         mode = _LAUNCH_ENV or self.launch_mode
@@ -498,10 +509,20 @@ class PackedTrainer:
             if prog is not None and not prog.complete_for(graph):
                 prog.release()  # fail closed: replay the graph
                 prog = None
+            if prog is not None and cur is not None and RELOCATE[0]:
+                prog.relocate([views[k].data_ptr() for k in ("gidx", "counts", "reset", "seed",
+                                                             "adam")] + [cur.data_ptr()],
+                              cur.data_ptr(), cur.numel() * cur.element_size())
             entry = self._graphs[key] = (graph, prog)
         graph, prog = entry
+        stream = torch.cuda.current_stream(self.device)
+        if row is not None and prog is not None and prog.relocs > 0:
+            prog.launch_at(stream, row.data_ptr())
+            return
+        if row is not None:
+            ops.copy_bytes(row, cur)
         if prog is not None:
-            prog.launch(torch.cuda.current_stream(self.device))
+            prog.launch(stream)
         else:
             graph.replay()
 

@@ -264,6 +264,7 @@ class Program:
 
     def __init__(self, handle, kernels):
         self.handle, self.kernels = handle, kernels
+        self.relocs = 0  # relocate(): argument words pointing at the per-step input slot
 
     @staticmethod
     def record_begin():
@@ -288,6 +289,22 @@ class Program:
 
     def launch(self, stream):
         call("fh_program_launch", self.handle, stream.cuda_stream)
+
+    def relocate(self, ptrs, base, nbytes) -> int:
+        """Mark the argument words pointing at the per-step input slot [base, base + nbytes)
+        (each equal to one of ptrs) for launch_at; returns how many, or -1 when some argument
+        points into the slot elsewhere (then only launch() is valid)."""
+        arr = (ctypes.c_uint64 * len(ptrs))(*ptrs)
+        n = ctypes.c_int32()
+        call("fh_program_relocate", self.handle, arr, len(ptrs), int(base), int(nbytes),
+             ctypes.byref(n))
+        self.relocs = n.value
+        return n.value
+
+    def launch_at(self, stream, base):
+        """launch() with the relocated words pointing into the row at `base` instead of the
+        slot (fh_program_launch_at): the step reads its inputs from that row directly."""
+        call("fh_program_launch_at", self.handle, stream.cuda_stream, int(base))
 
     def release(self):
         if getattr(self, "handle", None):

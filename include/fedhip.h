@@ -776,6 +776,16 @@ int fh_graph_node_counts(void* graph, int32_t* kernels_out, int32_t* others_out)
  */
 int fh_program_matches_graph(void* program, void* graph, int32_t* match_out);
 int fh_program_launch(void* program, void* stream);
+/* r06: relocation of the per-step input slot.  fh_program_relocate marks every 8-byte
+ * argument word of the recorded launches (struct fields included) equal to one of ptrs[0..n),
+ * each inside [base, base + len) — the step's per-step input slot and its views; *found = the
+ * number of words, or -1 when some other word points into the slot (then only
+ * fh_program_launch is valid).  fh_program_launch_at rewrites those words to the same offsets
+ * from new_base (another row laid out like the slot) and issues the program: the step reads
+ * its inputs in place, without a copy into the slot first. */
+int fh_program_relocate(void* program, const uint64_t* ptrs, int32_t nptrs, uint64_t base,
+                        int64_t len, int32_t* found);
+int fh_program_launch_at(void* program, void* stream, uint64_t new_base);
 int fh_program_destroy(void* program);
 
 /* Launch timestamps of the dual-role conv backward (bench.py's roofline over the TIMED
