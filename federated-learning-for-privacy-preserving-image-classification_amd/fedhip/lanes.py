@@ -118,10 +118,13 @@ class LanedTrainer:
         # two clients anywhere in the job share a stream
         for ln in self.lanes:
             ln.net.salt = (ln.net.salt + salt * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
-        if len(self.lanes) > 1:
-            for i, ln in enumerate(self.lanes):
+        for i, ln in enumerate(self.lanes):
+            # csrc/program.hip: +1.3 % over graph replay with concurrent lanes; since r06 (the
+            # step reads its input row in place, no copy) a single lane too: a rank holding
+            # only KT's 131-step client 52.1 -> 50.2-50.7 ms per round (profiles/r06_reloc/)
+            ln.launch_mode = "program"
+            if len(self.lanes) > 1:
                 ln.stream = self._lane_stream(i)
-                ln.launch_mode = "program"  # csrc/program.hip: +1.3 % over graph replay
         # split-K fill fraction per lane (ops.set_fill_fraction)
         self.fill = [1.0] * len(self.lanes)
         if len(self.lanes) > 1:
